@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""bench.py — GNCDE vector-field evals/sec on BASELINE.json configs[1]:
+Heat-Diffusion n=64, batch=1024 per GPU, L=3, hidden 16, fixed-step RK4 (100 steps) on MI355X.
+
+One "step" = one gncde_integrate launch that solves the whole per-GPU batch (1024 samples x 100 RK4
+steps x 4 vector-field evaluations = 409,600 sample-evals) with inputs already resident in HBM.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Multi-GPU: samples are independent, so each rank integrates its own 1024-sample shard
+with no collective in the data path ("scaling": "weak"); the timed region is bracketed by barrier +
+synchronize and the max over ranks is reported.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "perm-equiv-graph-neural-cdes_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+METRIC = "GNCDE vector-field evals/sec (batch×n×n) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32 MFMA dense (= f32 vector peak)
+
+
+def algorithmic_bytes_per_eval(n, d0, dL):
+    """fp32 (d,c,b,a) operator-channel coefficients of the active interval + stage state
+    in + k out."""
+    return 16 * n * n + 4 * n * (d0 + dL)
+
+
+def algorithmic_flops_per_eval(n, dims):
+    """19 n^2 (spline) + sum_l [22 n^2 + 2 n^2 d_l + 2 n d_{l-1} d_l + 6 n d_l]."""
+    f = 19 * n * n
+    for l in range(1, len(dims)):
+        f += 22 * n * n + 2 * n * n * dims[l] + 2 * n * dims[l - 1] * dims[l] + 6 * n * dims[l]
+    return f
+
+
+def load_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+        if d.get("workload") == workload:
+            return float(d["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def cpu_baseline(prob, spec, y0, layers, target_s):
+    """The C restatement (oracle/gncde_oracle.c, OpenMP) on a bounded sample of the same workload."""
+    from oracle import c_oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    lay = [{k: v.numpy() for k, v in L.items()} for L in layers]
+
+    def run(nb):
+        ts = prob.ts[:nb].cpu().numpy()
+        coef = prob.coef[:nb].cpu().numpy()
+        tcoef = prob.tcoef[:nb].cpu().numpy()
+        grid = spec.grid[:nb].cpu().numpy()
+        ns = spec.nsteps[:nb].cpu().numpy()
+        yy = y0[:nb].cpu().numpy()
+        t0 = time.perf_counter()
+        _, nev = c_oracle.rk4(ts, coef, tcoef, lay, grid, ns, yy, nthreads=threads)
+        return nev, time.perf_counter() - t0
+
+    c_oracle.load()
+    nev1, dt1 = run(1)  # calibration (1 sample, 1 thread busy)
+    nb = int(max(threads, min(prob.B, math.ceil(target_s / max(dt1, 1e-6)) * threads)))
+    nb = min(nb, prob.B)
+    nev, dt = run(nb)
+    return {"value": nev / dt, "unit": "sample-evals/s", "cores": threads, "kind": "port",
+            "sample": f"{nb} of the {prob.B} samples, full 100-step RK4 solve each ({nev} VF evals, "
+                      f"{dt:.1f} s, oracle/gncde_oracle.c fp32, literal reference fusion, OpenMP)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1024, help="samples per GPU")
+    ap.add_argument("--rk4-steps", type=int, default=100)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    import gncde
+    from gncde import layout, synthetic
+
+    n_nodes, hidden, L, T = 64, 16, 3, 120
+    B = args.batch
+    prob, y0, layers = synthetic.heat_batch(B, num_nodes=n_nodes, hidden=hidden, num_layers=L, T=T,
+                                            seed=1234 + rank)
+    grids = [layout.rk4_grid(0.0, 5.0, args.rk4_steps)] * B  # every sample spans [0, final_time]
+    grid, ns = layout.stack_grids(grids)
+    spec = gncde.SolverSpec(method=gncde._lib.RK4, save_mode=gncde._lib.SAVE_T1, grid=grid, nsteps=ns)
+    path = gncde.integrate_path(prob, spec)
+    workload = f"heat_n{prob.n}_b{B}_L{L}_h{hidden}_T{T}_rk4x{args.rk4_steps}"
+
+    ys, st = gncde.integrate(prob, spec, y0, stats=True)
+    evals_per_launch = int(st[:, gncde._lib.STAT_EVALS].sum().item())
+    for _ in range(args.warmup):
+        gncde.integrate(prob, spec, y0)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        gncde.integrate(prob, spec, y0)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one fused launch per step, same stream
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    tot = torch.tensor([evals_per_launch * args.steps], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    elapsed = float(el.item())
+    total_evals = float(tot.item())
+    value = total_evals / elapsed
+
+    if rank == 0:
+        n = prob.n
+        bpe = algorithmic_bytes_per_eval(n, hidden, hidden)
+        fpe = algorithmic_flops_per_eval(n, prob.dims)
+        gbs = evals_per_launch * bpe / (kernel_ms * 1e-3) / 1e9
+        tfs = evals_per_launch * fpe / (kernel_ms * 1e-3) / 1e12
+        hbm = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        mfma = {"bound": "mfma", "achieved": round(tfs, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4)}
+        roof, alt = (hbm, mfma) if hbm["frac"] >= mfma["frac"] else (mfma, hbm)
+        traffic = load_traffic(workload)
+        roof["traffic"] = traffic
+        roof["kernel_ms"] = round(kernel_ms, 4)
+        roof["algorithmic_per_launch"] = (evals_per_launch * bpe if roof["bound"] == "hbm"
+                                          else evals_per_launch * fpe)
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(prob, spec, y0, layers, args.cpu_seconds)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "sample-evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic: heat-diffusion-shaped 8x8 grid graph with edge events, normalized-Laplacian "
+                    "operator path, backward-Hermite coefficients built on device; random reference-init params",
+            "config": {"workload": workload, "global_batch": B * world, "per_gpu_batch": B, "n": n,
+                       "hidden": hidden, "layers": L, "knots": T, "solver": "rk4",
+                       "solver_steps": args.rk4_steps, "parallelism": f"dp{world}"},
+            "edge_evals_per_s": round(value * n * n, 1),
+            "kernel": path,
+            "roofline": roof,
+            "roofline_other": alt,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

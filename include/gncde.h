@@ -1,0 +1,162 @@
+/*
+ * gncde.h — C-ABI of the MI355X-native GNCDE integration engine (libgncde_hip.so, gfx950).
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference is
+ * pure JAX; the calls these entry points replace are:
+ *
+ *   gncde_vf_eval     <- PermEquivGraphVectorField.__call__(t, y, args)
+ *                        src/models/vector_fields/perm_equiv_graph_vector_field.py:85-129
+ *                        (+ GraphVectorField.__call__ graph_vector_field.py:80-115,
+ *                           PermEquivDirGraphVectorField.__call__ perm_equiv_dir_graph_vector_field.py:86-130,
+ *                           CDEWrapperVectorField.__call__ cde_wrapper_vector_field.py:19-26),
+ *                        batched over the jax.vmap axis of src/configs/loss_configs.py:44.
+ *   gncde_integrate   <- diffrax.diffeqsolve(ODETerm(vf), Tsit5(), t0, t1, dt0, y0, args=spline,
+ *                                            stepsize_controller, saveat)
+ *                        src/models/graph_neural_cde.py:94-104 (PIDController(1e-3,1e-6), dt0=None),
+ *                        src/models/pgt_graph_neural_cde.py:119-129 (ConstantStepSize, dt0=0.1),
+ *                        src/models/tgb_graph_neural_cde.py:152-162 (ConstantStepSize, dt0=0.01),
+ *                        plus fixed-step RK4 (build extension, BASELINE.json configs[1]).
+ *   gncde_node_affine <- jax.vmap(eqx.nn.Linear) per node: graph_neural_cde.py:87 (initial_linear),
+ *                        :106-109 (final_linear).
+ *   gncde_interval_index <- diffrax CubicInterpolation interval rule (searchsorted, 'left') used at
+ *                        perm_equiv_graph_vector_field.py:98-102 — exported so the index can be
+ *                        checked bit-exactly.
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer (hipMalloc / torch cuda tensor), fp32 unless stated,
+ *     contiguous row-major.  The caller owns all memory; the library never allocates or frees
+ *     caller memory.  Scratch comes from a caller-allocated workspace of gncde_workspace_bytes().
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).  All work is enqueued
+ *     asynchronously on it; no entry point synchronises the device, so calls are graph-capturable.
+ *   - Return value 0 = success, otherwise a GNCDE_ERR_* code; gncde_strerror() describes it.
+ *     No C++ exception crosses this boundary.  Per-sample solver failures (max_steps exceeded,
+ *     non-finite state) are reported in the stats array, not as a return code.
+ *   - Reentrant and thread-safe for distinct streams/workspaces.  No global mutable state.
+ *
+ * Data layout in HBM (one GPU holds its shard of the batch):
+ *   ts        [B, T]               knot times per sample (increasing)
+ *   coef      [B, T-1, 4, n, n]    operator-channel spline coefficients in diffrax tuple order
+ *                                  (d, c, b, a) — i.e. the reference's coeffs[q][..., 1], de-interleaved
+ *   tcoef     [B, T-1, 3, n]       column means over rows of the time-channel coefficients (d, c, b)[..., 0];
+ *                                  tg(t)[i] = tb + f*(2*tc + 3*f*td) == jnp.mean(derivative(t)[...,0], axis=0)
+ *   data_coef [B, T-1, 4, n, de, 2] CDE data spline (d, c, b, a) (CDE wrapper only, else NULL)
+ *   fusion    [L, GNCDE_FC]        factored fusion table (see GNCDE_FC_* below), one row per layer
+ *   params    per layer l, packed back to back: rms_w[d_l], rms_b[d_l], W[d_{l+1}, d_l], b[d_{l+1}]
+ *   y / y0    [B, n, d_0] state (node-major, like the reference's y [n, h])
+ */
+#ifndef GNCDE_H
+#define GNCDE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNCDE_ABI_VERSION 1
+#define GNCDE_MAX_LAYERS 8
+#define GNCDE_FC 24
+
+/* Fusion table columns.  For layer l:
+ *   (I + Abar) = e_A*A + e_dA*dA + eT_A*A^T + eT_dA*dA^T + diag(u) + w 1^T + 1 v^T
+ *   u_i = idc + uD_A*A_ii + uD_dA*dA_ii + uR_A*r_i + uR_dA*rd_i + uC_A*c_i + uC_dA*cd_i + uS_A*s + uS_dA*sd
+ *   w_i = wR_A*r_i + wR_dA*rd_i + wC_A*c_i + wC_dA*cd_i + wS_A*s + wS_dA*sd
+ *   v_k = vR_A*r_k + vR_dA*rd_k + vC_A*c_k + vC_dA*cd_k
+ * r/c = row/column sums, s = total sum (of A; "d" = of dA).  Mapping from the reference's
+ * param1..param8 (+ *_prime) is documented in DESIGN.md §3 and layers.py:102-160 / :256-337.
+ */
+enum {
+  GNCDE_FC_E_A = 0, GNCDE_FC_E_DA = 1, GNCDE_FC_ET_A = 2, GNCDE_FC_ET_DA = 3,
+  GNCDE_FC_UD_A = 4, GNCDE_FC_UD_DA = 5, GNCDE_FC_UR_A = 6, GNCDE_FC_UR_DA = 7,
+  GNCDE_FC_UC_A = 8, GNCDE_FC_UC_DA = 9, GNCDE_FC_US_A = 10, GNCDE_FC_US_DA = 11,
+  GNCDE_FC_WR_A = 12, GNCDE_FC_WR_DA = 13, GNCDE_FC_WC_A = 14, GNCDE_FC_WC_DA = 15,
+  GNCDE_FC_WS_A = 16, GNCDE_FC_WS_DA = 17,
+  GNCDE_FC_VR_A = 18, GNCDE_FC_VR_DA = 19, GNCDE_FC_VC_A = 20, GNCDE_FC_VC_DA = 21,
+  GNCDE_FC_IDC = 22
+};
+
+enum {
+  GNCDE_OK = 0,
+  GNCDE_ERR_ARG = 1,          /* NULL pointer / negative size */
+  GNCDE_ERR_SHAPE = 2,        /* inconsistent dims (e.g. CDE width != h*de*2) */
+  GNCDE_ERR_UNSUPPORTED = 3,  /* configuration outside what any kernel implements */
+  GNCDE_ERR_WORKSPACE = 4,    /* workspace smaller than gncde_workspace_bytes() */
+  GNCDE_ERR_HIP = 5           /* a HIP runtime call failed (launch error) */
+};
+
+enum { GNCDE_RK4 = 0, GNCDE_TSIT5 = 1 };
+enum { GNCDE_CTRL_GRID = 0, GNCDE_CTRL_PID = 1 };
+enum { GNCDE_SAVE_T1 = 0, GNCDE_SAVE_STEPS = 1, GNCDE_SAVE_TS = 2 };
+/* stats[b*4 + k]: k=0 accepted steps, 1 rejected steps, 2 vector-field evaluations, 3 status
+ * (0 ok, 1 max_steps exceeded, 2 non-finite error estimate) */
+enum { GNCDE_STAT_STEPS = 0, GNCDE_STAT_REJECTS = 1, GNCDE_STAT_EVALS = 2, GNCDE_STAT_STATUS = 3 };
+
+typedef struct GncdeProblem {
+  int32_t B;                         /* samples in this call (this rank's shard) */
+  int32_t n;                         /* nodes */
+  int32_t T;                         /* knots per sample (>= 2) */
+  int32_t L;                         /* layers (1..GNCDE_MAX_LAYERS) */
+  int32_t dims[GNCDE_MAX_LAYERS + 1];/* d_0 .. d_L */
+  int32_t cde_hidden;                /* 0: ODE vector field (output [n, d_L]); >0: CDE wrapper h */
+  int32_t cde_embed;                 /* CDE wrapper data_embed_dim de (d_L must equal h*de*2) */
+  const float* ts;
+  const float* coef;
+  const float* tcoef;
+  const float* data_coef;
+  const float* fusion;
+  const float* params;
+} GncdeProblem;
+
+typedef struct GncdeSolver {
+  int32_t method;                    /* GNCDE_RK4 | GNCDE_TSIT5 */
+  int32_t controller;                /* GNCDE_CTRL_GRID (host-planned grid) | GNCDE_CTRL_PID */
+  int32_t save_mode;                 /* GNCDE_SAVE_T1 | GNCDE_SAVE_STEPS | GNCDE_SAVE_TS */
+  int32_t max_steps;                 /* PID: accepted+rejected step cap (diffrax default 4096) */
+  int32_t grid_len;                  /* G: columns of grid (GRID controller; max steps + 1) */
+  int32_t n_save;                    /* S: columns of save_ts (SAVE_TS) */
+  float rtol, atol;                  /* PID tolerances */
+  const float* grid;                 /* [B, G] step grid (GRID controller) */
+  const int32_t* nsteps;             /* [B] steps per sample (GRID controller) */
+  const float* t0;                   /* [B] (PID) */
+  const float* t1;                   /* [B] (PID) */
+  const float* dt0;                  /* [B] (PID) initial step, or NULL for the Hairer heuristic */
+  const float* save_ts;              /* [B, S] (SAVE_TS), increasing, within [t0, t1] */
+} GncdeSolver;
+
+/* Library / error helpers */
+int gncde_abi_version(void);
+const char* gncde_strerror(int code);
+/* Name of the kernel path gncde_integrate would take for this problem ("fused<64,16,3,rk4>" or
+ * "generic"), written into buf (NUL-terminated).  Returns GNCDE_OK or an error code. */
+int gncde_integrate_path(const GncdeProblem* prob, const GncdeSolver* solver, char* buf, size_t buf_len);
+
+/* Workspace bytes needed by gncde_vf_eval (solver == NULL) or gncde_integrate. */
+size_t gncde_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* solver);
+
+/* dy[b] = VF(t[b], y[b]) for every sample.  t: [B], y: [B, n, d_0], dy: [B, n, d_out] with
+ * d_out = d_L (ODE) or cde_hidden (CDE wrapper). */
+int gncde_vf_eval(const GncdeProblem* prob, const float* t, const float* y, float* dy,
+                  void* workspace, size_t workspace_bytes, void* stream);
+
+/* Solve dy/dt = VF(t, y) per sample.  y0: [B, n, d_s] (d_s = d_0).  ys:
+ *   SAVE_T1: [B, n, d_s]; SAVE_STEPS: [B, G, n, d_s] (GRID controller); SAVE_TS: [B, S, n, d_s].
+ * stats: [B, 4] int32 (may be NULL). */
+int gncde_integrate(const GncdeProblem* prob, const GncdeSolver* solver, const float* y0, float* ys,
+                    int32_t* stats, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Per-node affine map out[r, :] = W @ x[r, :] + b for `rows` rows.  x: [rows, din], W: [dout, din],
+ * b: [dout] (may be NULL), out: [rows, dout]. */
+int gncde_node_affine(int32_t rows, int32_t din, int32_t dout, const float* x, const float* W,
+                      const float* b, float* out, void* stream);
+
+/* idx[k] = clip(searchsorted(ts[b], t[k], 'left') - 1, 0, T-2) with b = sample[k].
+ * ts: [B, T], t: [count], sample: [count] int32, idx: [count] int32. */
+int gncde_interval_index(const float* ts, int32_t B, int32_t T, const float* t, const int32_t* sample,
+                         int32_t* idx, int32_t count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GNCDE_H */

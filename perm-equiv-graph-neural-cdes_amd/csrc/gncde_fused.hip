@@ -1,0 +1,527 @@
+// Fused persistent integrate kernel for the dyn family (GraphNeuralCDE: use_control=False, all layer
+// widths equal H) — the BASELINE hot path (configs 1, 2, 4).
+//
+// One workgroup integrates one sample over its whole step grid.  NP/16 waves; wave w owns the node
+// block [16w, 16w+16).  Everything between the HBM coefficient reads and the final state stays on
+// chip:
+//
+//   per distinct stage time t (RK4: 2 per step, since k2/k3 share t+h/2 and k4/k1' share t+h):
+//     interval index (wave ballot over ts in LDS) -> Horner of the interval's (d,c,b,a) [4,n,n]
+//     (coalesced float4 HBM/L2 reads) -> A(t), dA(t) in LDS (XOR-swizzled, conflict-free row AND
+//     column access) -> row/col sums, diagonals, totals -> each lane builds its slice of
+//     (I + Abar_l) for every layer l IN REGISTERS (the MFMA B-operand layout), fusing the
+//     15-term equivariant basis (layers.py:102-160) into the operand construction.
+//   per vector-field evaluation (perm_equiv_graph_vector_field.py:122-128, layers.py:36-48):
+//     RMSNorm (in-register + 2 cross-lane shuffles) -> Linear on MFMA 16x16x4 f32 with the state
+//     tile as B operand (no LDS) -> m^T tile to LDS -> barrier -> (I+Abar) m on MFMA 16x16x4 f32,
+//     A operand = m^T from LDS (ds_read_b128), B operand = Abar registers -> ReLU -> next layer.
+//   RK stage combinations in registers; only y0 in and the saved states out touch HBM.
+//
+// State layout per wave ("T-layout", the MFMA 16x16 C/D map): lane l holds Y[f][i] for node
+// i = 16w + (l&15) and features f = 16*fb + 4*(l>>4) + r, r = 0..3, fb = 0..H/16-1.
+#include "gncde_internal.h"
+
+#include <cstdio>
+#include <cstring>
+
+namespace gncde {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTMax = 256;  // knots per sample held in LDS
+
+// Tsit5 rows a[s][0..5] for stages s = 1..6 (row 6 = b_sol), zero-padded; c[s] for s = 1..4.
+__constant__ float kTsit5A[7][6] = {
+    {0.f, 0.f, 0.f, 0.f, 0.f, 0.f},
+    {TSIT5_A21, 0.f, 0.f, 0.f, 0.f, 0.f},
+    {TSIT5_A31, TSIT5_A32, 0.f, 0.f, 0.f, 0.f},
+    {TSIT5_A41, TSIT5_A42, TSIT5_A43, 0.f, 0.f, 0.f},
+    {TSIT5_A51, TSIT5_A52, TSIT5_A53, TSIT5_A54, 0.f, 0.f},
+    {TSIT5_A61, TSIT5_A62, TSIT5_A63, TSIT5_A64, TSIT5_A65, 0.f},
+    {TSIT5_B1, TSIT5_B2, TSIT5_B3, TSIT5_B4, TSIT5_B5, TSIT5_B6},
+};
+__constant__ float kTsit5C[5] = {0.f, TSIT5_C2, TSIT5_C3, TSIT5_C4, TSIT5_C5};
+
+struct FusedArgs {
+  int B, n, T, G, save_mode;
+  const float* ts;
+  const float* coef;
+  const float* tcoef;
+  const float* fusion;
+  const float* params;
+  const float* grid;
+  const int32_t* nsteps;
+  const float* y0;
+  float* ys;
+  int32_t* stats;
+};
+
+// A(t)/dA(t) LDS images use a padded row stride NP+1: row AND column walks are bank-conflict free
+// and every address is lane base + compile-time offset (no per-element address registers).
+template <int NP>
+__device__ __forceinline__ int swz(int i, int k) {
+  return i * (NP + 1) + k;
+}
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int NP, int H, int L, int METHOD>
+constexpr int min_waves_per_eu() {
+  constexpr int regs = L * (NP / 4) + (METHOD == GNCDE_TSIT5 ? 9 : 4) * (H / 4) + 4 * (H / 4) + 40;
+  return NP >= 128 ? 2 : (regs > 120 ? 2 : 4);
+}
+
+template <int NP, int H, int L, int METHOD>
+__global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())) k_fused(FusedArgs a) {
+  constexpr int NT = NP * 4;
+  constexpr int FB = H / 16;
+  constexpr int KS = NP / 4;
+  constexpr int MS = NP + 4;
+  constexpr int AS = NP * (NP + 1);  // one padded A image
+  constexpr int R0 = (2 * AS > 2 * H * MS) ? 2 * AS : 2 * H * MS;
+  constexpr int PL = 3 * H + FB * FB * 4 * 64;  // rms_w, rms_b, bias, W operands
+
+  __shared__ __attribute__((aligned(16))) float sR0[R0];
+  __shared__ float sVec[6 * NP];
+  __shared__ float sTs[kTMax];
+  __shared__ __attribute__((aligned(16))) float sPar[L * PL];
+
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int w = tid >> 6;
+  const int lane = tid & 63;
+  const int lo = lane & 15, hi = lane >> 4;
+  const int n = a.n, T = a.T;
+  const size_t nn = (size_t)n * n;
+  const int node = 16 * w + lo;
+  const bool node_ok = node < n;
+
+  // ---- stage per-sample knots and the layer parameters in LDS --------------------------------------
+  for (int j = tid; j < T; j += NT) sTs[j] = a.ts[(size_t)b * T + j];
+  {
+    size_t off = 0;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      float* P = sPar + l * PL;
+      const float* g = a.params + off;
+      for (int j = tid; j < H; j += NT) {
+        P[j] = g[j];                       // rms_w
+        P[H + j] = g[H + j];               // rms_b
+        P[2 * H + j] = g[2 * H + H * H + j];  // bias
+      }
+      // W operand for (ob, fb, r) at lane: W[16ob + lo'][16fb + 4hi' + r]
+      for (int j = tid; j < FB * FB * 4 * 64; j += NT) {
+        const int ln = j & 63, r = (j >> 6) & 3, fb = (j >> 8) % FB, ob = (j >> 8) / FB;
+        const int row = 16 * ob + (ln & 15), col = 16 * fb + 4 * (ln >> 4) + r;
+        P[3 * H + j] = g[2 * H + row * H + col];
+      }
+      off += 2 * H + H * H + H;
+    }
+  }
+  __syncthreads();
+
+  float* sA = sR0;
+  float* sdA = sR0 + AS;
+  float Ab[L][KS];
+  float tg = 0.f;
+  int msel = 0;
+
+  // ---- (I + Abar_l) operands for stage time t --------------------------------------------------------
+  auto form = [&](float t) __attribute__((always_inline)) {
+    __syncthreads();  // readers of the aliased M buffers are done
+    // Opaque per-call copy of the thread id: stops LICM from hoisting every per-lane LDS/global
+    // address of this (large, fully unrolled) phase out of the time loop into live registers.
+    int ftid = tid;
+    asm volatile("" : "+v"(ftid));
+    const int lane = ftid & 63, lo = lane & 15, hi = lane >> 4;
+    const int node = 16 * (ftid >> 6) + lo;
+    const int tid = ftid;
+    const float* fus = a.fusion;
+    asm volatile("" : "+s"(fus));
+    int cnt = 0;
+    for (int j0 = 0; j0 < T; j0 += 64) {
+      const int j = j0 + lane;
+      const bool p = (j < T) && (sTs[j < T ? j : 0] < t);
+      cnt += __popcll(__ballot(p));
+    }
+    int idx = cnt - 1;
+    idx = idx < 0 ? 0 : (idx > T - 2 ? T - 2 : idx);
+    const float f = t - sTs[idx];
+    const float f3 = 3.0f * f;
+    const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
+    if (n == NP) {
+      const float4* c4 = reinterpret_cast<const float4*>(cb);
+      constexpr int NQ = NP * NP / 4;
+      for (int e4 = tid; e4 < NQ; e4 += NT) {
+        const float4 d = c4[e4], c = c4[NQ + e4], bb = c4[2 * NQ + e4], aa = c4[3 * NQ + e4];
+        const int i = (e4 * 4) / NP, k = (e4 * 4) % NP;
+        sA[swz<NP>(i, k + 0)] = fmaf(f, fmaf(f, fmaf(f, d.x, c.x), bb.x), aa.x);
+        sA[swz<NP>(i, k + 1)] = fmaf(f, fmaf(f, fmaf(f, d.y, c.y), bb.y), aa.y);
+        sA[swz<NP>(i, k + 2)] = fmaf(f, fmaf(f, fmaf(f, d.z, c.z), bb.z), aa.z);
+        sA[swz<NP>(i, k + 3)] = fmaf(f, fmaf(f, fmaf(f, d.w, c.w), bb.w), aa.w);
+        sdA[swz<NP>(i, k + 0)] = fmaf(f, fmaf(f3, d.x, 2.0f * c.x), bb.x);
+        sdA[swz<NP>(i, k + 1)] = fmaf(f, fmaf(f3, d.y, 2.0f * c.y), bb.y);
+        sdA[swz<NP>(i, k + 2)] = fmaf(f, fmaf(f3, d.z, 2.0f * c.z), bb.z);
+        sdA[swz<NP>(i, k + 3)] = fmaf(f, fmaf(f3, d.w, 2.0f * c.w), bb.w);
+      }
+    } else {
+      for (int e = tid; e < (int)nn; e += NT) {
+        const float d = cb[e], c = cb[nn + e], bb = cb[2 * nn + e], aa = cb[3 * nn + e];
+        const int i = e / n, k = e % n;
+        sA[swz<NP>(i, k)] = fmaf(f, fmaf(f, fmaf(f, d, c), bb), aa);
+        sdA[swz<NP>(i, k)] = fmaf(f, fmaf(f3, d, 2.0f * c), bb);
+      }
+    }
+    __syncthreads();
+    {  // r, rd (row sums), c, cd (column sums), diagonals
+      const int q = tid / NP, j = tid % NP;
+      const float* M = (q & 1) ? sdA : sA;
+      float acc = 0.f, dg = 0.f;
+      if (j < n) {
+        if (q < 2) {
+          for (int k = 0; k < n; ++k) acc += M[swz<NP>(j, k)];
+          dg = M[swz<NP>(j, j)];
+        } else {
+          for (int i = 0; i < n; ++i) acc += M[swz<NP>(i, j)];
+        }
+      }
+      sVec[q * NP + j] = acc;
+      if (q < 2) sVec[(4 + q) * NP + j] = dg;
+    }
+    __syncthreads();
+    float s = 0.f, sd = 0.f;
+    for (int j = lane; j < NP; j += 64) {
+      s += sVec[j];
+      sd += sVec[NP + j];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o);
+      sd += __shfl_xor(sd, o);
+    }
+    const int i = node;
+    const float ri = sVec[i], rdi = sVec[NP + i], ci = sVec[2 * NP + i], cdi = sVec[3 * NP + i];
+    const float dgi = sVec[4 * NP + i], dgdi = sVec[5 * NP + i];
+    float wl[L], ul[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      const float* fc = fus + l * GNCDE_FC;
+      wl[l] = fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci +
+              fc[GNCDE_FC_WC_DA] * cdi + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
+      ul[l] = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dgi + fc[GNCDE_FC_UD_DA] * dgdi +
+              fc[GNCDE_FC_UR_A] * ri + fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci +
+              fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      const float* fc = fus + l * GNCDE_FC;
+      const float e0 = fc[GNCDE_FC_E_A], e1 = fc[GNCDE_FC_E_DA], e2 = fc[GNCDE_FC_ET_A], e3 = fc[GNCDE_FC_ET_DA];
+      const float v0 = fc[GNCDE_FC_VR_A], v1 = fc[GNCDE_FC_VR_DA], v2 = fc[GNCDE_FC_VC_A], v3 = fc[GNCDE_FC_VC_DA];
+#pragma unroll
+      for (int sl = 0; sl < KS; ++sl) {
+        const int k = hi * KS + sl;
+        const float aik = sA[swz<NP>(i, k)], dik = sdA[swz<NP>(i, k)];
+        const float aki = sA[swz<NP>(k, i)], dki = sdA[swz<NP>(k, i)];
+        const float rk = sVec[k], rdk = sVec[NP + k], ck = sVec[2 * NP + k], cdk = sVec[3 * NP + k];
+        float v = fmaf(e0, aik, fmaf(e1, dik, fmaf(e2, aki, e3 * dki)));
+        v += wl[l] + fmaf(v0, rk, fmaf(v1, rdk, fmaf(v2, ck, v3 * cdk)));
+        if (i == k) v += ul[l];
+        Ab[l][sl] = (node_ok && k < n) ? v : 0.f;
+        if ((sl & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    {
+      const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
+      tg = node_ok ? fmaf(f, fmaf(f3, tc[i], 2.0f * tc[n + i]), tc[2 * n + i]) : 0.f;
+    }
+    __syncthreads();  // all A/dA reads done before the aliased M buffers are written
+  };
+
+  // ---- one vector-field evaluation: Kout = VF(Yin) at the formed time --------------------------------
+  auto eval = [&](const float (&Yin)[FB][4], float (&Kout)[FB][4]) __attribute__((always_inline)) {
+    float Z[FB][4];
+#pragma unroll
+    for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Z[fb][r] = Yin[fb][r];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      // Opaque base: keeps the (invariant) parameter reads inside the loop instead of hoisting
+      // L*(3H/4 + FB*FB*4) values into registers for the whole solve.
+      const float* P = sPar + l * PL;
+      asm volatile("" : "+v"(P));
+      float ss = 0.f;
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ss = fmaf(Z[fb][r], Z[fb][r], ss);
+      ss += __shfl_xor(ss, 16);
+      ss += __shfl_xor(ss, 32);
+      const float inv = 1.0f / sqrtf(ss / (float)H + 1e-5f);
+      float Zn[FB][4];
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 16 * fb + 4 * hi + r;
+          Zn[fb][r] = fmaf(Z[fb][r] * inv, P[f], P[H + f]);
+        }
+      float* Mb = sR0 + msel * (H * MS);
+      msel ^= 1;
+#pragma unroll
+      for (int ob = 0; ob < FB; ++ob) {
+        floatx4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = P[2 * H + 16 * ob + 4 * hi + r];
+#pragma unroll
+        for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            acc = mfma4(P[3 * H + ((ob * FB + fb) * 4 + r) * 64 + lane], Zn[fb][r], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Mb[(16 * ob + 4 * hi + r) * MS + node] = acc[r];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ob = 0; ob < FB; ++ob) {
+        floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+        const float* mrow = Mb + (16 * ob + lo) * MS + hi * KS;
+#pragma unroll
+        for (int q = 0; q < KS / 4; ++q) {
+          const float4 mv = *reinterpret_cast<const float4*>(mrow + 4 * q);
+          c0 = mfma4(mv.x, Ab[l][4 * q + 0], c0);
+          c1 = mfma4(mv.y, Ab[l][4 * q + 1], c1);
+          c0 = mfma4(mv.z, Ab[l][4 * q + 2], c0);
+          c1 = mfma4(mv.w, Ab[l][4 * q + 3], c1);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float z = c0[r] + c1[r];
+          Z[ob][r] = (l < L - 1) ? fmaxf(z, 0.f) : z;
+        }
+      }
+    }
+#pragma unroll
+    for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Kout[fb][r] = tg * Z[fb][r];
+  };
+
+  bool have = false;
+  float tcache = 0.f;
+  auto vf = [&](float t, const float (&Yin)[FB][4], float (&Kout)[FB][4]) __attribute__((always_inline)) {
+    if (!have || t != tcache) {
+      form(t);
+      tcache = t;
+      have = true;
+    }
+    eval(Yin, Kout);
+  };
+
+  // ---- state I/O (reference layout [n, H]) -------------------------------------------------------------
+  float y[FB][4];
+  const float* y0b = a.y0 + (size_t)b * n * H;
+#pragma unroll
+  for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[fb][r] = node_ok ? y0b[(size_t)node * H + 16 * fb + 4 * hi + r] : 0.f;
+
+  auto store = [&](float* dst) __attribute__((always_inline)) {
+    if (!node_ok) return;
+#pragma unroll
+    for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[(size_t)node * H + 16 * fb + 4 * hi + r] = y[fb][r];
+  };
+
+  const int G = a.G;
+  const float* g = a.grid + (size_t)b * G;
+  int ns = a.nsteps[b];
+  ns = ns < 0 ? 0 : (ns > G - 1 ? G - 1 : ns);  // never index past the grid row
+  const size_t E = (size_t)n * H;
+  if (a.save_mode == GNCDE_SAVE_STEPS) store(a.ys + ((size_t)b * G) * E);
+
+  // Single vf() call site per method (one inlined copy of form/eval keeps the register budget).
+  if constexpr (METHOD == GNCDE_RK4) {
+    float K[FB][4], acc[FB][4], yt[FB][4];
+    for (int k = 0; k < ns; ++k) {
+      const float t = g[k];
+      const float h = g[k + 1] - t;
+      const float hh = 0.5f * h;
+      const float tm = stage_time(t, 0.5f, h);
+      const float te = __fadd_rn(t, h);
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) yt[fb][r] = y[fb][r];
+#pragma unroll 1
+      for (int st = 0; st < 4; ++st) {
+        const float tst = st == 0 ? t : (st == 3 ? te : tm);
+        vf(tst, yt, K);
+        const float wk = (st == 0 || st == 3) ? 1.0f : 2.0f;  // k1 + 2k2 + 2k3 + k4
+        const float hn = st < 2 ? hh : h;                      // next stage input y + hn*K
+#pragma unroll
+        for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            acc[fb][r] = st == 0 ? K[fb][r] : fmaf(wk, K[fb][r], acc[fb][r]);
+            yt[fb][r] = fmaf(hn, K[fb][r], y[fb][r]);
+          }
+      }
+      const float h6 = h / 6.0f;
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[fb][r] = fmaf(h6, acc[fb][r], y[fb][r]);
+      if (a.save_mode == GNCDE_SAVE_STEPS) store(a.ys + ((size_t)b * G + k + 1) * E);
+    }
+  } else {
+    // Tsit5 on the grid (ConstantStepSize), FSAL: stage s (1..6) input y + h*sum_j a[s][j] k_j,
+    // stage 7 input == y1 (a[7][:] = b) and its evaluation is the next step's k_1.
+    float kk[7][FB][4], yt[FB][4], K[FB][4];
+    const float t0 = g[0];
+#pragma unroll
+    for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) yt[fb][r] = y[fb][r];
+    float tst = t0;
+    int st = 0;   // 0 = initial k1 evaluation; then stages 1..6 of every step
+    int k = 0;
+    float t = t0, h = 0.f;
+    while (true) {
+      vf(tst, yt, K);
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+        if (j == st)
+#pragma unroll
+          for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) kk[j][fb][r] = K[fb][r];
+      if (st == 6) {  // y1 accepted; stage-7 value is the next k1
+#pragma unroll
+        for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            y[fb][r] = yt[fb][r];
+            kk[0][fb][r] = K[fb][r];
+          }
+        if (a.save_mode == GNCDE_SAVE_STEPS) store(a.ys + ((size_t)b * G + k + 1) * E);
+        ++k;
+        st = 0;
+      }
+      if (k >= ns) break;
+      if (st == 0) {
+        t = g[k];
+        h = g[k + 1] - t;
+      }
+      // next stage st+1 (1..6): coefficients a[st+1][0..st]
+      const int ns1 = st + 1;
+      const float* arow = kTsit5A[ns1];
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float sacc = 0.f;
+#pragma unroll
+          for (int j = 0; j < 6; ++j) sacc = fmaf(arow[j], kk[j][fb][r], sacc);
+          yt[fb][r] = fmaf(h, sacc, y[fb][r]);
+        }
+      tst = ns1 >= 5 ? __fadd_rn(t, h) : stage_time(t, kTsit5C[ns1], h);
+      st = ns1;
+    }
+  }
+
+  if (a.save_mode == GNCDE_SAVE_STEPS) {
+    for (int k = ns + 1; k < G; ++k) store(a.ys + ((size_t)b * G + k) * E);
+  } else {
+    store(a.ys + (size_t)b * E);
+  }
+  if (a.stats && tid == 0) {
+    a.stats[b * 4 + GNCDE_STAT_STEPS] = ns;
+    a.stats[b * 4 + GNCDE_STAT_REJECTS] = 0;
+    a.stats[b * 4 + GNCDE_STAT_EVALS] = METHOD == GNCDE_RK4 ? 4 * ns : 1 + 6 * ns;
+    a.stats[b * 4 + GNCDE_STAT_STATUS] = 0;
+  }
+}
+
+using FusedFn = void (*)(FusedArgs);
+
+struct FusedEntry {
+  int np, h, l, method;
+  FusedFn fn;
+};
+
+#define GNCDE_FUSED(NP, H, L)                                        \
+  {NP, H, L, GNCDE_RK4, k_fused<NP, H, L, GNCDE_RK4>},             \
+  {NP, H, L, GNCDE_TSIT5, k_fused<NP, H, L, GNCDE_TSIT5>}
+
+const FusedEntry kFused[] = {
+    GNCDE_FUSED(16, 16, 1),  GNCDE_FUSED(16, 16, 2),  GNCDE_FUSED(16, 16, 3),  GNCDE_FUSED(16, 16, 4),
+    GNCDE_FUSED(32, 16, 1),  GNCDE_FUSED(32, 16, 2),  GNCDE_FUSED(32, 16, 3),  GNCDE_FUSED(32, 16, 4),
+    GNCDE_FUSED(64, 16, 1),  GNCDE_FUSED(64, 16, 2),  GNCDE_FUSED(64, 16, 3),  GNCDE_FUSED(64, 16, 4),
+    GNCDE_FUSED(128, 16, 1), GNCDE_FUSED(128, 16, 2), GNCDE_FUSED(128, 16, 3),
+    GNCDE_FUSED(16, 32, 1),  GNCDE_FUSED(16, 32, 2),  GNCDE_FUSED(16, 32, 3),  GNCDE_FUSED(16, 32, 4),
+    GNCDE_FUSED(32, 32, 1),  GNCDE_FUSED(32, 32, 2),  GNCDE_FUSED(32, 32, 3),  GNCDE_FUSED(32, 32, 4),
+    GNCDE_FUSED(64, 32, 1),  GNCDE_FUSED(64, 32, 2),  GNCDE_FUSED(64, 32, 3),  GNCDE_FUSED(64, 32, 4),
+    GNCDE_FUSED(128, 32, 1), GNCDE_FUSED(128, 32, 2),
+};
+
+const FusedEntry* find_fused(const GncdeProblem& p, const GncdeSolver& s) {
+  if (p.cde_hidden != 0) return nullptr;
+  if (s.controller != GNCDE_CTRL_GRID) return nullptr;
+  if (s.save_mode != GNCDE_SAVE_T1 && s.save_mode != GNCDE_SAVE_STEPS) return nullptr;
+  if (p.T > kTMax) return nullptr;
+  const int H = p.dims[0];
+  for (int l = 1; l <= p.L; ++l)
+    if (p.dims[l] != H) return nullptr;
+  int np = 0;
+  for (int c : {16, 32, 64, 128})
+    if (p.n <= c) {
+      np = c;
+      break;
+    }
+  if (np == 0) return nullptr;
+  for (const FusedEntry& e : kFused)
+    if (e.np == np && e.h == H && e.l == p.L && e.method == s.method) return &e;
+  return nullptr;
+}
+
+}  // namespace
+
+bool fused_supported(const GncdeProblem& p, const GncdeSolver& s, char* name, size_t name_len) {
+  const FusedEntry* e = find_fused(p, s);
+  if (!e) return false;
+  if (name && name_len)
+    snprintf(name, name_len, "fused<%d,%d,%d,%s>", e->np, e->h, e->l,
+             e->method == GNCDE_RK4 ? "rk4" : "tsit5");
+  return true;
+}
+
+int fused_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
+                    int32_t* stats, hipStream_t st) {
+  const FusedEntry* e = find_fused(p, s);
+  if (!e) return GNCDE_ERR_UNSUPPORTED;
+  FusedArgs a;
+  a.B = p.B;
+  a.n = p.n;
+  a.T = p.T;
+  a.G = s.grid_len;
+  a.save_mode = s.save_mode;
+  a.ts = p.ts;
+  a.coef = p.coef;
+  a.tcoef = p.tcoef;
+  a.fusion = p.fusion;
+  a.params = p.params;
+  a.grid = s.grid;
+  a.nsteps = s.nsteps;
+  a.y0 = y0;
+  a.ys = ys;
+  a.stats = stats;
+  hipLaunchKernelGGL(e->fn, dim3(p.B), dim3(e->np * 4), 0, st, a);
+  return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+}
+
+}  // namespace gncde

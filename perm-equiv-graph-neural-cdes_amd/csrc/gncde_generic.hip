@@ -1,0 +1,419 @@
+// Generic (any n, any layer widths, CDE wrapper, all fusion kinds) multi-kernel path.
+//
+// One launch per phase of a vector-field evaluation; used for shapes the fused persistent kernel
+// (gncde_fused.hip) does not cover and as the second HIP implementation the parity tests compare
+// against.  Every kernel is batched over samples on grid.y/grid.z.
+//
+// Reference semantics: spline (perm_equiv_graph_vector_field.py:98-102), fusion (layers.py:102-160,
+// :256-337 via the factored table of gncde.h), ConvLayer (layers.py:36-48), VF epilogue
+// (perm_equiv_graph_vector_field.py:122-128), CDE wrapper (cde_wrapper_vector_field.py:19-26).
+#include "gncde_internal.h"
+
+namespace gncde {
+namespace {
+
+constexpr int kRedStride = 8;  // red[b][q][n]: r, rd, c, cd, diagA, diagdA, {s}, {sd}
+
+// ---- spline: A(t), dA(t), tg(t) -------------------------------------------------------------------
+__global__ void k_spline(int n, int T, const float* __restrict__ ts, const float* __restrict__ coef,
+                         const float* __restrict__ tcoef, const float* __restrict__ t,
+                         float* __restrict__ A, float* __restrict__ dA, float* __restrict__ tg) {
+  const int b = blockIdx.y;
+  const size_t nn = (size_t)n * n;
+  const float tb = t[b];
+  const float* tsb = ts + (size_t)b * T;
+  const int idx = interval_index(tsb, T, tb);
+  const float f = tb - tsb[idx];
+  const float* cb = coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < nn) {
+    const float d = cb[e], c = cb[nn + e], bb = cb[2 * nn + e], a = cb[3 * nn + e];
+    A[(size_t)b * nn + e] = fmaf(f, fmaf(f, fmaf(f, d, c), bb), a);
+    dA[(size_t)b * nn + e] = fmaf(f, fmaf(3.0f * f, d, 2.0f * c), bb);
+  }
+  if (e < (size_t)n) {
+    const float* tc = tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
+    tg[(size_t)b * n + e] = fmaf(f, fmaf(3.0f * f, tc[e], 2.0f * tc[n + e]), tc[2 * n + e]);
+  }
+}
+
+// ---- row/col sums, diagonals, totals --------------------------------------------------------------
+__global__ void k_reduce(int n, const float* __restrict__ A, const float* __restrict__ dA,
+                         float* __restrict__ red) {
+  const int b = blockIdx.x;
+  const size_t nn = (size_t)n * n;
+  const float* Ab = A + b * nn;
+  const float* dAb = dA + b * nn;
+  float* rb = red + (size_t)b * kRedStride * n;
+  __shared__ float part[2][256];
+  float ps = 0.f, psd = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    float r = 0.f, rd = 0.f, c = 0.f, cd = 0.f;
+    for (int k = 0; k < n; ++k) {
+      r += Ab[(size_t)i * n + k];
+      rd += dAb[(size_t)i * n + k];
+      c += Ab[(size_t)k * n + i];
+      cd += dAb[(size_t)k * n + i];
+    }
+    rb[0 * n + i] = r;
+    rb[1 * n + i] = rd;
+    rb[2 * n + i] = c;
+    rb[3 * n + i] = cd;
+    rb[4 * n + i] = Ab[(size_t)i * n + i];
+    rb[5 * n + i] = dAb[(size_t)i * n + i];
+    ps += r;
+    psd += rd;
+  }
+  part[0][threadIdx.x] = ps;
+  part[1][threadIdx.x] = psd;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      part[0][threadIdx.x] += part[0][threadIdx.x + s];
+      part[1][threadIdx.x] += part[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    rb[6 * n] = part[0][0];
+    rb[7 * n] = part[1][0];
+  }
+}
+
+// ---- RMSNorm + Linear: m[b,i,o] = sum_k (rmsnorm(Z[b,i,:])[k]) W[o,k] + bias[o] -------------------
+__global__ void k_rms_linear(int n, int din, int dout, const float* __restrict__ Z,
+                             const float* __restrict__ rw, const float* __restrict__ rbias,
+                             const float* __restrict__ W, const float* __restrict__ bias,
+                             float* __restrict__ m) {
+  const int b = blockIdx.y;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (size_t)n * dout) return;
+  const int i = (int)(e / dout), o = (int)(e % dout);
+  const float* z = Z + ((size_t)b * n + i) * din;
+  float ss = 0.f;
+  for (int k = 0; k < din; ++k) ss = fmaf(z[k], z[k], ss);
+  const float inv = 1.0f / sqrtf(ss / (float)din + 1e-5f);
+  float acc = bias[o];
+  const float* w = W + (size_t)o * din;
+  for (int k = 0; k < din; ++k) acc = fmaf(fmaf(z[k] * inv, rw[k], rbias[k]), w[k], acc);
+  m[((size_t)b * n + i) * dout + o] = acc;
+}
+
+// ---- factored (I + Abar)[i,k] on the fly ----------------------------------------------------------
+__device__ __forceinline__ float abar_elem(const float* __restrict__ fc, const float* __restrict__ A,
+                                           const float* __restrict__ dA, const float* __restrict__ rb,
+                                           int n, int i, int k) {
+  const float aik = A[(size_t)i * n + k], aki = A[(size_t)k * n + i];
+  const float dik = dA[(size_t)i * n + k], dki = dA[(size_t)k * n + i];
+  const float s = rb[6 * n], sd = rb[7 * n];
+  float v = fc[GNCDE_FC_E_A] * aik + fc[GNCDE_FC_E_DA] * dik + fc[GNCDE_FC_ET_A] * aki +
+            fc[GNCDE_FC_ET_DA] * dki;
+  const float wi = fc[GNCDE_FC_WR_A] * rb[i] + fc[GNCDE_FC_WR_DA] * rb[n + i] +
+                   fc[GNCDE_FC_WC_A] * rb[2 * n + i] + fc[GNCDE_FC_WC_DA] * rb[3 * n + i] +
+                   fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
+  const float vk = fc[GNCDE_FC_VR_A] * rb[k] + fc[GNCDE_FC_VR_DA] * rb[n + k] +
+                   fc[GNCDE_FC_VC_A] * rb[2 * n + k] + fc[GNCDE_FC_VC_DA] * rb[3 * n + k];
+  v += wi + vk;
+  if (i == k) {
+    v += fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * rb[4 * n + i] + fc[GNCDE_FC_UD_DA] * rb[5 * n + i] +
+         fc[GNCDE_FC_UR_A] * rb[i] + fc[GNCDE_FC_UR_DA] * rb[n + i] + fc[GNCDE_FC_UC_A] * rb[2 * n + i] +
+         fc[GNCDE_FC_UC_DA] * rb[3 * n + i] + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
+  }
+  return v;
+}
+
+// ---- Zout[b,i,o] = sum_k (I+Abar)[i,k] m[b,k,o], ReLU optional; 16x16 LDS tiles ------------------
+__global__ void __launch_bounds__(256) k_prop(int n, int d, const float* __restrict__ fc,
+                                              const float* __restrict__ A, const float* __restrict__ dA,
+                                              const float* __restrict__ red, const float* __restrict__ m,
+                                              float* __restrict__ Zout, int relu) {
+  const int b = blockIdx.z;
+  const int o0 = blockIdx.x * 16, i0 = blockIdx.y * 16;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const size_t nn = (size_t)n * n;
+  const float* Ab = A + b * nn;
+  const float* dAb = dA + b * nn;
+  const float* rb = red + (size_t)b * kRedStride * n;
+  const float* mb = m + (size_t)b * n * d;
+  __shared__ float sA[16][17];
+  __shared__ float sM[16][17];
+  float acc = 0.f;
+  for (int k0 = 0; k0 < n; k0 += 16) {
+    {
+      const int i = i0 + ty, k = k0 + tx;
+      sA[ty][tx] = (i < n && k < n) ? abar_elem(fc, Ab, dAb, rb, n, i, k) : 0.f;
+      const int kk = k0 + ty, o = o0 + tx;
+      sM[ty][tx] = (kk < n && o < d) ? mb[(size_t)kk * d + o] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc = fmaf(sA[ty][q], sM[q][tx], acc);
+    __syncthreads();
+  }
+  const int i = i0 + ty, o = o0 + tx;
+  if (i < n && o < d) {
+    if (relu) acc = fmaxf(acc, 0.f);
+    Zout[((size_t)b * n + i) * d + o] = acc;
+  }
+}
+
+// ---- epilogue: ODE dy = tg * Z; CDE dy[i,m] = tg[i] * sum_{l,k} Z[i,(m*de+l)*2+k] dX[i,l,k] --------
+__global__ void k_finalize(int n, int dL, int h, int de, int T, const float* __restrict__ ts,
+                           const float* __restrict__ data_coef, const float* __restrict__ t,
+                           const float* __restrict__ tg, const float* __restrict__ Z,
+                           float* __restrict__ dy) {
+  const int b = blockIdx.y;
+  const int dout = h > 0 ? h : dL;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (size_t)n * dout) return;
+  const int i = (int)(e / dout), o = (int)(e % dout);
+  const float g = tg[(size_t)b * n + i];
+  const float* z = Z + ((size_t)b * n + i) * dL;
+  if (h == 0) {
+    dy[((size_t)b * n + i) * dout + o] = g * z[o];
+    return;
+  }
+  const float tb = t[b];
+  const float* tsb = ts + (size_t)b * T;
+  const int idx = interval_index(tsb, T, tb);
+  const float f = tb - tsb[idx];
+  const size_t blk = (size_t)n * de * 2;
+  const float* cb = data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)i * de * 2;
+  float acc = 0.f;
+  for (int l = 0; l < de; ++l) {
+    for (int k = 0; k < 2; ++k) {
+      const int q = l * 2 + k;
+      const float dX = fmaf(f, fmaf(3.0f * f, cb[q], 2.0f * cb[blk + q]), cb[2 * blk + q]);
+      acc = fmaf(g * z[(o * de + l) * 2 + k], dX, acc);
+    }
+  }
+  dy[((size_t)b * n + i) * dout + o] = acc;
+}
+
+// ---- solver helpers ---------------------------------------------------------------------------------
+// Per-sample step geometry for step k of the host-planned grid.
+__global__ void k_grid_step(int B, int G, int k, const float* __restrict__ grid,
+                            const int32_t* __restrict__ nsteps, float* __restrict__ tcur,
+                            float* __restrict__ hcur) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* g = grid + (size_t)b * G;
+  int ns = nsteps[b];
+  ns = ns < 0 ? 0 : (ns > G - 1 ? G - 1 : ns);
+  if (k < ns) {
+    tcur[b] = g[k];
+    hcur[b] = g[k + 1] - g[k];
+  } else {
+    tcur[b] = g[ns];
+    hcur[b] = 0.f;
+  }
+}
+
+__global__ void k_stage_time(int B, float c, const float* __restrict__ tcur,
+                             const float* __restrict__ hcur, float* __restrict__ tst) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  tst[b] = stage_time(tcur[b], c, hcur[b]);
+}
+
+// out = y + h_b * sum_j a_j K_j   (up to 7 terms; K_j == nullptr terms skipped)
+struct Combo {
+  const float* K[7];
+  float a[7];
+  int nk;
+};
+__global__ void k_combo(int B, size_t E, const float* __restrict__ y, Combo cb,
+                        const float* __restrict__ hcur, float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const size_t o = (size_t)b * E + e;
+  float s = 0.f;
+  for (int j = 0; j < cb.nk; ++j) s = fmaf(cb.a[j], cb.K[j][o], s);
+  out[o] = fmaf(hcur[b], s, y[o]);
+}
+
+__global__ void k_save_step(int B, size_t E, int G, int k, const float* __restrict__ y,
+                            float* __restrict__ ys) {
+  const int b = blockIdx.y;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  ys[((size_t)b * G + k) * E + e] = y[(size_t)b * E + e];
+}
+
+__global__ void k_grid_stats(int B, int method, const int32_t* __restrict__ nsteps,
+                             int32_t* __restrict__ stats) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int ns = nsteps[b];
+  stats[b * 4 + GNCDE_STAT_STEPS] = ns;
+  stats[b * 4 + GNCDE_STAT_REJECTS] = 0;
+  stats[b * 4 + GNCDE_STAT_EVALS] = method == GNCDE_RK4 ? 4 * ns : 1 + 6 * ns;
+  stats[b * 4 + GNCDE_STAT_STATUS] = 0;
+}
+
+inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+
+struct VfWs {
+  float *A, *dA, *red, *tg, *Z0, *Z1, *m;
+};
+
+VfWs carve_vf(const GncdeProblem& p, char* ws) {
+  const size_t B = p.B, n = p.n, nn = n * n, D = max_dim(p);
+  VfWs w;
+  size_t off = 0;
+  auto take = [&](size_t floats) {
+    float* ptr = reinterpret_cast<float*>(ws + off);
+    off += align_up(floats * sizeof(float), 256);
+    return ptr;
+  };
+  w.A = take(B * nn);
+  w.dA = take(B * nn);
+  w.red = take(B * kRedStride * n);
+  w.tg = take(B * n);
+  w.Z0 = take(B * n * D);
+  w.Z1 = take(B * n * D);
+  w.m = take(B * n * D);
+  return w;
+}
+
+}  // namespace
+
+size_t generic_vf_workspace(const GncdeProblem& p) {
+  const size_t B = p.B, n = p.n, nn = n * n, D = max_dim(p);
+  size_t s = 0;
+  s += 2 * align_up(B * nn * 4, 256);
+  s += align_up(B * kRedStride * n * 4, 256);
+  s += align_up(B * n * 4, 256);
+  s += 3 * align_up(B * n * D * 4, 256);
+  return s;
+}
+
+int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
+                    hipStream_t st) {
+  const int B = p.B, n = p.n;
+  const size_t nn = (size_t)n * n;
+  VfWs w = carve_vf(p, ws);
+  hipLaunchKernelGGL(k_spline, dim3(cdiv(nn > (size_t)n ? nn : n, 256), B), dim3(256), 0, st, n, p.T,
+                     p.ts, p.coef, p.tcoef, t, w.A, w.dA, w.tg);
+  hipLaunchKernelGGL(k_reduce, dim3(B), dim3(256), 0, st, n, w.A, w.dA, w.red);
+  const float* Zin = y;
+  float* bufs[2] = {w.Z0, w.Z1};
+  for (int l = 0; l < p.L; ++l) {
+    const int din = p.dims[l], dout = p.dims[l + 1];
+    const LayerOffsets o = layer_offsets(p, l);
+    hipLaunchKernelGGL(k_rms_linear, dim3(cdiv((size_t)n * dout, 256), B), dim3(256), 0, st, n, din,
+                       dout, Zin, p.params + o.rms_w, p.params + o.rms_b, p.params + o.W,
+                       p.params + o.b, w.m);
+    float* Zout = bufs[l & 1];
+    hipLaunchKernelGGL(k_prop, dim3(cdiv(dout, 16), cdiv(n, 16), B), dim3(256), 0, st, n, dout,
+                       p.fusion + (size_t)l * GNCDE_FC, w.A, w.dA, w.red, w.m, Zout,
+                       l < p.L - 1 ? 1 : 0);
+    Zin = Zout;
+  }
+  const int dout = out_dim(p);
+  hipLaunchKernelGGL(k_finalize, dim3(cdiv((size_t)n * dout, 256), B), dim3(256), 0, st, n,
+                     p.dims[p.L], p.cde_hidden, p.cde_embed, p.T, p.ts, p.data_coef, t, w.tg, Zin,
+                     dy);
+  return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+}
+
+size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s) {
+  (void)s;
+  const size_t B = p.B, E = (size_t)p.n * state_dim(p);
+  size_t sz = generic_vf_workspace(p);
+  sz += 9 * align_up(B * E * 4, 256);  // y, ytmp, K[7]
+  sz += 3 * align_up(B * 4, 256);      // tcur, hcur, tstage
+  return sz;
+}
+
+int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
+                      int32_t* stats, char* ws, hipStream_t st) {
+  if (s.controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
+  const int B = p.B;
+  const size_t E = (size_t)p.n * state_dim(p);
+  char* cur = ws + generic_vf_workspace(p);
+  auto take = [&](size_t floats) {
+    float* ptr = reinterpret_cast<float*>(cur);
+    cur += align_up(floats * sizeof(float), 256);
+    return ptr;
+  };
+  float* y = take(B * E);
+  float* yt = take(B * E);
+  float* K[7];
+  for (int j = 0; j < 7; ++j) K[j] = take(B * E);
+  float* tcur = take(B);
+  float* hcur = take(B);
+  float* tst = take(B);
+  const int G = s.grid_len;
+  const unsigned gb = cdiv(B, 256);
+  const dim3 ge(cdiv(E, 256), B);
+  (void)hipMemcpyAsync(y, y0, B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
+  if (s.save_mode == GNCDE_SAVE_STEPS)
+    hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, 0, y, ys);
+
+  auto eval = [&](float c, const float* yin, float* out) {
+    hipLaunchKernelGGL(k_stage_time, dim3(gb), dim3(256), 0, st, B, c, tcur, hcur, tst);
+    return generic_vf_eval(p, tst, yin, out, ws, st);
+  };
+  auto combo = [&](std::initializer_list<std::pair<int, float>> terms, float* out) {
+    Combo cb{};
+    cb.nk = 0;
+    for (auto& tr : terms) {
+      cb.K[cb.nk] = K[tr.first];
+      cb.a[cb.nk] = tr.second;
+      cb.nk++;
+    }
+    hipLaunchKernelGGL(k_combo, ge, dim3(256), 0, st, B, E, y, cb, hcur, out);
+  };
+
+  int rc = GNCDE_OK;
+  const int steps = G - 1;
+  if (s.method == GNCDE_RK4) {
+    for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
+      hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur);
+      rc |= eval(0.0f, y, K[0]);
+      combo({{0, 0.5f}}, yt);
+      rc |= eval(0.5f, yt, K[1]);
+      combo({{1, 0.5f}}, yt);
+      rc |= eval(0.5f, yt, K[2]);
+      combo({{2, 1.0f}}, yt);
+      rc |= eval(1.0f, yt, K[3]);
+      // y + h/6 (k1 + 2k2 + 2k3 + k4)
+      combo({{0, 1.0f / 6.0f}, {1, 2.0f / 6.0f}, {2, 2.0f / 6.0f}, {3, 1.0f / 6.0f}}, yt);
+      (void)hipMemcpyAsync(y, yt, B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
+      if (s.save_mode == GNCDE_SAVE_STEPS)
+        hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, k + 1, y, ys);
+    }
+  } else {  // Tsit5 on the grid (ConstantStepSize), FSAL
+    hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, 0, s.grid, s.nsteps, tcur, hcur);
+    rc |= eval(0.0f, y, K[0]);
+    for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
+      hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur);
+      combo({{0, TSIT5_A21}}, yt);
+      rc |= eval(TSIT5_C2, yt, K[1]);
+      combo({{0, TSIT5_A31}, {1, TSIT5_A32}}, yt);
+      rc |= eval(TSIT5_C3, yt, K[2]);
+      combo({{0, TSIT5_A41}, {1, TSIT5_A42}, {2, TSIT5_A43}}, yt);
+      rc |= eval(TSIT5_C4, yt, K[3]);
+      combo({{0, TSIT5_A51}, {1, TSIT5_A52}, {2, TSIT5_A53}, {3, TSIT5_A54}}, yt);
+      rc |= eval(TSIT5_C5, yt, K[4]);
+      combo({{0, TSIT5_A61}, {1, TSIT5_A62}, {2, TSIT5_A63}, {3, TSIT5_A64}, {4, TSIT5_A65}}, yt);
+      rc |= eval(1.0f, yt, K[5]);
+      combo({{0, TSIT5_B1}, {1, TSIT5_B2}, {2, TSIT5_B3}, {3, TSIT5_B4}, {4, TSIT5_B5}, {5, TSIT5_B6}},
+            yt);
+      rc |= eval(1.0f, yt, K[6]);
+      (void)hipMemcpyAsync(y, yt, B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
+      (void)hipMemcpyAsync(K[0], K[6], B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
+      if (s.save_mode == GNCDE_SAVE_STEPS)
+        hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, k + 1, y, ys);
+    }
+  }
+  if (s.save_mode == GNCDE_SAVE_T1)
+    (void)hipMemcpyAsync(ys, y, B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
+  if (stats) hipLaunchKernelGGL(k_grid_stats, dim3(gb), dim3(256), 0, st, B, s.method, s.nsteps, stats);
+  if (hipGetLastError() != hipSuccess) return GNCDE_ERR_HIP;
+  return rc;
+}
+
+}  // namespace gncde

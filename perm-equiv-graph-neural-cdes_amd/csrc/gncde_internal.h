@@ -1,0 +1,117 @@
+// Internal declarations shared by the HIP translation units of libgncde_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/gncde.h"
+
+namespace gncde {
+
+// ---- Tsit5 tableau (Tsitouras 2011), restated in oracle/gncde_oracle.py:TSIT5_* ----------------
+#define TSIT5_A21 0.161f
+#define TSIT5_A31 (-0.008480655492356989f)
+#define TSIT5_A32 0.335480655492357f
+#define TSIT5_A41 2.897153057105493f
+#define TSIT5_A42 (-6.359448489975075f)
+#define TSIT5_A43 4.3622954328695815f
+#define TSIT5_A51 5.325864828439257f
+#define TSIT5_A52 (-11.748883564062828f)
+#define TSIT5_A53 7.4955393428898365f
+#define TSIT5_A54 (-0.09249506636175525f)
+#define TSIT5_A61 5.86145544294642f
+#define TSIT5_A62 (-12.92096931784711f)
+#define TSIT5_A63 8.159367898576159f
+#define TSIT5_A64 (-0.071584973281401f)
+#define TSIT5_A65 (-0.028269050394068383f)
+#define TSIT5_B1 0.09646076681806523f
+#define TSIT5_B2 0.01f
+#define TSIT5_B3 0.4798896504144996f
+#define TSIT5_B4 1.379008574103742f
+#define TSIT5_B5 (-3.290069515436081f)
+#define TSIT5_B6 2.324710524099774f
+#define TSIT5_E1 0.001780011052226f
+#define TSIT5_E2 0.000816434459657f
+#define TSIT5_E3 (-0.007880878010262f)
+#define TSIT5_E4 0.144711007173263f
+#define TSIT5_E5 (-0.582357165452555f)
+#define TSIT5_E6 0.458082105929187f
+#define TSIT5_E7 (-0.015151515151515152f)
+#define TSIT5_C2 0.161f
+#define TSIT5_C3 0.327f
+#define TSIT5_C4 0.9f
+#define TSIT5_C5 0.9800255409045097f
+
+// Stage time t + c*h with exactly two fp32 roundings (no contraction), matching the oracle.
+__device__ __forceinline__ float stage_time(float t, float c, float h) {
+  return __fadd_rn(t, __fmul_rn(c, h));
+}
+
+// diffrax CubicInterpolation interval rule: clip(searchsorted(ts, t, 'left') - 1, 0, T-2).
+__device__ __forceinline__ int interval_index(const float* ts, int T, float t) {
+  int lo = 0, hi = T;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (ts[mid] < t) lo = mid + 1; else hi = mid;
+  }
+  int i = lo - 1;
+  i = i < 0 ? 0 : i;
+  return i > T - 2 ? T - 2 : i;
+}
+
+// Offsets of layer l's parameters inside the packed params buffer (see gncde.h).
+struct LayerOffsets {
+  size_t rms_w, rms_b, W, b;
+};
+inline LayerOffsets layer_offsets(const GncdeProblem& p, int l) {
+  size_t off = 0;
+  for (int j = 0; j < l; ++j) {
+    const size_t din = p.dims[j], dout = p.dims[j + 1];
+    off += 2 * din + dout * din + dout;
+  }
+  const size_t din = p.dims[l], dout = p.dims[l + 1];
+  LayerOffsets o;
+  o.rms_w = off;
+  o.rms_b = off + din;
+  o.W = off + 2 * din;
+  o.b = off + 2 * din + dout * din;
+  return o;
+}
+inline size_t params_floats(const GncdeProblem& p) {
+  size_t off = 0;
+  for (int j = 0; j < p.L; ++j) {
+    const size_t din = p.dims[j], dout = p.dims[j + 1];
+    off += 2 * din + dout * din + dout;
+  }
+  return off;
+}
+
+inline int state_dim(const GncdeProblem& p) { return p.dims[0]; }
+inline int out_dim(const GncdeProblem& p) { return p.cde_hidden > 0 ? p.cde_hidden : p.dims[p.L]; }
+inline int max_dim(const GncdeProblem& p) {
+  int m = 0;
+  for (int l = 0; l <= p.L; ++l) m = p.dims[l] > m ? p.dims[l] : m;
+  return m;
+}
+
+int validate_problem(const GncdeProblem* p);
+int validate_solver(const GncdeProblem* p, const GncdeSolver* s);
+
+// generic (any-shape, multi-kernel) path: gncde_generic.hip
+size_t generic_vf_workspace(const GncdeProblem& p);
+size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s);
+int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
+                    hipStream_t st);
+int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
+                      int32_t* stats, char* ws, hipStream_t st);
+
+// fused persistent path: gncde_fused.hip.  Returns GNCDE_ERR_UNSUPPORTED when no kernel fits.
+bool fused_supported(const GncdeProblem& p, const GncdeSolver& s, char* name, size_t name_len);
+int fused_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
+                    int32_t* stats, hipStream_t st);
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace gncde

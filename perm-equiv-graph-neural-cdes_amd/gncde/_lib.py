@@ -1,0 +1,122 @@
+"""ctypes binding of libgncde_hip.so (the C-ABI declared in include/gncde.h).
+
+The library is built in-tree (``make -C perm-equiv-graph-neural-cdes_amd``) and loaded from this
+directory.  There is deliberately NO fallback: if the shared object is missing, fails to load, or no
+GPU is visible, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int32, c_size_t, c_void_p
+
+MAX_LAYERS = 8
+FC = 24
+ABI_VERSION = 1
+
+RK4, TSIT5 = 0, 1
+CTRL_GRID, CTRL_PID = 0, 1
+SAVE_T1, SAVE_STEPS, SAVE_TS = 0, 1, 2
+STAT_STEPS, STAT_REJECTS, STAT_EVALS, STAT_STATUS = 0, 1, 2, 3
+
+LIB_NAME = "libgncde_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+# Every symbol include/gncde.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "gncde_abi_version",
+    "gncde_strerror",
+    "gncde_integrate_path",
+    "gncde_workspace_bytes",
+    "gncde_vf_eval",
+    "gncde_integrate",
+    "gncde_node_affine",
+    "gncde_interval_index",
+)
+
+
+class GncdeProblem(ctypes.Structure):
+    _fields_ = [
+        ("B", c_int32),
+        ("n", c_int32),
+        ("T", c_int32),
+        ("L", c_int32),
+        ("dims", c_int32 * (MAX_LAYERS + 1)),
+        ("cde_hidden", c_int32),
+        ("cde_embed", c_int32),
+        ("ts", c_void_p),
+        ("coef", c_void_p),
+        ("tcoef", c_void_p),
+        ("data_coef", c_void_p),
+        ("fusion", c_void_p),
+        ("params", c_void_p),
+    ]
+
+
+class GncdeSolver(ctypes.Structure):
+    _fields_ = [
+        ("method", c_int32),
+        ("controller", c_int32),
+        ("save_mode", c_int32),
+        ("max_steps", c_int32),
+        ("grid_len", c_int32),
+        ("n_save", c_int32),
+        ("rtol", c_float),
+        ("atol", c_float),
+        ("grid", c_void_p),
+        ("nsteps", c_void_p),
+        ("t0", c_void_p),
+        ("t1", c_void_p),
+        ("dt0", c_void_p),
+        ("save_ts", c_void_p),
+    ]
+
+
+class GncdeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load (once) and return the shared library; raise if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise GncdeError(
+            f"{p} not found: build it with `make -C perm-equiv-graph-neural-cdes_amd` "
+            "(there is no CPU fallback for the GNCDE hot path)")
+    lib = ctypes.CDLL(p)
+    lib.gncde_abi_version.restype = c_int32
+    lib.gncde_strerror.restype = c_char_p
+    lib.gncde_strerror.argtypes = [c_int32]
+    lib.gncde_integrate_path.restype = c_int32
+    lib.gncde_integrate_path.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver), c_char_p, c_size_t]
+    lib.gncde_workspace_bytes.restype = c_size_t
+    lib.gncde_workspace_bytes.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver)]
+    lib.gncde_vf_eval.restype = c_int32
+    lib.gncde_vf_eval.argtypes = [POINTER(GncdeProblem), c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                  c_void_p]
+    lib.gncde_integrate.restype = c_int32
+    lib.gncde_integrate.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver), c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_size_t, c_void_p]
+    lib.gncde_node_affine.restype = c_int32
+    lib.gncde_node_affine.argtypes = [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p]
+    lib.gncde_interval_index.restype = c_int32
+    lib.gncde_interval_index.argtypes = [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
+                                         c_void_p]
+    v = lib.gncde_abi_version()
+    if v != ABI_VERSION:
+        raise GncdeError(f"ABI mismatch: library {v}, bindings {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = load().gncde_strerror(rc).decode()
+        raise GncdeError(f"gncde error {rc}: {msg}")

@@ -1,0 +1,227 @@
+"""Batched entry points over torch device tensors -> libgncde_hip.so.
+
+``vf_eval`` replaces ``jax.vmap(PermEquivGraphVectorField.__call__)`` (perm_equiv_graph_vector_field.py:85-129)
+and ``integrate`` replaces ``jax.vmap`` of ``diffrax.diffeqsolve`` (graph_neural_cde.py:94-104 and the
+PGT/TGB drivers).  All tensors must already live on the current CUDA(HIP) device; work is enqueued on
+torch's current stream.  Errors from the library raise ``GncdeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib
+from . import layout
+
+
+def _require_gpu():
+    if not torch.cuda.is_available():
+        raise _lib.GncdeError("no HIP device visible: the GNCDE engine runs only on the GPU (no CPU path)")
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+@dataclass
+class Problem:
+    """Device-resident problem description (mirrors ``GncdeProblem``)."""
+
+    ts: torch.Tensor            # [B, T]
+    coef: torch.Tensor          # [B, T-1, 4, n, n]
+    tcoef: torch.Tensor         # [B, T-1, 3, n]
+    fusion: torch.Tensor        # [L, 24] fp32
+    params: torch.Tensor        # packed fp32
+    dims: list
+    data_coef: torch.Tensor | None = None  # [B, T-1, 4, n, de, 2]
+    cde_hidden: int = 0
+    cde_embed: int = 0
+    _keep: list = field(default_factory=list)
+
+    @property
+    def B(self):
+        return int(self.ts.shape[0])
+
+    @property
+    def n(self):
+        return int(self.coef.shape[-1])
+
+    @property
+    def T(self):
+        return int(self.ts.shape[1])
+
+    @property
+    def L(self):
+        return len(self.dims) - 1
+
+    def c_struct(self) -> _lib.GncdeProblem:
+        for name in ("ts", "coef", "tcoef", "fusion", "params"):
+            t = getattr(self, name)
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+                raise _lib.GncdeError(f"Problem.{name} must be a contiguous float32 CUDA tensor")
+        if len(self.dims) - 1 > _lib.MAX_LAYERS:
+            raise _lib.GncdeError("too many layers")
+        s = _lib.GncdeProblem()
+        s.B, s.n, s.T, s.L = self.B, self.n, self.T, self.L
+        for i, d in enumerate(self.dims):
+            s.dims[i] = int(d)
+        s.cde_hidden, s.cde_embed = int(self.cde_hidden), int(self.cde_embed)
+        s.ts, s.coef, s.tcoef = _ptr(self.ts).value, _ptr(self.coef).value, _ptr(self.tcoef).value
+        s.data_coef = _ptr(self.data_coef).value if self.data_coef is not None else None
+        s.fusion, s.params = _ptr(self.fusion).value, _ptr(self.params).value
+        return s
+
+    def shard(self, start: int, stop: int) -> "Problem":
+        """Contiguous batch shard (data-parallel ranks own [start, stop))."""
+        return Problem(ts=self.ts[start:stop], coef=self.coef[start:stop], tcoef=self.tcoef[start:stop],
+                       fusion=self.fusion, params=self.params, dims=list(self.dims),
+                       data_coef=None if self.data_coef is None else self.data_coef[start:stop],
+                       cde_hidden=self.cde_hidden, cde_embed=self.cde_embed)
+
+
+def make_problem(ts, coeffs, kind, layers, data_coeffs=None, cde_hidden=0, cde_embed=0, device="cuda"):
+    """Build a Problem from reference-layout inputs (ts [B,T], coeffs (d,c,b,a) [B,T-1,n,n,2], layer dicts)."""
+    coef, tcoef = layout.pack_control(coeffs, device=device)
+    ts = torch.as_tensor(ts, dtype=torch.float32)
+    if ts.dim() == 1:
+        ts = ts.unsqueeze(0)
+    n = coef.shape[-1]
+    fusion = layout.fusion_table(kind, layers, n).to(torch.float32).to(device).contiguous()
+    params = layout.pack_params(layers, device=device)
+    dc = layout.pack_data_control(data_coeffs, device=device) if data_coeffs is not None else None
+    return Problem(ts=ts.to(device).contiguous(), coef=coef, tcoef=tcoef, fusion=fusion, params=params,
+                   dims=layout.layer_dims(layers), data_coef=dc, cde_hidden=cde_hidden, cde_embed=cde_embed)
+
+
+class _Workspace:
+    """Grow-only device scratch buffer (one per device)."""
+
+    _bufs: dict = {}
+
+    @classmethod
+    def get(cls, nbytes: int):
+        dev = torch.cuda.current_device()
+        buf = cls._bufs.get(dev)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device="cuda")
+            cls._bufs[dev] = buf
+        return buf
+
+
+def vf_eval(prob: Problem, t: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """dy[b] = VF(t[b], y[b]) for every sample.  t [B], y [B, n, d_0] -> [B, n, d_out]."""
+    _require_gpu()
+    lib = _lib.load()
+    ps = prob.c_struct()
+    t = t.to(device=y.device, dtype=torch.float32).contiguous()
+    y = y.contiguous()
+    if y.shape != (prob.B, prob.n, prob.dims[0]) or t.shape != (prob.B,):
+        raise _lib.GncdeError(f"vf_eval: bad shapes t{tuple(t.shape)} y{tuple(y.shape)}")
+    dout = prob.cde_hidden if prob.cde_hidden > 0 else prob.dims[-1]
+    dy = torch.empty(prob.B, prob.n, dout, dtype=torch.float32, device=y.device)
+    nbytes = lib.gncde_workspace_bytes(ctypes.byref(ps), None)
+    ws = _Workspace.get(nbytes)
+    _lib.check(lib.gncde_vf_eval(ctypes.byref(ps), _ptr(t), _ptr(y), _ptr(dy), _ptr(ws), nbytes, _stream()))
+    return dy
+
+
+@dataclass
+class SolverSpec:
+    """Mirrors ``GncdeSolver``.  For fixed grids, ``grid`` [B, G] and ``nsteps`` [B] (layout.stack_grids)."""
+
+    method: int = _lib.RK4
+    controller: int = _lib.CTRL_GRID
+    save_mode: int = _lib.SAVE_T1
+    grid: torch.Tensor | None = None
+    nsteps: torch.Tensor | None = None
+    rtol: float = 1e-3
+    atol: float = 1e-6
+    max_steps: int = 4096
+    t0: torch.Tensor | None = None
+    t1: torch.Tensor | None = None
+    dt0: torch.Tensor | None = None
+    save_ts: torch.Tensor | None = None
+
+    def c_struct(self) -> _lib.GncdeSolver:
+        s = _lib.GncdeSolver()
+        s.method, s.controller, s.save_mode, s.max_steps = self.method, self.controller, self.save_mode, \
+            self.max_steps
+        s.grid_len = int(self.grid.shape[1]) if self.grid is not None else 0
+        s.n_save = int(self.save_ts.shape[1]) if self.save_ts is not None else 0
+        s.rtol, s.atol = self.rtol, self.atol
+        s.grid = _ptr(self.grid).value if self.grid is not None else None
+        s.nsteps = _ptr(self.nsteps).value if self.nsteps is not None else None
+        s.t0 = _ptr(self.t0).value if self.t0 is not None else None
+        s.t1 = _ptr(self.t1).value if self.t1 is not None else None
+        s.dt0 = _ptr(self.dt0).value if self.dt0 is not None else None
+        s.save_ts = _ptr(self.save_ts).value if self.save_ts is not None else None
+        return s
+
+    def shard(self, start, stop):
+        cut = lambda x: None if x is None else x[start:stop]  # noqa: E731
+        return SolverSpec(self.method, self.controller, self.save_mode, cut(self.grid), cut(self.nsteps),
+                          self.rtol, self.atol, self.max_steps, cut(self.t0), cut(self.t1), cut(self.dt0),
+                          cut(self.save_ts))
+
+
+def integrate_path(prob: Problem, solver: SolverSpec) -> str:
+    lib = _lib.load()
+    ps, ss = prob.c_struct(), solver.c_struct()
+    buf = ctypes.create_string_buffer(128)
+    _lib.check(lib.gncde_integrate_path(ctypes.byref(ps), ctypes.byref(ss), buf, 128))
+    return buf.value.decode()
+
+
+def integrate(prob: Problem, solver: SolverSpec, y0: torch.Tensor, stats: bool = False):
+    """Solve every sample.  Returns ys (and stats [B, 4] int32 if requested)."""
+    _require_gpu()
+    lib = _lib.load()
+    ps, ss = prob.c_struct(), solver.c_struct()
+    y0 = y0.to(torch.float32).contiguous()
+    ds = prob.dims[0]
+    if y0.shape != (prob.B, prob.n, ds):
+        raise _lib.GncdeError(f"integrate: y0 shape {tuple(y0.shape)} != {(prob.B, prob.n, ds)}")
+    if solver.save_mode == _lib.SAVE_T1:
+        ys = torch.empty(prob.B, prob.n, ds, dtype=torch.float32, device=y0.device)
+    elif solver.save_mode == _lib.SAVE_STEPS:
+        ys = torch.empty(prob.B, ss.grid_len, prob.n, ds, dtype=torch.float32, device=y0.device)
+    else:
+        ys = torch.empty(prob.B, ss.n_save, prob.n, ds, dtype=torch.float32, device=y0.device)
+    st = torch.zeros(prob.B, 4, dtype=torch.int32, device=y0.device)
+    nbytes = lib.gncde_workspace_bytes(ctypes.byref(ps), ctypes.byref(ss))
+    ws = _Workspace.get(nbytes) if nbytes else None
+    _lib.check(lib.gncde_integrate(ctypes.byref(ps), ctypes.byref(ss), _ptr(y0), _ptr(ys), _ptr(st),
+                                   _ptr(ws), nbytes, _stream()))
+    return (ys, st) if stats else ys
+
+
+def node_affine(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:
+    """out[..., :] = W @ x[..., :] + b per row (eqx.nn.Linear under vmap)."""
+    _require_gpu()
+    lib = _lib.load()
+    x = x.to(torch.float32).contiguous()
+    W = W.to(device=x.device, dtype=torch.float32).contiguous()
+    bb = b.to(device=x.device, dtype=torch.float32).contiguous() if b is not None else None
+    din, dout = int(W.shape[1]), int(W.shape[0])
+    rows = x.numel() // din
+    out = torch.empty(*x.shape[:-1], dout, dtype=torch.float32, device=x.device)
+    _lib.check(lib.gncde_node_affine(rows, din, dout, _ptr(x), _ptr(W), _ptr(bb), _ptr(out), _stream()))
+    return out
+
+
+def interval_index(ts: torch.Tensor, t: torch.Tensor, sample: torch.Tensor) -> torch.Tensor:
+    _require_gpu()
+    lib = _lib.load()
+    ts = ts.to(torch.float32).contiguous()
+    t = t.to(device=ts.device, dtype=torch.float32).contiguous()
+    sample = sample.to(device=ts.device, dtype=torch.int32).contiguous()
+    idx = torch.empty(t.numel(), dtype=torch.int32, device=ts.device)
+    _lib.check(lib.gncde_interval_index(_ptr(ts), int(ts.shape[0]), int(ts.shape[1]), _ptr(t), _ptr(sample),
+                                        _ptr(idx), int(t.numel()), _stream()))
+    return idx

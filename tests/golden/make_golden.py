@@ -1,0 +1,141 @@
+"""Generate the golden fixtures in tests/golden/*.npz from the fp64 CPU oracle (oracle/gncde_oracle.py).
+
+    python tests/golden/make_golden.py
+
+PARITY UNPINNED: the reference (JAX/diffrax/equinox) cannot be executed in this image, so these
+vectors come from the build's restatement of the reference algorithm, not from the reference itself.
+They freeze the oracle (tests/test_golden.py re-derives them) and are the GPU parity targets
+(tests/test_gpu_parity.py).  Parameters are injected (drawn from the reference's init distributions
+with numpy), so no JAX PRNG is involved.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", ".."))
+from oracle import gncde_oracle as O  # noqa: E402
+
+
+def flat_layers(prefix, params: O.VFParams, out: dict):
+    out[prefix + "kind"] = np.array(params.kind)
+    out[prefix + "L"] = np.array(len(params.layers))
+    for l, lay in enumerate(params.layers):
+        for k, v in lay.items():
+            out[f"{prefix}l{l}_{k}"] = np.asarray(v, dtype=np.float64)
+
+
+def load_layers(z, prefix=""):
+    kind = str(z[prefix + "kind"])
+    L = int(z[prefix + "L"])
+    layers = []
+    for l in range(L):
+        pre = f"{prefix}l{l}_"
+        lay = {k[len(pre):]: np.asarray(z[k]) for k in z.files if k.startswith(pre)}
+        layers.append(lay)
+    return O.VFParams(kind=kind, layers=layers)
+
+
+def problem(rng, B, n, T, kind, dims, irregular=True):
+    ts_all, coeffs_all = [], []
+    for _ in range(B):
+        ts, X = O.make_graph_control(rng, n, T, irregular=irregular)
+        ts_all.append(ts)
+        coeffs_all.append(O.backward_hermite_coefficients(ts, X))
+    params = O.init_vf_params(rng, kind, dims)
+    # perturb RMSNorm affine so its weight/bias paths are exercised
+    for lay in params.layers:
+        lay["rms_w"] = lay["rms_w"] + 0.1 * rng.standard_normal(lay["rms_w"].shape)
+        lay["rms_b"] = lay["rms_b"] + 0.1 * rng.standard_normal(lay["rms_b"].shape)
+    ts = np.stack(ts_all)
+    coeffs = tuple(np.stack([c[q] for c in coeffs_all]) for q in range(4))
+    return ts, coeffs, params
+
+
+def vf_case(rng, name, B, n, T, kind, dims):
+    ts, coeffs, params = problem(rng, B, n, T, kind, dims)
+    y = rng.standard_normal((B, n, dims[0]))
+    # times: interior points, an exact knot, t0 and t1 (index-rule edges)
+    t = np.array([rng.uniform(ts[b, 0], ts[b, -1]) for b in range(B)], dtype=np.float32).astype(np.float64)
+    t[0] = ts[0, 0]
+    if B > 1:
+        t[1] = ts[1, -1]
+    if B > 2:
+        t[2] = ts[2, T // 2]
+    dy = np.stack([O.vector_field(params, t[b], y[b], O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs)))
+                   for b in range(B)])
+    out = dict(ts=ts, d=coeffs[0], c=coeffs[1], b=coeffs[2], a=coeffs[3], y=y, t=t, dy=dy)
+    flat_layers("", params, out)
+    np.savez_compressed(os.path.join(HERE, name), **out)
+
+
+def solve_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None):
+    ts, coeffs, params = problem(rng, B, n, T, kind, dims)
+    y0 = rng.standard_normal((B, n, dims[0]))
+    grids, ys = [], []
+    for b in range(B):
+        ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
+        f = lambda t, y, ctrl=ctrl: O.vector_field(params, t, y, ctrl)  # noqa: E731
+        if method == "rk4":
+            g = O.rk4_grid(ts[b, 0], ts[b, -1], nsteps)
+        else:
+            g = O.constant_grid(ts[b, 0], ts[b, -1], dt0)
+        grids.append(g)
+        traj, _ = O.solve_fixed_grid(f, g, y0[b], method=method, save_every_step=True,
+                                     time_dtype=np.float32)
+        ys.append(traj)
+    G = max(len(g) for g in grids)
+    grid = np.stack([np.concatenate([g, np.full(G - len(g), g[-1], np.float32)]) for g in grids])
+    nst = np.array([len(g) - 1 for g in grids], dtype=np.int32)
+    traj = np.stack([np.concatenate([y, np.repeat(y[-1:], G - len(y), axis=0)]) for y in ys])
+    out = dict(ts=ts, d=coeffs[0], c=coeffs[1], b=coeffs[2], a=coeffs[3], y0=y0, grid=grid, nsteps=nst,
+               ys=traj, method=np.array(method))
+    flat_layers("", params, out)
+    np.savez_compressed(os.path.join(HERE, name), **out)
+
+
+def cde_case(rng, name, B, n, T, h, de, L):
+    dims = [h] + [h] * (L - 1) + [h * de * 2]
+    ts, coeffs, params = problem(rng, B, n, T, "undirected", dims)
+    # data spline: x [T, n, de] stacked with time (tgb_graph_neural_cde.py:115-130)
+    dcoef = []
+    for b in range(B):
+        x = rng.standard_normal((T, n, de))
+        X = np.stack([np.broadcast_to(ts[b][:, None, None], x.shape), x], axis=-1)
+        dcoef.append(O.backward_hermite_coefficients(ts[b], X))
+    dcoeffs = tuple(np.stack([c[q] for c in dcoef]) for q in range(4))
+    y = rng.standard_normal((B, n, h))
+    t = np.array([rng.uniform(ts[b, 0], ts[b, -1]) for b in range(B)], dtype=np.float32).astype(np.float64)
+    dy = []
+    for b in range(B):
+        ca = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
+        cd = O.CubicInterpolation(ts[b], tuple(c[b] for c in dcoeffs))
+        dy.append(O.cde_wrapper(params, h, de, t[b], y[b], ca, cd))
+    out = dict(ts=ts, d=coeffs[0], c=coeffs[1], b=coeffs[2], a=coeffs[3], xd=dcoeffs[0], xc=dcoeffs[1],
+               xb=dcoeffs[2], xa=dcoeffs[3], y=y, t=t, dy=np.stack(dy), h=np.array(h), de=np.array(de))
+    flat_layers("", params, out)
+    np.savez_compressed(os.path.join(HERE, name), **out)
+
+
+def main():
+    rng = np.random.default_rng(1234)
+    vf_case(rng, "vf_undirected_n16_L3.npz", 4, 16, 12, "undirected", [16, 16, 16, 16])
+    vf_case(rng, "vf_directed_n16_L2.npz", 4, 16, 12, "directed", [16, 16, 16])
+    vf_case(rng, "vf_plain_n16_L2.npz", 4, 16, 12, "plain", [16, 16, 16])
+    vf_case(rng, "vf_undirected_n10_mixed.npz", 3, 10, 9, "undirected", [8, 24, 12])
+    vf_case(rng, "vf_undirected_n4_L2.npz", 3, 4, 6, "undirected", [16, 16, 16])
+    solve_case(rng, "rk4_undirected_n16_L2.npz", 4, 16, 12, "undirected", [16, 16, 16], "rk4", nsteps=20)
+    solve_case(rng, "rk4_undirected_n10_L3.npz", 3, 10, 10, "undirected", [16, 16, 16, 16], "rk4", nsteps=15)
+    solve_case(rng, "tsit5c_undirected_n16_L2.npz", 3, 16, 8, "undirected", [16, 16, 16], "tsit5", dt0=0.5)
+    solve_case(rng, "rk4_directed_n32_h32_L2.npz", 2, 32, 8, "directed", [32, 32, 32], "rk4", nsteps=10)
+    cde_case(rng, "cde_n12_h8_de3.npz", 3, 12, 5, 8, 3, 2)
+    # widths differ between layers -> not covered by the fused kernel, exercises the generic solver
+    solve_case(rng, "rk4_undirected_n12_mixed.npz", 2, 12, 7, "undirected", [16, 24, 16], "rk4", nsteps=8)
+    solve_case(rng, "tsit5c_plain_n20_mixed.npz", 2, 20, 6, "plain", [8, 12, 8], "tsit5", dt0=0.7)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,101 @@
+"""The C-ABI library loads, exports every symbol include/gncde.h declares, and its struct layout matches
+the ctypes mirror.  Host-only entry points (version, strerror, workspace sizing, path selection) are
+exercised; nothing here launches a kernel."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from gncde import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gncde.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(gncde_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_declares_exactly_the_bound_symbols():
+    assert declared_functions() == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (gncde_\w+)", out))
+    missing = set(declared_functions()) - exported
+    assert not missing, missing
+
+
+def test_library_loads_and_reports_abi():
+    lib = _lib.load()
+    assert lib.gncde_abi_version() == _lib.ABI_VERSION
+    assert lib.gncde_strerror(0) == b"ok"
+    assert b"workspace" in lib.gncde_strerror(4)
+
+
+def test_struct_layout_matches_c(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(f'''#include <stdio.h>
+#include <stddef.h>
+#include "{HEADER}"
+int main(void) {{
+  printf("%zu %zu %zu %zu %zu\\n", sizeof(GncdeProblem), offsetof(GncdeProblem, ts),
+         offsetof(GncdeProblem, params), sizeof(GncdeSolver), offsetof(GncdeSolver, save_ts));
+  return 0;
+}}''')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", str(src), "-o", str(exe)], check=True)
+    vals = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
+    P, S = _lib.GncdeProblem, _lib.GncdeSolver
+    assert vals == [ctypes.sizeof(P), P.ts.offset, P.params.offset, ctypes.sizeof(S), S.save_ts.offset]
+
+
+def _fake_problem(B=4, n=64, T=10, dims=(16, 16, 16, 16)):
+    p = _lib.GncdeProblem()
+    p.B, p.n, p.T, p.L = B, n, T, len(dims) - 1
+    for i, d in enumerate(dims):
+        p.dims[i] = d
+    # host-only entry points only validate non-NULL-ness; nothing is dereferenced
+    p.ts = p.coef = p.tcoef = p.fusion = p.params = 0x1000
+    return p
+
+
+def _fake_solver(method=_lib.RK4):
+    s = _lib.GncdeSolver()
+    s.method, s.controller, s.save_mode, s.grid_len = method, _lib.CTRL_GRID, _lib.SAVE_T1, 101
+    s.grid = s.nsteps = 0x1000
+    return s
+
+
+def test_path_selection_and_workspace():
+    lib = _lib.load()
+    p, s = _fake_problem(), _fake_solver()
+    buf = ctypes.create_string_buffer(64)
+    assert lib.gncde_integrate_path(ctypes.byref(p), ctypes.byref(s), buf, 64) == 0
+    assert buf.value == b"fused<64,16,3,rk4>"
+    assert lib.gncde_workspace_bytes(ctypes.byref(p), ctypes.byref(s)) == 0  # fused path needs none
+    assert lib.gncde_workspace_bytes(ctypes.byref(p), None) > 64 * 64 * 4 * 4 * 2
+    p2 = _fake_problem(n=200)
+    assert lib.gncde_integrate_path(ctypes.byref(p2), ctypes.byref(s), buf, 64) == 0
+    assert buf.value == b"generic"
+    assert lib.gncde_workspace_bytes(ctypes.byref(p2), ctypes.byref(s)) > 0
+
+
+@pytest.mark.parametrize("mutate,code", [
+    (lambda p, s: setattr(p, "T", 1), 2),
+    (lambda p, s: setattr(p, "L", 0), 2),
+    (lambda p, s: setattr(p, "coef", None), 1),
+    (lambda p, s: setattr(s, "method", 7), 1),
+    (lambda p, s: setattr(s, "grid", None), 1),
+])
+def test_argument_validation_error_codes(mutate, code):
+    lib = _lib.load()
+    p, s = _fake_problem(), _fake_solver()
+    mutate(p, s)
+    buf = ctypes.create_string_buffer(64)
+    assert lib.gncde_integrate_path(ctypes.byref(p), ctypes.byref(s), buf, 64) == code

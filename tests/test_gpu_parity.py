@@ -1,0 +1,188 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle's golden fixtures and the fp64 oracle.
+
+Tolerances (fp32 kernel vs fp64 oracle, relative to the max magnitude of the reference tensor):
+  * one vector-field evaluation:   RTOL_VF    = 2e-5
+  * a fixed-grid solve trajectory: RTOL_SOLVE = 1e-4   (error accumulates over the steps)
+  * interval index / step counts:  bit-exact
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gncde_oracle as O
+from tests.golden import make_golden as MG
+
+pytestmark = pytest.mark.gpu
+
+RTOL_VF = 2e-5
+RTOL_SOLVE = 1e-4
+
+
+def rel_err(x, ref):
+    x = np.asarray(x, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    return float(np.max(np.abs(x - ref)) / max(np.max(np.abs(ref)), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def gncde():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    import gncde as G
+    G._lib.load()
+    return G
+
+
+def problem_from(G, z, params, data=False):
+    coeffs = (z["d"], z["c"], z["b"], z["a"])
+    kw = {}
+    if data:
+        kw = dict(data_coeffs=(z["xd"], z["xc"], z["xb"], z["xa"]), cde_hidden=int(z["h"]), cde_embed=int(z["de"]))
+    return G.make_problem(z["ts"], coeffs, params.kind, params.layers, **kw)
+
+
+VF_FIXTURES = ["vf_undirected_n16_L3.npz", "vf_directed_n16_L2.npz", "vf_plain_n16_L2.npz",
+               "vf_undirected_n10_mixed.npz", "vf_undirected_n4_L2.npz"]
+
+
+@pytest.mark.parametrize("name", VF_FIXTURES)
+def test_vf_eval_matches_golden(gncde, golden_dir, name):
+    z = np.load(os.path.join(golden_dir, name))
+    params = MG.load_layers(z)
+    prob = problem_from(gncde, z, params)
+    dy = gncde.vf_eval(prob, torch.tensor(z["t"], dtype=torch.float32, device="cuda"),
+                       torch.tensor(z["y"], dtype=torch.float32, device="cuda"))
+    err = rel_err(dy.cpu().numpy(), z["dy"])
+    print(f"{name}: rel err {err:.3e}")
+    assert err <= RTOL_VF
+
+
+def test_cde_wrapper_vf_matches_golden(gncde, golden_dir):
+    z = np.load(os.path.join(golden_dir, "cde_n12_h8_de3.npz"))
+    params = MG.load_layers(z)
+    prob = problem_from(gncde, z, params, data=True)
+    dy = gncde.vf_eval(prob, torch.tensor(z["t"], dtype=torch.float32, device="cuda"),
+                       torch.tensor(z["y"], dtype=torch.float32, device="cuda"))
+    assert dy.shape == z["dy"].shape
+    assert rel_err(dy.cpu().numpy(), z["dy"]) <= RTOL_VF
+
+
+SOLVE_FIXTURES = [
+    ("rk4_undirected_n16_L2.npz", "fused<16,16,2,rk4>"),
+    ("rk4_undirected_n10_L3.npz", "fused<16,16,3,rk4>"),
+    ("tsit5c_undirected_n16_L2.npz", "fused<16,16,2,tsit5>"),
+    ("rk4_directed_n32_h32_L2.npz", "fused<32,32,2,rk4>"),
+    ("rk4_undirected_n12_mixed.npz", "generic"),
+    ("tsit5c_plain_n20_mixed.npz", "generic"),
+]
+
+
+@pytest.mark.parametrize("name,path", SOLVE_FIXTURES)
+@pytest.mark.parametrize("save", ["steps", "t1"])
+def test_integrate_matches_golden(gncde, golden_dir, name, path, save):
+    G = gncde
+    z = np.load(os.path.join(golden_dir, name))
+    params = MG.load_layers(z)
+    prob = problem_from(G, z, params)
+    method = G._lib.RK4 if str(z["method"]) == "rk4" else G._lib.TSIT5
+    spec = G.SolverSpec(method=method, save_mode=G._lib.SAVE_STEPS if save == "steps" else G._lib.SAVE_T1,
+                        grid=torch.tensor(z["grid"], device="cuda"),
+                        nsteps=torch.tensor(z["nsteps"], device="cuda"))
+    assert G.integrate_path(prob, spec) == path
+    ys, st = G.integrate(prob, spec, torch.tensor(z["y0"], dtype=torch.float32, device="cuda"), stats=True)
+    ref = z["ys"] if save == "steps" else z["ys"][:, -1]
+    err = rel_err(ys.cpu().numpy(), ref)
+    print(f"{name} [{path}] save={save}: rel err {err:.3e}")
+    assert err <= RTOL_SOLVE
+    st = st.cpu().numpy()
+    ns = z["nsteps"]
+    assert np.array_equal(st[:, 0], ns)
+    assert np.array_equal(st[:, 2], 4 * ns if method == G._lib.RK4 else 1 + 6 * ns)
+
+
+def test_interval_index_bit_exact(gncde):
+    rng = np.random.default_rng(7)
+    B, T = 5, 33
+    ts = np.sort(rng.uniform(0, 5, (B, T)), axis=1).astype(np.float32)
+    ts[:, 0], ts[:, -1] = 0.0, 5.0
+    tq, sq = [], []
+    for b in range(B):
+        tq += list(ts[b])                                               # exact knots
+        tq += list(rng.uniform(-0.5, 5.5, 40).astype(np.float32))       # interior + out of range
+        tq += list(np.nextafter(ts[b], np.float32(np.inf)))             # just right of knots
+        tq += list(np.nextafter(ts[b], np.float32(-np.inf)))            # just left of knots
+        sq += [b] * (len(tq) - len(sq))
+    tq = np.asarray(tq, dtype=np.float32)
+    sq = np.asarray(sq, dtype=np.int32)
+    got = gncde.interval_index(torch.tensor(ts, device="cuda"), torch.tensor(tq, device="cuda"),
+                               torch.tensor(sq, device="cuda")).cpu().numpy()
+    want = np.array([min(max(int(np.searchsorted(ts[s], t, side="left")) - 1, 0), T - 2)
+                     for t, s in zip(tq, sq)])
+    assert np.array_equal(got, want)
+
+
+def test_node_affine_matches_torch(gncde):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(7, 64, 5, generator=g).cuda()
+    W = torch.randn(16, 5, generator=g).cuda()
+    b = torch.randn(16, generator=g).cuda()
+    out = gncde.node_affine(x, W, b)
+    ref = x.double() @ W.double().T + b.double()
+    assert rel_err(out.cpu().numpy(), ref.cpu().numpy()) <= 1e-6
+
+
+# ---- BASELINE config-2 shape: n=64, h=16, L=3, RK4 100 steps --------------------------------------
+def config2(G, B, seed=1234, nsteps=100):
+    from gncde import synthetic
+    prob, y0, layers = synthetic.heat_batch(B, num_nodes=64, hidden=16, num_layers=3, seed=seed)
+    grids = [G.layout.rk4_grid(float(prob.ts[b, 0]), float(prob.ts[b, -1]), nsteps) for b in range(B)]
+    grid, ns = G.layout.stack_grids(grids)
+    spec = G.SolverSpec(method=G._lib.RK4, save_mode=G._lib.SAVE_T1, grid=grid, nsteps=ns)
+    return prob, spec, y0, O.VFParams("undirected", [{k: v.numpy() for k, v in lay.items()} for lay in layers])
+
+
+def test_config2_fused_vs_oracle_and_generic(gncde):
+    from gncde import synthetic
+    G = gncde
+    B = 8
+    prob, spec, y0, params = config2(G, B)
+    assert G.integrate_path(prob, spec) == "fused<64,16,3,rk4>"
+    ys = G.integrate(prob, spec, y0).cpu().numpy()
+    y0n = y0.cpu().numpy().astype(np.float64)
+    for b in (0, B - 1):
+        ts, coeffs = synthetic.to_reference_coeffs(prob, b)
+        ctrl = O.CubicInterpolation(ts, coeffs)
+        f = lambda t, y, ctrl=ctrl: O.vector_field(params, t, y, ctrl)  # noqa: E731
+        ref, _ = O.solve_fixed_grid(f, spec.grid[b].cpu().numpy(), y0n[b], "rk4", time_dtype=np.float32)
+        err = rel_err(ys[b], ref)
+        print(f"config2 sample {b}: rel err vs fp64 oracle {err:.3e}")
+        assert err <= RTOL_SOLVE
+    # the generic multi-kernel VF path agrees with the oracle at the same shape
+    t = (prob.ts[:, 7] + 0.01).contiguous()
+    yv = torch.randn(B, 64, 16, device="cuda")
+    dy = G.vf_eval(prob, t, yv).cpu().numpy()
+    for b in range(B):
+        ts, coeffs = synthetic.to_reference_coeffs(prob, b)
+        ref = O.vector_field(params, float(t[b]), yv[b].cpu().numpy().astype(np.float64),
+                             O.CubicInterpolation(ts, coeffs))
+        assert rel_err(dy[b], ref) <= RTOL_VF
+
+
+def test_config2_full_batch_properties(gncde):
+    """B=1024 (the BASELINE batch): permutation equivariance and run-to-run determinism."""
+    G = gncde
+    prob, spec, y0, _ = config2(G, 1024, seed=99, nsteps=25)
+    ys1 = G.integrate(prob, spec, y0)
+    ys2 = G.integrate(prob, spec, y0)
+    assert torch.equal(ys1, ys2)  # no atomics / order nondeterminism
+    assert torch.isfinite(ys1).all()
+    P = torch.randperm(64, generator=torch.Generator().manual_seed(0)).cuda()
+    probP = G.Problem(ts=prob.ts, coef=prob.coef[:, :, :, P][:, :, :, :, P].contiguous(),
+                      tcoef=prob.tcoef[..., P].contiguous(), fusion=prob.fusion, params=prob.params,
+                      dims=prob.dims)
+    ysP = G.integrate(probP, spec, y0[:, P].contiguous())
+    err = rel_err(ysP.cpu().numpy(), ys1[:, P].cpu().numpy())
+    print(f"permutation equivariance rel err {err:.3e}")
+    assert err <= RTOL_SOLVE

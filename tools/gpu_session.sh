@@ -1,0 +1,45 @@
+#!/bin/bash
+# Run GPU steps on the gpurun box; each step has its own time limit and the session stops at the first
+# crash / abort / timeout (exit 124, 134, 137, 139).  Usage: tools/gpu_session.sh STEP...
+#   tests  : pytest -m gpu
+#   smoke  : __graft_entry__.smoke()
+#   bench  : python bench.py (default args)
+#   prof   : rocprofv3 --kernel-trace --stats on bench.py (summary into gpurun_out/prof)
+#   pmc    : rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes (separate runs)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
+ROOTDIR=$(pwd)
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  case $rc in 124|134|137|139) echo "FATAL in $name: stopping"; exit $rc;; esac
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -q -s -x -p no:cacheprovider ;;
+    smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 900 python bench.py ;;
+    bench8) run bench_quick 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    prof) (cd /tmp && run_dir="$ROOTDIR/gpurun_out/prof" && rm -rf "$run_dir" && \
+           timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$run_dir" -o run -- \
+             python3 "$ROOTDIR/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$ROOTDIR/gpurun_out/prof.log" 2>&1; \
+           rc=$?; echo "prof rc=$rc"; tail -n 5 "$ROOTDIR/gpurun_out/prof.log"; \
+           case $rc in 124|134|137|139) exit $rc;; esac) || exit $? ;;
+    pmc) for ctr in FETCH_SIZE WRITE_SIZE; do
+           (cd /tmp && run_dir="$ROOTDIR/gpurun_out/pmc_$ctr" && rm -rf "$run_dir" && \
+            timeout -k 10 900 rocprofv3 --pmc $ctr --output-format csv -d "$run_dir" -o run -- \
+              python3 "$ROOTDIR/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$ROOTDIR/gpurun_out/pmc_$ctr.log" 2>&1; \
+            rc=$?; echo "pmc $ctr rc=$rc"; tail -n 3 "$ROOTDIR/gpurun_out/pmc_$ctr.log"; \
+            case $rc in 124|134|137|139) exit $rc;; esac) || exit $?
+         done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "session done"
