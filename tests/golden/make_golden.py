@@ -72,8 +72,8 @@ def vf_case(rng, name, B, n, T, kind, dims):
     np.savez_compressed(os.path.join(HERE, name), **out)
 
 
-def solve_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None):
-    ts, coeffs, params = problem(rng, B, n, T, kind, dims)
+def solve_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None, irregular=True):
+    ts, coeffs, params = problem(rng, B, n, T, kind, dims, irregular=irregular)
     y0 = rng.standard_normal((B, n, dims[0]))
     grids, ys = [], []
     for b in range(B):
@@ -134,7 +134,10 @@ def main():
     cde_case(rng, "cde_n12_h8_de3.npz", 3, 12, 5, 8, 3, 2)
     # widths differ between layers -> not covered by the fused kernel, exercises the generic solver
     solve_case(rng, "rk4_undirected_n12_mixed.npz", 2, 12, 7, "undirected", [16, 24, 16], "rk4", nsteps=8)
-    solve_case(rng, "tsit5c_plain_n20_mixed.npz", 2, 20, 6, "plain", [8, 12, 8], "tsit5", dt0=0.7)
+    # regular knots: with irregular knots 0.04 apart the cubic's d coefficients reach ~4e3 and any fp32
+    # Horner evaluation (the reference's too) loses ~1e-4 relative over the solve (ill-conditioned)
+    solve_case(rng, "tsit5c_plain_n20_mixed.npz", 2, 20, 6, "plain", [8, 12, 8], "tsit5", dt0=0.7,
+               irregular=False)
 
 
 if __name__ == "__main__":

@@ -93,9 +93,14 @@ def test_integrate_matches_golden(gncde, golden_dir, name, path, save):
     assert G.integrate_path(prob, spec) == path
     ys, st = G.integrate(prob, spec, torch.tensor(z["y0"], dtype=torch.float32, device="cuda"), stats=True)
     ref = z["ys"] if save == "steps" else z["ys"][:, -1]
-    err = rel_err(ys.cpu().numpy(), ref)
-    print(f"{name} [{path}] save={save}: rel err {err:.3e}")
-    assert err <= RTOL_SOLVE
+    got = ys.cpu().numpy()
+    err = rel_err(got, ref)
+    detail = ""
+    if save == "steps":
+        detail = " per-sample/step: " + str([[f"{rel_err(got[b, k], ref[b, k]):.1e}" for k in range(ref.shape[1])]
+                                             for b in range(ref.shape[0])])
+    print(f"{name} [{path}] save={save}: rel err {err:.3e}{detail}")
+    assert err <= RTOL_SOLVE, detail
     st = st.cpu().numpy()
     ns = z["nsteps"]
     assert np.array_equal(st[:, 0], ns)

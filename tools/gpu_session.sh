@@ -39,6 +39,17 @@ for step in "$@"; do
             rc=$?; echo "pmc $ctr rc=$rc"; tail -n 3 "$ROOTDIR/gpurun_out/pmc_$ctr.log"; \
             case $rc in 124|134|137|139) exit $rc;; esac) || exit $?
          done ;;
+    listctr) run listctr 300 rocprofv3 -L ;;
+    pmcsq) i=0; for ctrs in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT" \
+                          "SQ_INSTS_VALU_MFMA_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
+                          "TCC_HIT_sum TCC_MISS_sum"; do
+           i=$((i+1))
+           (cd /tmp && run_dir="$ROOTDIR/gpurun_out/pmcsq_$i" && rm -rf "$run_dir" && \
+            timeout -k 10 900 rocprofv3 --pmc $ctrs --output-format csv -d "$run_dir" -o run -- \
+              python3 "$ROOTDIR/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$ROOTDIR/gpurun_out/pmcsq_$i.log" 2>&1; \
+            rc=$?; echo "pmcsq $i rc=$rc"; tail -n 3 "$ROOTDIR/gpurun_out/pmcsq_$i.log"; \
+            case $rc in 124|134|137|139) exit $rc;; esac) || exit $?
+         done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
