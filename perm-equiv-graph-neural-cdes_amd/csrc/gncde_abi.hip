@@ -35,7 +35,10 @@ int validate_solver(const GncdeProblem* p, const GncdeSolver* s) {
     if (!s->grid || !s->nsteps || s->grid_len < 1) return GNCDE_ERR_ARG;
     if (s->save_mode == GNCDE_SAVE_TS) return GNCDE_ERR_UNSUPPORTED;
   } else if (s->controller == GNCDE_CTRL_PID) {
-    return GNCDE_ERR_UNSUPPORTED;
+    if (!s->t0 || !s->t1 || s->max_steps < 1) return GNCDE_ERR_ARG;
+    if (!(s->rtol >= 0.f) || !(s->atol > 0.f)) return GNCDE_ERR_ARG;
+    if (s->save_mode == GNCDE_SAVE_STEPS) return GNCDE_ERR_UNSUPPORTED;
+    if (s->save_mode == GNCDE_SAVE_TS && (!s->save_ts || s->n_save < 1)) return GNCDE_ERR_ARG;
   } else {
     return GNCDE_ERR_ARG;
   }

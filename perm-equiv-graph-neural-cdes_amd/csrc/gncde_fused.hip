@@ -62,7 +62,29 @@ struct FusedArgs {
   const float* y0;
   float* ys;
   int32_t* stats;
+  // adaptive (PID) controller
+  const float* t0;
+  const float* t1;
+  const float* dt0;  // NULL -> Hairer initial step (diffrax dt0=None)
+  const float* save_ts;
+  int n_save, max_steps;
+  float rtol, atol;
 };
+
+constexpr int kTsit5Pid = 2;  // internal METHOD id: Tsit5 + PIDController (diffrax defaults)
+
+// Tsit5 free interpolant weights b_i(theta): y(t + theta h) = y + h * sum_i b_i(theta) f_i
+// (restated in oracle/gncde_oracle.py:tsit5_dense_weights).
+__device__ __forceinline__ void tsit5_dense(float th, float (&w)[7]) {
+  const float t2 = th * th;
+  w[0] = -1.0530884977290216f * th * (th - 1.3299890189751412f) * (t2 - 1.4364028541716351f * th + 0.7139816917074209f);
+  w[1] = 0.1017f * t2 * (t2 - 2.1966568338249754f * th + 1.2949852507374631f);
+  w[2] = 2.490627285651252793f * t2 * (t2 - 2.38535645472061657f * th + 1.57803468208092486f);
+  w[3] = -16.54810288924490272f * (th - 1.21712927295533244f) * (th - 0.61620406037800089f) * t2;
+  w[4] = 47.37952196281928122f * (th - 1.203071208372362603f) * (th - 0.658047292653547382f) * t2;
+  w[5] = -34.87065786149660974f * (th - 1.2f) * (th - 0.666666666666666667f) * t2;
+  w[6] = 2.5f * (th - 1.0f) * (th - 0.6f) * t2;
+}
 
 // A(t)/dA(t) LDS images use a padded row stride NP+1: row AND column walks are bank-conflict free
 // and every address is lane base + compile-time offset (no per-element address registers).
@@ -77,7 +99,7 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 
 template <int NP, int H, int L, int METHOD>
 constexpr int min_waves_per_eu() {
-  constexpr int regs = L * (NP / 4) + (METHOD == GNCDE_TSIT5 ? 9 : 4) * (H / 4) + 4 * (H / 4) + 40;
+  constexpr int regs = L * (NP / 4) + (METHOD != GNCDE_RK4 ? 9 : 4) * (H / 4) + 4 * (H / 4) + 40;
   return NP >= 128 ? 2 : (regs > 120 ? 2 : 4);
 }
 
@@ -96,6 +118,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
   __shared__ float sTs[kTMax];
   __shared__ __attribute__((aligned(16))) float sPar[L * PL];
   __shared__ float sFus[L * GNCDE_FC];
+  __shared__ float sRed[2][NP / 16];  // per-wave partials for workgroup sums (double-buffered)
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -203,18 +226,28 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     {  // r, rd (row sums), c, cd (column sums), diagonals: 4 NP threads, one line each
       const int q = ftid / NP, j = ftid % NP;
       const float* M = (q & 1) ? sdA : sA;
-      float acc = 0.f;
+      float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;  // 4 chains: latency, not adds, bound this
       if (q < 2) {
         const float* row = M + swz<NP>(j, 0);
-#pragma unroll 16
-        for (int k = 0; k < NP; ++k) acc += row[k];
+#pragma unroll 4
+        for (int k = 0; k < NP; k += 4) {
+          acc0 += row[k];
+          acc1 += row[k + 1];
+          acc2 += row[k + 2];
+          acc3 += row[k + 3];
+        }
         sVec[(4 + q) * NP + j] = M[swz<NP>(j, j)];
       } else {
         const float* col = M + j;
-#pragma unroll 16
-        for (int k = 0; k < NP; ++k) acc += col[swz<NP>(k, 0)];
+#pragma unroll 4
+        for (int k = 0; k < NP; k += 4) {
+          acc0 += col[swz<NP>(k, 0)];
+          acc1 += col[swz<NP>(k + 1, 0)];
+          acc2 += col[swz<NP>(k + 2, 0)];
+          acc3 += col[swz<NP>(k + 3, 0)];
+        }
       }
-      sVec[q * NP + j] = acc;
+      sVec[q * NP + j] = (acc0 + acc1) + (acc2 + acc3);
     }
     __syncthreads();
     // v_l[k] = vR_A r_k + vR_dA rd_k + vC_A c_k + vC_dA cd_k  (zero for padded k: sums are zero)
@@ -368,14 +401,15 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       for (int r = 0; r < 4; ++r) dst[(size_t)node * H + 16 * fb + 4 * hi + r] = y[fb][r];
   };
 
+  const size_t E = (size_t)n * H;
+
+  // Single vf() call site per method (one inlined copy of form/eval keeps the register budget).
+  if constexpr (METHOD == GNCDE_RK4 || METHOD == GNCDE_TSIT5) {
   const int G = a.G;
   const float* g = a.grid + (size_t)b * G;
   int ns = a.nsteps[b];
   ns = ns < 0 ? 0 : (ns > G - 1 ? G - 1 : ns);  // never index past the grid row
-  const size_t E = (size_t)n * H;
   if (a.save_mode == GNCDE_SAVE_STEPS) store(a.ys + ((size_t)b * G) * E);
-
-  // Single vf() call site per method (one inlined copy of form/eval keeps the register budget).
   if constexpr (METHOD == GNCDE_RK4) {
     float K[FB][4], acc[FB][4], yt[FB][4];
     for (int k = 0; k < ns; ++k) {
@@ -471,7 +505,6 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       st = ns1;
     }
   }
-
   if (a.save_mode == GNCDE_SAVE_STEPS) {
     for (int k = ns + 1; k < G; ++k) store(a.ys + ((size_t)b * G + k) * E);
   } else {
@@ -482,6 +515,194 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     a.stats[b * 4 + GNCDE_STAT_REJECTS] = 0;
     a.stats[b * 4 + GNCDE_STAT_EVALS] = METHOD == GNCDE_RK4 ? 4 * ns : 1 + 6 * ns;
     a.stats[b * 4 + GNCDE_STAT_STATUS] = 0;
+  }
+  } else {
+    // ---- Tsit5 + PIDController(rtol, atol) (graph_neural_cde.py:53-54,94-104; diffrax defaults:
+    // pcoeff 0, icoeff 1, dcoeff 0, safety 0.9, factormin 0.2 (1 on accept), factormax 10, RMS norm,
+    // error order 5), FSAL, optional Hairer initial step (dt0 = None), SaveAt(ts) via the Tsit5
+    // dense interpolant or SaveAt(t1).  Every wave follows the same (uniform) control flow.
+    int wsel = 0;
+    const float inv_cnt = 1.0f / (float)(n * H);
+    auto wg_sum = [&](float v) __attribute__((always_inline)) -> float {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      wsel ^= 1;
+      if (lane == 0) sRed[wsel][w] = v;
+      __syncthreads();
+      float tot = 0.f;
+#pragma unroll
+      for (int j = 0; j < NP / 16; ++j) tot += sRed[wsel][j];
+      return tot;
+    };
+    const float rtol = a.rtol, atol = a.atol;
+    const float t0 = a.t0[b], t1 = a.t1[b];
+    const int S = a.save_mode == GNCDE_SAVE_TS ? a.n_save : 0;
+    const float* sts = a.save_ts ? a.save_ts + (size_t)b * S : nullptr;
+    float* ysb = a.ys + (size_t)b * (S > 0 ? S : 1) * E;
+    int si = 0;
+    while (si < S && sts[si] <= t0) store(ysb + (size_t)(si++) * E);
+    float kk[7][FB][4], yt[FB][4], K[FB][4];
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) kk[j][fb][r] = 0.f;
+#pragma unroll
+    for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) yt[fb][r] = y[fb][r];
+    const bool auto_dt = a.dt0 == nullptr;
+    float dt = auto_dt ? 0.f : a.dt0[b];
+    float t = t0, tn = t0, h = 0.f, tst = t0, h0 = 0.f, d1 = 0.f;
+    int phase = 0, st = 0, steps = 0, rejects = 0, evals = 0, status = 0;
+    while (true) {
+      vf(tst, yt, K);
+      ++evals;
+      if (phase == 0) {  // f(t0, y0): FSAL k1 (and f0 of the initial-step heuristic)
+#pragma unroll
+        for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) kk[0][fb][r] = K[fb][r];
+        phase = 2;
+        if (auto_dt) {
+          float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+          for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float sc = fmaf(fabsf(y[fb][r]), rtol, atol);
+              const float u = y[fb][r] / sc, v = K[fb][r] / sc;
+              p0 = node_ok ? fmaf(u, u, p0) : p0;
+              p1 = node_ok ? fmaf(v, v, p1) : p1;
+            }
+          const float d0 = sqrtf(wg_sum(p0) * inv_cnt);
+          d1 = sqrtf(wg_sum(p1) * inv_cnt);
+          h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : 0.01f * (d0 / d1);
+#pragma unroll
+          for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) yt[fb][r] = fmaf(h0, K[fb][r], y[fb][r]);
+          tst = t0 + h0;
+          phase = 1;
+          continue;
+        }
+      } else if (phase == 1) {  // f(t0 + h0, y0 + h0 f0)
+        float p2 = 0.f;
+#pragma unroll
+        for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float sc = fmaf(fabsf(y[fb][r]), rtol, atol);
+            const float v = (K[fb][r] - kk[0][fb][r]) / sc;
+            p2 = node_ok ? fmaf(v, v, p2) : p2;
+          }
+        const float d2 = sqrtf(wg_sum(p2) * inv_cnt) / h0;
+        const float md = fmaxf(d1, d2);
+        const float h1 = md <= 1e-15f ? fmaxf(1e-6f, h0 * 1e-3f) : powf(0.01f / md, 0.2f);
+        dt = fminf(100.0f * h0, h1);
+        phase = 2;
+      } else {
+#pragma unroll
+        for (int j = 1; j < 7; ++j)
+          if (j == st)
+#pragma unroll
+            for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) kk[j][fb][r] = K[fb][r];
+        if (st == 6) {  // attempt done: yt = y1 candidate, kk[6] = f(tn, y1)
+          float pe = 0.f;
+#pragma unroll
+          for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float e = h * (TSIT5_E1 * kk[0][fb][r] + TSIT5_E2 * kk[1][fb][r] + TSIT5_E3 * kk[2][fb][r] +
+                                   TSIT5_E4 * kk[3][fb][r] + TSIT5_E5 * kk[4][fb][r] + TSIT5_E6 * kk[5][fb][r] +
+                                   TSIT5_E7 * kk[6][fb][r]);
+              const float sc = fmaf(fmaxf(fabsf(y[fb][r]), fabsf(yt[fb][r])), rtol, atol);
+              const float v = e / sc;
+              pe = node_ok ? fmaf(v, v, pe) : pe;
+            }
+          const float err = sqrtf(wg_sum(pe) * inv_cnt);
+          const bool finite = isfinite(err);
+          const bool keep = finite && err < 1.0f;
+          float factor;
+          if (!finite) {
+            factor = 0.2f;
+          } else {
+            const float f1 = err == 0.f ? 10.0f : 0.9f * powf(1.0f / err, 0.2f);
+            factor = fminf(fmaxf(f1, keep ? 1.0f : 0.2f), 10.0f);
+          }
+          if (keep) {
+            while (si < S && sts[si] <= tn) {  // dense output inside (t, tn]
+              float wts[7];
+              tsit5_dense((sts[si] - t) / h, wts);
+              if (node_ok) {
+                float* dst = ysb + (size_t)si * E;
+#pragma unroll
+                for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 7; ++j) acc = fmaf(wts[j], kk[j][fb][r], acc);
+                    dst[(size_t)node * H + 16 * fb + 4 * hi + r] = fmaf(h, acc, y[fb][r]);
+                  }
+              }
+              ++si;
+            }
+#pragma unroll
+            for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                y[fb][r] = yt[fb][r];
+                kk[0][fb][r] = kk[6][fb][r];
+              }
+            t = tn;
+            ++steps;
+          } else {
+            ++rejects;
+          }
+          dt = factor * h;
+          st = 0;
+        }
+      }
+      if (st == 0) {  // start a new attempt
+        if (!(t < t1)) break;
+        if (steps + rejects >= a.max_steps) {
+          status = 1;
+          break;
+        }
+        tn = t + dt;
+        if (tn > t1 - 1e-6f) tn = t1;  // diffrax _clip_to_end
+        h = tn - t;
+      }
+      const int ns1 = st + 1;
+      float arow[6], cst;
+      tsit5_row(ns1, arow, cst);
+#pragma unroll
+      for (int fb = 0; fb < FB; ++fb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float sacc = 0.f;
+#pragma unroll
+          for (int j = 0; j < 6; ++j) sacc = fmaf(arow[j], kk[j][fb][r], sacc);
+          yt[fb][r] = fmaf(h, sacc, y[fb][r]);
+        }
+      tst = ns1 >= 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);
+      st = ns1;
+    }
+    if (S == 0) {
+      store(ysb);
+    } else {
+      while (si < S) store(ysb + (size_t)(si++) * E);  // only reached on failure (status != 0)
+    }
+    if (a.stats && tid == 0) {
+      a.stats[b * 4 + GNCDE_STAT_STEPS] = steps;
+      a.stats[b * 4 + GNCDE_STAT_REJECTS] = rejects;
+      a.stats[b * 4 + GNCDE_STAT_EVALS] = evals;
+      a.stats[b * 4 + GNCDE_STAT_STATUS] = status;
+    }
   }
 }
 
@@ -494,7 +715,8 @@ struct FusedEntry {
 
 #define GNCDE_FUSED(NP, H, L)                                        \
   {NP, H, L, GNCDE_RK4, k_fused<NP, H, L, GNCDE_RK4>},             \
-  {NP, H, L, GNCDE_TSIT5, k_fused<NP, H, L, GNCDE_TSIT5>}
+  {NP, H, L, GNCDE_TSIT5, k_fused<NP, H, L, GNCDE_TSIT5>},         \
+  {NP, H, L, kTsit5Pid, k_fused<NP, H, L, kTsit5Pid>}
 
 const FusedEntry kFused[] = {
     GNCDE_FUSED(16, 16, 1),  GNCDE_FUSED(16, 16, 2),  GNCDE_FUSED(16, 16, 3),  GNCDE_FUSED(16, 16, 4),
@@ -509,8 +731,14 @@ const FusedEntry kFused[] = {
 
 const FusedEntry* find_fused(const GncdeProblem& p, const GncdeSolver& s) {
   if (p.cde_hidden != 0) return nullptr;
-  if (s.controller != GNCDE_CTRL_GRID) return nullptr;
-  if (s.save_mode != GNCDE_SAVE_T1 && s.save_mode != GNCDE_SAVE_STEPS) return nullptr;
+  int method = s.method;
+  if (s.controller == GNCDE_CTRL_GRID) {
+    if (s.save_mode != GNCDE_SAVE_T1 && s.save_mode != GNCDE_SAVE_STEPS) return nullptr;
+  } else {  // PID: Tsit5 only (the reference's adaptive configuration)
+    if (s.method != GNCDE_TSIT5) return nullptr;
+    if (s.save_mode != GNCDE_SAVE_T1 && s.save_mode != GNCDE_SAVE_TS) return nullptr;
+    method = kTsit5Pid;
+  }
   if (p.T > kTMax) return nullptr;
   const int H = p.dims[0];
   for (int l = 1; l <= p.L; ++l)
@@ -523,7 +751,7 @@ const FusedEntry* find_fused(const GncdeProblem& p, const GncdeSolver& s) {
     }
   if (np == 0) return nullptr;
   for (const FusedEntry& e : kFused)
-    if (e.np == np && e.h == H && e.l == p.L && e.method == s.method) return &e;
+    if (e.np == np && e.h == H && e.l == p.L && e.method == method) return &e;
   return nullptr;
 }
 
@@ -534,7 +762,7 @@ bool fused_supported(const GncdeProblem& p, const GncdeSolver& s, char* name, si
   if (!e) return false;
   if (name && name_len)
     snprintf(name, name_len, "fused<%d,%d,%d,%s>", e->np, e->h, e->l,
-             e->method == GNCDE_RK4 ? "rk4" : "tsit5");
+             e->method == GNCDE_RK4 ? "rk4" : (e->method == GNCDE_TSIT5 ? "tsit5" : "tsit5_pid"));
   return true;
 }
 
@@ -558,6 +786,14 @@ int fused_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0
   a.y0 = y0;
   a.ys = ys;
   a.stats = stats;
+  a.t0 = s.t0;
+  a.t1 = s.t1;
+  a.dt0 = s.dt0;
+  a.save_ts = s.save_ts;
+  a.n_save = s.n_save;
+  a.max_steps = s.max_steps;
+  a.rtol = s.rtol;
+  a.atol = s.atol;
   hipLaunchKernelGGL(e->fn, dim3(p.B), dim3(e->np * 4), 0, st, a);
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }

@@ -97,6 +97,31 @@ def solve_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None, ir
     np.savez_compressed(os.path.join(HERE, name), **out)
 
 
+def pid_case(rng, name, B, n, T, kind, dims, rtol=1e-3, atol=1e-6, dt0=None):
+    """Tsit5 + PIDController, SaveAt(ts=ts) — the GraphNeuralCDE solve (graph_neural_cde.py:94-104)."""
+    ts, coeffs, params = problem(rng, B, n, T, kind, dims)
+    y0 = rng.standard_normal((B, n, dims[0]))
+    ys, st, truth = [], [], []
+    for b in range(B):
+        ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
+        f = lambda t, y, ctrl=ctrl: O.vector_field(params, t, y, ctrl)  # noqa: E731
+        out, stats = O.solve_tsit5_pid(f, ts[b, 0], ts[b, -1], y0[b], rtol=rtol, atol=atol, dt0=dt0,
+                                       save_ts=ts[b])
+        ys.append(out)
+        st.append([stats["steps"], stats["rejects"], stats["evals"]])
+        # near-exact solution: the adaptive step sequence is chaotic in the last bits (a 1e-4 relative
+        # change of rtol moves the output by ~1e-2), so parity is judged by accuracy against this
+        tr, _ = O.solve_tsit5_pid(f, ts[b, 0], ts[b, -1], y0[b], rtol=1e-10, atol=1e-12, save_ts=ts[b],
+                                  max_steps=200000)
+        truth.append(tr)
+    out = dict(ts=ts, d=coeffs[0], c=coeffs[1], b=coeffs[2], a=coeffs[3], y0=y0, ys=np.stack(ys),
+               truth=np.stack(truth),
+               stats=np.array(st), rtol=np.array(rtol), atol=np.array(atol),
+               dt0=np.array(np.nan if dt0 is None else dt0))
+    flat_layers("", params, out)
+    np.savez_compressed(os.path.join(HERE, name), **out)
+
+
 def cde_case(rng, name, B, n, T, h, de, L):
     dims = [h] + [h] * (L - 1) + [h * de * 2]
     ts, coeffs, params = problem(rng, B, n, T, "undirected", dims)
@@ -138,6 +163,8 @@ def main():
     # Horner evaluation (the reference's too) loses ~1e-4 relative over the solve (ill-conditioned)
     solve_case(rng, "tsit5c_plain_n20_mixed.npz", 2, 20, 6, "plain", [8, 12, 8], "tsit5", dt0=0.7,
                irregular=False)
+    pid_case(rng, "pid_undirected_n16_L2.npz", 3, 16, 10, "undirected", [16, 16, 16])
+    pid_case(rng, "pid_directed_n12_L3_dt0.npz", 2, 12, 8, "directed", [16, 16, 16, 16], dt0=0.05)
 
 
 if __name__ == "__main__":
