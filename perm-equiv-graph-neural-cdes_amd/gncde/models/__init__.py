@@ -1,0 +1,212 @@
+"""Solve drivers mirroring ``src/models/{graph,pgt,tgb}_graph_neural_cde.py``.
+
+Same constructor arguments ``(cfg, vector_field, interpolation, model_key)`` and single-sample
+``__call__`` signatures as the reference; every call is a batch-of-one instance of ``batched(...)``,
+which replaces ``jax.vmap(model)`` (``loss_configs.py:44``) with one ``gncde_integrate`` launch over
+the whole batch.  Encoders / read-outs run on ``gncde_node_affine`` (+ ReLU for the MLPs).
+"""
+from __future__ import annotations
+
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+from torch import nn
+
+from .. import _lib, engine, layout
+from ..interpolation import CubicInterpolation
+from ..synthetic import hermite_coefficients
+from . import vector_fields
+from .vector_fields.layers import _gen
+
+__all__ = ["GraphNeuralCDE", "PGTGraphNeuralCDE", "TGBGraphNeuralCDE", "MLP", "vector_fields"]
+
+
+def _linear(din, dout, g):
+    lin = nn.Linear(din, dout)
+    lim = 1.0 / din ** 0.5
+    with torch.no_grad():
+        lin.weight.copy_((2 * torch.rand(dout, din, generator=g) - 1) * lim)
+        lin.bias.copy_((2 * torch.rand(dout, generator=g) - 1) * lim)
+    return lin
+
+
+def _affine(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    return engine.node_affine(x, lin.weight.detach().to(x.device), lin.bias.detach().to(x.device))
+
+
+class MLP(nn.Module):
+    """``eqx.nn.MLP(in, out, width_size, depth)``: Linear -> ReLU -> ... -> Linear."""
+
+    def __init__(self, in_size, out_size, width_size=16, depth=2, key=None):
+        super().__init__()
+        g = _gen(key)
+        dims = [in_size] + [width_size] * depth + [out_size]
+        self.layers = nn.ModuleList(_linear(dims[i], dims[i + 1], g) for i in range(len(dims) - 1))
+
+    def run(self, x):
+        for i, lin in enumerate(self.layers):
+            x = _affine(lin, x)
+            if i < len(self.layers) - 1:
+                x = torch.relu(x)
+        return x
+
+
+def _cfg(cfg, **defaults):
+    if cfg is None:
+        return SimpleNamespace(**defaults)
+    if isinstance(cfg, dict):
+        d = dict(defaults)
+        d.update(cfg)
+        return SimpleNamespace(**d)
+    return cfg
+
+
+def _as_batched_coeffs(coeffs, batched):
+    return coeffs if batched else tuple(torch.as_tensor(np.asarray(c) if not torch.is_tensor(c) else c)
+                                        .unsqueeze(0) for c in coeffs)
+
+
+class GraphNeuralCDE(nn.Module):
+    """``graph_neural_cde.py:12-113``: Linear(1->h) encoder, Tsit5 + PIDController(1e-3, 1e-6),
+    dt0=None, SaveAt(ts) (evolving_out) or SaveAt(t1), Linear(h->1) read-out per node.
+
+    ``solver`` (build extension, BASELINE config 2) may override the reference solve:
+    {"method": "rk4"|"tsit5", "steps": N} for a fixed grid of N steps on [ts[0], ts[-1]].
+    """
+
+    def __init__(self, cfg, vector_field, interpolation="cubic", model_key=None, solver=None, **kwargs):
+        super().__init__()
+        self.cfg = _cfg(cfg, hidden_dim=16, method="Tsit5", return_sequence=True)
+        if interpolation != "cubic":
+            raise NotImplementedError("only cubic (backward-Hermite) controls are on the hot path")
+        if getattr(self.cfg, "method", "Tsit5") != "Tsit5":
+            raise NotImplementedError(f"method {self.cfg.method}: only Tsit5 (explicit) is implemented")
+        self.vector_field = vector_field
+        self.interpolation = interpolation
+        g = _gen(model_key)
+        self.initial_linear = _linear(1, self.cfg.hidden_dim, g)
+        self.final_linear = _linear(self.cfg.hidden_dim, 1, g)
+        self.rtol, self.atol = 1e-3, 1e-6
+        self.solver = solver
+
+    def _spec(self, ts: torch.Tensor, evolving_out: bool) -> engine.SolverSpec:
+        if self.solver is None:
+            return engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_PID,
+                                     save_mode=_lib.SAVE_TS if evolving_out else _lib.SAVE_T1,
+                                     rtol=self.rtol, atol=self.atol, t0=ts[:, 0].contiguous(),
+                                     t1=ts[:, -1].contiguous(), save_ts=ts.contiguous() if evolving_out else None)
+        method = _lib.RK4 if self.solver.get("method", "rk4") == "rk4" else _lib.TSIT5
+        tsn = ts.cpu().numpy()
+        grids = [layout.rk4_grid(t[0], t[-1], int(self.solver["steps"])) for t in tsn]
+        grid, ns = layout.stack_grids(grids, device=ts.device)
+        return engine.SolverSpec(method=method, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_T1, grid=grid,
+                                 nsteps=ns)
+
+    def batched(self, ts, coeffs_adj, x0, evolving_out=True, return_stats=False):
+        """ts [B, T], coeffs_adj (d, c, b, a) each [B, T-1, n, n, 2], x0 [B, n, 1] -> [B, T, n, 1]
+        (evolving_out & return_sequence) or [B, n, 1]."""
+        control = CubicInterpolation(ts, coeffs_adj)
+        ts_d = control.graph_layout()[0]
+        x0 = torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device)
+        y0 = _affine(self.initial_linear, x0)
+        prob = self.vector_field.problem(control)
+        spec = self._spec(ts_d, evolving_out)
+        if self.solver is not None and evolving_out:
+            raise NotImplementedError("fixed-grid solver override saves at t1 only")
+        ys, st = engine.integrate(prob, spec, y0, stats=True)
+        if torch.any(st[:, _lib.STAT_STATUS] != 0):
+            raise RuntimeError("diffrax-equivalent failure: max_steps reached or non-finite state")
+        out = _affine(self.final_linear, ys)
+        return (out, st) if return_stats else out
+
+    def __call__(self, ts, coeffs_adj, x0, evolving_out=True):
+        ts = torch.as_tensor(np.asarray(ts) if not torch.is_tensor(ts) else ts, dtype=torch.float32)
+        out = self.batched(ts.unsqueeze(0), _as_batched_coeffs(coeffs_adj, False),
+                           torch.as_tensor(x0).unsqueeze(0), evolving_out)
+        return out[0]
+
+
+class PGTGraphNeuralCDE(nn.Module):
+    """``pgt_graph_neural_cde.py:13-136``: MLP encoder (data_dim -> h), CDEWrapper(vf) against the
+    node-data spline, Tsit5 + ConstantStepSize(dt0 = 0.1), SaveAt(t1), MLP decoder, global sum read-out."""
+
+    def __init__(self, cfg, vector_field, interpolation="cubic", model_key=None, dt0=0.1, **kwargs):
+        super().__init__()
+        self.cfg = _cfg(cfg, hidden_dim=64, data_dim=8, feature_dim=1, method="Tsit5")
+        self.vector_field = vector_field
+        self.interpolation = interpolation
+        g = _gen(model_key)
+        enc_state = g.get_state()
+        self.encoder = MLP(self.cfg.data_dim, self.cfg.hidden_dim, 16, 2, key=g)
+        g.set_state(enc_state)  # pgt_graph_neural_cde.py:62: the decoder is built with encoder_key
+        self.decoder = MLP(self.cfg.hidden_dim, self.cfg.feature_dim, 16, 2, key=g)
+        self.wrapped_vector_field = vector_fields.CDEWrapperVectorField(vector_field, self.cfg.hidden_dim)
+        self.dt0 = dt0
+
+    def batched(self, ts, coeffs_adj, x_coeffs, x0, evolving_out=False, global_readout=True):
+        if evolving_out:
+            raise NotImplementedError("PGT drivers save at t1 (pgt_graph_neural_cde.py:116-117)")
+        control_adj = CubicInterpolation(ts, coeffs_adj)
+        control_data = CubicInterpolation(ts, x_coeffs)
+        ts_d = control_adj.graph_layout()[0]
+        y0 = self.encoder.run(torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device))
+        prob = self.wrapped_vector_field.problem(control_adj, control_data)
+        grids = [layout.constant_step_grid(t[0], t[-1], self.dt0) for t in ts_d.cpu().numpy()]
+        grid, ns = layout.stack_grids(grids, device=ts_d.device)
+        spec = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_T1, grid=grid,
+                                 nsteps=ns)
+        yT = engine.integrate(prob, spec, y0)
+        out = self.decoder.run(yT)
+        return out.sum(dim=1) if global_readout else out
+
+    def __call__(self, ts, coeffs_adj, x_coeffs, x0, evolving_out=False, global_readout=True):
+        ts = torch.as_tensor(np.asarray(ts) if not torch.is_tensor(ts) else ts, dtype=torch.float32)
+        return self.batched(ts.unsqueeze(0), _as_batched_coeffs(coeffs_adj, False),
+                            _as_batched_coeffs(x_coeffs, False), torch.as_tensor(x0).unsqueeze(0),
+                            evolving_out, global_readout)[0]
+
+
+class TGBGraphNeuralCDE(nn.Module):
+    """``tgb_graph_neural_cde.py:13-171``: data spline built inside forward from Linear(n -> de) embeddings
+    of the adjacency rows, Linear(n -> h) encoder, CDEWrapper(vf), Tsit5 + ConstantStepSize(dt0 = 0.01),
+    Linear(h -> n) decoder per node."""
+
+    def __init__(self, cfg, vector_field, interpolation="cubic", model_key=None, dt0=0.01, **kwargs):
+        super().__init__()
+        self.cfg = _cfg(cfg, hidden_dim=32, method="Tsit5", return_sequence=False, use_mlps=False)
+        if getattr(self.cfg, "use_mlps", False):
+            raise NotImplementedError("use_mlps=True variant not on the hot path")
+        self.vector_field = vector_field
+        n, de = vector_field.num_nodes, vector_field.data_embed_dim
+        g = _gen(model_key)
+        enc_state = g.get_state()
+        self.encoder = _linear(n, self.cfg.hidden_dim, g)
+        self.decoder = _linear(self.cfg.hidden_dim, n, g)
+        g.set_state(enc_state)  # tgb_graph_neural_cde.py:86-89: data_encoder reuses encoder_key
+        self.data_encoder = _linear(n, de, g)
+        self.wrapped_vector_field = vector_fields.CDEWrapperVectorField(vector_field, self.cfg.hidden_dim)
+        self.dt0 = dt0
+
+    def batched(self, ts, coeffs_adj, x_data, x0, start_time=None, evolving_out=False):
+        if evolving_out:
+            raise NotImplementedError("SaveAt(ts) with ConstantStepSize (dense output) is not implemented")
+        control_adj = CubicInterpolation(ts, coeffs_adj)
+        ts_d = control_adj.graph_layout()[0]
+        xd = _affine(self.data_encoder, torch.as_tensor(x_data, dtype=torch.float32, device=ts_d.device))
+        X = torch.stack([ts_d[:, :, None, None].expand_as(xd), xd], dim=-1)  # [B, T, n, de, 2]
+        control_data = CubicInterpolation(ts_d, hermite_coefficients(ts_d, X))
+        y0 = _affine(self.encoder, torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device))
+        prob = self.wrapped_vector_field.problem(control_adj, control_data)
+        grids = [layout.constant_step_grid(t[0], t[-1], self.dt0) for t in ts_d.cpu().numpy()]
+        grid, ns = layout.stack_grids(grids, device=ts_d.device)
+        spec = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_T1, grid=grid,
+                                 nsteps=ns)
+        ys = engine.integrate(prob, spec, y0)
+        return _affine(self.decoder, ys)
+
+    def __call__(self, ts, coeffs_adj, x_data, x0, start_time=None, evolving_out=False):
+        ts = torch.as_tensor(np.asarray(ts) if not torch.is_tensor(ts) else ts, dtype=torch.float32)
+        return self.batched(ts.unsqueeze(0), _as_batched_coeffs(coeffs_adj, False),
+                            torch.as_tensor(x_data).unsqueeze(0), torch.as_tensor(x0).unsqueeze(0),
+                            start_time, evolving_out)[0]

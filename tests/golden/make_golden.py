@@ -101,7 +101,7 @@ def pid_case(rng, name, B, n, T, kind, dims, rtol=1e-3, atol=1e-6, dt0=None):
     """Tsit5 + PIDController, SaveAt(ts=ts) — the GraphNeuralCDE solve (graph_neural_cde.py:94-104)."""
     ts, coeffs, params = problem(rng, B, n, T, kind, dims)
     y0 = rng.standard_normal((B, n, dims[0]))
-    ys, st, truth = [], [], []
+    ys, st, truth, ens = [], [], [], []
     for b in range(B):
         ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
         f = lambda t, y, ctrl=ctrl: O.vector_field(params, t, y, ctrl)  # noqa: E731
@@ -114,8 +114,14 @@ def pid_case(rng, name, B, n, T, kind, dims, rtol=1e-3, atol=1e-6, dt0=None):
         tr, _ = O.solve_tsit5_pid(f, ts[b, 0], ts[b, -1], y0[b], rtol=1e-10, atol=1e-12, save_ts=ts[b],
                                   max_steps=200000)
         truth.append(tr)
+        # accuracy spread of the reference algorithm itself: rtol perturbed by +-1e-4 relative
+        for scale in (1 - 1e-4, 1 + 1e-4):
+            pe, _ = O.solve_tsit5_pid(f, ts[b, 0], ts[b, -1], y0[b], rtol=rtol * scale, atol=atol, dt0=dt0,
+                                      save_ts=ts[b])
+            ens.append(np.max(np.abs(pe - tr)) / np.max(np.abs(tr)))
+        ens.append(np.max(np.abs(out - tr)) / np.max(np.abs(tr)))
     out = dict(ts=ts, d=coeffs[0], c=coeffs[1], b=coeffs[2], a=coeffs[3], y0=y0, ys=np.stack(ys),
-               truth=np.stack(truth),
+               truth=np.stack(truth), ens_err=np.array(max(ens)),
                stats=np.array(st), rtol=np.array(rtol), atol=np.array(atol),
                dt0=np.array(np.nan if dt0 is None else dt0))
     flat_layers("", params, out)

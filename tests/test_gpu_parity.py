@@ -4,7 +4,7 @@ Tolerances (fp32 kernel vs fp64 oracle, relative to the max magnitude of the ref
   * one vector-field evaluation:   RTOL_VF    = 2e-5
   * a fixed-grid solve trajectory: RTOL_SOLVE = 1e-4   (error accumulates over the steps)
   * interval index / fixed-grid step counts: bit-exact
-  * Tsit5+PID: accuracy vs a near-exact solve within ACC_PID_FACTOR of the oracle's own accuracy
+  * Tsit5+PID: accuracy vs a near-exact solve within ACC_PID_FACTOR of the oracle's own accuracy spread
 """
 import os
 
@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 RTOL_VF = 2e-5
 RTOL_SOLVE = 1e-4
-ACC_PID_FACTOR = 3.0  # adaptive solve: GPU error vs the near-exact solution <= 3x the oracle's error
+ACC_PID_FACTOR = 2.0  # adaptive solve: GPU error vs near-exact <= 2x the worst oracle solve (rtol +-1e-4)
 
 
 def rel_err(x, ref):
@@ -145,7 +145,7 @@ def test_integrate_pid_matches_golden(gncde, golden_dir, name, save):
         assert err <= RTOL_SOLVE  # same decisions: fp32 rounding only
     # otherwise the step sequences diverged (chaotic in the last bits): the GPU solve must be as
     # accurate as the reference algorithm's own solve at the same tolerances
-    assert acc_gpu <= ACC_PID_FACTOR * acc_oracle
+    assert acc_gpu <= ACC_PID_FACTOR * float(z["ens_err"])
     assert np.all(np.abs(st[:, 0] - z["stats"][:, 0]) <= 0.25 * z["stats"][:, 0])
 
 
