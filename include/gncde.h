@@ -145,10 +145,40 @@ int gncde_vf_eval(const GncdeProblem* prob, const float* t, const float* y, floa
 int gncde_integrate(const GncdeProblem* prob, const GncdeSolver* solver, const float* y0, float* ys,
                     int32_t* stats, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Reverse mode of gncde_integrate for the GRID controller (the discrete adjoint that
+ * jax.value_and_grad through diffrax.diffeqsolve's RecursiveCheckpointAdjoint computes:
+ * trainer.py:315 over graph_neural_cde.py:94-104 / pgt_graph_neural_cde.py:84-93).
+ *   ys:  [B, G, n, d_s] the forward's SAVE_STEPS states (the checkpoints; y_0 .. y_G-1)
+ *   gys: cotangents of the forward's outputs in solver->save_mode layout: SAVE_T1 [B, n, d_s] (cotangent
+ *        of the final state) or SAVE_STEPS [B, G, n, d_s]
+ *   gy0:     [B, n, d_s]  cotangent of y0
+ *   gparams: [P]          sum over samples of the cotangent of prob->params (packed layout above)
+ *   gfusion: [L, GNCDE_FC] sum over samples of the cotangent of the fusion table
+ * Deterministic (fixed reduction order, no atomics).  Workspace: gncde_vjp_workspace_bytes. */
+size_t gncde_vjp_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* solver);
+int gncde_integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
+                        float* gy0, float* gparams, float* gfusion, void* workspace, size_t workspace_bytes,
+                        void* stream);
+
 /* Per-node affine map out[r, :] = W @ x[r, :] + b for `rows` rows.  x: [rows, din], W: [dout, din],
  * b: [dout] (may be NULL), out: [rows, dout]. */
 int gncde_node_affine(int32_t rows, int32_t din, int32_t dout, const float* x, const float* W,
                       const float* b, float* out, void* stream);
+
+/* Reverse mode of gncde_node_affine (encoders / read-outs, graph_neural_cde.py:87,106-111):
+ *   gx[r, :] = W^T g[r, :]  (gx may be NULL);  gW = sum_r g[r]^T x[r]  (may be NULL);  gb = sum_r g[r]  (may be NULL).
+ * g: [rows, dout].  Deterministic. */
+int gncde_node_affine_grad(int32_t rows, int32_t din, int32_t dout, const float* x, const float* W,
+                           const float* g, float* gx, float* gW, float* gb, void* stream);
+
+/* One optimiser update over a flat fp32 parameter buffer: optax.chain(clip_by_global_norm(max_norm),
+ * adamw(lr, b1, b2, eps, weight_decay)) as built by optimiser_configs.py:70-88 (max_norm <= 0: no clipping).
+ * step is the 1-based update count (bias correction).  stats[3] (device): global grad norm, max|grad|,
+ * max|update| (the values trainer.py:318-326 logs).  Workspace: gncde_adamw_workspace_bytes(P). */
+size_t gncde_adamw_workspace_bytes(int32_t P);
+int gncde_clip_adamw(int32_t P, float* params, const float* grads, float* m, float* v, int32_t step, float lr,
+                     float b1, float b2, float eps, float weight_decay, float max_norm, float* stats,
+                     void* workspace, size_t workspace_bytes, void* stream);
 
 /* idx[k] = clip(searchsorted(ts[b], t[k], 'left') - 1, 0, T-2) with b = sample[k].
  * ts: [B, T], t: [count], sample: [count] int32, idx: [count] int32. */

@@ -1,0 +1,194 @@
+"""CPU oracle for the reverse mode of the GNCDE hot path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/`` (and the golden-fixture generator) may import this module, as the checker.
+
+What it is
+    A hand-written numpy (float64) reverse mode of ``oracle.gncde_oracle``'s forward, i.e. of what
+    ``jax.value_and_grad`` computes for the reference's training step (``src/train/trainer.py:315``):
+
+    * the vector field's VJP — ConvLayer (layers.py:36-48: RMSNorm -> Linear -> m + Abar m), the ReLU
+      between layers (perm_equiv_graph_vector_field.py:117-121), the time-channel scaling (:127) and the
+      CDE wrapper contraction (cde_wrapper_vector_field.py:19-26).  The fusion matrices are used in their
+      LITERAL reference form (oracle.fusion_undirected/directed/plain, quirks included): each fusion
+      parameter's gradient is <dL/dAbar, dAbar/dparam>, with dAbar/dparam obtained by evaluating the
+      literal fusion with a unit parameter (the fusion is affine in its parameters).
+    * the discrete adjoint of the fixed-grid RK4 / Tsit5 solve — what diffrax's default
+      RecursiveCheckpointAdjoint differentiates (graph_neural_cde.py:94-104, pgt_graph_neural_cde.py:119-129).
+
+PARITY: jax is not installed, so this cannot be compared with jax.grad itself.  It is pinned instead by
+central finite differences of the fp64 forward oracle (tests/test_oracle_grad.py), which checks the
+restatement independently of how it was derived.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import gncde_oracle as O
+
+FUSION_NAMES = {"undirected": O.UNDIRECTED_PARAMS, "directed": O.DIRECTED_PARAMS, "plain": ()}
+
+
+def _fusion_basis(kind, lay, A, dA):
+    """{(name, j): dAbar/dparam[name][j]} for the literal fusion of ``kind`` (affine in the params)."""
+    names = FUSION_NAMES[kind]
+    if not names:
+        return {}
+    zero = {nm: np.zeros(2) for nm in names}
+    f = O.fusion_undirected if kind == "undirected" else O.fusion_directed
+    base = f(zero, A, dA)
+    out = {}
+    for nm in names:
+        for j in range(2):
+            p = {k: v.copy() for k, v in zero.items()}
+            p[nm][j] = 1.0
+            out[(nm, j)] = f(p, A, dA) - base
+    return out
+
+
+def _control(control, t):
+    X = control.evaluate(t)
+    dX = control.derivative(t)
+    return X[..., -1], dX[..., -1], dX[..., 0]
+
+
+def vector_field_vjp(params: O.VFParams, t, y, control, g):
+    """(g_y, grads) for out = vector_field(params, t, y, control) and cotangent g [n, d_L].
+
+    grads[l] is a dict with the same keys as params.layers[l] (fusion params, W, b, rms_w, rms_b).
+    """
+    A, dA, tg = _control(control, t)
+    tgm = np.mean(tg, axis=0)
+    L = len(params.layers)
+    # forward tape
+    tape = []
+    Z = np.asarray(y, np.float64)
+    for l in range(L):
+        lay = params.layers[l]
+        Abar = O.fused_matrix(params, l, A, dA)
+        inv = 1.0 / np.sqrt(np.mean(Z * Z, axis=-1, keepdims=True) + 1e-5)
+        xh = Z * inv
+        zn = xh * lay["rms_w"] + lay["rms_b"]
+        m = zn @ lay["W"].T + lay["b"]
+        pre = m + Abar @ m
+        tape.append((Z, inv, xh, zn, m, Abar, pre))
+        Z = np.maximum(pre, 0.0) if l < L - 1 else pre
+    # backward
+    gZ = tgm[:, None] * np.asarray(g, np.float64)
+    grads = [None] * L
+    for l in range(L - 1, -1, -1):
+        lay = params.layers[l]
+        Zin, inv, xh, zn, m, Abar, pre = tape[l]
+        gpre = gZ * (pre > 0) if l < L - 1 else gZ
+        gAbar = gpre @ m.T
+        gm = gpre + Abar.T @ gpre
+        gr = {"b": gm.sum(axis=0), "W": gm.T @ zn}
+        gzn = gm @ lay["W"]
+        gr["rms_w"] = (gzn * xh).sum(axis=0)
+        gr["rms_b"] = gzn.sum(axis=0)
+        gxh = gzn * lay["rms_w"]
+        d = Zin.shape[-1]
+        gZ = inv * (gxh - xh * np.sum(gxh * xh, axis=-1, keepdims=True) / d)
+        for (nm, j), basis in _fusion_basis(params.kind, lay, A, dA).items():
+            gr.setdefault(nm, np.zeros(2))[j] = float(np.sum(gAbar * basis))
+        grads[l] = gr
+    return gZ, grads
+
+
+def cde_wrapper_vjp(params: O.VFParams, hidden_dim, data_embed_dim, t, y, control_adj, control_data, g):
+    """VJP of oracle.cde_wrapper: out[n,m] = sum_lk F[n,m,l,k] dX[n,l,k]."""
+    dX = control_data.derivative(t)
+    gF = np.einsum("nm,nlk->nmlk", np.asarray(g, np.float64), dX).reshape(g.shape[0], -1)
+    return vector_field_vjp(params, t, y, control_adj, gF)
+
+
+def _tableau(method):
+    if method == "rk4":
+        return [0.0, 0.5, 0.5, 1.0], [[], [0.5], [0.0, 0.5], [0.0, 0.0, 1.0]], [1 / 6, 2 / 6, 2 / 6, 1 / 6]
+    if method == "tsit5":
+        return list(O.TSIT5_C[:6]), [list(r) for r in O.TSIT5_A[:6]], list(O.TSIT5_B[:6])
+    raise ValueError(method)
+
+
+def _acc(total, grads):
+    if total is None:
+        return [{k: np.array(v, np.float64) for k, v in g.items()} for g in grads]
+    for tl, gl in zip(total, grads):
+        for k, v in gl.items():
+            tl[k] = tl[k] + v
+    return total
+
+
+def solve_fixed_grid_vjp(f, f_vjp, grid, y0, method="rk4", g_final=None, g_steps=None, time_dtype=np.float32):
+    """Reverse mode of oracle.solve_fixed_grid (same stage times, same grid).
+
+    f(t, y) -> dy; f_vjp(t, y, g) -> (g_y, grads).  Cotangent of the final state ``g_final`` [n, d] or of
+    every saved step state ``g_steps`` [G, n, d].  Returns (g_y0, summed parameter grads).
+    """
+    cs, a, b = _tableau(method)
+    y = np.asarray(y0, np.float64)
+    ys = [y]
+    G = len(grid)
+    geo = []
+    for k in range(G - 1):
+        if time_dtype is None:
+            t, h = float(grid[k]), float(grid[k + 1]) - float(grid[k])
+        else:
+            t = float(time_dtype(grid[k]))
+            h = float(time_dtype(time_dtype(grid[k + 1]) - time_dtype(grid[k])))
+        geo.append((t, h))
+        if method == "rk4":
+            y = O.rk4_step(f, t, y, h, time_dtype)
+        else:
+            y, _, _ = O.tsit5_step(f, t, y, h, time_dtype=time_dtype)
+        ys.append(y)
+    lam = np.array(g_steps[-1] if g_steps is not None else g_final, np.float64)
+    total = None
+    S = len(cs)
+    for k in range(G - 2, -1, -1):
+        t, h = geo[k]
+        tst = O._stage_times(t, h, cs, time_dtype)
+        yk = ys[k]
+        U, K = [], []
+        for i in range(S):
+            u = yk + h * sum((a[i][j] * K[j] for j in range(i)), np.zeros_like(yk))
+            U.append(u)
+            K.append(f(tst[i], u))
+        gK = [h * b[i] * lam for i in range(S)]
+        gy = lam.copy()
+        for i in range(S - 1, -1, -1):
+            gu, gr = f_vjp(tst[i], U[i], gK[i])
+            total = _acc(total, gr)
+            gy = gy + gu
+            for j in range(i):
+                if a[i][j] != 0.0:
+                    gK[j] = gK[j] + h * a[i][j] * gu
+        lam = gy + (g_steps[k] if g_steps is not None else 0.0)
+    return lam, total
+
+
+def grads_to_vector(grads, kind):
+    """Flatten per-layer grads in a fixed order (for comparisons): fusion params then rms_w, rms_b, W, b."""
+    out = []
+    for g in grads:
+        for nm in FUSION_NAMES[kind]:
+            out.append(np.asarray(g[nm]).ravel())
+        for nm in ("rms_w", "rms_b", "W", "b"):
+            out.append(np.asarray(g[nm]).ravel())
+    return np.concatenate(out)
+
+
+def params_to_vector(params: O.VFParams):
+    return grads_to_vector(params.layers, params.kind)
+
+
+def vector_to_params(vec, like: O.VFParams) -> O.VFParams:
+    layers, off = [], 0
+    for lay in like.layers:
+        new = {}
+        for nm in list(FUSION_NAMES[like.kind]) + ["rms_w", "rms_b", "W", "b"]:
+            shape = np.asarray(lay[nm]).shape
+            size = int(np.prod(shape))
+            new[nm] = np.asarray(vec[off:off + size]).reshape(shape)
+            off += size
+        layers.append(new)
+    return O.VFParams(kind=like.kind, layers=layers)

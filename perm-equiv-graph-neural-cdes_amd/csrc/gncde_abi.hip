@@ -107,6 +107,33 @@ int gncde_integrate(const GncdeProblem* prob, const GncdeSolver* solver, const f
   return generic_integrate(*prob, *solver, y0, ys, stats, static_cast<char*>(workspace), st);
 }
 
+size_t gncde_vjp_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* solver) {
+  if (validate_problem(prob) != GNCDE_OK || validate_solver(prob, solver) != GNCDE_OK) return 0;
+  return generic_vjp_workspace(*prob, *solver);
+}
+
+int gncde_integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
+                        float* gy0, float* gparams, float* gfusion, void* workspace, size_t workspace_bytes,
+                        void* stream) {
+  int rc = validate_problem(prob);
+  if (rc) return rc;
+  rc = validate_solver(prob, solver);
+  if (rc) return rc;
+  if (solver->controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
+  if (solver->save_mode != GNCDE_SAVE_T1 && solver->save_mode != GNCDE_SAVE_STEPS) return GNCDE_ERR_UNSUPPORTED;
+  if (!gparams || !gfusion) return GNCDE_ERR_ARG;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (prob->B == 0) {  // empty shard: zero gradients (an all-reduce still sees this rank's contribution)
+    size_t P = params_floats(*prob);
+    (void)hipMemsetAsync(gparams, 0, P * sizeof(float), st);
+    (void)hipMemsetAsync(gfusion, 0, (size_t)prob->L * GNCDE_FC * sizeof(float), st);
+    return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+  }
+  if (!ys || !gys || !gy0) return GNCDE_ERR_ARG;
+  if (workspace_bytes < generic_vjp_workspace(*prob, *solver) || !workspace) return GNCDE_ERR_WORKSPACE;
+  return generic_integrate_vjp(*prob, *solver, ys, gys, gy0, gparams, gfusion, static_cast<char*>(workspace), st);
+}
+
 }  // extern "C"
 
 namespace {
@@ -123,6 +150,120 @@ __global__ void k_node_affine(int rows, int din, int dout, const float* __restri
   const float* w = W + (size_t)o * din;
   for (int k = 0; k < din; ++k) acc = fmaf(w[k], xr[k], acc);
   out[e] = acc;
+}
+
+// gx[r, f] = sum_o g[r, o] W[o, f]
+__global__ void k_affine_grad_x(int rows, int din, int dout, const float* __restrict__ W, const float* __restrict__ g,
+                                float* __restrict__ gx) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (size_t)rows * din) return;
+  const size_t r = e / din;
+  const int f = (int)(e % din);
+  const float* gr = g + r * dout;
+  float acc = 0.f;
+  for (int o = 0; o < dout; ++o) acc = fmaf(gr[o], W[(size_t)o * din + f], acc);
+  gx[e] = acc;
+}
+
+// One block per weight entry (o, f) (f == din: the bias): gW[o, f] = sum_r g[r, o] x[r, f], gb[o] = sum_r g[r, o].
+// Fixed strided partition + tree reduction: deterministic.
+__global__ void __launch_bounds__(256) k_affine_grad_w(int rows, int din, int dout, const float* __restrict__ x,
+                                                       const float* __restrict__ g, float* __restrict__ gW,
+                                                       float* __restrict__ gb) {
+  const int e = blockIdx.x;
+  const int o = e / (din + 1), f = e % (din + 1);
+  float acc = 0.f;
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+    const float gv = g[(size_t)r * dout + o];
+    acc = f < din ? fmaf(gv, x[(size_t)r * din + f], acc) : acc + gv;
+  }
+  __shared__ float red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (f < din) {
+      if (gW) gW[(size_t)o * din + f] = red[0];
+    } else if (gb) {
+      gb[o] = red[0];
+    }
+  }
+}
+
+// optax.chain(clip_by_global_norm(max_norm), adamw(lr, b1, b2, eps, weight_decay)) over one flat buffer.
+// Pass 1 (single block): global norm and max|g|.
+__global__ void __launch_bounds__(1024) k_grad_norm(int P, const float* __restrict__ g, float* __restrict__ stats) {
+  double ss = 0.0;
+  float mx = 0.f;
+  for (int e = threadIdx.x; e < P; e += blockDim.x) {
+    const float v = g[e];
+    ss += (double)v * v;
+    mx = fmaxf(mx, fabsf(v));
+  }
+  __shared__ double rs[1024];
+  __shared__ float rm[1024];
+  rs[threadIdx.x] = ss;
+  rm[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      rs[threadIdx.x] += rs[threadIdx.x + s];
+      rm[threadIdx.x] = fmaxf(rm[threadIdx.x], rm[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    stats[0] = (float)sqrt(rs[0]);
+    stats[1] = rm[0];
+    stats[2] = 0.f;
+  }
+}
+
+// Pass 2: clip (optax: g if norm < max_norm else g / norm * max_norm), Adam moments with bias correction,
+// decoupled weight decay (optax.adamw: u = -lr * (m_hat / (sqrt(v_hat) + eps) + wd * p)).
+__global__ void k_adamw(int P, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                        float* __restrict__ v, float lr, float b1, float b2, float eps, float wd, float max_norm,
+                        float bc1, float bc2, float* __restrict__ stats, float* __restrict__ upd_max) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  float u = 0.f;
+  if (e < P) {
+    const float norm = stats[0];
+    float gv = g[e];
+    if (max_norm > 0.f && !(norm < max_norm)) gv = gv / norm * max_norm;
+    const float mn = b1 * m[e] + (1.f - b1) * gv;
+    const float vn = b2 * v[e] + (1.f - b2) * gv * gv;
+    m[e] = mn;
+    v[e] = vn;
+    const float mh = mn / bc1, vh = vn / bc2;
+    u = -lr * (mh / (sqrtf(vh) + eps) + wd * p[e]);
+    p[e] += u;
+  }
+  // per-block max |update| (reduced by the host-facing entry afterwards)
+  __shared__ float red[256];
+  red[threadIdx.x] = fabsf(u);
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) upd_max[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(1024) k_max_reduce(int nblk, const float* __restrict__ upd_max,
+                                                     float* __restrict__ stats) {
+  float mx = 0.f;
+  for (int e = threadIdx.x; e < nblk; e += blockDim.x) mx = fmaxf(mx, upd_max[e]);
+  __shared__ float red[1024];
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) stats[2] = red[0];
 }
 
 __global__ void k_interval_index(const float* __restrict__ ts, int B, int T, const float* __restrict__ t,
@@ -146,6 +287,42 @@ int gncde_node_affine(int32_t rows, int32_t din, int32_t dout, const float* x, c
   const size_t total = (size_t)rows * dout;
   hipLaunchKernelGGL(k_node_affine, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), rows, din, dout, x, W, b, out);
+  return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+}
+
+int gncde_node_affine_grad(int32_t rows, int32_t din, int32_t dout, const float* x, const float* W,
+                           const float* g, float* gx, float* gW, float* gb, void* stream) {
+  if (rows < 0 || din <= 0 || dout <= 0) return GNCDE_ERR_SHAPE;
+  if (!g || (gx && !W) || (gW && !x)) return GNCDE_ERR_ARG;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (gx && rows > 0) {
+    const size_t total = (size_t)rows * din;
+    hipLaunchKernelGGL(k_affine_grad_x, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, rows, din, dout, W,
+                       g, gx);
+  }
+  if (gW || gb)
+    hipLaunchKernelGGL(k_affine_grad_w, dim3((unsigned)(dout * (din + 1))), dim3(256), 0, st, rows, din, dout, x, g,
+                       gW, gb);
+  return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+}
+
+size_t gncde_adamw_workspace_bytes(int32_t P) { return P <= 0 ? 0 : (size_t)((P + 255) / 256) * sizeof(float); }
+
+int gncde_clip_adamw(int32_t P, float* params, const float* grads, float* m, float* v, int32_t step, float lr,
+                     float b1, float b2, float eps, float weight_decay, float max_norm, float* stats,
+                     void* workspace, size_t workspace_bytes, void* stream) {
+  if (P < 0 || step < 1) return GNCDE_ERR_ARG;
+  if (P == 0) return GNCDE_OK;
+  if (!params || !grads || !m || !v || !stats) return GNCDE_ERR_ARG;
+  if (!workspace || workspace_bytes < gncde_adamw_workspace_bytes(P)) return GNCDE_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int nblk = (P + 255) / 256;
+  const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+  float* upd = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(k_grad_norm, dim3(1), dim3(1024), 0, st, P, grads, stats);
+  hipLaunchKernelGGL(k_adamw, dim3(nblk), dim3(256), 0, st, P, params, grads, m, v, lr, b1, b2, eps, weight_decay,
+                     max_norm, bc1, bc2, stats, upd);
+  hipLaunchKernelGGL(k_max_reduce, dim3(1), dim3(1024), 0, st, nblk, upd, stats);
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }
 

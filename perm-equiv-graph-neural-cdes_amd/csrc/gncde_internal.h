@@ -107,6 +107,11 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
 int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
                       int32_t* stats, char* ws, hipStream_t st);
 
+// reverse mode (discrete adjoint, GRID controller): gncde_vjp.hip
+size_t generic_vjp_workspace(const GncdeProblem& p, const GncdeSolver& s);
+int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys,
+                          float* gy0, float* gparams, float* gfusion, char* ws, hipStream_t st);
+
 // fused persistent path: gncde_fused.hip.  Returns GNCDE_ERR_UNSUPPORTED when no kernel fits.
 bool fused_supported(const GncdeProblem& p, const GncdeSolver& s, char* name, size_t name_len);
 int fused_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,

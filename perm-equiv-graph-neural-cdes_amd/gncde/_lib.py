@@ -30,7 +30,12 @@ EXPORTED_SYMBOLS = (
     "gncde_workspace_bytes",
     "gncde_vf_eval",
     "gncde_integrate",
+    "gncde_vjp_workspace_bytes",
+    "gncde_integrate_vjp",
     "gncde_node_affine",
+    "gncde_node_affine_grad",
+    "gncde_adamw_workspace_bytes",
+    "gncde_clip_adamw",
     "gncde_interval_index",
 )
 
@@ -103,9 +108,22 @@ def load(path: str | None = None):
     lib.gncde_integrate.restype = c_int32
     lib.gncde_integrate.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver), c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_size_t, c_void_p]
+    lib.gncde_vjp_workspace_bytes.restype = c_size_t
+    lib.gncde_vjp_workspace_bytes.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver)]
+    lib.gncde_integrate_vjp.restype = c_int32
+    lib.gncde_integrate_vjp.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver), c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
     lib.gncde_node_affine.restype = c_int32
     lib.gncde_node_affine.argtypes = [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p]
+    lib.gncde_node_affine_grad.restype = c_int32
+    lib.gncde_node_affine_grad.argtypes = [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p]
+    lib.gncde_adamw_workspace_bytes.restype = c_size_t
+    lib.gncde_adamw_workspace_bytes.argtypes = [c_int32]
+    lib.gncde_clip_adamw.restype = c_int32
+    lib.gncde_clip_adamw.argtypes = [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_float, c_float,
+                                     c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_size_t, c_void_p]
     lib.gncde_interval_index.restype = c_int32
     lib.gncde_interval_index.argtypes = [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
                                          c_void_p]

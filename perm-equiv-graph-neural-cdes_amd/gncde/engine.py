@@ -201,6 +201,36 @@ def integrate(prob: Problem, solver: SolverSpec, y0: torch.Tensor, stats: bool =
     return (ys, st) if stats else ys
 
 
+def integrate_vjp(prob: Problem, solver: SolverSpec, ys_steps: torch.Tensor, gys: torch.Tensor):
+    """Reverse mode of ``integrate`` for a fixed grid (the discrete adjoint ``jax.grad`` takes through
+    diffrax's RecursiveCheckpointAdjoint, trainer.py:315).
+
+    ys_steps: [B, G, n, d] the forward's SAVE_STEPS states; gys: cotangent of the forward output in
+    ``solver.save_mode`` layout (SAVE_T1 [B, n, d] or SAVE_STEPS [B, G, n, d]).
+    Returns (gy0 [B, n, d], gparams [P] summed over samples, gfusion [L, 24] summed over samples).
+    """
+    _require_gpu()
+    lib = _lib.load()
+    ps, ss = prob.c_struct(), solver.c_struct()
+    ys_steps = ys_steps.to(torch.float32).contiguous()
+    gys = gys.to(torch.float32).contiguous()
+    B, n, ds = prob.B, prob.n, prob.dims[0]
+    if ys_steps.shape != (B, ss.grid_len, n, ds):
+        raise _lib.GncdeError(f"integrate_vjp: ys_steps shape {tuple(ys_steps.shape)}")
+    want = (B, n, ds) if solver.save_mode == _lib.SAVE_T1 else (B, ss.grid_len, n, ds)
+    if gys.shape != want:
+        raise _lib.GncdeError(f"integrate_vjp: gys shape {tuple(gys.shape)} != {want}")
+    dev = prob.params.device
+    gy0 = torch.empty(B, n, ds, dtype=torch.float32, device=dev)
+    gparams = torch.empty_like(prob.params)
+    gfusion = torch.empty_like(prob.fusion)
+    nbytes = lib.gncde_vjp_workspace_bytes(ctypes.byref(ps), ctypes.byref(ss))
+    ws = _Workspace.get(nbytes) if nbytes else None
+    _lib.check(lib.gncde_integrate_vjp(ctypes.byref(ps), ctypes.byref(ss), _ptr(ys_steps), _ptr(gys), _ptr(gy0),
+                                       _ptr(gparams), _ptr(gfusion), _ptr(ws), nbytes, _stream()))
+    return gy0, gparams, gfusion
+
+
 def node_affine(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:
     """out[..., :] = W @ x[..., :] + b per row (eqx.nn.Linear under vmap)."""
     _require_gpu()
@@ -213,6 +243,41 @@ def node_affine(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None) -> tor
     out = torch.empty(*x.shape[:-1], dout, dtype=torch.float32, device=x.device)
     _lib.check(lib.gncde_node_affine(rows, din, dout, _ptr(x), _ptr(W), _ptr(bb), _ptr(out), _stream()))
     return out
+
+
+def node_affine_grad(x: torch.Tensor, W: torch.Tensor, g: torch.Tensor, need_x=True, need_w=True, need_b=True):
+    """Reverse mode of ``node_affine``: (gx, gW, gb) for cotangent g [..., dout] (None where not needed)."""
+    _require_gpu()
+    lib = _lib.load()
+    x = x.to(torch.float32).contiguous()
+    W = W.to(device=x.device, dtype=torch.float32).contiguous()
+    g = g.to(device=x.device, dtype=torch.float32).contiguous()
+    din, dout = int(W.shape[1]), int(W.shape[0])
+    rows = x.numel() // din
+    gx = torch.empty_like(x) if need_x else None
+    gW = torch.empty_like(W) if need_w else None
+    gb = torch.empty(dout, dtype=torch.float32, device=x.device) if need_b else None
+    _lib.check(lib.gncde_node_affine_grad(rows, din, dout, _ptr(x), _ptr(W), _ptr(g), _ptr(gx), _ptr(gW), _ptr(gb),
+                                          _stream()))
+    return gx, gW, gb
+
+
+def clip_adamw(params: torch.Tensor, grads: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int, lr: float,
+               b1: float, b2: float, eps: float, weight_decay: float, max_norm: float) -> torch.Tensor:
+    """In-place optax.chain(clip_by_global_norm, adamw) update of a flat fp32 buffer.  Returns the device
+    stats [3] = (global grad norm, max|grad|, max|update|)."""
+    _require_gpu()
+    lib = _lib.load()
+    for t in (params, grads, m, v):
+        if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == params.numel()):
+            raise _lib.GncdeError("clip_adamw: params/grads/m/v must be contiguous fp32 CUDA buffers of one size")
+    P = params.numel()
+    stats = torch.zeros(3, dtype=torch.float32, device=params.device)
+    nbytes = lib.gncde_adamw_workspace_bytes(P)
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=params.device)
+    _lib.check(lib.gncde_clip_adamw(P, _ptr(params), _ptr(grads), _ptr(m), _ptr(v), int(step), lr, b1, b2, eps,
+                                    weight_decay, max_norm, _ptr(stats), _ptr(ws), nbytes, _stream()))
+    return stats
 
 
 def interval_index(ts: torch.Tensor, t: torch.Tensor, sample: torch.Tensor) -> torch.Tensor:

@@ -53,48 +53,76 @@ def pack_data_control(coeffs, device="cuda"):
     return torch.stack([p.to(device=device, dtype=torch.float32) for p in parts], dim=2).contiguous()
 
 
-def fusion_table(kind: str, layers, n: int) -> torch.Tensor:
-    """Map the reference's fusion parameters to the factored table [L, 24] (float64 on host).
+FUSION_PARAM_NAMES = {
+    "undirected": ("param1", "param2", "param3", "param4", "param5", "param6", "param7", "param8"),
+    "directed": ("param1", "param2", "param3", "param4", "param4_prime", "param5", "param5_prime", "param6",
+                 "param6_prime", "param7", "param8"),
+    "plain": (),
+}
+
+
+def fusion_map(kind: str, n: int):
+    """The (linear) map from one layer's reference fusion parameters to its factored-table row:
+
+        row = base + concat(param_a, param_b, ...) @ M        (names in FUSION_PARAM_NAMES[kind] order)
 
     kind "undirected": ConvEquivFusionLayer._fusion (layers.py:102-160)
     kind "directed":   ConvEquivFusionDirectedLayer._fusion (layers.py:256-337)
     kind "plain":      GraphVectorField message matrix A + dA (graph_vector_field.py:94)
+    Returns (names, base [24] float64, M [2*len(names), 24] float64).
     """
-    L = len(layers)
-    tab = torch.zeros(L, FC, dtype=torch.float64)
+    if kind not in FUSION_PARAM_NAMES:
+        raise ValueError(kind)
+    names = FUSION_PARAM_NAMES[kind]
+    base = torch.zeros(FC, dtype=torch.float64)
+    base[IDC] = 1.0  # ConvLayer residual: m + Abar @ m (layers.py:47)
+    base[E_A] = base[E_DA] = 1.0  # plain: A + dA; fusion kinds: term_1 = (1 + param1) * (A, dA)
+    M = torch.zeros(2 * len(names), FC, dtype=torch.float64)
 
-    def p(lay, name, j):
-        return float(torch.as_tensor(lay[name]).double().reshape(-1)[j])
+    def put(name, j, col, coef):
+        M[2 * names.index(name) + j, col] += coef
 
-    for l, lay in enumerate(layers):
-        t = tab[l]
-        t[IDC] = 1.0  # ConvLayer residual: m + Abar @ m (layers.py:47)
-        if kind == "plain":
-            t[E_A] = t[E_DA] = 1.0
-            continue
-        t[E_A], t[E_DA] = 1.0 + p(lay, "param1", 0), 1.0 + p(lay, "param1", 1)  # term_1
-        t[ET_A], t[ET_DA] = p(lay, "param2", 0), p(lay, "param2", 1)  # term_2 transpose
-        t[UD_A], t[UD_DA] = p(lay, "param3", 0), p(lay, "param3", 1)  # term_3 diag(diag)
-        # term_7: both halves multiply sum(adjacency) (layers.py:144-148)
-        t[WS_A] = p(lay, "param7", 0) / n**2 + p(lay, "param7", 1) / n**2
-        t[US_A], t[US_DA] = p(lay, "param8", 0) / n**2, p(lay, "param8", 1) / n**2  # term_8
-        if kind == "undirected":
-            t[WR_A], t[WR_DA] = p(lay, "param4", 0) / n, p(lay, "param4", 1) / n  # row sums -> rows
-            t[VR_A], t[VR_DA] = p(lay, "param5", 0) / n, p(lay, "param5", 1) / n  # row sums -> cols
-            t[UR_A], t[UR_DA] = p(lay, "param6", 0) / n, p(lay, "param6", 1) / n  # diag(row sums)
-        elif kind == "directed":
-            t[WC_A], t[WC_DA] = p(lay, "param4", 0) / n, p(lay, "param4", 1) / n  # col sums -> rows
-            t[VR_A] += p(lay, "param4_prime", 0) / n  # tile(rowsum A)
-            t[VC_DA] += p(lay, "param4_prime", 1) / n  # tile(colsum dA)  (quirk :288-293)
-            t[VC_A] += p(lay, "param5", 0) / n
-            t[VC_DA] += p(lay, "param5", 1) / n
-            t[VR_A] += p(lay, "param5_prime", 0) / n
-            t[VR_DA] += p(lay, "param5_prime", 1) / n
-            t[UC_A], t[UC_DA] = p(lay, "param6", 0) / n, p(lay, "param6", 1) / n
-            t[UR_A], t[UR_DA] = p(lay, "param6_prime", 0) / n, p(lay, "param6_prime", 1) / n
-        else:
-            raise ValueError(kind)
-    return tab
+    if kind == "plain":
+        return names, base, M
+    put("param1", 0, E_A, 1.0), put("param1", 1, E_DA, 1.0)  # term_1
+    put("param2", 0, ET_A, 1.0), put("param2", 1, ET_DA, 1.0)  # term_2 transpose
+    put("param3", 0, UD_A, 1.0), put("param3", 1, UD_DA, 1.0)  # term_3 diag(diag)
+    # term_7: both halves multiply sum(adjacency) (layers.py:144-148)
+    put("param7", 0, WS_A, 1.0 / n**2), put("param7", 1, WS_A, 1.0 / n**2)
+    put("param8", 0, US_A, 1.0 / n**2), put("param8", 1, US_DA, 1.0 / n**2)  # term_8
+    if kind == "undirected":
+        put("param4", 0, WR_A, 1.0 / n), put("param4", 1, WR_DA, 1.0 / n)  # row sums -> rows
+        put("param5", 0, VR_A, 1.0 / n), put("param5", 1, VR_DA, 1.0 / n)  # row sums -> cols
+        put("param6", 0, UR_A, 1.0 / n), put("param6", 1, UR_DA, 1.0 / n)  # diag(row sums)
+    else:
+        put("param4", 0, WC_A, 1.0 / n), put("param4", 1, WC_DA, 1.0 / n)  # col sums -> rows
+        put("param4_prime", 0, VR_A, 1.0 / n)  # tile(rowsum A)
+        put("param4_prime", 1, VC_DA, 1.0 / n)  # tile(colsum dA)  (quirk :288-293)
+        put("param5", 0, VC_A, 1.0 / n), put("param5", 1, VC_DA, 1.0 / n)
+        put("param5_prime", 0, VR_A, 1.0 / n), put("param5_prime", 1, VR_DA, 1.0 / n)
+        put("param6", 0, UC_A, 1.0 / n), put("param6", 1, UC_DA, 1.0 / n)
+        put("param6_prime", 0, UR_A, 1.0 / n), put("param6_prime", 1, UR_DA, 1.0 / n)
+    return names, base, M
+
+
+def fusion_table(kind: str, layers, n: int) -> torch.Tensor:
+    """Map the reference's fusion parameters (layer dicts) to the factored table [L, 24] (float64, host)."""
+    names, base, M = fusion_map(kind, n)
+    rows = []
+    for lay in layers:
+        flat = [torch.as_tensor(lay[nm]).detach().double().cpu().reshape(2) for nm in names]
+        rows.append(base + (torch.cat(flat) @ M if names else 0.0))
+    return torch.stack(rows)
+
+
+def fusion_table_torch(kind: str, layer_params, n: int) -> torch.Tensor:
+    """Differentiable ``fusion_table``: layer_params[l] = list of (2,) tensors in FUSION_PARAM_NAMES order.
+    The backward of the table is M^T (gfusion rows -> parameter gradients)."""
+    names, base, M = fusion_map(kind, n)
+    dev = layer_params[0][0].device if names else "cpu"
+    base, M = base.to(dev), M.to(dev)
+    rows = [base + (torch.cat([p.double().reshape(2) for p in ps]) @ M if names else 0.0) for ps in layer_params]
+    return torch.stack(rows)
 
 
 def pack_params(layers, device="cuda") -> torch.Tensor:
@@ -125,6 +153,24 @@ def rk4_grid(t0: float, t1: float, nsteps: int) -> np.ndarray:
         g[k] = f32(t0 + f32(f32(k) * h))
     g[-1] = t1
     return g
+
+
+def knot_grid(ts, steps_per_interval: int) -> np.ndarray:
+    """Fixed grid that contains every knot: each [ts_i, ts_{i+1}] split into m equal fp32 steps (the knot
+    itself exact).  Step states at indices i*m are then exactly the SaveAt(ts) outputs of the solve, so a
+    fixed-step solve can be trained on trajectories like graph_neural_cde.py:89-92 (evolving_out)."""
+    f32 = np.float32
+    ts = np.asarray(ts, dtype=f32)
+    m = int(steps_per_interval)
+    if m < 1 or ts.ndim != 1 or ts.shape[0] < 2:
+        raise ValueError("knot_grid: need ts [T>=2] and steps_per_interval >= 1")
+    out = [ts[0]]
+    for i in range(ts.shape[0] - 1):
+        a, b = ts[i], ts[i + 1]
+        h = f32(f32(b - a) / f32(m))
+        out.extend(f32(a + f32(f32(k) * h)) for k in range(1, m))
+        out.append(b)
+    return np.asarray(out, dtype=f32)
 
 
 def constant_step_grid(t0: float, t1: float, dt0: float, tol: float = 1e-6) -> np.ndarray:

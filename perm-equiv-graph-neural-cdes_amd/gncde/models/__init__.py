@@ -13,7 +13,7 @@ import numpy as np
 import torch
 from torch import nn
 
-from .. import _lib, engine, layout
+from .. import _lib, autograd, engine, layout
 from ..interpolation import CubicInterpolation
 from ..synthetic import hermite_coefficients
 from . import vector_fields
@@ -32,7 +32,8 @@ def _linear(din, dout, g):
 
 
 def _affine(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
-    return engine.node_affine(x, lin.weight.detach().to(x.device), lin.bias.detach().to(x.device))
+    """Per-node Linear on gncde_node_affine; differentiable (gncde_node_affine_grad) when grad is enabled."""
+    return autograd.node_affine(x, lin.weight, lin.bias)
 
 
 class MLP(nn.Module):
@@ -71,8 +72,10 @@ class GraphNeuralCDE(nn.Module):
     """``graph_neural_cde.py:12-113``: Linear(1->h) encoder, Tsit5 + PIDController(1e-3, 1e-6),
     dt0=None, SaveAt(ts) (evolving_out) or SaveAt(t1), Linear(h->1) read-out per node.
 
-    ``solver`` (build extension, BASELINE config 2) may override the reference solve:
-    {"method": "rk4"|"tsit5", "steps": N} for a fixed grid of N steps on [ts[0], ts[-1]].
+    ``solver`` (build extension, BASELINE configs 2/4) may override the reference solve with a fixed grid:
+    {"method": "rk4"|"tsit5", "steps": N} — N equal steps on [ts[0], ts[-1]] (saves t1 only), or
+    {"method": ..., "steps_per_interval": m} — m steps between consecutive knots, so the step states at the
+    knots are the SaveAt(ts) outputs (evolving_out, differentiable: ``loss_terms``).
     """
 
     def __init__(self, cfg, vector_field, interpolation="cubic", model_key=None, solver=None, **kwargs):
@@ -98,10 +101,20 @@ class GraphNeuralCDE(nn.Module):
                                      t1=ts[:, -1].contiguous(), save_ts=ts.contiguous() if evolving_out else None)
         method = _lib.RK4 if self.solver.get("method", "rk4") == "rk4" else _lib.TSIT5
         tsn = ts.cpu().numpy()
-        grids = [layout.rk4_grid(t[0], t[-1], int(self.solver["steps"])) for t in tsn]
+        if "steps_per_interval" in self.solver:
+            grids = [layout.knot_grid(t, int(self.solver["steps_per_interval"])) for t in tsn]
+            save = _lib.SAVE_STEPS if evolving_out else _lib.SAVE_T1
+        else:
+            if evolving_out:
+                raise NotImplementedError("a uniform fixed grid saves at t1 only: use steps_per_interval")
+            grids = [layout.rk4_grid(t[0], t[-1], int(self.solver["steps"])) for t in tsn]
+            save = _lib.SAVE_T1
         grid, ns = layout.stack_grids(grids, device=ts.device)
-        return engine.SolverSpec(method=method, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_T1, grid=grid,
-                                 nsteps=ns)
+        return engine.SolverSpec(method=method, controller=_lib.CTRL_GRID, save_mode=save, grid=grid, nsteps=ns)
+
+    def _knot_states(self, ys: torch.Tensor, T: int) -> torch.Tensor:
+        m = int(self.solver["steps_per_interval"])
+        return ys[:, torch.arange(T, device=ys.device) * m]
 
     def batched(self, ts, coeffs_adj, x0, evolving_out=True, return_stats=False):
         """ts [B, T], coeffs_adj (d, c, b, a) each [B, T-1, n, n, 2], x0 [B, n, 1] -> [B, T, n, 1]
@@ -109,16 +122,44 @@ class GraphNeuralCDE(nn.Module):
         control = CubicInterpolation(ts, coeffs_adj)
         ts_d = control.graph_layout()[0]
         x0 = torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device)
+        with torch.no_grad():
+            y0 = _affine(self.initial_linear, x0)
+            prob = self.vector_field.problem(control)
+            spec = self._spec(ts_d, evolving_out)
+            ys, st = engine.integrate(prob, spec, y0, stats=True)
+            if torch.any(st[:, _lib.STAT_STATUS] != 0):
+                raise RuntimeError("diffrax-equivalent failure: max_steps reached or non-finite state")
+            if spec.save_mode == _lib.SAVE_STEPS:
+                ys = self._knot_states(ys, ts_d.shape[1])
+            out = _affine(self.final_linear, ys)
+        return (out, st) if return_stats else out
+
+    def predict(self, ts, coeffs_adj, x0, evolving_out=True):
+        """Differentiable batched forward (fixed-grid ``solver`` only): the prediction of ``batched`` with
+        an autograd graph through the read-out, the GPU solve (discrete adjoint) and the encoder."""
+        if self.solver is None:
+            raise NotImplementedError("training needs a fixed-grid solver override (adaptive PID is forward-only)")
+        control = CubicInterpolation(ts, coeffs_adj)
+        ts_d = control.graph_layout()[0]
+        x0 = torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device)
         y0 = _affine(self.initial_linear, x0)
         prob = self.vector_field.problem(control)
+        params, fusion = self.vector_field.diff_tensors(prob.n, ts_d.device)
         spec = self._spec(ts_d, evolving_out)
-        if self.solver is not None and evolving_out:
-            raise NotImplementedError("fixed-grid solver override saves at t1 only")
-        ys, st = engine.integrate(prob, spec, y0, stats=True)
-        if torch.any(st[:, _lib.STAT_STATUS] != 0):
-            raise RuntimeError("diffrax-equivalent failure: max_steps reached or non-finite state")
-        out = _affine(self.final_linear, ys)
-        return (out, st) if return_stats else out
+        ys = autograd.solve(prob, spec, y0, params, fusion)
+        if spec.save_mode == _lib.SAVE_STEPS:
+            ys = self._knot_states(ys, ts_d.shape[1])
+        return _affine(self.final_linear, ys)
+
+    def loss_terms(self, ts, coeffs_adj, x0, labels, evolving_out=True):
+        """(sum of squared errors, element count) of ``MSECfg.mse_loss`` (loss_configs.py:22-47:
+        mean((squeeze(pred, -1) - label)^2)) on this shard — summed, so data-parallel ranks can all-reduce
+        before dividing by the global count."""
+        pred = self.predict(ts, coeffs_adj, x0, evolving_out).squeeze(-1)
+        labels = torch.as_tensor(labels, dtype=torch.float32, device=pred.device)
+        if labels.shape != pred.shape:
+            raise ValueError(f"labels {tuple(labels.shape)} != predictions {tuple(pred.shape)}")
+        return ((pred - labels) ** 2).sum(), pred.numel()
 
     def __call__(self, ts, coeffs_adj, x0, evolving_out=True):
         ts = torch.as_tensor(np.asarray(ts) if not torch.is_tensor(ts) else ts, dtype=torch.float32)
@@ -156,9 +197,20 @@ class PGTGraphNeuralCDE(nn.Module):
         grid, ns = layout.stack_grids(grids, device=ts_d.device)
         spec = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_T1, grid=grid,
                                  nsteps=ns)
-        yT = engine.integrate(prob, spec, y0)
+        if torch.is_grad_enabled():  # differentiable: GPU discrete adjoint through the CDE solve
+            params, fusion = self.vector_field.diff_tensors(prob.n, ts_d.device)
+            yT = autograd.solve(prob, spec, y0, params, fusion)
+        else:
+            yT = engine.integrate(prob, spec, y0)
         out = self.decoder.run(yT)
         return out.sum(dim=1) if global_readout else out
+
+    def loss_terms(self, ts, coeffs_adj, x_coeffs, x0, labels):
+        """(sum of squared errors, count) of trainer_pgt.mse_loss (trainer_pgt.py:45-66) over the windows of
+        this shard: prediction = global read-out [B, feature_dim] vs labels."""
+        pred = self.batched(ts, coeffs_adj, x_coeffs, x0)
+        labels = torch.as_tensor(labels, dtype=torch.float32, device=pred.device).reshape(pred.shape)
+        return ((pred - labels) ** 2).sum(), pred.numel()
 
     def __call__(self, ts, coeffs_adj, x_coeffs, x0, evolving_out=False, global_readout=True):
         ts = torch.as_tensor(np.asarray(ts) if not torch.is_tensor(ts) else ts, dtype=torch.float32)

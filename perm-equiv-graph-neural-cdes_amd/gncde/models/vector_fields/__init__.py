@@ -56,6 +56,13 @@ class _GraphVectorFieldBase(nn.Module):
                               data_coef=dc, cde_hidden=cde_hidden,
                               cde_embed=self.data_embed_dim if cde_hidden else 0)
 
+    def diff_tensors(self, n: int, device) -> tuple:
+        """(params, fusion) as differentiable device tensors: the packed parameter buffer and the factored
+        fusion table [L, 24] (layout.fusion_table_torch), for ``autograd.solve``."""
+        params = torch.cat([lay.packed() for lay in self.gnn_layers]).to(device=device, dtype=torch.float32)
+        fusion = layout.fusion_table_torch(self.kind, [lay.fusion_params() for lay in self.gnn_layers], n)
+        return params, fusion.to(device=device, dtype=torch.float32)
+
     def __call__(self, t, y, args):
         """``vf(t, y [n, d_0], control) -> [n, d_L]`` for one sample (reference signature)."""
         prob = self.problem(args)

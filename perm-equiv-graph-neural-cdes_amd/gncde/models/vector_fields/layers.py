@@ -50,6 +50,13 @@ class ConvLayer(nn.Module):
         return {"W": self.linear.weight.detach(), "b": self.linear.bias.detach(),
                 "rms_w": self.norm.weight.detach(), "rms_b": self.norm.bias.detach()}
 
+    def fusion_params(self):
+        return []  # GraphVectorField: A + dA, no fusion parameters
+
+    def packed(self) -> torch.Tensor:
+        """Differentiable packed parameters in the engine layout (rms_w, rms_b, W row-major, b; gncde.h)."""
+        return torch.cat([self.norm.weight, self.norm.bias, self.linear.weight.reshape(-1), self.linear.bias])
+
 
 class ConvEquivFusionLayer(nn.Module):
     """``ConvEquivFusionLayer`` (layers.py:51-177): 8 (A, dA) coefficient pairs + ConvLayer."""
@@ -68,6 +75,12 @@ class ConvEquivFusionLayer(nn.Module):
         d = {nm: getattr(self, nm).detach() for nm in self.names}
         d.update(self.conv_layer.as_dict())
         return d
+
+    def fusion_params(self):
+        return [getattr(self, nm) for nm in self.names]
+
+    def packed(self) -> torch.Tensor:
+        return self.conv_layer.packed()
 
 
 class ConvEquivFusionDirectedLayer(ConvEquivFusionLayer):
@@ -100,3 +113,9 @@ class PlainConvLayer(nn.Module):
 
     def as_dict(self):
         return self.conv_layer.as_dict()
+
+    def fusion_params(self):
+        return []
+
+    def packed(self) -> torch.Tensor:
+        return self.conv_layer.packed()

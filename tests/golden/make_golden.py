@@ -18,6 +18,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", ".."))
 from oracle import gncde_oracle as O  # noqa: E402
+from oracle import gncde_oracle_grad as OG  # noqa: E402
 
 
 def flat_layers(prefix, params: O.VFParams, out: dict):
@@ -151,6 +152,69 @@ def cde_case(rng, name, B, n, T, h, de, L):
     np.savez_compressed(os.path.join(HERE, name), **out)
 
 
+def grad_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None, cotangent="final", cde=None):
+    """Reverse mode of a fixed-grid solve (oracle/gncde_oracle_grad.py): expected dL/dy0 per sample and
+    dL/dparams summed over samples for L = sum(g * y) with a random cotangent g."""
+    if cde is not None:
+        h, de = cde
+        dims = [h] + list(dims[1:-1]) + [h * de * 2]
+    ts, coeffs, params = problem(rng, B, n, T, kind, dims, irregular=cde is None)
+    if cde is not None:
+        ts = np.tile(np.linspace(0.0, 3.0, T), (B, 1))
+        co = []
+        for b in range(B):
+            _, X = O.make_graph_control(rng, n, T, irregular=False, t1=3.0)
+            co.append(O.backward_hermite_coefficients(ts[b], X))
+        coeffs = tuple(np.stack([c[q] for c in co]) for q in range(4))
+    for lay in params.layers:  # fusion params large enough that their gradients are well conditioned
+        for nm in OG.FUSION_NAMES[kind]:
+            lay[nm] = lay[nm] * 3.0
+    ds = dims[0]
+    y0 = rng.standard_normal((B, n, ds))
+    grids, gys, gy0s, total, dco = [], [], [], None, []
+    for b in range(B):
+        ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
+        if cde is None:
+            f = lambda t, y, ctrl=ctrl: O.vector_field(params, t, y, ctrl)  # noqa: E731
+            fv = lambda t, y, g, ctrl=ctrl: OG.vector_field_vjp(params, t, y, ctrl, g)  # noqa: E731
+        else:
+            x = rng.standard_normal((T, n, de))
+            Xd = np.stack([np.broadcast_to(ts[b][:, None, None], x.shape), x], axis=-1)
+            dc = O.backward_hermite_coefficients(ts[b], Xd)
+            dco.append(dc)
+            cx = O.CubicInterpolation(ts[b], dc)
+            f = lambda t, y, ctrl=ctrl, cx=cx: O.cde_wrapper(params, h, de, t, y, ctrl, cx)  # noqa: E731
+            fv = lambda t, y, g, ctrl=ctrl, cx=cx: OG.cde_wrapper_vjp(params, h, de, t, y, ctrl, cx, g)  # noqa
+        g = O.rk4_grid(ts[b, 0], ts[b, -1], nsteps) if method == "rk4" else O.constant_grid(ts[b, 0], ts[b, -1],
+                                                                                             dt0)
+        grids.append(g)
+        if cotangent == "final":
+            gy = rng.standard_normal((n, ds))
+            gy0, gr = OG.solve_fixed_grid_vjp(f, fv, g, y0[b], method, g_final=gy)
+        else:
+            gy = rng.standard_normal((len(g), n, ds))
+            gy0, gr = OG.solve_fixed_grid_vjp(f, fv, g, y0[b], method, g_steps=gy)
+        gys.append(gy)
+        gy0s.append(gy0)
+        total = OG._acc(total, gr)
+    G = max(len(g) for g in grids)
+    grid = np.stack([np.concatenate([g, np.full(G - len(g), g[-1], np.float32)]) for g in grids])
+    nst = np.array([len(g) - 1 for g in grids], dtype=np.int32)
+    if cotangent == "steps":  # padded steps repeat the final state: their cotangent is zero
+        gys = [np.concatenate([gy, np.zeros((G - len(gy),) + gy.shape[1:])]) for gy in gys]
+    out = dict(ts=ts, d=coeffs[0], c=coeffs[1], b=coeffs[2], a=coeffs[3], y0=y0, grid=grid, nsteps=nst,
+               gys=np.stack(gys), gy0=np.stack(gy0s), method=np.array(method), cotangent=np.array(cotangent))
+    if cde is not None:
+        out.update(xd=np.stack([c[0] for c in dco]), xc=np.stack([c[1] for c in dco]),
+                   xb=np.stack([c[2] for c in dco]), xa=np.stack([c[3] for c in dco]), h=np.array(h),
+                   de=np.array(de))
+    flat_layers("", params, out)
+    for l, gl in enumerate(total):
+        for k, v in gl.items():
+            out[f"grad_l{l}_{k}"] = np.asarray(v, np.float64)
+    np.savez_compressed(os.path.join(HERE, name), **out)
+
+
 def main():
     rng = np.random.default_rng(1234)
     vf_case(rng, "vf_undirected_n16_L3.npz", 4, 16, 12, "undirected", [16, 16, 16, 16])
@@ -171,6 +235,14 @@ def main():
                irregular=False)
     pid_case(rng, "pid_undirected_n16_L2.npz", 3, 16, 10, "undirected", [16, 16, 16])
     pid_case(rng, "pid_directed_n12_L3_dt0.npz", 2, 12, 8, "directed", [16, 16, 16, 16], dt0=0.05)
+    # reverse mode (training step); a fresh stream so earlier fixtures stay byte-identical
+    rng = np.random.default_rng(4321)
+    grad_case(rng, "grad_rk4_undirected_n16_L2.npz", 3, 16, 8, "undirected", [16, 16, 16], "rk4", nsteps=10)
+    grad_case(rng, "grad_tsit5c_directed_n12_L3.npz", 2, 12, 6, "directed", [16, 16, 16, 16], "tsit5",
+              dt0=0.7, cotangent="steps")
+    grad_case(rng, "grad_rk4_plain_n10_mixed.npz", 2, 10, 6, "plain", [8, 12, 8], "rk4", nsteps=7)
+    grad_case(rng, "grad_rk4_cde_n10_h8_de2.npz", 2, 10, 4, "undirected", [8, 8, 0], "rk4", nsteps=9,
+              cde=(8, 2))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,245 @@
+"""GPU: reverse mode — gncde_integrate_vjp, node_affine_grad and gncde_clip_adamw through the
+C-ABI, against the fp64 reverse-mode oracle (oracle/gncde_oracle_grad.py, pinned by finite differences in
+tests/test_oracle_grad.py) and the committed grad_* fixtures.
+
+Tolerance: RTOL_GRAD = 2e-4 relative to the max magnitude of each reference gradient tensor (fp32 forward
+checkpoints + fp32 adjoint accumulated over the steps vs fp64).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gncde_oracle as O
+from oracle import gncde_oracle_grad as OG
+from tests.golden import make_golden as MG
+
+pytestmark = pytest.mark.gpu
+
+RTOL_GRAD = 2e-4
+
+
+def rel_err(x, ref):
+    x, ref = np.asarray(x, np.float64), np.asarray(ref, np.float64)
+    return float(np.max(np.abs(x - ref)) / max(np.max(np.abs(ref)), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def G():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    import gncde
+    gncde._lib.load()
+    return gncde
+
+
+def _leaf(x):
+    return torch.tensor(np.asarray(x), dtype=torch.float32, device="cuda", requires_grad=True)
+
+
+GRAD_FIXTURES = ["grad_rk4_undirected_n16_L2.npz", "grad_tsit5c_directed_n12_L3.npz", "grad_rk4_plain_n10_mixed.npz",
+                 "grad_rk4_cde_n10_h8_de2.npz"]
+
+
+@pytest.mark.parametrize("name", GRAD_FIXTURES)
+def test_integrate_vjp_matches_golden(G, golden_dir, name):
+    z = np.load(os.path.join(golden_dir, name))
+    P = MG.load_layers(z)
+    cde = "h" in z.files
+    kw = {}
+    if cde:
+        kw = dict(data_coeffs=(z["xd"], z["xc"], z["xb"], z["xa"]), cde_hidden=int(z["h"]), cde_embed=int(z["de"]))
+    prob = G.make_problem(z["ts"], (z["d"], z["c"], z["b"], z["a"]), P.kind, P.layers, **kw)
+    names = OG.FUSION_NAMES[P.kind]
+    fus_leaves = [[_leaf(lay[nm]) for nm in names] for lay in P.layers]
+    fusion = G.layout.fusion_table_torch(P.kind, fus_leaves, prob.n).float() if names else prob.fusion
+    params = prob.params.clone().requires_grad_(True)
+    y0 = _leaf(z["y0"])
+    steps = str(z["cotangent"]) == "steps"
+    spec = G.SolverSpec(method=G._lib.RK4 if str(z["method"]) == "rk4" else G._lib.TSIT5,
+                        save_mode=G._lib.SAVE_STEPS if steps else G._lib.SAVE_T1,
+                        grid=torch.tensor(z["grid"], device="cuda"), nsteps=torch.tensor(z["nsteps"], device="cuda"))
+    out = G.autograd.solve(prob, spec, y0, params, fusion)
+    loss = (out.double() * torch.tensor(z["gys"], device="cuda")).sum()
+    loss.backward()
+    errs = {"y0": rel_err(y0.grad.cpu().numpy(), z["gy0"])}
+    gp = params.grad.cpu().numpy()
+    off = 0
+    for l, lay in enumerate(P.layers):
+        for k in ("rms_w", "rms_b", "W", "b"):
+            sz = np.asarray(lay[k]).size
+            errs[f"l{l}.{k}"] = rel_err(gp[off:off + sz].reshape(np.asarray(lay[k]).shape), z[f"grad_l{l}_{k}"])
+            off += sz
+        for j, nm in enumerate(names):
+            errs[f"l{l}.{nm}"] = rel_err(fus_leaves[l][j].grad.cpu().numpy(), z[f"grad_l{l}_{nm}"])
+    assert off == gp.size
+    worst = max(errs, key=errs.get)
+    print(f"{name}: worst {worst} {errs[worst]:.2e}")
+    for k, e in errs.items():
+        assert e <= RTOL_GRAD, (k, e)
+
+
+def test_vjp_fused_forward_checkpoints(G, golden_dir):
+    """The forward of autograd.solve takes the fused kernel when it fits; the gradient is unchanged."""
+    z = np.load(os.path.join(golden_dir, "grad_rk4_undirected_n16_L2.npz"))
+    P = MG.load_layers(z)
+    prob = G.make_problem(z["ts"], (z["d"], z["c"], z["b"], z["a"]), P.kind, P.layers)
+    spec = G.SolverSpec(method=G._lib.RK4, save_mode=G._lib.SAVE_STEPS, grid=torch.tensor(z["grid"], device="cuda"),
+                        nsteps=torch.tensor(z["nsteps"], device="cuda"))
+    assert G.integrate_path(prob, spec).startswith("fused<")
+    y0 = _leaf(z["y0"])
+    out = G.autograd.solve(prob, G.SolverSpec(method=G._lib.RK4, save_mode=G._lib.SAVE_T1, grid=spec.grid,
+                                              nsteps=spec.nsteps), y0)
+    (out.double() * torch.tensor(z["gys"], device="cuda")).sum().backward()
+    assert rel_err(y0.grad.cpu().numpy(), z["gy0"]) <= RTOL_GRAD
+
+
+def test_vjp_is_deterministic(G, golden_dir):
+    z = np.load(os.path.join(golden_dir, "grad_tsit5c_directed_n12_L3.npz"))
+    P = MG.load_layers(z)
+    prob = G.make_problem(z["ts"], (z["d"], z["c"], z["b"], z["a"]), P.kind, P.layers)
+    spec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS, grid=torch.tensor(z["grid"], device="cuda"),
+                        nsteps=torch.tensor(z["nsteps"], device="cuda"))
+    y0 = torch.tensor(z["y0"], dtype=torch.float32, device="cuda")
+    ys = G.integrate(prob, spec, y0)
+    g = torch.tensor(z["gys"], dtype=torch.float32, device="cuda")
+    a = G.integrate_vjp(prob, spec, ys, g)
+    b = G.integrate_vjp(prob, spec, ys, g)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def test_node_affine_grad_matches_torch(G):
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(3, 37, 5, generator=gen)
+    W = torch.randn(7, 5, generator=gen)
+    b = torch.randn(7, generator=gen)
+    g = torch.randn(3, 37, 7, generator=gen)
+    xr, Wr, br = (t.clone().requires_grad_(True) for t in (x, W, b))
+    (torch.einsum("rnf,of->rno", xr, Wr) + br).backward(g)  # plain fp32 torch reference
+    gx, gW, gb = G.engine.node_affine_grad(x.cuda(), W.cuda(), g.cuda())
+    for mine, ref in ((gx, xr.grad), (gW, Wr.grad), (gb, br.grad)):
+        assert torch.allclose(mine.cpu(), ref, rtol=1e-5, atol=1e-5)
+
+
+def _optax_clip_adamw(p, grads, lr, wd, b1=0.9, b2=0.999, eps=1e-8, max_norm=1.0):
+    """numpy restatement of optax.chain(clip_by_global_norm, adamw) (optimiser_configs.py:70-88)."""
+    p = p.astype(np.float64).copy()
+    m = np.zeros_like(p)
+    v = np.zeros_like(p)
+    for k, g in enumerate(grads, start=1):
+        norm = np.sqrt(np.sum(g.astype(np.float64) ** 2))
+        g = g if norm < max_norm else g / norm * max_norm
+        m = b1 * m + (1 - b1) * g
+        v = b2 * v + (1 - b2) * g * g
+        mh, vh = m / (1 - b1 ** k), v / (1 - b2 ** k)
+        p = p - lr * (mh / (np.sqrt(vh) + eps) + wd * p)
+    return p
+
+
+def test_clip_adamw_matches_optax_restatement(G):
+    rng = np.random.default_rng(5)
+    P = 1500
+    p0 = rng.standard_normal(P).astype(np.float32)
+    grads = [(rng.standard_normal(P) * s).astype(np.float32) for s in (0.001, 0.5, 0.01)]  # clip on step 2
+    flat = torch.tensor(p0, device="cuda")
+    m, v = torch.zeros_like(flat), torch.zeros_like(flat)
+    for k, g in enumerate(grads, start=1):
+        st = G.engine.clip_adamw(flat, torch.tensor(g, device="cuda"), m, v, k, 1e-2, 0.9, 0.999, 1e-8, 1e-4, 1.0)
+    ref = _optax_clip_adamw(p0, grads, 1e-2, 1e-4)
+    assert np.max(np.abs(flat.cpu().numpy() - ref)) <= 1e-5
+    assert abs(float(st[0]) - np.sqrt(np.sum(grads[-1].astype(np.float64) ** 2))) <= 1e-4
+    assert abs(float(st[1]) - np.abs(grads[-1]).max()) <= 1e-7
+
+
+def _graph_controls(rng, B, n, T):
+    ts_l, co_l = [], []
+    for _ in range(B):
+        ts, X = O.make_graph_control(rng, n, T)
+        ts_l.append(ts)
+        co_l.append(O.backward_hermite_coefficients(ts, X))
+    return np.stack(ts_l), tuple(np.stack([c[q] for c in co_l]) for q in range(4))
+
+
+def test_graph_neural_cde_loss_gradient_matches_oracle(G):
+    """GraphNeuralCDE.loss_terms (knot-aligned RK4, SaveAt(ts) states, read-out, MSE) — every module
+    parameter's gradient against the oracle's reverse mode of the same composition."""
+    from gncde.layout import knot_grid
+    from gncde.models import GraphNeuralCDE, vector_fields as V
+    rng = np.random.default_rng(31)
+    B, n, T, h, m = 3, 12, 5, 16, 3
+    ts, coeffs = _graph_controls(rng, B, n, T)
+    x0 = rng.standard_normal((B, n, 1))
+    labels = rng.standard_normal((B, T, n))
+    vf = V.PermEquivGraphVectorField(h, h, h, 2, 16, n, key=4)
+    model = GraphNeuralCDE({"hidden_dim": h}, vf, "cubic", 6, solver={"method": "rk4", "steps_per_interval": m})
+    model.to("cuda")
+    sse, cnt = model.loss_terms(torch.tensor(ts), coeffs, torch.tensor(x0), torch.tensor(labels))
+    sse.backward()
+    # oracle
+    P = O.VFParams("undirected", [{k: v.double().cpu().numpy() for k, v in d.items()} for d in vf.layer_dicts()])
+    Wi, bi = (model.initial_linear.weight.detach().double().cpu().numpy(),
+              model.initial_linear.bias.detach().double().cpu().numpy())
+    Wf, bf = model.final_linear.weight.detach().double().cpu().numpy(), model.final_linear.bias.detach().double().cpu().numpy()
+    g_Wi, g_bi, g_Wf, g_bf, total, sse_ref = 0, 0, 0, 0, None, 0.0
+    for b in range(B):
+        ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
+        f = lambda t, y, ctrl=ctrl: O.vector_field(P, t, y, ctrl)  # noqa: E731
+        fv = lambda t, y, g, ctrl=ctrl: OG.vector_field_vjp(P, t, y, ctrl, g)  # noqa: E731
+        grid = knot_grid(ts[b], m)
+        y0 = x0[b] @ Wi.T + bi
+        ys, _ = O.solve_fixed_grid(f, grid, y0, "rk4", save_every_step=True, time_dtype=np.float32)
+        yk = ys[np.arange(T) * m]
+        pred = (yk @ Wf.T + bf)[..., 0]
+        r = pred - labels[b]
+        sse_ref += float(np.sum(r * r))
+        gpred = 2 * r[..., None]
+        g_Wf = g_Wf + np.einsum("tno,tnh->oh", gpred, yk)
+        g_bf = g_bf + gpred.sum(axis=(0, 1))
+        gsteps = np.zeros_like(ys)
+        gsteps[np.arange(T) * m] = gpred @ Wf
+        gy0, gr = OG.solve_fixed_grid_vjp(f, fv, grid, y0, "rk4", g_steps=gsteps)
+        total = OG._acc(total, gr)
+        g_Wi = g_Wi + gy0.T @ x0[b]
+        g_bi = g_bi + gy0.sum(axis=0)
+    assert cnt == B * T * n
+    assert abs(float(sse) - sse_ref) <= 1e-4 * sse_ref
+    checks = {"initial_linear.weight": g_Wi, "initial_linear.bias": g_bi, "final_linear.weight": g_Wf,
+              "final_linear.bias": g_bf}
+    for l in range(2):
+        pre = f"vector_field.gnn_layers.{l}."
+        for nm in O.UNDIRECTED_PARAMS:
+            checks[pre + nm] = total[l][nm]
+        checks[pre + "conv_layer.linear.weight"] = total[l]["W"]
+        checks[pre + "conv_layer.linear.bias"] = total[l]["b"]
+        checks[pre + "conv_layer.norm.weight"] = total[l]["rms_w"]
+        checks[pre + "conv_layer.norm.bias"] = total[l]["rms_b"]
+    named = dict(model.named_parameters())
+    for k, ref in checks.items():
+        e = rel_err(named[k].grad.cpu().numpy(), ref)
+        assert e <= RTOL_GRAD, (k, e)
+
+
+def test_make_step_trains(G):
+    """A few ClipAdamW steps on a small GraphNeuralCDE decrease the loss; the flat buffer is the model."""
+    from gncde import train
+    from gncde.models import GraphNeuralCDE, vector_fields as V
+    rng = np.random.default_rng(32)
+    B, n, T, h = 4, 16, 6, 16
+    ts, coeffs = _graph_controls(rng, B, n, T)
+    x0 = torch.tensor(rng.standard_normal((B, n, 1)))
+    labels = torch.tensor(np.tanh(rng.standard_normal((B, T, n))))
+    vf = V.PermEquivGraphVectorField(h, h, h, 2, 16, n, key=1)
+    model = GraphNeuralCDE({"hidden_dim": h}, vf, "cubic", 2, solver={"method": "rk4", "steps_per_interval": 2})
+    model.to("cuda")
+    opt = train.ClipAdamW(model, learning_rate=1e-2, weight_decay=1e-4)
+    losses = []
+    for _ in range(8):
+        loss, mg, mu = train.make_step(opt, model.loss_terms, torch.tensor(ts), coeffs, x0, labels)
+        losses.append(float(loss))
+        assert np.isfinite(float(mg)) and 0.0 < float(mu) < 1.0
+    assert losses[-1] < losses[0]
+    # the module's parameters ARE the optimiser's flat buffer (updated in place by the kernel)
+    for p in model.parameters():
+        assert p.untyped_storage().data_ptr() == opt.flat.untyped_storage().data_ptr()
