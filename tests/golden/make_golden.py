@@ -188,12 +188,22 @@ def grad_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None, cot
         g = O.rk4_grid(ts[b, 0], ts[b, -1], nsteps) if method == "rk4" else O.constant_grid(ts[b, 0], ts[b, -1],
                                                                                              dt0)
         grids.append(g)
-        if cotangent == "final":
-            gy = rng.standard_normal((n, ds))
-            gy0, gr = OG.solve_fixed_grid_vjp(f, fv, g, y0[b], method, g_final=gy)
+        gy = rng.standard_normal((n, ds) if cotangent == "final" else (len(g), n, ds))
+        kw = dict(g_final=gy) if cotangent == "final" else dict(g_steps=gy)
+        # ReLU networks have gradients that jump where a pre-activation crosses 0: an fp32 solve (GPU or
+        # reference) lands on the other side of a nearby kink and legitimately differs by ~1%.  Keep only
+        # samples whose gradient is stable under a 1e-6 relative perturbation of y0 (redraw y0 otherwise).
+        for _ in range(20):
+            gy0, gr = OG.solve_fixed_grid_vjp(f, fv, g, y0[b], method, **kw)
+            gy0p, grp = OG.solve_fixed_grid_vjp(f, fv, g, y0[b] * (1 + 1e-6), method, **kw)
+            va, vb = OG.grads_to_vector(gr, kind), OG.grads_to_vector(grp, kind)
+            spread = max(np.max(np.abs(gy0p - gy0)) / np.max(np.abs(gy0)),
+                         np.max(np.abs(vb - va)) / np.max(np.abs(va)))
+            if spread < 1e-5:
+                break
+            y0[b] = rng.standard_normal((n, ds))
         else:
-            gy = rng.standard_normal((len(g), n, ds))
-            gy0, gr = OG.solve_fixed_grid_vjp(f, fv, g, y0[b], method, g_steps=gy)
+            raise RuntimeError(f"{name}: no gradient-stable sample found")
         gys.append(gy)
         gy0s.append(gy0)
         total = OG._acc(total, gr)

@@ -120,8 +120,9 @@ def test_pgt_driver_matches_oracle(G):
     x0 = np.stack(x0s)
     vf = V.PermEquivGraphVectorField(h, h, h * de * 2, 2, de, n, key=9)
     model = PGTGraphNeuralCDE({"hidden_dim": h, "data_dim": data_dim, "feature_dim": 1}, vf, "cubic", 5)
-    out = model.batched(torch.tensor(ts), ca, cx, torch.tensor(x0)).cpu().numpy()
-    per_node = model.batched(torch.tensor(ts), ca, cx, torch.tensor(x0), global_readout=False).cpu().numpy()
+    with torch.no_grad():  # batched() records a backward (GPU adjoint) when grad is enabled
+        out = model.batched(torch.tensor(ts), ca, cx, torch.tensor(x0)).cpu().numpy()
+        per_node = model.batched(torch.tensor(ts), ca, cx, torch.tensor(x0), global_readout=False).cpu().numpy()
     P = oracle_params(vf)
 
     def mlp(m, x):
