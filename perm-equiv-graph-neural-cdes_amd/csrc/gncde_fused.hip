@@ -7,7 +7,7 @@
 //
 //   per distinct stage time t (RK4: 2 per step, since k2/k3 share t+h/2 and k4/k1' share t+h):
 //     interval index (wave ballot over ts in LDS) -> Horner of the interval's (d,c,b,a) [4,n,n]
-//     (coalesced float4 HBM/L2 reads) -> A(t), dA(t) in LDS (XOR-swizzled, conflict-free row AND
+//     (coalesced float4 HBM/L2 reads) -> A(t), dA(t) in LDS (padded row stride NP+1: conflict-free row AND
 //     column access) -> row/col sums, diagonals, totals -> each lane builds its slice of
 //     (I + Abar_l) for every layer l IN REGISTERS (the MFMA B-operand layout), fusing the
 //     15-term equivariant basis (layers.py:102-160) into the operand construction.
