@@ -109,6 +109,7 @@ int gncde_integrate(const GncdeProblem* prob, const GncdeSolver* solver, const f
 
 size_t gncde_vjp_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* solver) {
   if (validate_problem(prob) != GNCDE_OK || validate_solver(prob, solver) != GNCDE_OK) return 0;
+  if (stage_vjp_supported(*prob, *solver)) return stage_vjp_workspace(*prob);
   return generic_vjp_workspace(*prob, *solver);
 }
 
@@ -130,6 +131,10 @@ int gncde_integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, con
     return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
   }
   if (!ys || !gys || !gy0) return GNCDE_ERR_ARG;
+  if (stage_vjp_supported(*prob, *solver)) {
+    if (workspace_bytes < stage_vjp_workspace(*prob) || !workspace) return GNCDE_ERR_WORKSPACE;
+    return stage_integrate_vjp(*prob, *solver, ys, gys, gy0, gparams, gfusion, static_cast<char*>(workspace), st);
+  }
   if (workspace_bytes < generic_vjp_workspace(*prob, *solver) || !workspace) return GNCDE_ERR_WORKSPACE;
   return generic_integrate_vjp(*prob, *solver, ys, gys, gy0, gparams, gfusion, static_cast<char*>(workspace), st);
 }

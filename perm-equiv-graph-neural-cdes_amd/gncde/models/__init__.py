@@ -142,13 +142,16 @@ class GraphNeuralCDE(nn.Module):
         control = CubicInterpolation(ts, coeffs_adj)
         ts_d = control.graph_layout()[0]
         x0 = torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device)
+        return self.predict_packed(self.vector_field.problem(control), x0, self._spec(ts_d, evolving_out))
+
+    def predict_packed(self, prob: engine.Problem, x0: torch.Tensor, spec: engine.SolverSpec) -> torch.Tensor:
+        """``predict`` on an already packed device Problem (coefficients resident in HBM): encoder ->
+        differentiable GPU solve (this module's parameters) -> read-out."""
         y0 = _affine(self.initial_linear, x0)
-        prob = self.vector_field.problem(control)
-        params, fusion = self.vector_field.diff_tensors(prob.n, ts_d.device)
-        spec = self._spec(ts_d, evolving_out)
+        params, fusion = self.vector_field.diff_tensors(prob.n, x0.device)
         ys = autograd.solve(prob, spec, y0, params, fusion)
         if spec.save_mode == _lib.SAVE_STEPS:
-            ys = self._knot_states(ys, ts_d.shape[1])
+            ys = self._knot_states(ys, prob.T)
         return _affine(self.final_linear, ys)
 
     def loss_terms(self, ts, coeffs_adj, x0, labels, evolving_out=True):

@@ -34,6 +34,18 @@ def grid_adjacency(side: int, device="cuda") -> torch.Tensor:
     return A
 
 
+def community_adjacency(n: int, communities: int = 4, p_in: float = 0.3, p_out: float = 0.02, seed: int = 1234,
+                        device="cuda") -> torch.Tensor:
+    """Undirected stochastic-block graph on exactly n nodes (the gene-dynamics ``graph_type: community``
+    shape of SURVEY §8d C4; networkx is not used)."""
+    g = torch.Generator().manual_seed(seed)
+    block = torch.arange(n) * communities // n
+    same = block[:, None] == block[None, :]
+    p = torch.where(same, torch.tensor(p_in), torch.tensor(p_out))
+    up = torch.triu((torch.rand(n, n, generator=g) < p).float(), diagonal=1)
+    return (up + up.T).to(device)
+
+
 def normalized_laplacian(A: torch.Tensor) -> torch.Tensor:
     """I - D_out^-1/2 (A + I) D_in^-1/2, batched over leading dims (misc.py:83-99)."""
     n = A.shape[-1]
@@ -78,12 +90,19 @@ def init_layers(kind: str, dims, generator: torch.Generator, fusion_scale: float
 
 def heat_batch(B: int, num_nodes: int = 64, hidden: int = 16, num_layers: int = 3, T: int = 120,
                final_time: float = 5.0, events: int = 12, kind: str = "undirected", seed: int = 1234,
-               device="cuda", chunk: int = 128):
-    """Returns (Problem, y0 [B, n, hidden], layers).  n = ceil(sqrt(num_nodes))^2 like the reference grid."""
-    side = int(math.ceil(math.sqrt(num_nodes)))
-    n = side * side
+               device="cuda", chunk: int = 128, graph: str = "grid"):
+    """Returns (Problem, y0 [B, n, hidden], layers).  graph "grid": n = ceil(sqrt(num_nodes))^2 like the
+    reference grid; "community": exactly num_nodes nodes in 4 blocks (config 4)."""
     g = torch.Generator(device="cpu").manual_seed(seed)
-    base = grid_adjacency(side, device=device)
+    if graph == "grid":
+        side = int(math.ceil(math.sqrt(num_nodes)))
+        n = side * side
+        base = grid_adjacency(side, device=device)
+    elif graph == "community":
+        n = num_nodes
+        base = community_adjacency(n, seed=seed, device=device)
+    else:
+        raise ValueError(graph)
     inner = torch.sort(torch.rand(B, T - 2, generator=g) * final_time, dim=1).values
     ts = torch.cat([torch.zeros(B, 1), inner, torch.full((B, 1), final_time)], dim=1).to(device)
     coef = torch.empty(B, T - 1, 4, n, n, device=device)
