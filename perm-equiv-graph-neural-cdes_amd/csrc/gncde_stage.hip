@@ -90,27 +90,40 @@ __global__ void k_stage_prep(const float* __restrict__ params, float* __restrict
   }
 }
 
-struct StageArgs {
-  int n, T;
+enum { kEval1 = 0, kEval2 = 1, kVjpMid = 2, kVjpPair = 3, kBoundary = 4 };
+
+struct RevArgs {
+  int n, T, G, k, S, stage, has_next, has_cur, write_next;
   const float* ts;
   const float* coef;
   const float* tcoef;
   const float* fusion;
-  const float* ops;   // [L, kOpStride]
-  const float* t;     // [B] stage time
-  const float* h;     // [B] step size (scales the cotangent scatter)
-  const float* U;     // [B, n, H]
-  const float* gK;    // [B, n, H] (VJP)
-  float* out;         // EVAL: K [B, n, H]
-  float* gp;          // VJP: [B, L, kGradStride] (+=)
-  float* acc[7];      // VJP: acc[j][b] += coef[j] * (scale_h[j] ? h_b : 1) * gU[b]
-  float accw[7];
-  int scale_h[7];
-  int nacc;
+  const float* ops;     // [L, kOpStride]
+  const float* grid;    // [B, G]
+  const int32_t* nsteps;
+  const float* ys;      // checkpoints [B, G, n, H]
+  const float* gys;     // saved-state cotangents [B, G, n, H] (SAVE_STEPS) or nullptr
+  float* K[6];          // stage values      [B, n, H] each
+  float* U[6];          // stage inputs
+  float* gK[6];         // stage cotangents
+  float* gyacc;         // cotangent of y_k being accumulated
+  float* lam;           // lambda at the last grid point (boundary with has_next == 0)
+  float* gy0;           // boundary with has_cur == 0: output
+  float* gp;            // [B, L, kGradStride] (+=)
+  float c[6], bw[6], a[6][6];
 };
 
-template <int NP, int L, bool VJP>
-__global__ void __launch_bounds__(NP * 4, 1) k_stage(StageArgs a) {
+// Reverse-sweep kernels.  PROG:
+//   kEval1    stage `stage` of step k: U = y_k + h sum_j a[stage][j] K_j; K_stage = VF(U)   (write_next: also
+//             U_{stage+1}, the input of the last stage)
+//   kEval2    RK4 stages 1, 2 (shared time t + h/2): U1, K1, U2, K2 and U3 = y + h K2
+//   kVjpMid   one middle stage: gU = J^T gK_stage; gyacc += gU; gK_j += h a[stage][j] gU
+//   kVjpPair  RK4 stages 2 then 1 at t + h/2 (gK1 updated in registers between them)
+//   kBoundary at t_{k+1}: stage 0 of step k+1 (has_next) -> lambda_{k+1}; seeds gK_j = h b_j lambda of step
+//             k and its last stage (has_cur) -> gyacc, gK_j.  has_cur == 0 writes gy0 = lambda_0.
+template <int NP, int L, int PROG>
+__global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
+  constexpr bool VJP = PROG >= kVjpMid;
   constexpr int NT = NP * 4;
   constexpr int NW = NP / 16;
   constexpr int KS = NP / 4;
@@ -132,200 +145,205 @@ __global__ void __launch_bounds__(NP * 4, 1) k_stage(StageArgs a) {
   const int w = tid >> 6;
   const int lane = tid & 63;
   const int lo = lane & 15, hi = lane >> 4;
-  const int n = a.n, T = a.T;
+  const int n = a.n, T = a.T, G = a.G;
   const size_t nn = (size_t)n * n;
   const int node = 16 * w + lo;
   const bool node_ok = node < n;
+  const size_t E = (size_t)n * H;
+  const size_t rowoff = (size_t)b * E + (size_t)(node_ok ? node : 0) * H + 4 * hi;
+  auto rowk = [&](int k) -> size_t { return ((size_t)b * G + k) * E + (size_t)(node_ok ? node : 0) * H + 4 * hi; };
   float* sA = sR0;
   float* sdA = sR0 + AS;
-  float* sW = sVec + 6 * NP;        // w_l[i]
-  float* sV = sVec + (6 + L) * NP;  // v_l[k]
+  float* sW = sVec + 6 * NP;
+  float* sV = sVec + (6 + L) * NP;
 
   for (int j = tid; j < T; j += NT) sTs[j] = a.ts[(size_t)b * T + j];
   for (int j = tid; j < L * GNCDE_FC; j += NT) sFus[j] = a.fusion[j];
-  __syncthreads();
 
-  // ---- form the interval at t: A, dA images, reductions, fusion vectors ------------------------------
-  const float t = a.t[b];
-  int cnt = 0;
-  for (int j0 = 0; j0 < T; j0 += 64) {
-    const int j = j0 + lane;
-    const bool p = (j < T) && (sTs[j < T ? j : 0] < t);
-    cnt += __popcll(__ballot(p));
-  }
-  int idx = cnt - 1;
-  idx = idx < 0 ? 0 : (idx > T - 2 ? T - 2 : idx);
-  const float f = t - sTs[idx];
-  const float f3 = 3.0f * f;
-  const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
-  if (n == NP) {
-    const float4* c4 = reinterpret_cast<const float4*>(cb);
-    constexpr int NQ = NP * NP / 4;
-    for (int e4 = tid; e4 < NQ; e4 += NT) {
-      const float4 d = c4[e4], c = c4[NQ + e4], bb = c4[2 * NQ + e4], aa = c4[3 * NQ + e4];
-      const int r = (e4 * 4) / NP, k = (e4 * 4) % NP;
-      float* pa = sA + swz<NP>(r, k);
-      float* pd = sdA + swz<NP>(r, k);
-      pa[0] = fmaf(f, fmaf(f, fmaf(f, d.x, c.x), bb.x), aa.x);
-      pa[1] = fmaf(f, fmaf(f, fmaf(f, d.y, c.y), bb.y), aa.y);
-      pa[2] = fmaf(f, fmaf(f, fmaf(f, d.z, c.z), bb.z), aa.z);
-      pa[3] = fmaf(f, fmaf(f, fmaf(f, d.w, c.w), bb.w), aa.w);
-      pd[0] = fmaf(f, fmaf(f3, d.x, 2.0f * c.x), bb.x);
-      pd[1] = fmaf(f, fmaf(f3, d.y, 2.0f * c.y), bb.y);
-      pd[2] = fmaf(f, fmaf(f3, d.z, 2.0f * c.z), bb.z);
-      pd[3] = fmaf(f, fmaf(f3, d.w, 2.0f * c.w), bb.w);
-    }
-  } else {
-    for (int e = tid; e < NP * NP; e += NT) {
-      const int r = e / NP, k = e % NP;
-      float va = 0.f, vd = 0.f;
-      if (r < n && k < n) {
-        const int ce = r * n + k;
-        const float d = cb[ce], c = cb[nn + ce], bb = cb[2 * nn + ce], aa = cb[3 * nn + ce];
-        va = fmaf(f, fmaf(f, fmaf(f, d, c), bb), aa);
-        vd = fmaf(f, fmaf(f3, d, 2.0f * c), bb);
-      }
-      sA[swz<NP>(r, k)] = va;
-      sdA[swz<NP>(r, k)] = vd;
-    }
-  }
-  __syncthreads();
-  {
-    const int q = tid / NP, j = tid % NP;
-    const float* M = (q & 1) ? sdA : sA;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-    if (q < 2) {
-      const float* row = M + swz<NP>(j, 0);
-      for (int k = 0; k < NP; k += 4) {
-        acc0 += row[k];
-        acc1 += row[k + 1];
-        acc2 += row[k + 2];
-        acc3 += row[k + 3];
-      }
-      sVec[(4 + q) * NP + j] = M[swz<NP>(j, j)];
-    } else {
-      const float* col = M + j;
-      for (int k = 0; k < NP; k += 4) {
-        acc0 += col[swz<NP>(k, 0)];
-        acc1 += col[swz<NP>(k + 1, 0)];
-        acc2 += col[swz<NP>(k + 2, 0)];
-        acc3 += col[swz<NP>(k + 3, 0)];
-      }
-    }
-    sVec[q * NP + j] = (acc0 + acc1) + (acc2 + acc3);
-  }
-  __syncthreads();
-  float s = 0.f, sd = 0.f;
-  for (int j = lane; j < NP; j += 64) {
-    s += sVec[j];
-    sd += sVec[NP + j];
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    s += __shfl_xor(s, o);
-    sd += __shfl_xor(sd, o);
-  }
-  for (int e = tid; e < L * NP; e += NT) {
-    const int l = e / NP, k = e % NP;
-    const float* fc = sFus + l * GNCDE_FC;
-    const float r = sVec[k], rd = sVec[NP + k], c = sVec[2 * NP + k], cd = sVec[3 * NP + k];
-    sV[e] = fc[GNCDE_FC_VR_A] * r + fc[GNCDE_FC_VR_DA] * rd + fc[GNCDE_FC_VC_A] * c + fc[GNCDE_FC_VC_DA] * cd;
-    const float wv = fc[GNCDE_FC_WR_A] * r + fc[GNCDE_FC_WR_DA] * rd + fc[GNCDE_FC_WC_A] * c +
-                     fc[GNCDE_FC_WC_DA] * cd + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
-    sW[e] = k < n ? wv : 0.f;
-  }
-  const float rn = sVec[node], rdn = sVec[NP + node], cn = sVec[2 * NP + node], cdn = sVec[3 * NP + node];
-  const float dgn = sVec[4 * NP + node], dgdn = sVec[5 * NP + node];
+  // step geometry of this sample (padded steps past nsteps have h = 0 and contribute nothing)
+  const float* gr = a.grid + (size_t)b * G;
+  int ns = a.nsteps[b];
+  ns = ns < 0 ? 0 : (ns > G - 1 ? G - 1 : ns);
+  auto geom = [&](int k, float& t, float& h) {
+    t = k < ns ? gr[k] : gr[ns];
+    h = k < ns ? gr[k + 1] - gr[k] : 0.f;
+  };
+
+  // ---- form: interval at t -> LDS images, reductions, fusion vectors, per-node terms ------------------
   float ul[L];
+  float tg = 0.f, rn = 0.f, rdn = 0.f, cn = 0.f, cdn = 0.f, dgn = 0.f, dgdn = 0.f, s = 0.f, sd = 0.f;
+  auto form = [&](float t) __attribute__((always_inline)) {
+    __syncthreads();  // previous readers of the LDS images / staging buffers are done
+    int cnt = 0;
+    for (int j0 = 0; j0 < T; j0 += 64) {
+      const int j = j0 + lane;
+      const bool p = (j < T) && (sTs[j < T ? j : 0] < t);
+      cnt += __popcll(__ballot(p));
+    }
+    int idx = cnt - 1;
+    idx = idx < 0 ? 0 : (idx > T - 2 ? T - 2 : idx);
+    const float f = t - sTs[idx];
+    const float f3 = 3.0f * f;
+    const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
+    if (n == NP) {
+      const float4* c4 = reinterpret_cast<const float4*>(cb);
+      constexpr int NQ = NP * NP / 4;
+      for (int e4 = tid; e4 < NQ; e4 += NT) {
+        const float4 d = c4[e4], c = c4[NQ + e4], bb = c4[2 * NQ + e4], aa = c4[3 * NQ + e4];
+        const int r = (e4 * 4) / NP, k = (e4 * 4) % NP;
+        float* pa = sA + swz<NP>(r, k);
+        float* pd = sdA + swz<NP>(r, k);
+        pa[0] = fmaf(f, fmaf(f, fmaf(f, d.x, c.x), bb.x), aa.x);
+        pa[1] = fmaf(f, fmaf(f, fmaf(f, d.y, c.y), bb.y), aa.y);
+        pa[2] = fmaf(f, fmaf(f, fmaf(f, d.z, c.z), bb.z), aa.z);
+        pa[3] = fmaf(f, fmaf(f, fmaf(f, d.w, c.w), bb.w), aa.w);
+        pd[0] = fmaf(f, fmaf(f3, d.x, 2.0f * c.x), bb.x);
+        pd[1] = fmaf(f, fmaf(f3, d.y, 2.0f * c.y), bb.y);
+        pd[2] = fmaf(f, fmaf(f3, d.z, 2.0f * c.z), bb.z);
+        pd[3] = fmaf(f, fmaf(f3, d.w, 2.0f * c.w), bb.w);
+      }
+    } else {
+      for (int e = tid; e < NP * NP; e += NT) {
+        const int r = e / NP, k = e % NP;
+        float va = 0.f, vd = 0.f;
+        if (r < n && k < n) {
+          const int ce = r * n + k;
+          const float d = cb[ce], c = cb[nn + ce], bb = cb[2 * nn + ce], aa = cb[3 * nn + ce];
+          va = fmaf(f, fmaf(f, fmaf(f, d, c), bb), aa);
+          vd = fmaf(f, fmaf(f3, d, 2.0f * c), bb);
+        }
+        sA[swz<NP>(r, k)] = va;
+        sdA[swz<NP>(r, k)] = vd;
+      }
+    }
+    __syncthreads();
+    {
+      const int q = tid / NP, j = tid % NP;
+      const float* M = (q & 1) ? sdA : sA;
+      float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+      if (q < 2) {
+        const float* row = M + swz<NP>(j, 0);
+        for (int k = 0; k < NP; k += 4) {
+          acc0 += row[k];
+          acc1 += row[k + 1];
+          acc2 += row[k + 2];
+          acc3 += row[k + 3];
+        }
+        sVec[(4 + q) * NP + j] = M[swz<NP>(j, j)];
+      } else {
+        const float* col = M + j;
+        for (int k = 0; k < NP; k += 4) {
+          acc0 += col[swz<NP>(k, 0)];
+          acc1 += col[swz<NP>(k + 1, 0)];
+          acc2 += col[swz<NP>(k + 2, 0)];
+          acc3 += col[swz<NP>(k + 3, 0)];
+        }
+      }
+      sVec[q * NP + j] = (acc0 + acc1) + (acc2 + acc3);
+    }
+    __syncthreads();
+    s = 0.f;
+    sd = 0.f;
+    for (int j = lane; j < NP; j += 64) {
+      s += sVec[j];
+      sd += sVec[NP + j];
+    }
 #pragma unroll
-  for (int l = 0; l < L; ++l) {
-    const float* fc = sFus + l * GNCDE_FC;
-    ul[l] = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dgn + fc[GNCDE_FC_UD_DA] * dgdn + fc[GNCDE_FC_UR_A] * rn +
-            fc[GNCDE_FC_UR_DA] * rdn + fc[GNCDE_FC_UC_A] * cn + fc[GNCDE_FC_UC_DA] * cdn + fc[GNCDE_FC_US_A] * s +
-            fc[GNCDE_FC_US_DA] * sd;
-  }
-  float tg = 0.f;
-  {
+    for (int o = 32; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o);
+      sd += __shfl_xor(sd, o);
+    }
+    for (int e = tid; e < L * NP; e += NT) {
+      const int l = e / NP, k = e % NP;
+      const float* fc = sFus + l * GNCDE_FC;
+      const float r = sVec[k], rd = sVec[NP + k], c = sVec[2 * NP + k], cd = sVec[3 * NP + k];
+      sV[e] = fc[GNCDE_FC_VR_A] * r + fc[GNCDE_FC_VR_DA] * rd + fc[GNCDE_FC_VC_A] * c + fc[GNCDE_FC_VC_DA] * cd;
+      const float wv = fc[GNCDE_FC_WR_A] * r + fc[GNCDE_FC_WR_DA] * rd + fc[GNCDE_FC_WC_A] * c +
+                       fc[GNCDE_FC_WC_DA] * cd + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
+      sW[e] = k < n ? wv : 0.f;
+    }
+    rn = sVec[node];
+    rdn = sVec[NP + node];
+    cn = sVec[2 * NP + node];
+    cdn = sVec[3 * NP + node];
+    dgn = sVec[4 * NP + node];
+    dgdn = sVec[5 * NP + node];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      const float* fc = sFus + l * GNCDE_FC;
+      ul[l] = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dgn + fc[GNCDE_FC_UD_DA] * dgdn + fc[GNCDE_FC_UR_A] * rn +
+              fc[GNCDE_FC_UR_DA] * rdn + fc[GNCDE_FC_UC_A] * cn + fc[GNCDE_FC_UC_DA] * cdn + fc[GNCDE_FC_US_A] * s +
+              fc[GNCDE_FC_US_DA] * sd;
+    }
     const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
     const int ii = node_ok ? node : 0;
     tg = node_ok ? fmaf(f, fmaf(f3, tc[ii], 2.0f * tc[n + ii]), tc[2 * n + ii]) : 0.f;
-  }
-  __syncthreads();
+    __syncthreads();  // sW / sV visible
+  };
 
-  // ---- forward, activations kept ------------------------------------------------------------------------
-  const size_t rowoff = ((size_t)b * n + (node_ok ? node : 0)) * H + 4 * hi;
-  float Z[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) Z[r] = node_ok ? a.U[rowoff + r] : 0.f;
+  // ---- forward at the formed time, activations kept for the backward ----------------------------------
   float Zin[L][4], invl[L], ml[L][4], prel[L][4];
   const int oAr = swz<NP>(node, hi * KS), oAc = swz<NP>(hi * KS, node);
+  auto forward = [&](float (&Z)[4]) __attribute__((always_inline)) {
 #pragma unroll
-  for (int l = 0; l < L; ++l) {
-    const float* op = a.ops + (size_t)l * kOpStride;
-    const float* fc = sFus + l * GNCDE_FC;
+    for (int l = 0; l < L; ++l) {
+      const float* op = a.ops + (size_t)l * kOpStride;
+      const float* fc = sFus + l * GNCDE_FC;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Zin[l][r] = Z[r];
-    float ss = 0.f;
+      for (int r = 0; r < 4; ++r) Zin[l][r] = Z[r];
+      float ss = 0.f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ss = fmaf(Z[r], Z[r], ss);
-    ss = xor_sum4(ss);
-    const float inv = 1.0f / sqrtf(ss / (float)H + 1e-5f);
-    invl[l] = inv;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < 4; ++r) ss = fmaf(Z[r], Z[r], ss);
+      ss = xor_sum4(ss);
+      const float inv = 1.0f / sqrtf(ss / (float)H + 1e-5f);
+      invl[l] = inv;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc = mfma4(op[kOpWf + r * 64 + lane], Z[r], acc);
-    float mown[4];
+      for (int r = 0; r < 4; ++r) acc = mfma4(op[kOpWf + r * 64 + lane], Z[r], acc);
+      float mown[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      mown[r] = fmaf(inv, acc[r], op[kOpBias + 4 * hi + r]);
-      ml[l][r] = node_ok ? mown[r] : 0.f;
-      sMb[(4 * hi + r) * MS + node] = ml[l][r];
+      for (int r = 0; r < 4; ++r) {
+        mown[r] = fmaf(inv, acc[r], op[kOpBias + 4 * hi + r]);
+        ml[l][r] = node_ok ? mown[r] : 0.f;
+        sMb[(4 * hi + r) * MS + node] = ml[l][r];
+      }
+      float Ab[KS];
+      {
+        const float e0 = fc[GNCDE_FC_E_A], e1 = fc[GNCDE_FC_E_DA], e2 = fc[GNCDE_FC_ET_A], e3 = fc[GNCDE_FC_ET_DA];
+        const float wi = sW[l * NP + node];
+        const float* vv = sV + l * NP + hi * KS;
+#pragma unroll
+        for (int sl = 0; sl < KS; ++sl)
+          Ab[sl] = fmaf(e0, sA[oAr + sl], fmaf(e1, sdA[oAr + sl], fmaf(e2, sA[oAc + sl * (NP + 1)],
+                        fmaf(e3, sdA[oAc + sl * (NP + 1)], wi + vv[sl]))));
+      }
+      __syncthreads();
+      floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+      const float* mrow = sMb + lo * MS + hi * KS;
+#pragma unroll
+      for (int q = 0; q < KS / 4; ++q) {
+        const float4 mv = *reinterpret_cast<const float4*>(mrow + 4 * q);
+        c0 = mfma4(mv.x, Ab[4 * q + 0], c0);
+        c1 = mfma4(mv.y, Ab[4 * q + 1], c1);
+        c0 = mfma4(mv.z, Ab[4 * q + 2], c0);
+        c1 = mfma4(mv.w, Ab[4 * q + 3], c1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = fmaf(ul[l], mown[r], c0[r] + c1[r]);
+        prel[l][r] = z;
+        Z[r] = (l < L - 1) ? fmaxf(z, 0.f) : z;
+      }
+      __syncthreads();  // m^T reads done before sMb is rewritten
     }
-    // this layer's operand slice: row `node` of (Abar - diag(u)), columns k = hi*KS + sl
-    float Ab[KS];
-    {
-      const float e0 = fc[GNCDE_FC_E_A], e1 = fc[GNCDE_FC_E_DA], e2 = fc[GNCDE_FC_ET_A], e3 = fc[GNCDE_FC_ET_DA];
-      const float wi = sW[l * NP + node];
-      const float* vv = sV + l * NP + hi * KS;
 #pragma unroll
-      for (int sl = 0; sl < KS; ++sl)
-        Ab[sl] = fmaf(e0, sA[oAr + sl], fmaf(e1, sdA[oAr + sl], fmaf(e2, sA[oAc + sl * (NP + 1)],
-                      fmaf(e3, sdA[oAc + sl * (NP + 1)], wi + vv[sl]))));
-    }
-    __syncthreads();
-    floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-    const float* mrow = sMb + lo * MS + hi * KS;
-#pragma unroll
-    for (int q = 0; q < KS / 4; ++q) {
-      const float4 mv = *reinterpret_cast<const float4*>(mrow + 4 * q);
-      c0 = mfma4(mv.x, Ab[4 * q + 0], c0);
-      c1 = mfma4(mv.y, Ab[4 * q + 1], c1);
-      c0 = mfma4(mv.z, Ab[4 * q + 2], c0);
-      c1 = mfma4(mv.w, Ab[4 * q + 3], c1);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float z = fmaf(ul[l], mown[r], c0[r] + c1[r]);
-      prel[l][r] = z;
-      Z[r] = (l < L - 1) ? fmaxf(z, 0.f) : z;
-    }
-    __syncthreads();  // m^T reads done before the next layer (or the backward) rewrites sMb
-  }
+    for (int r = 0; r < 4; ++r) Z[r] = node_ok ? tg * Z[r] : 0.f;
+  };
 
-  if constexpr (!VJP) {
-    if (node_ok) {
-      float* o = a.out + rowoff;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = tg * Z[r];
-    }
-    return;
-  } else {
-    // ---- backward ---------------------------------------------------------------------------------------
-    float gZ[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) gZ[r] = node_ok ? tg * a.gK[rowoff + r] : 0.f;
-    floatx4 gWacc[L];
-    float gbA[L][4], grwA[L][4], grbA[L][4], gfA[L];
+  // ---- backward of the last forward: gU = J^T gK; gradients accumulated lane-distributed ---------------
+  floatx4 gWacc[L];
+  float gbA[L][4], grwA[L][4], grbA[L][4], gfA[L];
+  if constexpr (VJP) {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       gWacc[l] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -333,6 +351,11 @@ __global__ void __launch_bounds__(NP * 4, 1) k_stage(StageArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) gbA[l][r] = grwA[l][r] = grbA[l][r] = 0.f;
     }
+  }
+  auto backward = [&](const float (&gK)[4], float (&gU)[4]) __attribute__((always_inline)) {
+    float gZ[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gZ[r] = node_ok ? tg * gK[r] : 0.f;
 #pragma unroll
     for (int l = L - 1; l >= 0; --l) {
       const float* op = a.ops + (size_t)l * kOpStride;
@@ -344,7 +367,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_stage(StageArgs a) {
         sGb[(4 * hi + r) * MS + node] = gpre[r];
         sMb[(4 * hi + r) * MS + node] = ml[l][r];
       }
-      {  // per-wave column sums of m and gpre (feature 4hi + r)
+      {
         float cm[4], cg[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -376,7 +399,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_stage(StageArgs a) {
       R = xor_sum4(R);
       C = xor_sum4(C);
       D = xor_sum4(D);
-      if (hi != 0) R = C = D = 0.f;  // count every node once
+      if (hi != 0) R = C = D = 0.f;  // every node once
       float fq[GNCDE_FC];
 #pragma unroll
       for (int q = 0; q < GNCDE_FC; ++q) fq[q] = 0.f;
@@ -399,8 +422,6 @@ __global__ void __launch_bounds__(NP * 4, 1) k_stage(StageArgs a) {
       fq[GNCDE_FC_VR_DA] = C * rdn;
       fq[GNCDE_FC_VC_A] = C * cn;
       fq[GNCDE_FC_VC_DA] = C * cdn;
-      // G = gpre m^T (16 rows per MFMA tile) contracted with A, dA, A^T, dA^T while building the column
-      // slice of Abar (rows i = 16 it + 4 hi + r, column `node`) as the backward operand
       const float e0 = fc[GNCDE_FC_E_A], e1 = fc[GNCDE_FC_E_DA], e2 = fc[GNCDE_FC_ET_A], e3 = fc[GNCDE_FC_ET_DA];
       const float vk = sV[l * NP + node];
       const float* wv = sW + l * NP + 4 * hi;
@@ -428,7 +449,6 @@ __global__ void __launch_bounds__(NP * 4, 1) k_stage(StageArgs a) {
       fq[GNCDE_FC_E_DA] = q1;
       fq[GNCDE_FC_ET_A] = q2;
       fq[GNCDE_FC_ET_DA] = q3;
-      // gm^T = gpre^T (I + Abar): A operand gpre^T rows from LDS, B operand the column slice
       floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
       const float* grow = sGb + lo * MS + 4 * hi;
 #pragma unroll
@@ -442,7 +462,6 @@ __global__ void __launch_bounds__(NP * 4, 1) k_stage(StageArgs a) {
       float gm[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) gm[r] = node_ok ? fmaf(ul[l], gpre[r], c0[r] + c1[r]) : 0.f;
-      // fusion-table gradients of this layer: wave reduction, lane q keeps entry q
 #pragma unroll
       for (int q = 0; q < GNCDE_FC; ++q) {
         float v = fq[q];
@@ -450,8 +469,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_stage(StageArgs a) {
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         if (lane == q) gfA[l] += v;
       }
-      __syncthreads();  // all waves done with sGb / sMb (G, gm) before they are restaged
-      // Linear / RMSNorm backward
+      __syncthreads();  // sGb / sMb (G, gm) consumed by every wave before restaging
       float xh[4], zn[4], rw4[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -463,7 +481,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_stage(StageArgs a) {
         gbA[l][r] += xor_sum16(gm[r]);
       }
       __syncthreads();
-      {  // gW[o][f] += sum over this wave's nodes of gm[node][o] zn[node][f]
+      {
         const float4 ga = *reinterpret_cast<const float4*>(sGb + lo * MS + 16 * w + 4 * hi);
         const float4 za = *reinterpret_cast<const float4*>(sMb + lo * MS + 16 * w + 4 * hi);
         gWacc[l] = mfma4(ga.x, za.x, gWacc[l]);
@@ -485,19 +503,184 @@ __global__ void __launch_bounds__(NP * 4, 1) k_stage(StageArgs a) {
       dot = xor_sum4(dot);
 #pragma unroll
       for (int r = 0; r < 4; ++r) gZ[r] = node_ok ? invl[l] * (gxh[r] - xh[r] * dot * (1.0f / (float)H)) : 0.f;
-      if (l > 0) __syncthreads();  // restaged buffers read before the next layer writes them
+      __syncthreads();  // restaged buffers read before the next layer / form writes them
     }
-    // scatter gU into the cotangent accumulators
-    if (node_ok) {
-      const float hb = a.h[b];
-      for (int j = 0; j < a.nacc; ++j) {
-        const float cf = a.accw[j] * (a.scale_h[j] ? hb : 1.0f);
-        float* o = a.acc[j] + rowoff;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = fmaf(cf, gZ[r], o[r]);
+    for (int r = 0; r < 4; ++r) gU[r] = gZ[r];
+  };
+
+  auto load4 = [&](const float* p, size_t off, float (&v)[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = node_ok ? p[off + r] : 0.f;
+  };
+  auto store4 = [&](float* p, size_t off, const float (&v)[4]) {
+    if (node_ok)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p[off + r] = v[r];
+  };
+  __syncthreads();  // sTs / sFus staged
+
+  const int k = a.k;
+  float tk = 0.f, hk = 0.f;
+  if (k >= 0) geom(k, tk, hk);
+
+  if constexpr (PROG == kEval1) {
+    const int i = a.stage;
+    float y[4], U[4];
+    load4(a.ys, rowk(k), y);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) U[r] = 0.f;
+    for (int j = 0; j < i; ++j) {
+      float Kj[4];
+      load4(a.K[j], rowoff, Kj);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) U[r] = fmaf(a.a[i][j], Kj[r], U[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) U[r] = fmaf(hk, U[r], y[r]);
+    if (i > 0) store4(a.U[i], rowoff, U);
+    form(stage_time(tk, a.c[i], hk));
+    forward(U);
+    store4(a.K[i], rowoff, U);
+    if (a.write_next) {  // input of stage i+1 (the last stage, whose value the sweep never needs)
+      float Un[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Un[r] = 0.f;
+      for (int j = 0; j <= i; ++j) {
+        float Kj[4];
+        if (j < i) {
+          load4(a.K[j], rowoff, Kj);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Kj[r] = U[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Un[r] = fmaf(a.a[i + 1][j], Kj[r], Un[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Un[r] = fmaf(hk, Un[r], y[r]);
+      store4(a.U[i + 1], rowoff, Un);
+    }
+    return;
+  } else if constexpr (PROG == kEval2) {  // RK4: stages 1 and 2 share t + h/2
+    float y[4], K0[4], U[4], Kv[4];
+    load4(a.ys, rowk(k), y);
+    load4(a.K[0], rowoff, K0);
+    const float hh = 0.5f * hk;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) U[r] = fmaf(hh, K0[r], y[r]);
+    store4(a.U[1], rowoff, U);
+    form(stage_time(tk, 0.5f, hk));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Kv[r] = U[r];
+    forward(Kv);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) U[r] = fmaf(hh, Kv[r], y[r]);
+    store4(a.U[2], rowoff, U);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Kv[r] = U[r];
+    forward(Kv);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) U[r] = fmaf(hk, Kv[r], y[r]);
+    store4(a.U[3], rowoff, U);
+    return;
+  } else {
+    if constexpr (PROG == kVjpMid) {
+      const int i = a.stage;
+      float U[4], gK[4], gU[4], acc[4];
+      load4(a.U[i], rowoff, U);
+      load4(a.gK[i], rowoff, gK);
+      form(stage_time(tk, a.c[i], hk));
+      forward(U);
+      backward(gK, gU);
+      load4(a.gyacc, rowoff, acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] += gU[r];
+      store4(a.gyacc, rowoff, acc);
+      for (int j = 0; j < i; ++j) {
+        if (a.a[i][j] == 0.f) continue;
+        const float cf = hk * a.a[i][j];
+        load4(a.gK[j], rowoff, acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = fmaf(cf, gU[r], acc[r]);
+        store4(a.gK[j], rowoff, acc);
+      }
+    } else if constexpr (PROG == kVjpPair) {  // RK4 stages 2 then 1 at t + h/2
+      float U[4], gK[4], gU[4], gy[4], g1[4];
+      load4(a.U[2], rowoff, U);
+      load4(a.gK[2], rowoff, gK);
+      form(stage_time(tk, 0.5f, hk));
+      forward(U);
+      backward(gK, gU);
+      load4(a.gyacc, rowoff, gy);
+      load4(a.gK[1], rowoff, g1);
+      const float hh = 0.5f * hk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gy[r] += gU[r];
+        g1[r] = fmaf(hh, gU[r], g1[r]);  // a[2][1] = 1/2
+      }
+      load4(a.U[1], rowoff, U);
+      forward(U);
+      backward(g1, gU);
+      load4(a.gK[0], rowoff, g1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gy[r] += gU[r];
+        g1[r] = fmaf(hh, gU[r], g1[r]);  // a[1][0] = 1/2
+      }
+      store4(a.gyacc, rowoff, gy);
+      store4(a.gK[0], rowoff, g1);
+    } else {  // kBoundary
+      const int S = a.S;
+      float lam[4];
+      float tn = 0.f, hn = 0.f;
+      bool formed = false;
+      if (a.has_next) {  // stage 0 of step k+1 at t_{k+1}: lambda_{k+1} = gyacc + gU (+ gys[k+1])
+        geom(k + 1, tn, hn);
+        float U[4], gK[4], gU[4];
+        load4(a.ys, rowk(k + 1), U);
+        load4(a.gK[0], rowoff, gK);
+        form(tn);
+        formed = true;
+        forward(U);
+        backward(gK, gU);
+        load4(a.gyacc, rowoff, lam);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lam[r] += gU[r];
+        if (a.gys) {
+          float gs[4];
+          load4(a.gys, rowk(k + 1), gs);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) lam[r] += gs[r];
+        }
+      } else {
+        load4(a.lam, rowoff, lam);
+      }
+      if (a.has_cur) {  // seeds of step k and its last stage
+        const int il = S - 1;
+        const float tl = stage_time(tk, a.c[il], hk);
+        float U[4], gK[4], gU[4];
+        load4(a.U[il], rowoff, U);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gK[r] = hk * a.bw[il] * lam[r];
+        if (!formed || tl != tn) form(tl);
+        forward(U);
+        backward(gK, gU);
+        float acc[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = lam[r] + gU[r];
+        store4(a.gyacc, rowoff, acc);
+        for (int j = 0; j < il; ++j) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[r] = hk * fmaf(a.a[il][j], gU[r], a.bw[j] * lam[r]);
+          store4(a.gK[j], rowoff, acc);
+        }
+      } else {
+        store4(a.gy0, rowoff, lam);
       }
     }
-    // ---- cross-wave reduction of the gradient accumulators, then += into this sample's block ----------
+    // ---- cross-wave reduction of the gradient accumulators, += into this sample's block --------------
     __syncthreads();
     float* red = sR0 + w * (L * kGradStride);
 #pragma unroll
@@ -540,108 +723,133 @@ __global__ void k_stage_grad_sum(int B, int L, const float* __restrict__ gp, flo
     gfusion[l * GNCDE_FC + (q - kLayerP)] = sum;
 }
 
-typedef void (*StageFn)(StageArgs);
-struct StageEntry {
+// lambda at the last grid point: gys (SAVE_T1) or gys[:, G-1] (SAVE_STEPS)
+__global__ void k_lam_init(size_t E, int G, int steps, const float* __restrict__ gys, float* __restrict__ lam) {
+  const int b = blockIdx.y;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  lam[(size_t)b * E + e] = steps ? gys[((size_t)b * G + (G - 1)) * E + e] : gys[(size_t)b * E + e];
+}
+
+typedef void (*RevFn)(RevArgs);
+struct RevEntry {
   int np, l;
-  StageFn eval, vjp;
+  RevFn fn[5];
 };
 
-#define GNCDE_STAGE(NP, L) {NP, L, k_stage<NP, L, false>, k_stage<NP, L, true>}
-const StageEntry kStage[] = {
-    GNCDE_STAGE(16, 1),  GNCDE_STAGE(16, 2),  GNCDE_STAGE(16, 3),  GNCDE_STAGE(16, 4),
-    GNCDE_STAGE(32, 1),  GNCDE_STAGE(32, 2),  GNCDE_STAGE(32, 3),  GNCDE_STAGE(32, 4),
-    GNCDE_STAGE(64, 1),  GNCDE_STAGE(64, 2),  GNCDE_STAGE(64, 3),  GNCDE_STAGE(64, 4),
-    GNCDE_STAGE(128, 1), GNCDE_STAGE(128, 2), GNCDE_STAGE(128, 3),
+#define GNCDE_REV(NP, L) \
+  {NP, L, {k_rev<NP, L, kEval1>, k_rev<NP, L, kEval2>, k_rev<NP, L, kVjpMid>, k_rev<NP, L, kVjpPair>, \
+           k_rev<NP, L, kBoundary>}}
+const RevEntry kRev[] = {
+    GNCDE_REV(16, 1),  GNCDE_REV(16, 2),  GNCDE_REV(16, 3),  GNCDE_REV(16, 4),
+    GNCDE_REV(32, 1),  GNCDE_REV(32, 2),  GNCDE_REV(32, 3),  GNCDE_REV(32, 4),
+    GNCDE_REV(64, 1),  GNCDE_REV(64, 2),  GNCDE_REV(64, 3),  GNCDE_REV(64, 4),
+    GNCDE_REV(128, 1), GNCDE_REV(128, 2), GNCDE_REV(128, 3),
 };
-#undef GNCDE_STAGE
+#undef GNCDE_REV
 
-const StageEntry* find_stage(const GncdeProblem& p) {
+const RevEntry* find_rev(const GncdeProblem& p) {
   if (p.cde_hidden != 0 || p.T > kTMaxS) return nullptr;
   for (int l = 0; l <= p.L; ++l)
     if (p.dims[l] != H) return nullptr;
   int np = 16;
   while (np < p.n) np *= 2;
-  for (const StageEntry& e : kStage)
+  for (const RevEntry& e : kRev)
     if (e.np == np && e.l == p.L) return &e;
   return nullptr;
 }
 
 inline unsigned cdivs(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
-__global__ void s_step_geom(int B, int G, int k, const float* __restrict__ grid, const int32_t* __restrict__ nsteps,
-                            float* __restrict__ tcur, float* __restrict__ hcur) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  int ns = nsteps[b];
-  ns = ns < 0 ? 0 : (ns > G - 1 ? G - 1 : ns);
-  const float* g = grid + (size_t)b * G;
-  tcur[b] = k < ns ? g[k] : g[ns];
-  hcur[b] = k < ns ? g[k + 1] - g[k] : 0.f;
-}
-
-__global__ void s_stage_time(int B, float c, const float* __restrict__ tcur, const float* __restrict__ hcur,
-                             float* __restrict__ tst) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < B) tst[b] = stage_time(tcur[b], c, hcur[b]);
-}
-
-struct SLin {
-  const float* x[7];
-  float a[7];
-  int nx;
-};
-// out[b] = base[b] + h_b * sum_j a_j x_j[b]  (base row = traj[b, k] when traj != nullptr, else base)
-__global__ void s_lincomb(size_t E, int G, int k, const float* __restrict__ traj, SLin lc,
-                          const float* __restrict__ hcur, float* __restrict__ out) {
-  const int b = blockIdx.y;
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  const size_t o = (size_t)b * E + e;
-  float sum = 0.f;
-  for (int j = 0; j < lc.nx; ++j) sum = fmaf(lc.a[j], lc.x[j][o], sum);
-  out[o] = fmaf(hcur[b], sum, traj[((size_t)b * G + k) * E + e]);
-}
-
-// gK_i = h b_i lam for every stage, gyacc = lam (+ the saved-state cotangent of row k if given)
-__global__ void s_seed(size_t E, int S, const float* __restrict__ lam, const float* __restrict__ hcur, SLin bw,
-                       float* const* __restrict__ gK, float* __restrict__ gyacc) {
-  const int b = blockIdx.y;
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  const size_t o = (size_t)b * E + e;
-  const float l = lam[o], hb = hcur[b];
-  for (int i = 0; i < S; ++i) gK[i][o] = hb * bw.a[i] * l;
-  gyacc[o] = l;
-}
-
-// lam = gyacc (+ gys[:, k] when given)
-__global__ void s_lam(size_t E, int G, int k, const float* __restrict__ gyacc, const float* __restrict__ gys,
-                      float* __restrict__ lam) {
-  const int b = blockIdx.y;
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  const size_t o = (size_t)b * E + e;
-  lam[o] = gyacc[o] + (gys ? gys[((size_t)b * G + k) * E + e] : 0.f);
-}
-
-struct Tab {
-  int S;
-  float c[6], a[6][6], bw[6];
+struct StageWs {
+  float *ops, *gp, *lam, *gyacc;
+  float *U[6], *K[6], *gK[6];
 };
 
-Tab make_tab(int method) {
-  Tab t{};
-  if (method == GNCDE_RK4) {
-    t.S = 4;
-    t.c[1] = t.c[2] = 0.5f;
-    t.c[3] = 1.f;
-    t.a[1][0] = 0.5f;
-    t.a[2][1] = 0.5f;
-    t.a[3][2] = 1.f;
-    t.bw[0] = t.bw[3] = 1.f / 6.f;
-    t.bw[1] = t.bw[2] = 2.f / 6.f;
+size_t carve_stage(const GncdeProblem& p, char* ws, StageWs& w) {
+  const size_t B = p.B, E = (size_t)p.n * H;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    float* ptr = ws ? reinterpret_cast<float*>(ws + off) : nullptr;
+    off += align_up(bytes, 256);
+    return ptr;
+  };
+  w.ops = take((size_t)p.L * kOpStride * 4);
+  w.gp = take(B * p.L * kGradStride * 4);
+  w.lam = take(B * E * 4);
+  w.gyacc = take(B * E * 4);
+  for (int i = 0; i < 6; ++i) {
+    w.U[i] = take(B * E * 4);
+    w.K[i] = take(B * E * 4);
+    w.gK[i] = take(B * E * 4);
+  }
+  return off;
+}
+
+}  // namespace
+
+bool stage_vjp_supported(const GncdeProblem& p, const GncdeSolver& s) {
+  return s.controller == GNCDE_CTRL_GRID && find_rev(p) != nullptr;
+}
+
+size_t stage_vjp_workspace(const GncdeProblem& p) {
+  StageWs w;
+  return carve_stage(p, nullptr, w);
+}
+
+// Reverse sweep, per step k = G-2 .. 0 (RK4: 4 launches, Tsit5: 10):
+//   recompute  RK4: kEval1 (stage 0, t_k), kEval2 (stages 1-2 at t_k + h/2, and U_3)
+//              Tsit5: kEval1 for stages 0..4 (the last writes U_5)
+//   kBoundary  at t_{k+1}: stage 0 of step k+1 closes lambda_{k+1}; seeds + last stage of step k
+//   middle     RK4: kVjpPair (stages 2, 1);  Tsit5: kVjpMid for stages 4..1
+// and a final kBoundary (stage 0 of step 0 -> gy0).
+int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys, float* gy0,
+                        float* gparams, float* gfusion, char* ws, hipStream_t st) {
+  const RevEntry* e = find_rev(p);
+  if (!e || s.controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
+  const int B = p.B, G = s.grid_len;
+  const size_t E = (size_t)p.n * H;
+  StageWs w;
+  carve_stage(p, ws, w);
+  const bool rk4 = s.method == GNCDE_RK4;
+  const bool steps = s.save_mode == GNCDE_SAVE_STEPS;
+  hipLaunchKernelGGL(k_stage_prep, dim3(p.L), dim3(256), 0, st, p.params, w.ops);
+  (void)hipMemsetAsync(w.gp, 0, (size_t)B * p.L * kGradStride * sizeof(float), st);
+  hipLaunchKernelGGL(k_lam_init, dim3(cdivs(E, 256), B), dim3(256), 0, st, E, G, steps ? 1 : 0, gys, w.lam);
+
+  RevArgs a{};
+  a.n = p.n;
+  a.T = p.T;
+  a.G = G;
+  a.ts = p.ts;
+  a.coef = p.coef;
+  a.tcoef = p.tcoef;
+  a.fusion = p.fusion;
+  a.ops = w.ops;
+  a.grid = s.grid;
+  a.nsteps = s.nsteps;
+  a.ys = ys;
+  a.gys = steps ? gys : nullptr;
+  for (int i = 0; i < 6; ++i) {
+    a.K[i] = w.K[i];
+    a.U[i] = w.U[i];
+    a.gK[i] = w.gK[i];
+  }
+  a.gyacc = w.gyacc;
+  a.lam = w.lam;
+  a.gy0 = gy0;
+  a.gp = w.gp;
+  if (rk4) {
+    a.S = 4;
+    a.c[1] = a.c[2] = 0.5f;
+    a.c[3] = 1.f;
+    a.a[1][0] = 0.5f;
+    a.a[2][1] = 0.5f;
+    a.a[3][2] = 1.f;
+    a.bw[0] = a.bw[3] = 1.f / 6.f;
+    a.bw[1] = a.bw[2] = 2.f / 6.f;
   } else {
-    t.S = 6;
+    a.S = 6;
     const float c[6] = {0.f, TSIT5_C2, TSIT5_C3, TSIT5_C4, TSIT5_C5, 1.f};
     const float A[6][6] = {{0, 0, 0, 0, 0, 0},
                            {TSIT5_A21, 0, 0, 0, 0, 0},
@@ -651,132 +859,43 @@ Tab make_tab(int method) {
                            {TSIT5_A61, TSIT5_A62, TSIT5_A63, TSIT5_A64, TSIT5_A65, 0}};
     const float bw[6] = {TSIT5_B1, TSIT5_B2, TSIT5_B3, TSIT5_B4, TSIT5_B5, TSIT5_B6};
     for (int i = 0; i < 6; ++i) {
-      t.c[i] = c[i];
-      t.bw[i] = bw[i];
-      for (int j = 0; j < 6; ++j) t.a[i][j] = A[i][j];
+      a.c[i] = c[i];
+      a.bw[i] = bw[i];
+      for (int j = 0; j < 6; ++j) a.a[i][j] = A[i][j];
     }
   }
-  return t;
-}
-
-struct StageWs {
-  float *ops, *gp, *lam, *gyacc, *tcur, *hcur, *tst;
-  float *U[6], *K[6], *gK[6];
-  float** gKptr;
-};
-
-size_t carve_stage(const GncdeProblem& p, char* ws, StageWs& w) {
-  const size_t B = p.B, E = (size_t)p.n * H;
-  size_t off = 0;
-  auto take = [&](size_t bytes) {
-    char* ptr = ws ? ws + off : nullptr;
-    off += align_up(bytes, 256);
-    return ptr;
-  };
-  w.ops = reinterpret_cast<float*>(take((size_t)p.L * kOpStride * 4));
-  w.gp = reinterpret_cast<float*>(take(B * p.L * kGradStride * 4));
-  w.lam = reinterpret_cast<float*>(take(B * E * 4));
-  w.gyacc = reinterpret_cast<float*>(take(B * E * 4));
-  for (int i = 0; i < 6; ++i) {
-    w.U[i] = reinterpret_cast<float*>(take(B * E * 4));
-    w.K[i] = reinterpret_cast<float*>(take(B * E * 4));
-    w.gK[i] = reinterpret_cast<float*>(take(B * E * 4));
-  }
-  w.tcur = reinterpret_cast<float*>(take(B * 4));
-  w.hcur = reinterpret_cast<float*>(take(B * 4));
-  w.tst = reinterpret_cast<float*>(take(B * 4));
-  w.gKptr = reinterpret_cast<float**>(take(6 * sizeof(float*)));
-  return off;
-}
-
-}  // namespace
-
-bool stage_vjp_supported(const GncdeProblem& p, const GncdeSolver& s) {
-  return s.controller == GNCDE_CTRL_GRID && find_stage(p) != nullptr;
-}
-
-size_t stage_vjp_workspace(const GncdeProblem& p) {
-  StageWs w;
-  return carve_stage(p, nullptr, w);
-}
-
-int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys, float* gy0,
-                        float* gparams, float* gfusion, char* ws, hipStream_t st) {
-  const StageEntry* e = find_stage(p);
-  if (!e || s.controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
-  const int B = p.B, G = s.grid_len;
-  const size_t E = (size_t)p.n * H;
-  StageWs w;
-  carve_stage(p, ws, w);
-  const Tab tab = make_tab(s.method);
-  const int S = tab.S;
-  const dim3 ge(cdivs(E, 256), B);
-  const unsigned gb = cdivs(B, 256);
-  const dim3 wg(e->np * 4);
-  (void)hipMemcpyAsync(w.gKptr, w.gK, sizeof(w.gK), hipMemcpyHostToDevice, st);
-  hipLaunchKernelGGL(k_stage_prep, dim3(p.L), dim3(256), 0, st, p.params, w.ops);
-  (void)hipMemsetAsync(w.gp, 0, (size_t)B * p.L * kGradStride * sizeof(float), st);
-  const bool steps = s.save_mode == GNCDE_SAVE_STEPS;
-  // lambda = cotangent of the final state (saved-state cotangents are added as the sweep passes them)
-  if (steps) {
-    (void)hipMemsetAsync(w.gyacc, 0, (size_t)B * E * sizeof(float), st);
-    hipLaunchKernelGGL(s_lam, ge, dim3(256), 0, st, E, G, G - 1, w.gyacc, gys, w.lam);
-  } else {
-    (void)hipMemcpyAsync(w.lam, gys, (size_t)B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
-  }
-
-  StageArgs a{};
-  a.n = p.n;
-  a.T = p.T;
-  a.ts = p.ts;
-  a.coef = p.coef;
-  a.tcoef = p.tcoef;
-  a.fusion = p.fusion;
-  a.ops = w.ops;
-  a.t = w.tst;
-  a.h = w.hcur;
-  a.gp = w.gp;
+  const dim3 grid(B), wg(e->np * 4);
   for (int k = G - 2; k >= 0; --k) {
-    hipLaunchKernelGGL(s_step_geom, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, w.tcur, w.hcur);
-    // recompute the stage inputs U_i (U_0 = y_k) and values K_i (i < S-1)
-    for (int i = 0; i < S; ++i) {
-      SLin lc{};
-      for (int j = 0; j < i; ++j)
-        if (tab.a[i][j] != 0.f) {
-          lc.x[lc.nx] = w.K[j];
-          lc.a[lc.nx++] = tab.a[i][j];
-        }
-      hipLaunchKernelGGL(s_lincomb, ge, dim3(256), 0, st, E, G, k, ys, lc, w.hcur, w.U[i]);
-      if (i + 1 < S) {
-        hipLaunchKernelGGL(s_stage_time, dim3(gb), dim3(256), 0, st, B, tab.c[i], w.tcur, w.hcur, w.tst);
-        a.U = w.U[i];
-        a.out = w.K[i];
-        hipLaunchKernelGGL(e->eval, dim3(B), wg, 0, st, a);
+    a.k = k;
+    if (rk4) {
+      a.stage = 0;
+      a.write_next = 0;
+      hipLaunchKernelGGL(e->fn[kEval1], grid, wg, 0, st, a);
+      hipLaunchKernelGGL(e->fn[kEval2], grid, wg, 0, st, a);
+    } else {
+      for (int i = 0; i + 1 < a.S; ++i) {
+        a.stage = i;
+        a.write_next = (i + 2 == a.S) ? 1 : 0;
+        hipLaunchKernelGGL(e->fn[kEval1], grid, wg, 0, st, a);
       }
     }
-    // reverse: gK_i = h b_i lam, gy = lam; stage VJPs scatter into gy and the earlier gK_j
-    SLin bw{};
-    for (int i = 0; i < S; ++i) bw.a[i] = tab.bw[i];
-    hipLaunchKernelGGL(s_seed, ge, dim3(256), 0, st, E, S, w.lam, w.hcur, bw, w.gKptr, w.gyacc);
-    for (int i = S - 1; i >= 0; --i) {
-      hipLaunchKernelGGL(s_stage_time, dim3(gb), dim3(256), 0, st, B, tab.c[i], w.tcur, w.hcur, w.tst);
-      a.U = w.U[i];
-      a.gK = w.gK[i];
-      a.nacc = 0;
-      a.acc[a.nacc] = w.gyacc;
-      a.accw[a.nacc] = 1.f;
-      a.scale_h[a.nacc++] = 0;
-      for (int j = 0; j < i; ++j)
-        if (tab.a[i][j] != 0.f) {
-          a.acc[a.nacc] = w.gK[j];
-          a.accw[a.nacc] = tab.a[i][j];
-          a.scale_h[a.nacc++] = 1;
-        }
-      hipLaunchKernelGGL(e->vjp, dim3(B), wg, 0, st, a);
+    a.has_next = (k + 1 <= G - 2) ? 1 : 0;
+    a.has_cur = 1;
+    hipLaunchKernelGGL(e->fn[kBoundary], grid, wg, 0, st, a);
+    if (rk4) {
+      hipLaunchKernelGGL(e->fn[kVjpPair], grid, wg, 0, st, a);
+    } else {
+      for (int i = a.S - 2; i >= 1; --i) {
+        a.stage = i;
+        hipLaunchKernelGGL(e->fn[kVjpMid], grid, wg, 0, st, a);
+      }
     }
-    hipLaunchKernelGGL(s_lam, ge, dim3(256), 0, st, E, G, k, w.gyacc, steps ? gys : nullptr, w.lam);
   }
-  (void)hipMemcpyAsync(gy0, w.lam, (size_t)B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
+  // stage 0 of step 0 closes lambda_0 = dL/dy0
+  a.k = -1;
+  a.has_next = G >= 2 ? 1 : 0;
+  a.has_cur = 0;
+  hipLaunchKernelGGL(e->fn[kBoundary], grid, wg, 0, st, a);
   hipLaunchKernelGGL(k_stage_grad_sum, dim3(cdivs((size_t)p.L * kGradStride, 256)), dim3(256), 0, st, B, p.L, w.gp,
                      gparams, gfusion);
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
