@@ -47,12 +47,44 @@ __device__ __forceinline__ int swz(int i, int k) {
   return i * (NP + 1) + k;
 }
 
-__device__ __forceinline__ float xor_sum16(float v) {  // sum over the 16 lanes sharing lane>>4
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 8);
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+template <int MASK>
+__device__ __forceinline__ float swzf(float v) {  // lane ^ MASK within each 32-lane half (MASK < 32)
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), (MASK << 10) | 0x1F));
+}
+
+// Sum over the 16 lanes sharing lane>>4, all on DPP (quad swaps, half-row and row mirrors): no LDS traffic.
+__device__ __forceinline__ float xor_sum16(float v) {
+  v += dppf<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dppf<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dppf<0x141>(v);  // row_half_mirror
+  v += dppf<0x140>(v);  // row_mirror
   return v;
+}
+
+// Reduce 32 per-lane values over the wave: recursive halving (xor 16, 8, 4, 2, 1 inside each 32-lane half, then
+// one xor 32) -> lane l holds the wave total of value (l & 31).  31 + 1 exchanges instead of 32 x 6.
+__device__ __forceinline__ float reduce_scatter32(float (&v)[32], int lane) {
+#define GNCDE_RS_STEP(M, XCH)                                   \
+  {                                                             \
+    const bool up = (lane & (M)) != 0;                          \
+    _Pragma("unroll") for (int i = 0; i < (M); ++i) {           \
+      const float send = up ? v[i] : v[(M) + i];                \
+      const float keep = up ? v[(M) + i] : v[i];                \
+      v[i] = keep + XCH(send);                                  \
+    }                                                           \
+  }
+  GNCDE_RS_STEP(16, swzf<16>)
+  GNCDE_RS_STEP(8, swzf<8>)
+  GNCDE_RS_STEP(4, swzf<4>)
+  GNCDE_RS_STEP(2, dppf<0x4E>)
+  GNCDE_RS_STEP(1, dppf<0xB1>)
+#undef GNCDE_RS_STEP
+  return v[0] + __shfl_xor(v[0], 32);
 }
 
 __device__ __forceinline__ float xor_sum4(float v) {  // sum over the 4 lane groups (same lane&15)
@@ -462,12 +494,11 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       float gm[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) gm[r] = node_ok ? fmaf(ul[l], gpre[r], c0[r] + c1[r]) : 0.f;
+      {
+        float v32[32];
 #pragma unroll
-      for (int q = 0; q < GNCDE_FC; ++q) {
-        float v = fq[q];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (lane == q) gfA[l] += v;
+        for (int q = 0; q < 32; ++q) v32[q] = q < GNCDE_FC ? fq[q] : 0.f;
+        gfA[l] += reduce_scatter32(v32, lane);  // lane q (q < 24) owns fusion-table entry q
       }
       __syncthreads();  // sGb / sMb (G, gm) consumed by every wave before restaging
       float xh[4], zn[4], rw4[4];

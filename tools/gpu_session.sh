@@ -50,6 +50,16 @@ for step in "$@"; do
             rc=$?; echo "pmcsq $i rc=$rc"; tail -n 3 "$ROOTDIR/gpurun_out/pmcsq_$i.log"; \
             case $rc in 124|134|137|139) exit $rc;; esac) || exit $?
          done ;;
+    pmctrain) i=0; for ctrs in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT" \
+                          "SQ_INSTS_VALU_MFMA_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
+                          "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+           i=$((i+1))
+           (cd /tmp && run_dir="$ROOTDIR/gpurun_out/pmctrain_$i" && rm -rf "$run_dir" && \
+            timeout -k 10 900 rocprofv3 --pmc $ctrs --output-format csv -d "$run_dir" -o run -- \
+              python3 "$ROOTDIR/tools/bench_train.py" --steps 1 --warmup 0 --rk4-steps 10 > "$ROOTDIR/gpurun_out/pmctrain_$i.log" 2>&1; \
+            rc=$?; echo "pmctrain $i rc=$rc"; tail -n 2 "$ROOTDIR/gpurun_out/pmctrain_$i.log"; \
+            case $rc in 124|134|137|139) exit $rc;; esac) || exit $?
+         done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -43,7 +43,7 @@ def main():
             print(f'{float(r["Percentage"]):6.2f}%  calls={r["Calls"]:>5}  avg={float(r["AverageNs"]) / 1e3:10.1f} us  '
                   f'{r["Name"][:100]}')
     elif mode == "counters":
-        for (k, c), v in sorted(counters(sys.argv[2:]).items()):
+        for (k, c), v in sorted(counters(sys.argv[2:], os.environ.get("MATCH", "k_fused")).items()):
             print(f"{c:32s} {v:16.1f}  {k}")
     elif mode == "traffic":
         fetch_dir, write_dir, workload, out = sys.argv[2:6]
