@@ -107,6 +107,11 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
 int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
                       int32_t* stats, char* ws, hipStream_t st);
 
+// generic Tsit5 + PIDController (any shape, CDE wrapper): gncde_pid.hip
+size_t generic_pid_workspace(const GncdeProblem& p);
+int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
+                          char* ws, hipStream_t st);
+
 // reverse mode (discrete adjoint, GRID controller): gncde_vjp.hip
 size_t generic_vjp_workspace(const GncdeProblem& p, const GncdeSolver& s);
 int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys,

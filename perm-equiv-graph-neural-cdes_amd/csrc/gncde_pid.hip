@@ -1,0 +1,330 @@
+// Generic (any shape, CDE wrapper included) Tsit5 + PIDController solve — the adaptive configuration of
+// graph_neural_cde.py:53-54,94-104 (and BASELINE config 5) for problems the fused persistent kernel does not
+// cover.  Same controller as gncde_fused.hip (diffrax defaults: pcoeff 0, icoeff 1, safety 0.9, factormin 0.2
+// but 1 after an accepted step, factormax 10, RMS error norm, error order 5, FSAL, _clip_to_end 1e-6, Hairer
+// initial step for dt0 = None, SaveAt(ts) through the Tsit5 dense interpolant).
+//
+// Every sample runs its own step sequence.  The host loop issues one batched vector-field evaluation per
+// iteration (each sample at its own stage time and input), then k_pid_advance — one workgroup per sample —
+// advances that sample's controller state machine by one stage: norms are workgroup reductions, the accept /
+// reject decision and the next stage input are formed in place.  Finished samples idle.  Completion is polled
+// every kPoll iterations.
+#include "gncde_internal.h"
+
+namespace gncde {
+namespace {
+
+constexpr int kPoll = 16;
+
+struct PidState {
+  int phase, st, steps, rejects, evals, status, done, si;
+  float t, tn, h, dt, h0, d1, tst;
+};
+
+struct PidArgs {
+  int B, E, S, max_steps, auto_dt;
+  float rtol, atol;
+  const float* t0;
+  const float* t1;
+  const float* dt0;
+  const float* save_ts;  // [B, S] or nullptr
+  PidState* state;
+  float* y;     // [B, E]
+  float* yt;    // [B, E] stage input (next evaluation)
+  float* kk;    // [7, B, E]
+  const float* K;  // [B, E] value of the last evaluation
+  float* ys;    // output: [B, S, E] (SAVE_TS) or [B, E]
+};
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float tot = 0.f;
+  for (int j = 0; j < (int)(blockDim.x >> 6); ++j) tot += red[j];
+  return tot;
+}
+
+__device__ __forceinline__ void tsit5_dense_w(float th, float (&w)[7]) {
+  const float t2 = th * th;
+  w[0] = -1.0530884977290216f * th * (th - 1.3299890189751412f) * (t2 - 1.4364028541716351f * th + 0.7139816917074209f);
+  w[1] = 0.1017f * t2 * (t2 - 2.1966568338249754f * th + 1.2949852507374631f);
+  w[2] = 2.490627285651252793f * t2 * (t2 - 2.38535645472061657f * th + 1.57803468208092486f);
+  w[3] = -16.54810288924490272f * (th - 1.21712927295533244f) * (th - 0.61620406037800089f) * t2;
+  w[4] = 47.37952196281928122f * (th - 1.203071208372362603f) * (th - 0.658047292653547382f) * t2;
+  w[5] = -34.87065786149660974f * (th - 1.2f) * (th - 0.666666666666666667f) * t2;
+  w[6] = 2.5f * (th - 1.0f) * (th - 0.6f) * t2;
+}
+
+__device__ __forceinline__ void stage_row(int s, float (&a)[6], float& c) {
+  for (int j = 0; j < 6; ++j) a[j] = 0.f;
+  c = 1.f;
+  switch (s) {
+    case 1: a[0] = TSIT5_A21; c = TSIT5_C2; break;
+    case 2: a[0] = TSIT5_A31; a[1] = TSIT5_A32; c = TSIT5_C3; break;
+    case 3: a[0] = TSIT5_A41; a[1] = TSIT5_A42; a[2] = TSIT5_A43; c = TSIT5_C4; break;
+    case 4: a[0] = TSIT5_A51; a[1] = TSIT5_A52; a[2] = TSIT5_A53; a[3] = TSIT5_A54; c = TSIT5_C5; break;
+    case 5: a[0] = TSIT5_A61; a[1] = TSIT5_A62; a[2] = TSIT5_A63; a[3] = TSIT5_A64; a[4] = TSIT5_A65; break;
+    default:
+      a[0] = TSIT5_B1; a[1] = TSIT5_B2; a[2] = TSIT5_B3; a[3] = TSIT5_B4; a[4] = TSIT5_B5; a[5] = TSIT5_B6;
+      break;
+  }
+}
+
+// initial state: t = t0, saved states at save_ts <= t0, first evaluation f(t0, y0)
+__global__ void k_pid_init(PidArgs a, const float* __restrict__ y0) {
+  const int b = blockIdx.x;
+  const size_t base = (size_t)b * a.E;
+  for (int e = threadIdx.x; e < a.E; e += blockDim.x) {
+    a.y[base + e] = y0[base + e];
+    a.yt[base + e] = y0[base + e];
+  }
+  const float t0 = a.t0[b];
+  int si = 0;
+  if (a.S > 0) {
+    const float* sts = a.save_ts + (size_t)b * a.S;
+    while (si < a.S && sts[si] <= t0) {
+      for (int e = threadIdx.x; e < a.E; e += blockDim.x) a.ys[((size_t)b * a.S + si) * a.E + e] = y0[base + e];
+      ++si;
+    }
+  }
+  if (threadIdx.x == 0) {
+    PidState s{};
+    s.t = s.tn = s.tst = t0;
+    s.dt = a.auto_dt ? 0.f : a.dt0[b];
+    s.si = si;
+    a.state[b] = s;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_pid_advance(PidArgs a) {
+  __shared__ float red[4];
+  __shared__ PidState sh;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid == 0) sh = a.state[b];
+  __syncthreads();
+  PidState s = sh;
+  if (s.done) return;
+  const int E = a.E;
+  const size_t base = (size_t)b * E;
+  const size_t BE = (size_t)gridDim.x * E;
+  const float rtol = a.rtol, atol = a.atol;
+  const float t0 = a.t0[b], t1 = a.t1[b];
+  const float inv_cnt = 1.0f / (float)E;
+  float* y = a.y + base;
+  float* yt = a.yt + base;
+  const float* K = a.K + base;
+  auto kk = [&](int j) { return a.kk + (size_t)j * BE + base; };
+  s.evals++;
+  bool start = false;
+  if (s.phase == 0) {  // f(t0, y0): FSAL k1 and f0 of the initial-step heuristic
+    for (int e = tid; e < E; e += blockDim.x) kk(0)[e] = K[e];
+    s.phase = 2;
+    if (a.auto_dt) {
+      float p0 = 0.f, p1 = 0.f;
+      for (int e = tid; e < E; e += blockDim.x) {
+        const float sc = fmaf(fabsf(y[e]), rtol, atol);
+        const float u = y[e] / sc, v = K[e] / sc;
+        p0 = fmaf(u, u, p0);
+        p1 = fmaf(v, v, p1);
+      }
+      const float d0 = sqrtf(block_sum(p0, red) * inv_cnt);
+      const float d1 = sqrtf(block_sum(p1, red) * inv_cnt);
+      s.d1 = d1;
+      s.h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : 0.01f * (d0 / d1);
+      for (int e = tid; e < E; e += blockDim.x) yt[e] = fmaf(s.h0, K[e], y[e]);
+      s.tst = t0 + s.h0;
+      s.phase = 1;
+    } else {
+      start = true;
+    }
+  } else if (s.phase == 1) {  // f(t0 + h0, y0 + h0 f0)
+    float p2 = 0.f;
+    for (int e = tid; e < E; e += blockDim.x) {
+      const float sc = fmaf(fabsf(y[e]), rtol, atol);
+      const float v = (K[e] - kk(0)[e]) / sc;
+      p2 = fmaf(v, v, p2);
+    }
+    const float d2 = sqrtf(block_sum(p2, red) * inv_cnt) / s.h0;
+    const float md = fmaxf(s.d1, d2);
+    const float h1 = md <= 1e-15f ? fmaxf(1e-6f, s.h0 * 1e-3f) : powf(0.01f / md, 0.2f);
+    s.dt = fminf(100.0f * s.h0, h1);
+    s.phase = 2;
+    start = true;
+  } else {
+    for (int e = tid; e < E; e += blockDim.x) kk(s.st)[e] = K[e];
+    if (s.st == 6) {  // attempt complete: yt = y1 candidate, kk6 = f(tn, y1)
+      float pe = 0.f;
+      for (int e = tid; e < E; e += blockDim.x) {
+        const float err = s.h * (TSIT5_E1 * kk(0)[e] + TSIT5_E2 * kk(1)[e] + TSIT5_E3 * kk(2)[e] +
+                                 TSIT5_E4 * kk(3)[e] + TSIT5_E5 * kk(4)[e] + TSIT5_E6 * kk(5)[e] +
+                                 TSIT5_E7 * kk(6)[e]);
+        const float sc = fmaf(fmaxf(fabsf(y[e]), fabsf(yt[e])), rtol, atol);
+        const float v = err / sc;
+        pe = fmaf(v, v, pe);
+      }
+      const float err = sqrtf(block_sum(pe, red) * inv_cnt);
+      const bool finite = isfinite(err);
+      const bool keep = finite && err < 1.0f;
+      float factor;
+      if (!finite) {
+        factor = 0.2f;
+      } else {
+        const float f1 = err == 0.f ? 10.0f : 0.9f * powf(1.0f / err, 0.2f);
+        factor = fminf(fmaxf(f1, keep ? 1.0f : 0.2f), 10.0f);
+      }
+      if (keep) {
+        if (a.S > 0) {
+          const float* sts = a.save_ts + (size_t)b * a.S;
+          while (s.si < a.S && sts[s.si] <= s.tn) {  // dense output inside (t, tn]
+            float wts[7];
+            tsit5_dense_w((sts[s.si] - s.t) / s.h, wts);
+            float* dst = a.ys + ((size_t)b * a.S + s.si) * E;
+            for (int e = tid; e < E; e += blockDim.x) {
+              float acc = 0.f;
+              for (int j = 0; j < 7; ++j) acc = fmaf(wts[j], kk(j)[e], acc);
+              dst[e] = fmaf(s.h, acc, y[e]);
+            }
+            ++s.si;
+          }
+        }
+        __syncthreads();  // every thread has read y / kk before they are overwritten
+        for (int e = tid; e < E; e += blockDim.x) {
+          y[e] = yt[e];
+          kk(0)[e] = kk(6)[e];
+        }
+        s.t = s.tn;
+        ++s.steps;
+      } else {
+        ++s.rejects;
+      }
+      s.dt = factor * s.h;
+      s.st = 0;
+      start = true;
+    }
+  }
+  if (start) {  // begin a new attempt (or finish)
+    bool finish = false;
+    if (!(s.t < t1)) {
+      finish = true;
+    } else if (s.steps + s.rejects >= a.max_steps) {
+      s.status = 1;
+      finish = true;
+    }
+    if (finish) {
+      __syncthreads();
+      if (a.S == 0) {
+        for (int e = tid; e < E; e += blockDim.x) a.ys[base + e] = y[e];
+      } else {
+        for (; s.si < a.S; ++s.si)  // only on failure
+          for (int e = tid; e < E; e += blockDim.x) a.ys[((size_t)b * a.S + s.si) * E + e] = y[e];
+      }
+      s.done = 1;
+      if (tid == 0) a.state[b] = s;
+      return;
+    }
+    s.tn = s.t + s.dt;
+    if (s.tn > t1 - 1e-6f) s.tn = t1;  // diffrax _clip_to_end
+    s.h = s.tn - s.t;
+  }
+  if (s.phase == 2) {  // next stage input and time
+    const int ns1 = s.st + 1;
+    float ar[6], cst;
+    stage_row(ns1, ar, cst);
+    __syncthreads();
+    for (int e = tid; e < E; e += blockDim.x) {
+      float acc = 0.f;
+      for (int j = 0; j < ns1 && j < 6; ++j) acc = fmaf(ar[j], kk(j)[e], acc);
+      yt[e] = fmaf(s.h, acc, y[e]);
+    }
+    s.tst = ns1 >= 5 ? __fadd_rn(s.t, s.h) : stage_time(s.t, cst, s.h);
+    s.st = ns1;
+  }
+  if (tid == 0) a.state[b] = s;
+}
+
+__global__ void k_pid_tst(int B, const PidState* __restrict__ st, float* __restrict__ tst, int* __restrict__ active) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  tst[b] = st[b].tst;
+  if (!st[b].done) atomicAdd(active, 1);
+}
+
+__global__ void k_pid_stats(int B, const PidState* __restrict__ st, int32_t* __restrict__ stats) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  stats[b * 4 + GNCDE_STAT_STEPS] = st[b].steps;
+  stats[b * 4 + GNCDE_STAT_REJECTS] = st[b].rejects;
+  stats[b * 4 + GNCDE_STAT_EVALS] = st[b].evals;
+  stats[b * 4 + GNCDE_STAT_STATUS] = st[b].status;
+}
+
+}  // namespace
+
+size_t generic_pid_workspace(const GncdeProblem& p) {
+  const size_t B = p.B, E = (size_t)p.n * state_dim(p);
+  size_t sz = generic_vf_workspace(p);
+  sz += 10 * align_up(B * E * 4, 256);                 // y, yt, K, kk[7]
+  sz += align_up(B * sizeof(PidState), 256) + 2 * align_up(B * 4, 256) + 256;
+  return sz;
+}
+
+int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
+                          char* ws, hipStream_t st) {
+  if (s.method != GNCDE_TSIT5) return GNCDE_ERR_UNSUPPORTED;
+  const int B = p.B;
+  const size_t E = (size_t)p.n * state_dim(p);
+  if (out_dim(p) != state_dim(p)) return GNCDE_ERR_SHAPE;
+  char* cur = ws + generic_vf_workspace(p);
+  auto take = [&](size_t bytes) {
+    char* ptr = cur;
+    cur += align_up(bytes, 256);
+    return ptr;
+  };
+  PidArgs a{};
+  a.B = B;
+  a.E = (int)E;
+  a.S = s.save_mode == GNCDE_SAVE_TS ? s.n_save : 0;
+  a.max_steps = s.max_steps;
+  a.auto_dt = s.dt0 == nullptr;
+  a.rtol = s.rtol;
+  a.atol = s.atol;
+  a.t0 = s.t0;
+  a.t1 = s.t1;
+  a.dt0 = s.dt0;
+  a.save_ts = s.save_ts;
+  a.y = reinterpret_cast<float*>(take(B * E * 4));
+  a.yt = reinterpret_cast<float*>(take(B * E * 4));
+  float* K = reinterpret_cast<float*>(take(B * E * 4));
+  a.K = K;
+  a.kk = reinterpret_cast<float*>(take(7 * B * E * 4));
+  a.state = reinterpret_cast<PidState*>(take(B * sizeof(PidState)));
+  float* tst = reinterpret_cast<float*>(take(B * 4));
+  int* active = reinterpret_cast<int*>(take(B * 4));
+  a.ys = ys;
+  hipLaunchKernelGGL(k_pid_init, dim3(B), dim3(256), 0, st, a, y0);
+  // each sample needs at most 2 + 6 * max_steps + 1 evaluations
+  const long max_iter = 3L + 6L * (long)s.max_steps;
+  int rc = GNCDE_OK;
+  for (long it = 0; it < max_iter; ++it) {
+    hipLaunchKernelGGL(k_pid_tst, dim3((B + 255) / 256), dim3(256), 0, st, B, a.state, tst, active);
+    rc = generic_vf_eval(p, tst, a.yt, K, ws, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_pid_advance, dim3(B), dim3(256), 0, st, a);
+    if ((it + 1) % kPoll == 0) {
+      int h_active = 0;
+      (void)hipMemsetAsync(active, 0, sizeof(int), st);
+      hipLaunchKernelGGL(k_pid_tst, dim3((B + 255) / 256), dim3(256), 0, st, B, a.state, tst, active);
+      (void)hipMemcpyAsync(&h_active, active, sizeof(int), hipMemcpyDeviceToHost, st);
+      if (hipStreamSynchronize(st) != hipSuccess) return GNCDE_ERR_HIP;
+      if (h_active == 0) break;
+    }
+  }
+  if (stats) hipLaunchKernelGGL(k_pid_stats, dim3((B + 255) / 256), dim3(256), 0, st, B, a.state, stats);
+  return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+}
+
+}  // namespace gncde
