@@ -1,0 +1,185 @@
+// Batched fp32 MFMA GEMM + the small kernels that turn the generic vector field into two GEMMs per layer:
+//
+//   m      = inv_row * (Z  W'^T) + bias'      (Linear with RMSNorm folded: W' = W diag(rms_w),
+//                                              bias' = bias + W rms_b; one GEMM over all B*n node rows)
+//   Z_next = act((I + Abar)  m)               (per-sample GEMM; (I + Abar) materialised once per layer)
+//
+// This is what makes the wide CDE-wrapper layers of configs 3 / 5 (d_L = 1024 / 512, MFMA-bound, SURVEY
+// §8d) run on the matrix cores instead of scalar FMAs.  The GEMM is a plain 64x64-tile, K-chunk-16 LDS
+// kernel on v_mfma_f32_16x16x4f32 (each wave a 32x32 sub-tile, 4 independent accumulators); bounds are
+// zero-filled so any M, N, K (n = 129, 255 ...) works.
+#include "gncde_internal.h"
+
+namespace gncde {
+
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+template <bool TRANS_B>
+__global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
+  const int b = blockIdx.z;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const float* A = g.A + (size_t)b * g.sA;
+  const float* B = g.B + (size_t)b * g.sB;
+  float* C = g.C + (size_t)b * g.sC;
+  __shared__ float As[64][17];
+  __shared__ float Bs[16][68];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  floatx4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int ar = tid >> 2, aq = (tid & 3) * 4;  // A tile: row, 4 k
+  for (int k0 = 0; k0 < g.K; k0 += 16) {
+    {
+      const int r = m0 + ar;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int kk = k0 + aq + q;
+        As[ar][aq + q] = (r < g.M && kk < g.K) ? A[(size_t)r * g.lda + kk] : 0.f;
+      }
+    }
+    if (TRANS_B) {  // B[k][j] = Bt[j][k], Bt row-major [N, K]
+      const int j = tid >> 2, kq = (tid & 3) * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int kk = k0 + kq + q;
+        Bs[kq + q][j] = (n0 + j < g.N && kk < g.K) ? B[(size_t)(n0 + j) * g.ldb + kk] : 0.f;
+      }
+    } else {
+      const int kr = tid >> 4, jq = (tid & 15) * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = n0 + jq + q;
+        Bs[kr][jq + q] = (k0 + kr < g.K && j < g.N) ? B[(size_t)(k0 + kr) * g.ldb + j] : 0.f;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      float av[2], bv[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        av[t] = As[wm + 16 * t + lo][4 * kk + hi];
+        bv[t] = Bs[4 * kk + hi][wn + 16 * t + lo];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + 4 * hi + r, col = n0 + wn + 16 * j + lo;
+        if (row < g.M && col < g.N) {
+          float v = acc[i][j][r];
+          if (g.rowscale) v *= g.rowscale[(size_t)b * g.sR + row];
+          if (g.colbias) v += g.colbias[col];
+          if (g.relu) v = fmaxf(v, 0.f);
+          C[(size_t)row * g.ldc + col] = v;
+        }
+      }
+}
+
+__global__ void k_fold(int din, int dout, const float* __restrict__ rw, const float* __restrict__ rb,
+                       const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ Wf,
+                       float* __restrict__ bf) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < dout * din) {
+    const int k = e % din;
+    Wf[e] = W[e] * rw[k];
+  }
+  if (e < dout) {
+    float acc = bias[e];
+    for (int k = 0; k < din; ++k) acc = fmaf(W[(size_t)e * din + k], rb[k], acc);
+    bf[e] = acc;
+  }
+}
+
+// inv[r] = rsqrt(mean(Z[r]^2) + eps), one wave per row
+__global__ void k_row_inv(int rows, int d, const float* __restrict__ Z, float* __restrict__ inv) {
+  const int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float* z = Z + (size_t)r * d;
+  float ss = 0.f;
+  for (int k = lane; k < d; k += 64) ss = fmaf(z[k], z[k], ss);
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  if (lane == 0) inv[r] = 1.0f / sqrtf(ss / (float)d + 1e-5f);
+}
+
+// (I + Abar)[b, i, k] from the factored table; 32x32 tiles so both A[i][k] and A[k][i] are read coalesced
+__global__ void __launch_bounds__(256) k_abar_full(int n, const float* __restrict__ fc, const float* __restrict__ A,
+                                                   const float* __restrict__ dA, const float* __restrict__ red,
+                                                   int red_stride, float* __restrict__ out) {
+  const int b = blockIdx.z;
+  const int i0 = blockIdx.y * 32, k0 = blockIdx.x * 32;
+  const size_t nn = (size_t)n * n;
+  const float* Ab = A + b * nn;
+  const float* dAb = dA + b * nn;
+  const float* rb = red + (size_t)b * red_stride * n;
+  float* ob = out + b * nn;
+  __shared__ float tA[32][33], tD[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int y = ty; y < 32; y += 8) {  // transposed block: rows k0.., cols i0..
+    const int k = k0 + y, i = i0 + tx;
+    const bool ok = k < n && i < n;
+    tA[y][tx] = ok ? Ab[(size_t)k * n + i] : 0.f;
+    tD[y][tx] = ok ? dAb[(size_t)k * n + i] : 0.f;
+  }
+  __syncthreads();
+  const float s = rb[6 * n], sd = rb[7 * n];
+  for (int y = ty; y < 32; y += 8) {
+    const int i = i0 + y, k = k0 + tx;
+    if (i >= n || k >= n) continue;
+    const float aik = Ab[(size_t)i * n + k], dik = dAb[(size_t)i * n + k];
+    const float aki = tA[tx][y], dki = tD[tx][y];
+    float v = fc[GNCDE_FC_E_A] * aik + fc[GNCDE_FC_E_DA] * dik + fc[GNCDE_FC_ET_A] * aki + fc[GNCDE_FC_ET_DA] * dki;
+    v += fc[GNCDE_FC_WR_A] * rb[i] + fc[GNCDE_FC_WR_DA] * rb[n + i] + fc[GNCDE_FC_WC_A] * rb[2 * n + i] +
+         fc[GNCDE_FC_WC_DA] * rb[3 * n + i] + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
+    v += fc[GNCDE_FC_VR_A] * rb[k] + fc[GNCDE_FC_VR_DA] * rb[n + k] + fc[GNCDE_FC_VC_A] * rb[2 * n + k] +
+         fc[GNCDE_FC_VC_DA] * rb[3 * n + k];
+    if (i == k)
+      v += fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * rb[4 * n + i] + fc[GNCDE_FC_UD_DA] * rb[5 * n + i] +
+           fc[GNCDE_FC_UR_A] * rb[i] + fc[GNCDE_FC_UR_DA] * rb[n + i] + fc[GNCDE_FC_UC_A] * rb[2 * n + i] +
+           fc[GNCDE_FC_UC_DA] * rb[3 * n + i] + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
+    ob[(size_t)i * n + k] = v;
+  }
+}
+
+}  // namespace
+
+void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st) {
+  const dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, batch);
+  if (trans_b)
+    hipLaunchKernelGGL(k_gemm<true>, grid, dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL(k_gemm<false>, grid, dim3(256), 0, st, g);
+}
+
+void fold_linear(int din, int dout, const float* rw, const float* rb, const float* W, const float* bias, float* Wf,
+                 float* bf, hipStream_t st) {
+  const int tot = din * dout > dout ? din * dout : dout;
+  hipLaunchKernelGGL(k_fold, dim3((tot + 255) / 256), dim3(256), 0, st, din, dout, rw, rb, W, bias, Wf, bf);
+}
+
+void row_inv(int rows, int d, const float* Z, float* inv, hipStream_t st) {
+  hipLaunchKernelGGL(k_row_inv, dim3((rows + 3) / 4), dim3(256), 0, st, rows, d, Z, inv);
+}
+
+void abar_full(int B, int n, const float* fc, const float* A, const float* dA, const float* red, int red_stride,
+               float* out, hipStream_t st) {
+  const dim3 grid((n + 31) / 32, (n + 31) / 32, B);
+  hipLaunchKernelGGL(k_abar_full, grid, dim3(256), 0, st, n, fc, A, dA, red, red_stride, out);
+}
+
+}  // namespace gncde

@@ -80,83 +80,6 @@ __global__ void k_reduce(int n, const float* __restrict__ A, const float* __rest
   }
 }
 
-// ---- RMSNorm + Linear: m[b,i,o] = sum_k (rmsnorm(Z[b,i,:])[k]) W[o,k] + bias[o] -------------------
-__global__ void k_rms_linear(int n, int din, int dout, const float* __restrict__ Z,
-                             const float* __restrict__ rw, const float* __restrict__ rbias,
-                             const float* __restrict__ W, const float* __restrict__ bias,
-                             float* __restrict__ m) {
-  const int b = blockIdx.y;
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (size_t)n * dout) return;
-  const int i = (int)(e / dout), o = (int)(e % dout);
-  const float* z = Z + ((size_t)b * n + i) * din;
-  float ss = 0.f;
-  for (int k = 0; k < din; ++k) ss = fmaf(z[k], z[k], ss);
-  const float inv = 1.0f / sqrtf(ss / (float)din + 1e-5f);
-  float acc = bias[o];
-  const float* w = W + (size_t)o * din;
-  for (int k = 0; k < din; ++k) acc = fmaf(fmaf(z[k] * inv, rw[k], rbias[k]), w[k], acc);
-  m[((size_t)b * n + i) * dout + o] = acc;
-}
-
-// ---- factored (I + Abar)[i,k] on the fly ----------------------------------------------------------
-__device__ __forceinline__ float abar_elem(const float* __restrict__ fc, const float* __restrict__ A,
-                                           const float* __restrict__ dA, const float* __restrict__ rb,
-                                           int n, int i, int k) {
-  const float aik = A[(size_t)i * n + k], aki = A[(size_t)k * n + i];
-  const float dik = dA[(size_t)i * n + k], dki = dA[(size_t)k * n + i];
-  const float s = rb[6 * n], sd = rb[7 * n];
-  float v = fc[GNCDE_FC_E_A] * aik + fc[GNCDE_FC_E_DA] * dik + fc[GNCDE_FC_ET_A] * aki +
-            fc[GNCDE_FC_ET_DA] * dki;
-  const float wi = fc[GNCDE_FC_WR_A] * rb[i] + fc[GNCDE_FC_WR_DA] * rb[n + i] +
-                   fc[GNCDE_FC_WC_A] * rb[2 * n + i] + fc[GNCDE_FC_WC_DA] * rb[3 * n + i] +
-                   fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
-  const float vk = fc[GNCDE_FC_VR_A] * rb[k] + fc[GNCDE_FC_VR_DA] * rb[n + k] +
-                   fc[GNCDE_FC_VC_A] * rb[2 * n + k] + fc[GNCDE_FC_VC_DA] * rb[3 * n + k];
-  v += wi + vk;
-  if (i == k) {
-    v += fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * rb[4 * n + i] + fc[GNCDE_FC_UD_DA] * rb[5 * n + i] +
-         fc[GNCDE_FC_UR_A] * rb[i] + fc[GNCDE_FC_UR_DA] * rb[n + i] + fc[GNCDE_FC_UC_A] * rb[2 * n + i] +
-         fc[GNCDE_FC_UC_DA] * rb[3 * n + i] + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
-  }
-  return v;
-}
-
-// ---- Zout[b,i,o] = sum_k (I+Abar)[i,k] m[b,k,o], ReLU optional; 16x16 LDS tiles ------------------
-__global__ void __launch_bounds__(256) k_prop(int n, int d, const float* __restrict__ fc,
-                                              const float* __restrict__ A, const float* __restrict__ dA,
-                                              const float* __restrict__ red, const float* __restrict__ m,
-                                              float* __restrict__ Zout, int relu) {
-  const int b = blockIdx.z;
-  const int o0 = blockIdx.x * 16, i0 = blockIdx.y * 16;
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const size_t nn = (size_t)n * n;
-  const float* Ab = A + b * nn;
-  const float* dAb = dA + b * nn;
-  const float* rb = red + (size_t)b * kRedStride * n;
-  const float* mb = m + (size_t)b * n * d;
-  __shared__ float sA[16][17];
-  __shared__ float sM[16][17];
-  float acc = 0.f;
-  for (int k0 = 0; k0 < n; k0 += 16) {
-    {
-      const int i = i0 + ty, k = k0 + tx;
-      sA[ty][tx] = (i < n && k < n) ? abar_elem(fc, Ab, dAb, rb, n, i, k) : 0.f;
-      const int kk = k0 + ty, o = o0 + tx;
-      sM[ty][tx] = (kk < n && o < d) ? mb[(size_t)kk * d + o] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc = fmaf(sA[ty][q], sM[q][tx], acc);
-    __syncthreads();
-  }
-  const int i = i0 + ty, o = o0 + tx;
-  if (i < n && o < d) {
-    if (relu) acc = fmaxf(acc, 0.f);
-    Zout[((size_t)b * n + i) * d + o] = acc;
-  }
-}
-
 // ---- epilogue: ODE dy = tg * Z; CDE dy[i,m] = tg[i] * sum_{l,k} Z[i,(m*de+l)*2+k] dX[i,l,k] --------
 __global__ void k_finalize(int n, int dL, int h, int de, int T, const float* __restrict__ ts,
                            const float* __restrict__ data_coef, const float* __restrict__ t,
@@ -255,15 +178,19 @@ __global__ void k_grid_stats(int B, int method, const int32_t* __restrict__ nste
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
 struct VfWs {
-  float *A, *dA, *red, *tg, *Z0, *Z1, *m;
+  float *A, *dA, *red, *tg, *Z0, *Z1, *m, *abar, *wf, *bf, *inv;
 };
 
-VfWs carve_vf(const GncdeProblem& p, char* ws) {
+size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   const size_t B = p.B, n = p.n, nn = n * n, D = max_dim(p);
-  VfWs w;
+  size_t wmax = 0;
+  for (int l = 0; l < p.L; ++l) {
+    const size_t e = (size_t)p.dims[l] * p.dims[l + 1];
+    wmax = e > wmax ? e : wmax;
+  }
   size_t off = 0;
   auto take = [&](size_t floats) {
-    float* ptr = reinterpret_cast<float*>(ws + off);
+    float* ptr = ws ? reinterpret_cast<float*>(ws + off) : nullptr;
     off += align_up(floats * sizeof(float), 256);
     return ptr;
   };
@@ -274,26 +201,28 @@ VfWs carve_vf(const GncdeProblem& p, char* ws) {
   w.Z0 = take(B * n * D);
   w.Z1 = take(B * n * D);
   w.m = take(B * n * D);
-  return w;
+  w.abar = take(B * nn);
+  w.wf = take(wmax);
+  w.bf = take(D);
+  w.inv = take(B * n);
+  return off;
 }
 
 }  // namespace
 
 size_t generic_vf_workspace(const GncdeProblem& p) {
-  const size_t B = p.B, n = p.n, nn = n * n, D = max_dim(p);
-  size_t s = 0;
-  s += 2 * align_up(B * nn * 4, 256);
-  s += align_up(B * kRedStride * n * 4, 256);
-  s += align_up(B * n * 4, 256);
-  s += 3 * align_up(B * n * D * 4, 256);
-  return s;
+  VfWs w;
+  return carve_vf(p, nullptr, w);
 }
 
+// One evaluation = spline + reductions, then per layer two MFMA GEMMs (gncde_gemm.hip): the Linear over all
+// B*n node rows with RMSNorm folded in, and the per-sample (I + Abar) m with (I + Abar) materialised once.
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
-  VfWs w = carve_vf(p, ws);
+  VfWs w;
+  carve_vf(p, ws, w);
   hipLaunchKernelGGL(k_spline, dim3(cdiv(nn > (size_t)n ? nn : n, 256), B), dim3(256), 0, st, n, p.T,
                      p.ts, p.coef, p.tcoef, t, w.A, w.dA, w.tg);
   hipLaunchKernelGGL(k_reduce, dim3(B), dim3(256), 0, st, n, w.A, w.dA, w.red);
@@ -302,13 +231,38 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
     const LayerOffsets o = layer_offsets(p, l);
-    hipLaunchKernelGGL(k_rms_linear, dim3(cdiv((size_t)n * dout, 256), B), dim3(256), 0, st, n, din,
-                       dout, Zin, p.params + o.rms_w, p.params + o.rms_b, p.params + o.W,
-                       p.params + o.b, w.m);
+    fold_linear(din, dout, p.params + o.rms_w, p.params + o.rms_b, p.params + o.W, p.params + o.b, w.wf, w.bf, st);
+    row_inv(B * n, din, Zin, w.inv, st);
+    GemmArgs lin{};
+    lin.M = B * n;
+    lin.N = dout;
+    lin.K = din;
+    lin.A = Zin;
+    lin.lda = din;
+    lin.B = w.wf;
+    lin.ldb = din;
+    lin.C = w.m;
+    lin.ldc = dout;
+    lin.rowscale = w.inv;
+    lin.colbias = w.bf;
+    gemm(lin, 1, true, st);
+    abar_full(B, n, p.fusion + (size_t)l * GNCDE_FC, w.A, w.dA, w.red, kRedStride, w.abar, st);
     float* Zout = bufs[l & 1];
-    hipLaunchKernelGGL(k_prop, dim3(cdiv(dout, 16), cdiv(n, 16), B), dim3(256), 0, st, n, dout,
-                       p.fusion + (size_t)l * GNCDE_FC, w.A, w.dA, w.red, w.m, Zout,
-                       l < p.L - 1 ? 1 : 0);
+    GemmArgs pr{};
+    pr.M = n;
+    pr.N = dout;
+    pr.K = n;
+    pr.A = w.abar;
+    pr.lda = n;
+    pr.sA = (long)nn;
+    pr.B = w.m;
+    pr.ldb = dout;
+    pr.sB = (long)n * dout;
+    pr.C = Zout;
+    pr.ldc = dout;
+    pr.sC = (long)n * dout;
+    pr.relu = l < p.L - 1 ? 1 : 0;
+    gemm(pr, B, false, st);
     Zin = Zout;
   }
   const int dout = out_dim(p);

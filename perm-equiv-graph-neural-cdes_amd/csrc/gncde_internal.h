@@ -99,6 +99,27 @@ inline int max_dim(const GncdeProblem& p) {
 int validate_problem(const GncdeProblem* p);
 int validate_solver(const GncdeProblem* p, const GncdeSolver* s);
 
+// batched fp32 MFMA GEMM and helpers: gncde_gemm.hip
+struct GemmArgs {
+  int M, N, K;
+  const float* A;  // A[b] + r * lda + k
+  long lda, sA;
+  const float* B;  // NN: B[b] + k * ldb + j;  TRANS_B: B[b] + j * ldb + k
+  long ldb, sB;
+  float* C;
+  long ldc, sC;
+  const float* rowscale;  // optional: C = rowscale[b * sR + r] * acc
+  long sR;
+  const float* colbias;  // optional [N]
+  int relu;
+};
+void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st);
+void fold_linear(int din, int dout, const float* rw, const float* rb, const float* W, const float* bias, float* Wf,
+                 float* bf, hipStream_t st);
+void row_inv(int rows, int d, const float* Z, float* inv, hipStream_t st);
+void abar_full(int B, int n, const float* fc, const float* A, const float* dA, const float* red, int red_stride,
+               float* out, hipStream_t st);
+
 // generic (any-shape, multi-kernel) path: gncde_generic.hip
 size_t generic_vf_workspace(const GncdeProblem& p);
 size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s);

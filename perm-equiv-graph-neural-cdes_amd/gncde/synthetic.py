@@ -148,3 +148,36 @@ def to_reference_coeffs(prob: Problem, b: int):
             time_ch = tc[:, q, None, :].expand(-1, n, n).clone()
         out.append(torch.stack([time_ch, co[:, q]], dim=-1).numpy())
     return ts.numpy(), tuple(out)
+
+
+def cde_batch(B: int, n: int, T: int, hidden: int, embed: int, num_layers: int, t1: float, kind: str = "undirected",
+              seed: int = 1234, device="cuda", chunk: int = 16):
+    """PGT/TGB-shaped CDE-wrapper batch: a community graph with log-normal edge weights
+    whose edges toggle between knots, normalised-Laplacian operator path, node data x [T, n, embed] stacked
+    with time into the data spline; knots evenly spaced on [0, t1].  Returns (Problem, y0 [B, n, hidden])."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    ts = torch.linspace(0.0, t1, T).repeat(B, 1).to(device)
+    coef = torch.empty(B, T - 1, 4, n, n, device=device)
+    base = community_adjacency(n, seed=seed, device=device)
+    for s in range(0, B, chunk):
+        e = min(B, s + chunk)
+        b = e - s
+        w = torch.exp(torch.randn(b, T, n, n, generator=g)).to(device)
+        keep = (torch.rand(b, T, n, n, generator=g) > 0.05).to(device)
+        A = base * w * keep
+        d, c, bb, a = hermite_coefficients(ts[s:e], normalized_laplacian(A))
+        coef[s:e, :, 0], coef[s:e, :, 1], coef[s:e, :, 2], coef[s:e, :, 3] = d, c, bb, a
+    tcoef = torch.zeros(B, T - 1, 3, n, device=device)
+    tcoef[:, :, 2] = 1.0
+    x = torch.randn(B, T, n, embed, generator=g).to(device)
+    X = torch.stack([ts[:, :, None, None].expand(B, T, n, embed), x], dim=-1)
+    d, c, bb, a = hermite_coefficients(ts, X)
+    data_coef = torch.stack([d, c, bb, a], dim=2).contiguous()  # [B, T-1, 4, n, de, 2]
+    dims = [hidden] * num_layers + [hidden * embed * 2]
+    layers = init_layers(kind, dims, g)
+    fusion = layout.fusion_table(kind, layers, n).to(torch.float32).to(device).contiguous()
+    params = layout.pack_params(layers, device=device)
+    prob = Problem(ts=ts.contiguous(), coef=coef, tcoef=tcoef, fusion=fusion, params=params, dims=dims,
+                   data_coef=data_coef, cde_hidden=hidden, cde_embed=embed)
+    y0 = torch.randn(B, n, hidden, generator=g).to(device)
+    return prob, y0
