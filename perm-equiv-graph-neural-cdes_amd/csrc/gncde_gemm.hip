@@ -5,9 +5,10 @@
 //   Z_next = act((I + Abar)  m)               (per-sample GEMM; (I + Abar) materialised once per layer)
 //
 // This is what makes the wide CDE-wrapper layers of configs 3 / 5 (d_L = 1024 / 512, MFMA-bound, SURVEY
-// §8d) run on the matrix cores instead of scalar FMAs.  The GEMM is a plain 64x64-tile, K-chunk-16 LDS
-// kernel on v_mfma_f32_16x16x4f32 (each wave a 32x32 sub-tile, 4 independent accumulators); bounds are
-// zero-filled so any M, N, K (n = 129, 255 ...) works.
+// §8d) run on the matrix cores instead of scalar FMAs.  The GEMM is a 64x64-tile, K-chunk-32 LDS kernel on
+// v_mfma_f32_16x16x4f32 (each wave a 32x32 sub-tile, 4 independent accumulators) whose next chunk is
+// prefetched into registers while the current one is consumed; bounds are zero-filled so any M, N, K
+// (n = 129, 255 ...) works.
 #include "gncde_internal.h"
 
 namespace gncde {
@@ -18,13 +19,14 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 template <bool TRANS_B>
 __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
+  constexpr int KC = 32;
   const int b = blockIdx.z;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
   const float* A = g.A + (size_t)b * g.sA;
   const float* B = g.B + (size_t)b * g.sB;
   float* C = g.C + (size_t)b * g.sC;
-  __shared__ float As[64][17];
-  __shared__ float Bs[16][68];
+  __shared__ float As[64][KC + 1];
+  __shared__ float Bs[KC][68];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
   floatx4 acc[2][2];
@@ -32,34 +34,42 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int ar = tid >> 2, aq = (tid & 3) * 4;  // A tile: row, 4 k
-  for (int k0 = 0; k0 < g.K; k0 += 16) {
-    {
-      const int r = m0 + ar;
+  // per-thread slices of the next chunk, prefetched into registers while the current one is consumed
+  const int ar = tid >> 2, aq = (tid & 3) * 8;                                   // A: row, 8 k
+  const int br = TRANS_B ? (tid >> 2) : (tid >> 3), bq = TRANS_B ? (tid & 3) * 8 : (tid & 7) * 8;
+  float ra[8], rb[8];
+  auto fetch = [&](int k0) {
+    const int r = m0 + ar;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int kk = k0 + aq + q;
-        As[ar][aq + q] = (r < g.M && kk < g.K) ? A[(size_t)r * g.lda + kk] : 0.f;
+    for (int q = 0; q < 8; ++q) {
+      const int kk = k0 + aq + q;
+      ra[q] = (r < g.M && kk < g.K) ? A[(size_t)r * g.lda + kk] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (TRANS_B) {  // B[k][j] = Bt[j][k]: row j = n0 + br, k = k0 + bq + q
+        const int j = n0 + br, kk = k0 + bq + q;
+        rb[q] = (j < g.N && kk < g.K) ? B[(size_t)j * g.ldb + kk] : 0.f;
+      } else {        // row k = k0 + br, col j = n0 + bq + q
+        const int kk = k0 + br, j = n0 + bq + q;
+        rb[q] = (kk < g.K && j < g.N) ? B[(size_t)kk * g.ldb + j] : 0.f;
       }
     }
-    if (TRANS_B) {  // B[k][j] = Bt[j][k], Bt row-major [N, K]
-      const int j = tid >> 2, kq = (tid & 3) * 4;
+  };
+  fetch(0);
+  for (int k0 = 0; k0 < g.K; k0 += KC) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int kk = k0 + kq + q;
-        Bs[kq + q][j] = (n0 + j < g.N && kk < g.K) ? B[(size_t)(n0 + j) * g.ldb + kk] : 0.f;
-      }
-    } else {
-      const int kr = tid >> 4, jq = (tid & 15) * 4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = n0 + jq + q;
-        Bs[kr][jq + q] = (k0 + kr < g.K && j < g.N) ? B[(size_t)(k0 + kr) * g.ldb + j] : 0.f;
-      }
+    for (int q = 0; q < 8; ++q) {
+      As[ar][aq + q] = ra[q];
+      if (TRANS_B)
+        Bs[bq + q][br] = rb[q];
+      else
+        Bs[br][bq + q] = rb[q];
     }
     __syncthreads();
+    if (k0 + KC < g.K) fetch(k0 + KC);
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
+    for (int kk = 0; kk < KC / 4; ++kk) {
       float av[2], bv[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {

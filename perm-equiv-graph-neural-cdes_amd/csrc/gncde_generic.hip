@@ -38,46 +38,45 @@ __global__ void k_spline(int n, int T, const float* __restrict__ ts, const float
 }
 
 // ---- row/col sums, diagonals, totals --------------------------------------------------------------
-__global__ void k_reduce(int n, const float* __restrict__ A, const float* __restrict__ dA,
-                         float* __restrict__ red) {
-  const int b = blockIdx.x;
+// grid (B, 4): q = blockIdx.y selects row sums of A / dA (one wave per row, lanes along the row: coalesced;
+// these blocks also write the diagonals and the totals) or column sums of A / dA (one thread per column,
+// walking down the rows: coalesced across the threads).
+__global__ void __launch_bounds__(256) k_reduce(int n, const float* __restrict__ A, const float* __restrict__ dA,
+                                                float* __restrict__ red) {
+  const int b = blockIdx.x, q = blockIdx.y;
   const size_t nn = (size_t)n * n;
-  const float* Ab = A + b * nn;
-  const float* dAb = dA + b * nn;
+  const float* M = ((q & 1) ? dA : A) + b * nn;
   float* rb = red + (size_t)b * kRedStride * n;
-  __shared__ float part[2][256];
-  float ps = 0.f, psd = 0.f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    float r = 0.f, rd = 0.f, c = 0.f, cd = 0.f;
-    for (int k = 0; k < n; ++k) {
-      r += Ab[(size_t)i * n + k];
-      rd += dAb[(size_t)i * n + k];
-      c += Ab[(size_t)k * n + i];
-      cd += dAb[(size_t)k * n + i];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  if (q >= 2) {
+    for (int j = tid; j < n; j += blockDim.x) {
+      float c0 = 0.f, c1 = 0.f;
+      int k = 0;
+      for (; k + 1 < n; k += 2) {
+        c0 += M[(size_t)k * n + j];
+        c1 += M[(size_t)(k + 1) * n + j];
+      }
+      if (k < n) c0 += M[(size_t)k * n + j];
+      rb[q * n + j] = c0 + c1;
     }
-    rb[0 * n + i] = r;
-    rb[1 * n + i] = rd;
-    rb[2 * n + i] = c;
-    rb[3 * n + i] = cd;
-    rb[4 * n + i] = Ab[(size_t)i * n + i];
-    rb[5 * n + i] = dAb[(size_t)i * n + i];
-    ps += r;
-    psd += rd;
+    return;
   }
-  part[0][threadIdx.x] = ps;
-  part[1][threadIdx.x] = psd;
+  __shared__ float part[4];
+  float tot = 0.f;
+  for (int i = w; i < n; i += 4) {
+    const float* row = M + (size_t)i * n;
+    float s = 0.f;
+    for (int k = lane; k < n; k += 64) s += row[k];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) {
+      rb[q * n + i] = s;
+      rb[(4 + q) * n + i] = row[i];
+    }
+    tot += s;
+  }
+  if (lane == 0) part[w] = tot;
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      part[0][threadIdx.x] += part[0][threadIdx.x + s];
-      part[1][threadIdx.x] += part[1][threadIdx.x + s];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    rb[6 * n] = part[0][0];
-    rb[7 * n] = part[1][0];
-  }
+  if (tid == 0) rb[(6 + q) * n] = (part[0] + part[1]) + (part[2] + part[3]);
 }
 
 // ---- epilogue: ODE dy = tg * Z; CDE dy[i,m] = tg[i] * sum_{l,k} Z[i,(m*de+l)*2+k] dX[i,l,k] --------
@@ -183,10 +182,10 @@ struct VfWs {
 
 size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   const size_t B = p.B, n = p.n, nn = n * n, D = max_dim(p);
-  size_t wmax = 0;
+  size_t wsum = 0, bsum = 0;
   for (int l = 0; l < p.L; ++l) {
-    const size_t e = (size_t)p.dims[l] * p.dims[l + 1];
-    wmax = e > wmax ? e : wmax;
+    wsum += (size_t)p.dims[l] * p.dims[l + 1];
+    bsum += (size_t)p.dims[l + 1];
   }
   size_t off = 0;
   auto take = [&](size_t floats) {
@@ -202,8 +201,8 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.Z1 = take(B * n * D);
   w.m = take(B * n * D);
   w.abar = take(B * nn);
-  w.wf = take(wmax);
-  w.bf = take(D);
+  w.wf = take(wsum);  // W' = W diag(rms_w) per layer, back to back
+  w.bf = take(bsum);  // bias' = bias + W rms_b per layer
   w.inv = take(B * n);
   return off;
 }
@@ -217,21 +216,36 @@ size_t generic_vf_workspace(const GncdeProblem& p) {
 
 // One evaluation = spline + reductions, then per layer two MFMA GEMMs (gncde_gemm.hip): the Linear over all
 // B*n node rows with RMSNorm folded in, and the per-sample (I + Abar) m with (I + Abar) materialised once.
+// Fold every layer's RMSNorm affine into its Linear (once per solve, not per evaluation).
+void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
+  VfWs w;
+  carve_vf(p, ws, w);
+  size_t wo = 0, bo = 0;
+  for (int l = 0; l < p.L; ++l) {
+    const int din = p.dims[l], dout = p.dims[l + 1];
+    const LayerOffsets o = layer_offsets(p, l);
+    fold_linear(din, dout, p.params + o.rms_w, p.params + o.rms_b, p.params + o.W, p.params + o.b, w.wf + wo,
+                w.bf + bo, st);
+    wo += (size_t)din * dout;
+    bo += dout;
+  }
+}
+
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st) {
+                    hipStream_t st, bool prepared) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
   VfWs w;
   carve_vf(p, ws, w);
+  if (!prepared) generic_vf_prepare(p, ws, st);
   hipLaunchKernelGGL(k_spline, dim3(cdiv(nn > (size_t)n ? nn : n, 256), B), dim3(256), 0, st, n, p.T,
                      p.ts, p.coef, p.tcoef, t, w.A, w.dA, w.tg);
-  hipLaunchKernelGGL(k_reduce, dim3(B), dim3(256), 0, st, n, w.A, w.dA, w.red);
+  hipLaunchKernelGGL(k_reduce, dim3(B, 4), dim3(256), 0, st, n, w.A, w.dA, w.red);
   const float* Zin = y;
   float* bufs[2] = {w.Z0, w.Z1};
+  size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
-    const LayerOffsets o = layer_offsets(p, l);
-    fold_linear(din, dout, p.params + o.rms_w, p.params + o.rms_b, p.params + o.W, p.params + o.b, w.wf, w.bf, st);
     row_inv(B * n, din, Zin, w.inv, st);
     GemmArgs lin{};
     lin.M = B * n;
@@ -239,13 +253,15 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     lin.K = din;
     lin.A = Zin;
     lin.lda = din;
-    lin.B = w.wf;
+    lin.B = w.wf + wo;
     lin.ldb = din;
     lin.C = w.m;
     lin.ldc = dout;
     lin.rowscale = w.inv;
-    lin.colbias = w.bf;
+    lin.colbias = w.bf + bo;
     gemm(lin, 1, true, st);
+    wo += (size_t)din * dout;
+    bo += dout;
     abar_full(B, n, p.fusion + (size_t)l * GNCDE_FC, w.A, w.dA, w.red, kRedStride, w.abar, st);
     float* Zout = bufs[l & 1];
     GemmArgs pr{};
@@ -306,10 +322,11 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   (void)hipMemcpyAsync(y, y0, B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
   if (s.save_mode == GNCDE_SAVE_STEPS)
     hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, 0, y, ys);
+  generic_vf_prepare(p, ws, st);
 
   auto eval = [&](float c, const float* yin, float* out) {
     hipLaunchKernelGGL(k_stage_time, dim3(gb), dim3(256), 0, st, B, c, tcur, hcur, tst);
-    return generic_vf_eval(p, tst, yin, out, ws, st);
+    return generic_vf_eval(p, tst, yin, out, ws, st, true);
   };
   auto combo = [&](std::initializer_list<std::pair<int, float>> terms, float* out) {
     Combo cb{};

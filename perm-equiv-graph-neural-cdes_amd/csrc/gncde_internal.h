@@ -123,8 +123,9 @@ void abar_full(int B, int n, const float* fc, const float* A, const float* dA, c
 // generic (any-shape, multi-kernel) path: gncde_generic.hip
 size_t generic_vf_workspace(const GncdeProblem& p);
 size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s);
+void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st);
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st);
+                    hipStream_t st, bool prepared = false);
 int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
                       int32_t* stats, char* ws, hipStream_t st);
 

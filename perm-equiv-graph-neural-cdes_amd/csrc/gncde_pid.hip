@@ -306,12 +306,13 @@ int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const flo
   int* active = reinterpret_cast<int*>(take(B * 4));
   a.ys = ys;
   hipLaunchKernelGGL(k_pid_init, dim3(B), dim3(256), 0, st, a, y0);
+  generic_vf_prepare(p, ws, st);
   // each sample needs at most 2 + 6 * max_steps + 1 evaluations
   const long max_iter = 3L + 6L * (long)s.max_steps;
   int rc = GNCDE_OK;
   for (long it = 0; it < max_iter; ++it) {
     hipLaunchKernelGGL(k_pid_tst, dim3((B + 255) / 256), dim3(256), 0, st, B, a.state, tst, active);
-    rc = generic_vf_eval(p, tst, a.yt, K, ws, st);
+    rc = generic_vf_eval(p, tst, a.yt, K, ws, st, true);
     if (rc) return rc;
     hipLaunchKernelGGL(k_pid_advance, dim3(B), dim3(256), 0, st, a);
     if ((it + 1) % kPoll == 0) {

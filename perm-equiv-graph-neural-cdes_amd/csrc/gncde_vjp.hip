@@ -616,6 +616,7 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
   carve(p, ws, w, &bytes);
   char* vf_ws = ws + bytes;
   const Tableau tab = s.method == GNCDE_RK4 ? rk4_tab() : tsit5_tab();
+  generic_vf_prepare(p, vf_ws, st);
   const unsigned gb = cdiv(B, 256);
   const dim3 ge(cdiv(E, 256), B);
   (void)hipMemsetAsync(w.gp, 0, (size_t)B * P * sizeof(float), st);
@@ -642,7 +643,7 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
       hipLaunchKernelGGL(v_lincomb, ge, dim3(256), 0, st, B, E, w.y, lc, w.hcur, w.U[i], 0);
       hipLaunchKernelGGL(v_stage_time, dim3(gb), dim3(256), 0, st, B, tab.c[i], w.tcur, w.hcur, w.tst);
       if (i + 1 < tab.stages) {  // the last stage's value is not needed for the reverse sweep
-        const int rc = generic_vf_eval(p, w.tst, w.U[i], w.K[i], vf_ws, st);
+        const int rc = generic_vf_eval(p, w.tst, w.U[i], w.K[i], vf_ws, st, true);
         if (rc) return rc;
       }
     }
