@@ -194,7 +194,11 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     if (n == NP) {
       const float4* c4 = reinterpret_cast<const float4*>(cb);
       constexpr int NQ = NP * NP / 4;
-      for (int e4 = ftid; e4 < NQ; e4 += NT) {
+      // fully unrolled: every coefficient load of the interval is in flight before the first use (one HBM
+      // round trip per form instead of NP/16 dependent ones)
+#pragma unroll
+      for (int it = 0; it < NQ / NT; ++it) {
+        const int e4 = ftid + it * NT;
         const float4 d = c4[e4], c = c4[NQ + e4], bb = c4[2 * NQ + e4], aa = c4[3 * NQ + e4];
         const int r = (e4 * 4) / NP, k = (e4 * 4) % NP;
         float* pa = sA + swz<NP>(r, k);
