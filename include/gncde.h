@@ -180,6 +180,22 @@ int gncde_clip_adamw(int32_t P, float* params, const float* grads, float* m, flo
                      float b1, float b2, float eps, float weight_decay, float max_norm, float* stats,
                      void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- input side ------------------------------------------------------------------------------ */
+/* Graph operators of misc.py:58-113 (get_graph_operator), per graph, fp32:
+ *   NORM_LAP        I - D_out^-1/2 (A + I) D_in^-1/2, degrees of A + I   (default, misc.py:83-99)
+ *   NORM_ADJ, KIPF  D_out^-1/2 (A + I) D_in^-1/2, degrees of A + I        (misc.py:101-113, zipf_smoothing :16-33)
+ *   NORMALIZED_PLUS D_out^-1/2 (A + I) D_in^-1/2, degrees of A (0 -> 0)   (misc.py:36-57)
+ * A, out: [graphs, n, n]; workspace: 2 * graphs * n floats (device). */
+enum { GNCDE_OP_NORM_LAP = 0, GNCDE_OP_NORM_ADJ = 1, GNCDE_OP_KIPF = 2, GNCDE_OP_NORMALIZED_PLUS = 3 };
+int gncde_graph_operator(int32_t kind, int32_t graphs, int32_t n, const float* A, float* out, float* workspace,
+                         void* stream);
+
+/* diffrax.backward_hermite_coefficients over knots ts [B, T] of X [B, T, C] (any channel count C), written in
+ * the engine layout out [B, T-1, ncoef, C] with (d, c, b, a) order; ncoef = 4, or 3 to drop a (the tcoef
+ * layout).  dataset_configs.py:170, tgb_graph_neural_cde.py:130. */
+int gncde_hermite_coefficients(int32_t B, int32_t T, int32_t C, int32_t ncoef, const float* ts, const float* X,
+                               float* out, void* stream);
+
 /* idx[k] = clip(searchsorted(ts[b], t[k], 'left') - 1, 0, T-2) with b = sample[k].
  * ts: [B, T], t: [count], sample: [count] int32, idx: [count] int32. */
 int gncde_interval_index(const float* ts, int32_t B, int32_t T, const float* t, const int32_t* sample,

@@ -18,6 +18,7 @@ RK4, TSIT5 = 0, 1
 CTRL_GRID, CTRL_PID = 0, 1
 SAVE_T1, SAVE_STEPS, SAVE_TS = 0, 1, 2
 STAT_STEPS, STAT_REJECTS, STAT_EVALS, STAT_STATUS = 0, 1, 2, 3
+OP_NORM_LAP, OP_NORM_ADJ, OP_KIPF, OP_NORMALIZED_PLUS = 0, 1, 2, 3
 
 LIB_NAME = "libgncde_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
@@ -37,6 +38,8 @@ EXPORTED_SYMBOLS = (
     "gncde_adamw_workspace_bytes",
     "gncde_clip_adamw",
     "gncde_interval_index",
+    "gncde_graph_operator",
+    "gncde_hermite_coefficients",
 )
 
 
@@ -127,6 +130,11 @@ def load(path: str | None = None):
     lib.gncde_interval_index.restype = c_int32
     lib.gncde_interval_index.argtypes = [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32,
                                          c_void_p]
+    lib.gncde_graph_operator.restype = c_int32
+    lib.gncde_graph_operator.argtypes = [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.gncde_hermite_coefficients.restype = c_int32
+    lib.gncde_hermite_coefficients.argtypes = [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                               c_void_p]
     v = lib.gncde_abi_version()
     if v != ABI_VERSION:
         raise GncdeError(f"ABI mismatch: library {v}, bindings {ABI_VERSION}")

@@ -280,6 +280,39 @@ def clip_adamw(params: torch.Tensor, grads: torch.Tensor, m: torch.Tensor, v: to
     return stats
 
 
+_OPERATORS = {"norm_lap": _lib.OP_NORM_LAP, "norm_adj": _lib.OP_NORM_ADJ, "kipf": _lib.OP_KIPF,
+              "normalized_plus": _lib.OP_NORMALIZED_PLUS}
+
+
+def graph_operator(A: torch.Tensor, operator_type: str = "norm_lap") -> torch.Tensor:
+    """``get_graph_operator(operator_type, A, L)`` (misc.py:104-113) on the GPU for a stack of graphs
+    A [..., n, n].  Unknown names fall back to norm_lap exactly like the reference's ``else`` branch."""
+    _require_gpu()
+    lib = _lib.load()
+    kind = _OPERATORS.get(operator_type.lower(), _lib.OP_NORM_LAP)
+    A = A.to(device="cuda", dtype=torch.float32).contiguous()
+    n = int(A.shape[-1])
+    graphs = A.numel() // (n * n)
+    out = torch.empty_like(A)
+    ws = torch.empty(2 * max(graphs, 1) * n, dtype=torch.float32, device=A.device)
+    _lib.check(lib.gncde_graph_operator(kind, graphs, n, _ptr(A), _ptr(out), _ptr(ws), _stream()))
+    return out
+
+
+def hermite_coefficients(ts: torch.Tensor, X: torch.Tensor, ncoef: int = 4) -> torch.Tensor:
+    """Backward-Hermite coefficients of X [B, T, ...] over ts [B, T] in the engine layout
+    [B, T-1, ncoef, ...] ((d, c, b, a) order; ncoef=3 drops a)."""
+    _require_gpu()
+    lib = _lib.load()
+    X = X.to(device="cuda", dtype=torch.float32).contiguous()
+    ts = ts.to(device=X.device, dtype=torch.float32).contiguous()
+    B, T = int(X.shape[0]), int(X.shape[1])
+    C = X.numel() // max(B * T, 1)
+    out = torch.empty((B, T - 1, ncoef) + tuple(X.shape[2:]), dtype=torch.float32, device=X.device)
+    _lib.check(lib.gncde_hermite_coefficients(B, T, C, ncoef, _ptr(ts), _ptr(X), _ptr(out), _stream()))
+    return out
+
+
 def interval_index(ts: torch.Tensor, t: torch.Tensor, sample: torch.Tensor) -> torch.Tensor:
     _require_gpu()
     lib = _lib.load()

@@ -45,6 +45,27 @@ def pack_control(coeffs, ts=None, device="cuda"):
     return coef, tcoef
 
 
+def control_from_knots(ts, X_op, X_time=None):
+    """Engine control layout straight from knot values on the GPU (gncde_hermite_coefficients):
+    X_op [B, T, n, n] operator path -> coef [B, T-1, 4, n, n]; the time channel X_time [B, T, n, n] (default:
+    ts broadcast, the reference's stacking at dataset_configs.py:168-170) -> tcoef [B, T-1, 3, n] (coefficients
+    of its column means; for X_time = ts that is d = c = 0, b = 1)."""
+    from . import engine
+    ts = torch.as_tensor(ts, dtype=torch.float32, device="cuda")
+    if ts.dim() == 1:
+        ts = ts.unsqueeze(0)
+    coef = engine.hermite_coefficients(ts, X_op, 4)
+    B, T, n = int(X_op.shape[0]), int(X_op.shape[1]), int(X_op.shape[-1])
+    if X_time is None:
+        tcoef = torch.zeros(B, T - 1, 3, n, device=coef.device)
+        tcoef[:, :, 2] = 1.0
+    else:
+        # coefficients first, column means second (as the reference's VF does): the mean of the knots first
+        # would round and the cubic term of a short interval would amplify that (d ~ 1/dt^2)
+        tcoef = engine.hermite_coefficients(ts, torch.as_tensor(X_time, device="cuda"), 3).mean(dim=-2)
+    return coef, tcoef
+
+
 def pack_data_control(coeffs, device="cuda"):
     """CDE data spline (d, c, b, a) each [B, T-1, n, de, 2] -> [B, T-1, 4, n, de, 2]."""
     parts = [torch.as_tensor(np.asarray(x) if not torch.is_tensor(x) else x) for x in coeffs]

@@ -15,7 +15,6 @@ from torch import nn
 
 from .. import _lib, autograd, engine, layout
 from ..interpolation import CubicInterpolation
-from ..synthetic import hermite_coefficients
 from . import vector_fields
 from .vector_fields.layers import _gen
 
@@ -250,9 +249,11 @@ class TGBGraphNeuralCDE(nn.Module):
         ts_d = control_adj.graph_layout()[0]
         xd = _affine(self.data_encoder, torch.as_tensor(x_data, dtype=torch.float32, device=ts_d.device))
         X = torch.stack([ts_d[:, :, None, None].expand_as(xd), xd], dim=-1)  # [B, T, n, de, 2]
-        control_data = CubicInterpolation(ts_d, hermite_coefficients(ts_d, X))
+        # the data spline rebuilt inside every forward (tgb_graph_neural_cde.py:118-130), on the GPU and
+        # directly in the engine layout [B, T-1, 4, n, de, 2]
+        data_coef = engine.hermite_coefficients(ts_d, X.detach())
         y0 = _affine(self.encoder, torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device))
-        prob = self.wrapped_vector_field.problem(control_adj, control_data)
+        prob = self.wrapped_vector_field.problem(control_adj, None, data_coef=data_coef)
         grids = [layout.constant_step_grid(t[0], t[-1], self.dt0) for t in ts_d.cpu().numpy()]
         grid, ns = layout.stack_grids(grids, device=ts_d.device)
         spec = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_T1, grid=grid,

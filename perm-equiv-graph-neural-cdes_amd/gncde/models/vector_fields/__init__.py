@@ -44,14 +44,15 @@ class _GraphVectorFieldBase(nn.Module):
         return [lay.as_dict() for lay in self.gnn_layers]
 
     def problem(self, control_adj: CubicInterpolation, control_data: CubicInterpolation | None = None,
-                cde_hidden: int = 0) -> engine.Problem:
+                cde_hidden: int = 0, data_coef: torch.Tensor | None = None) -> engine.Problem:
         ts, coef, tcoef = control_adj.graph_layout()
         n = coef.shape[-1]
         dev = coef.device
         layers = self.layer_dicts()
         fusion = layout.fusion_table(self.kind, layers, n).to(torch.float32).to(dev).contiguous()
         params = layout.pack_params(layers, device=dev)
-        dc = control_data.data_layout() if control_data is not None else None
+        dc = data_coef if data_coef is not None else (control_data.data_layout() if control_data is not None
+                                                      else None)
         return engine.Problem(ts=ts, coef=coef, tcoef=tcoef, fusion=fusion, params=params, dims=list(self.dims),
                               data_coef=dc, cde_hidden=cde_hidden,
                               cde_embed=self.data_embed_dim if cde_hidden else 0)
@@ -109,8 +110,8 @@ class CDEWrapperVectorField(nn.Module):
         self.vector_field = vector_field
         self.hidden_dim = hidden_dim
 
-    def problem(self, control_adj, control_data):
-        return self.vector_field.problem(control_adj, control_data, cde_hidden=self.hidden_dim)
+    def problem(self, control_adj, control_data, data_coef=None):
+        return self.vector_field.problem(control_adj, control_data, cde_hidden=self.hidden_dim, data_coef=data_coef)
 
     def __call__(self, t, y, args):
         control_adj, control_data = args

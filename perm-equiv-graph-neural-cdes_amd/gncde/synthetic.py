@@ -13,7 +13,7 @@ import math
 
 import torch
 
-from . import layout
+from . import engine, layout
 from .engine import Problem
 
 
@@ -118,11 +118,10 @@ def heat_batch(B: int, num_nodes: int = 64, hidden: int = 16, num_layers: int = 
         flips[:, 0] = False
         flips = flips.cumsum(1) % 2 == 1  # cumulative toggles per epoch
         A = torch.where(flips, 1.0 - base, base)  # [b, E+1, n, n]
-        ops = normalized_laplacian(A)  # [b, E+1, n, n]
+        ops = engine.graph_operator(A, "norm_lap")  # [b, E+1, n, n] (gncde_graph_operator)
         X = torch.gather(ops, 1, which[:, :, None, None].expand(b, T, n, n))  # [b, T, n, n]
-        d, c, bb, a = hermite_coefficients(ts[s:e], X)
-        coef[s:e, :, 0], coef[s:e, :, 1], coef[s:e, :, 2], coef[s:e, :, 3] = d, c, bb, a
-        del A, ops, X, d, c, bb, a
+        coef[s:e] = engine.hermite_coefficients(ts[s:e], X)  # engine layout directly (gncde_hermite_coefficients)
+        del A, ops, X
     # time channel: knots = ts -> d = c = 0, b = 1 exactly (column means identical)
     tcoef = torch.zeros(B, T - 1, 3, n, device=device)
     tcoef[:, :, 2] = 1.0
@@ -165,14 +164,12 @@ def cde_batch(B: int, n: int, T: int, hidden: int, embed: int, num_layers: int, 
         w = torch.exp(torch.randn(b, T, n, n, generator=g)).to(device)
         keep = (torch.rand(b, T, n, n, generator=g) > 0.05).to(device)
         A = base * w * keep
-        d, c, bb, a = hermite_coefficients(ts[s:e], normalized_laplacian(A))
-        coef[s:e, :, 0], coef[s:e, :, 1], coef[s:e, :, 2], coef[s:e, :, 3] = d, c, bb, a
+        coef[s:e] = engine.hermite_coefficients(ts[s:e], engine.graph_operator(A, "norm_lap"))
     tcoef = torch.zeros(B, T - 1, 3, n, device=device)
     tcoef[:, :, 2] = 1.0
     x = torch.randn(B, T, n, embed, generator=g).to(device)
     X = torch.stack([ts[:, :, None, None].expand(B, T, n, embed), x], dim=-1)
-    d, c, bb, a = hermite_coefficients(ts, X)
-    data_coef = torch.stack([d, c, bb, a], dim=2).contiguous()  # [B, T-1, 4, n, de, 2]
+    data_coef = engine.hermite_coefficients(ts, X)  # [B, T-1, 4, n, de, 2]
     dims = [hidden] * num_layers + [hidden * embed * 2]
     layers = init_layers(kind, dims, g)
     fusion = layout.fusion_table(kind, layers, n).to(torch.float32).to(device).contiguous()
