@@ -285,21 +285,32 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
               fc[GNCDE_FC_UR_A] * ri + fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci +
               fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
     }
-    // operand slice: row i of A/dA at columns k = hi*KS + sl, column i at rows k.  Offsets are
-    // re-made opaque per layer (integers, so the accesses stay ds_read, not flat): CSE of the loads
-    // across layers would keep 4*KS values live next to the L*KS operands and spill.
-    const int oAr = swz<NP>(i, hi * KS), oAc = swz<NP>(hi * KS, i);
+    // operand slice: row i of A/dA at columns k = hi*KS + sl, column i at rows k.  Each of the four image
+    // elements is read ONCE and feeds every layer's operand (4 + L LDS reads per element instead of 5 L);
+    // the per-layer coefficients are wave-uniform and live in SGPRs.  Offsets are opaque integers (the
+    // accesses stay ds_read, not flat) and every operand is pinned as soon as it is formed, so the loaded
+    // values stay short-lived.
+    float ec[L][4];
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       const float* fc = fus + l * GNCDE_FC;
-      const float e0 = fc[GNCDE_FC_E_A], e1 = fc[GNCDE_FC_E_DA], e2 = fc[GNCDE_FC_ET_A], e3 = fc[GNCDE_FC_ET_DA];
-      int r0 = oAr, c0 = oAc, v0 = 6 * NP + l * NP + hi * KS;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        ec[l][q] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, fc[q])));
+    }
+    {
+      int r0 = swz<NP>(i, hi * KS), c0 = swz<NP>(hi * KS, i), v0 = 6 * NP + hi * KS;
       asm volatile("" : "+v"(r0), "+v"(c0), "+v"(v0));
 #pragma unroll
       for (int sl = 0; sl < KS; ++sl) {
-        Ab[l][sl] = fmaf(e0, sR0[r0 + sl], fmaf(e1, sR0[AS + r0 + sl], fmaf(e2, sR0[c0 + sl * (NP + 1)],
-                         fmaf(e3, sR0[AS + c0 + sl * (NP + 1)], wl[l] + sVec[v0 + sl]))));
-        asm volatile("" : "+v"(Ab[l][sl]));  // materialise now: keeps the loaded values short-lived
+        const float ar = sR0[r0 + sl], dr = sR0[AS + r0 + sl];
+        const float ac = sR0[c0 + sl * (NP + 1)], dc = sR0[AS + c0 + sl * (NP + 1)];
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+          Ab[l][sl] = fmaf(ec[l][0], ar, fmaf(ec[l][1], dr, fmaf(ec[l][2], ac, fmaf(ec[l][3], dc,
+                           wl[l] + sVec[v0 + l * NP + sl]))));
+          asm volatile("" : "+v"(Ab[l][sl]));
+        }
         if ((sl & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
     }
