@@ -191,6 +191,15 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     const float f = t - sTs[idx];
     const float f3 = 3.0f * f;
     const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
+    // time-channel coefficients: loaded first so their HBM round trip overlaps the interval's Horner pass
+    float tc0, tc1, tc2;
+    {
+      const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
+      const int ii = i < n ? i : 0;
+      tc0 = tc[ii];
+      tc1 = tc[n + ii];
+      tc2 = tc[2 * n + ii];
+    }
     if (n == NP) {
       const float4* c4 = reinterpret_cast<const float4*>(cb);
       constexpr int NQ = NP * NP / 4;
@@ -314,11 +323,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
         if ((sl & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
     }
-    {
-      const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
-      const int ii = i < n ? i : 0;
-      tg = i < n ? fmaf(f, fmaf(f3, tc[ii], 2.0f * tc[n + ii]), tc[2 * n + ii]) : 0.f;
-    }
+    tg = i < n ? fmaf(f, fmaf(f3, tc0, 2.0f * tc1), tc2) : 0.f;
     __syncthreads();  // all A/dA reads done before the aliased M buffers are written
   };
 
