@@ -1,0 +1,242 @@
+"""Dynamical-system graph datasets: heat diffusion and gene regulation on grid / community
+graphs whose edges change at random events, sampled at equal or irregular times — restating
+``src/dataset/ode_dataset.py`` (ODEDataset), ``src/dataset/data_tools.py`` (grid graph, events) and the
+graph-path preparation of ``src/configs/dataset_configs.py:107-199`` (padding by events, graph operator,
+backward-Hermite coefficients).
+
+The trajectories are integrated on the GPU with torch (batched RK4 with at most ``max_dt`` sub-steps
+between samples; the reference integrates with diffrax ``cfg.method`` — this is data generation, not the
+hot path).  The graph operators and spline coefficients go through the engine's kernels
+(``gncde_graph_operator``, ``gncde_hermite_coefficients``) straight into the engine layout.  networkx is not
+installed: the community graph is a 4-block stochastic block model with the reference's block sizes
+(n/3, n/3, n/4, rest) and probabilities (0.25 inside, 0.01 across), ode_dataset.py:189-202.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field, fields
+
+import numpy as np
+import torch
+
+from . import engine, layout
+
+
+@dataclass
+class DynDataCfg:
+    """The ``dataset:`` block of configs/dynamical_systems/*.yaml (unknown keys are ignored)."""
+
+    name: str = "heat"
+    batch_size: int = 4
+    dynamic_graph: bool = True
+    all_dynamic: bool = True
+    graph_type: str = "grid"
+    split_ratio: tuple = (0.8, 0.2)
+    num_nodes: int = 400
+    final_time: float = 5.0
+    time_tick: int = 100
+    sampling_type: str = "irregular"
+    method: str = "Tsit5"
+    operator_type: str = "norm_lap"
+    seed: int = 1234
+    padding_mode: str = "same"
+    interpolation: str = "cubic"
+    amp_range: tuple = (1.0, 1.0)
+    max_dt: float = 0.01
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "DynDataCfg":
+        names = {f.name for f in fields(cls)}
+        return cls(**{k: v for k, v in (d or {}).items() if k in names})
+
+
+def grid_8_neighbor_graph(N: int) -> np.ndarray:
+    """data_tools.py:8-30: N x N grid, 8-neighbour connectivity."""
+    A = np.zeros((N * N, N * N))
+    for r in range(N):
+        for c in range(N):
+            for dr in (-1, 0, 1):
+                for dc in (-1, 0, 1):
+                    if (dr or dc) and 0 <= r + dr < N and 0 <= c + dc < N:
+                        A[r * N + c, (r + dr) * N + c + dc] = 1.0
+    return A
+
+
+def community_graph(n: int, rng: np.random.Generator) -> np.ndarray:
+    sizes = [n // 3, n // 3, n // 4]
+    sizes.append(n - sum(sizes))
+    block = np.repeat(np.arange(4), sizes)
+    p = np.where(block[:, None] == block[None, :], 0.25, 0.01)
+    up = np.triu(rng.random((n, n)) < p, 1).astype(float)
+    return up + up.T
+
+
+def events_happen_time(rng, t: np.ndarray, event_times: int, split_ratio, all_dynamic: bool):
+    """data_tools.py:75-108 (the returned indices are the last batch row's, as in the reference)."""
+    B, num_t = t.shape
+    n_train = int(num_t * split_ratio[0])
+    if not all_dynamic:
+        idx = (rng.permutation(n_train - 2) + 2)[:event_times]
+        return t[:, np.sort(idx)], np.sort(idx)
+    train_events = math.ceil(event_times * split_ratio[0])
+    test_events = event_times - train_events
+    ev_t = []
+    for i in range(B):
+        tr = rng.permutation(n_train - 2) + 2
+        te = rng.permutation(num_t - n_train) + n_train
+        idx = np.sort(np.concatenate((tr[:train_events], te[:test_events])))
+        ev_t.append(t[i, idx])
+    return np.stack(ev_t), idx
+
+
+def events_happen_graph(rng, A: np.ndarray, event_times: int, p: float):
+    """data_tools.py:111-158: each event drops edges with prob 20 p and adds edges with prob p."""
+    out = [A.copy()]
+    for _ in range(event_times):
+        A_new = A.copy()
+        A_new[rng.random(A.shape) < 20 * p] = 0.0
+        A_new[rng.random(A.shape) < p] = 1.0
+        out.append(A_new.copy())
+        A = A_new
+    return np.stack(out, axis=1)  # [B, E+1, n, n]
+
+
+def split_indices(rng, sampling_type: str, time_tick: int, split_ratio):
+    """ode_dataset.py:344-386 -> (id_train, id_test_extra, id_test_inter)."""
+    if sampling_type == "equal":
+        k = round(time_tick * split_ratio[0])
+        return list(range(k)), list(range(k, time_tick)), None
+    extra = list(range(time_tick, round(time_tick * (1.0 + split_ratio[1]))))
+    inter = sorted(rng.permutation(list(range(1, time_tick)))[: round(time_tick * split_ratio[1])].tolist())
+    train = sorted(set(range(time_tick)) - set(inter))
+    return train, extra, inter
+
+
+def padding_by_time(num_knots: int, events_indices: np.ndarray) -> np.ndarray:
+    """dataset_configs.py:107-150 (padding_mode 'same'): epoch of every knot, events beyond the knots
+    invisible (prepare_graph_path's truncation)."""
+    visible = events_indices[events_indices < num_knots]
+    mark = np.zeros(num_knots, dtype=np.int64)
+    mark[visible] = 1
+    return np.cumsum(mark)
+
+
+class DynDataset:
+    """Generates the data and exposes the engine-layout graph paths.
+
+    Attributes: t [B, Tt] (np), true_y [B, Tt, n] (torch, device), x0 [B, n, 1] (torch), A [B, E+1, n, n]
+    (np adjacencies), events_indices, id_train / id_test_extra / id_test_inter.
+    """
+
+    def __init__(self, cfg: DynDataCfg, device="cuda"):
+        self.cfg = cfg
+        rng = np.random.default_rng(cfg.seed)
+        B = cfg.batch_size
+        if cfg.graph_type == "grid":
+            self.N = int(math.ceil(math.sqrt(cfg.num_nodes)))
+            base = np.tile(grid_8_neighbor_graph(self.N)[None], (B, 1, 1))
+        elif cfg.graph_type == "community":
+            base = np.stack([community_graph(cfg.num_nodes, rng) for _ in range(B)])
+            self.N = None
+        else:
+            raise NotImplementedError(f"graph_type {cfg.graph_type}: grid and community are generated here")
+        self.n = base.shape[-1]
+        event_times = 10
+        if cfg.all_dynamic:  # ode_dataset.py:79-91
+            event_times += int(event_times / cfg.split_ratio[0] * cfg.split_ratio[1])
+        self.t = self._sampling(rng)
+        self.x0 = torch.tensor(self._initial(rng), dtype=torch.float32, device=device)
+        if cfg.dynamic_graph:
+            _, self.events_indices = events_happen_time(rng, self.t, event_times, cfg.split_ratio, cfg.all_dynamic)
+            self.A = events_happen_graph(rng, base, event_times, 0.001)
+        else:
+            self.events_indices = np.zeros(0, dtype=np.int64)
+            self.A = base[:, None]
+        self.true_y = self._solve(device)
+        self.id_train, self.id_test_extra, self.id_test_inter = split_indices(
+            rng, cfg.sampling_type, cfg.time_tick, cfg.split_ratio)
+        self.device = device
+
+    def _sampling(self, rng) -> np.ndarray:
+        """ode_dataset.py:303-342."""
+        c = self.cfg
+        if c.sampling_type == "equal":
+            return np.tile(np.linspace(0.0, c.final_time, c.time_tick), (c.batch_size, 1))
+        full = np.linspace(0.0, c.final_time, c.time_tick * 10)
+        k = int(c.time_tick * 1.2)
+        rows = []
+        for _ in range(c.batch_size):
+            ts = np.sort(rng.permutation(full)[:k])
+            ts[0] = 0.0
+            rows.append(ts)
+        return np.stack(rows)
+
+    def _initial(self, rng) -> np.ndarray:
+        """ode_dataset.py:93-140: three non-overlapping patches of amplitude ~U(amp_range) (grid layout);
+        a community graph gets three random node blocks instead."""
+        c = self.cfg
+        B, n = c.batch_size, self.n
+        x0 = np.zeros((B, n))
+        if self.N is not None:
+            N = self.N
+            grid = np.zeros((B, N, N))
+            for i in range(B):
+                placed = []
+                for fh, fw in ((0.2, 0.2), (0.3, 0.3), (0.2, 0.3)):
+                    h, w = max(1, int(fh * N)), max(1, int(fw * N))
+                    for _ in range(1000):
+                        r1, c1 = rng.integers(0, N - h + 1), rng.integers(0, N - w + 1)
+                        if all(r1 + h <= a or a + hh <= r1 or c1 + w <= b or b + ww <= c1
+                               for a, b, hh, ww in placed):
+                            break
+                    placed.append((r1, c1, h, w))
+                    grid[i, r1:r1 + h, c1:c1 + w] = rng.uniform(*c.amp_range)
+            x0 = grid.reshape(B, -1)
+        else:
+            for i in range(B):
+                for _ in range(3):
+                    s = rng.integers(0, n)
+                    x0[i, s:s + max(1, n // 10)] = rng.uniform(*c.amp_range)
+        return x0[..., None]
+
+    def _rhs(self, A: torch.Tensor):
+        if self.cfg.name == "heat":  # heat_diffusion_model.py: dX/dt = -k L X, L = D - A, k = 1
+            L = torch.diag_embed(A.sum(-1)) - A
+            return lambda x: -torch.bmm(L, x)
+        if self.cfg.name == "gene":  # gene_dynamic_model.py: -b x^f + A x^h / (x^h + 1), b=1, f=1, h=2
+            return lambda x: -x + torch.bmm(A, x * x) / (x * x + 1.0)
+        raise NotImplementedError(f"dataset {self.cfg.name}: heat and gene are generated here")
+
+    def _solve(self, device) -> torch.Tensor:
+        t = torch.tensor(self.t, dtype=torch.float64, device=device)
+        A_all = torch.tensor(self.A, dtype=torch.float64, device=device)
+        epoch = padding_by_time(self.t.shape[1], self.events_indices) if self.cfg.dynamic_graph else \
+            np.zeros(self.t.shape[1], dtype=np.int64)
+        x = self.x0.to(torch.float64)
+        out = [x[..., 0].clone()]
+        for j in range(1, self.t.shape[1]):
+            f = self._rhs(A_all[:, int(epoch[j - 1])])
+            span = t[:, j] - t[:, j - 1]  # [B]
+            steps = max(1, int(math.ceil(float(span.max()) / self.cfg.max_dt)))
+            h = (span / steps)[:, None, None]
+            for _ in range(steps):
+                k1 = f(x)
+                k2 = f(x + 0.5 * h * k1)
+                k3 = f(x + 0.5 * h * k2)
+                k4 = f(x + h * k3)
+                x = x + h / 6.0 * (k1 + 2 * k2 + 2 * k3 + k4)
+            out.append(x[..., 0].clone())
+        return torch.stack(out, dim=1).to(torch.float32)  # [B, Tt, n]
+
+    def graph_path(self, idx):
+        """Engine-layout control over the knots ``idx`` (dataset_configs.py:159-199): graph operator of every
+        event epoch (gncde_graph_operator), padded to the knots, backward-Hermite coefficients
+        (gncde_hermite_coefficients).  Returns (ts [B, K] device, coef, tcoef)."""
+        idx = np.asarray(idx)
+        ts = torch.tensor(self.t[:, idx], dtype=torch.float32, device=self.device)
+        ops = engine.graph_operator(torch.tensor(self.A, dtype=torch.float32), self.cfg.operator_type)
+        epoch = padding_by_time(len(idx), self.events_indices) if self.cfg.dynamic_graph else \
+            np.zeros(len(idx), dtype=np.int64)
+        X = ops[:, torch.as_tensor(epoch, device=ops.device)]  # [B, K, n, n]
+        coef, tcoef = layout.control_from_knots(ts, X)
+        return ts, coef, tcoef

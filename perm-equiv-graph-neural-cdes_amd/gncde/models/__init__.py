@@ -143,6 +143,22 @@ class GraphNeuralCDE(nn.Module):
         x0 = torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device)
         return self.predict_packed(self.vector_field.problem(control), x0, self._spec(ts_d, evolving_out))
 
+    def forward_packed(self, prob: engine.Problem, x0: torch.Tensor, ts: torch.Tensor,
+                       evolving_out: bool = True) -> torch.Tensor:
+        """The reference solve (Tsit5 + PIDController(1e-3, 1e-6), dt0=None, SaveAt(ts) or t1) on an already
+        packed Problem: encoder -> gncde_integrate -> read-out.  No autograd graph."""
+        with torch.no_grad():
+            y0 = _affine(self.initial_linear, x0)
+            ts = ts.to(y0.device, torch.float32)
+            spec = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_PID,
+                                     save_mode=_lib.SAVE_TS if evolving_out else _lib.SAVE_T1,
+                                     rtol=self.rtol, atol=self.atol, t0=ts[:, 0].contiguous(),
+                                     t1=ts[:, -1].contiguous(), save_ts=ts.contiguous() if evolving_out else None)
+            ys, st = engine.integrate(prob, spec, y0, stats=True)
+            if torch.any(st[:, _lib.STAT_STATUS] != 0):
+                raise RuntimeError("diffrax-equivalent failure: max_steps reached or non-finite state")
+            return _affine(self.final_linear, ys)
+
     def predict_packed(self, prob: engine.Problem, x0: torch.Tensor, spec: engine.SolverSpec) -> torch.Tensor:
         """``predict`` on an already packed device Problem (coefficients resident in HBM): encoder ->
         differentiable GPU solve (this module's parameters) -> read-out."""

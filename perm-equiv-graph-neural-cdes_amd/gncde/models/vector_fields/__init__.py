@@ -57,6 +57,20 @@ class _GraphVectorFieldBase(nn.Module):
                               data_coef=dc, cde_hidden=cde_hidden,
                               cde_embed=self.data_embed_dim if cde_hidden else 0)
 
+    def problem_from_layout(self, ts: torch.Tensor, coef: torch.Tensor, tcoef: torch.Tensor,
+                            data_coef: torch.Tensor | None = None, cde_hidden: int = 0) -> engine.Problem:
+        """Problem over an engine-layout control (layout.control_from_knots / gncde.data) with this module's
+        current parameters."""
+        n = int(coef.shape[-1])
+        dev = coef.device
+        layers = self.layer_dicts()
+        fusion = layout.fusion_table(self.kind, layers, n).to(torch.float32).to(dev).contiguous()
+        params = layout.pack_params(layers, device=dev)
+        return engine.Problem(ts=ts.to(dev, torch.float32).contiguous(), coef=coef.contiguous(),
+                              tcoef=tcoef.contiguous(), fusion=fusion, params=params, dims=list(self.dims),
+                              data_coef=data_coef, cde_hidden=cde_hidden,
+                              cde_embed=self.data_embed_dim if cde_hidden else 0)
+
     def diff_tensors(self, n: int, device) -> tuple:
         """(params, fusion) as differentiable device tensors: the packed parameter buffer and the factored
         fusion table [L, 24] (layout.fusion_table_torch), for ``autograd.solve``."""
