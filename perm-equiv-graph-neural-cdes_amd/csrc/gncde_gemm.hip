@@ -17,7 +17,7 @@ namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-template <bool TRANS_B>
+template <bool TRANS_A, bool TRANS_B>
 __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
   constexpr int KC = 32;
   const int b = blockIdx.z;
@@ -35,15 +35,20 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   // per-thread slices of the next chunk, prefetched into registers while the current one is consumed
-  const int ar = tid >> 2, aq = (tid & 3) * 8;                                   // A: row, 8 k
+  // A slice: 8 consecutive k of one row (row-major A) or 8 consecutive rows of one k (TRANS_A: At[k][r])
+  const int ar = TRANS_A ? (tid & 7) * 8 : tid >> 2, aq = TRANS_A ? tid >> 3 : (tid & 3) * 8;
   const int br = TRANS_B ? (tid >> 2) : (tid >> 3), bq = TRANS_B ? (tid & 3) * 8 : (tid & 7) * 8;
   float ra[8], rb[8];
   auto fetch = [&](int k0) {
-    const int r = m0 + ar;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const int kk = k0 + aq + q;
-      ra[q] = (r < g.M && kk < g.K) ? A[(size_t)r * g.lda + kk] : 0.f;
+      if (TRANS_A) {
+        const int r = m0 + ar + q, kk = k0 + aq;
+        ra[q] = (r < g.M && kk < g.K) ? A[(size_t)kk * g.lda + r] : 0.f;
+      } else {
+        const int r = m0 + ar, kk = k0 + aq + q;
+        ra[q] = (r < g.M && kk < g.K) ? A[(size_t)r * g.lda + kk] : 0.f;
+      }
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -60,7 +65,10 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
   for (int k0 = 0; k0 < g.K; k0 += KC) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      As[ar][aq + q] = ra[q];
+      if (TRANS_A)
+        As[ar + q][aq] = ra[q];
+      else
+        As[ar][aq + q] = ra[q];
       if (TRANS_B)
         Bs[bq + q][br] = rb[q];
       else
@@ -95,6 +103,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
           if (g.rowscale) v *= g.rowscale[(size_t)b * g.sR + row];
           if (g.colbias) v += g.colbias[col];
           if (g.relu) v = fmaxf(v, 0.f);
+          if (g.accumulate) v += C[(size_t)row * g.ldc + col];
           C[(size_t)row * g.ldc + col] = v;
         }
       }
@@ -168,12 +177,19 @@ __global__ void __launch_bounds__(256) k_abar_full(int n, const float* __restric
 
 }  // namespace
 
-void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st) {
+void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st, bool trans_a) {
   const dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, batch);
-  if (trans_b)
-    hipLaunchKernelGGL(k_gemm<true>, grid, dim3(256), 0, st, g);
-  else
-    hipLaunchKernelGGL(k_gemm<false>, grid, dim3(256), 0, st, g);
+  if (trans_a) {
+    if (trans_b)
+      hipLaunchKernelGGL((k_gemm<true, true>), grid, dim3(256), 0, st, g);
+    else
+      hipLaunchKernelGGL((k_gemm<true, false>), grid, dim3(256), 0, st, g);
+  } else {
+    if (trans_b)
+      hipLaunchKernelGGL((k_gemm<false, true>), grid, dim3(256), 0, st, g);
+    else
+      hipLaunchKernelGGL((k_gemm<false, false>), grid, dim3(256), 0, st, g);
+  }
 }
 
 void fold_linear(int din, int dout, const float* rw, const float* rb, const float* W, const float* bias, float* Wf,

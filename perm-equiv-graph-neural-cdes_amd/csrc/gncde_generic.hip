@@ -217,6 +217,14 @@ size_t generic_vf_workspace(const GncdeProblem& p) {
 // One evaluation = spline + reductions, then per layer two MFMA GEMMs (gncde_gemm.hip): the Linear over all
 // B*n node rows with RMSNorm folded in, and the per-sample (I + Abar) m with (I + Abar) materialised once.
 // Fold every layer's RMSNorm affine into its Linear (once per solve, not per evaluation).
+void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, hipStream_t st) {
+  const int B = p.B, n = p.n;
+  const size_t nn = (size_t)n * n;
+  hipLaunchKernelGGL(k_spline, dim3(cdiv(nn > (size_t)n ? nn : n, 256), B), dim3(256), 0, st, n, p.T, p.ts, p.coef,
+                     p.tcoef, t, A, dA, tg);
+  hipLaunchKernelGGL(k_reduce, dim3(B, 4), dim3(256), 0, st, n, A, dA, red);
+}
+
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
   VfWs w;
   carve_vf(p, ws, w);

@@ -112,8 +112,10 @@ struct GemmArgs {
   long sR;
   const float* colbias;  // optional [N]
   int relu;
+  int accumulate;  // C += result
 };
-void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st);
+// TRANS_A: A[b] + k * lda + r (A^T stored row-major)
+void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st, bool trans_a = false);
 void fold_linear(int din, int dout, const float* rw, const float* rb, const float* W, const float* bias, float* Wf,
                  float* bf, hipStream_t st);
 void row_inv(int rows, int d, const float* Z, float* inv, hipStream_t st);
@@ -123,6 +125,8 @@ void abar_full(int B, int n, const float* fc, const float* A, const float* dA, c
 // generic (any-shape, multi-kernel) path: gncde_generic.hip
 size_t generic_vf_workspace(const GncdeProblem& p);
 size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s);
+// A(t), dA/dt(t), the time-channel derivative tg and the row/col/diag/total reductions (stride 8 n per sample)
+void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, hipStream_t st);
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st);
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared = false);

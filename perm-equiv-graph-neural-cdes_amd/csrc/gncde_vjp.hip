@@ -22,148 +22,6 @@ constexpr int kRedStride = 8;  // same reduction layout as gncde_generic.hip
 
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
-// ---- forward pieces (with activations kept) --------------------------------------------------------
-__global__ void v_spline(int n, int T, const float* __restrict__ ts, const float* __restrict__ coef,
-                         const float* __restrict__ tcoef, const float* __restrict__ t, float* __restrict__ A,
-                         float* __restrict__ dA, float* __restrict__ tg) {
-  const int b = blockIdx.y;
-  const size_t nn = (size_t)n * n;
-  const float tb = t[b];
-  const float* tsb = ts + (size_t)b * T;
-  const int idx = interval_index(tsb, T, tb);
-  const float f = tb - tsb[idx];
-  const float* cb = coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < nn) {
-    const float d = cb[e], c = cb[nn + e], bb = cb[2 * nn + e], a = cb[3 * nn + e];
-    A[(size_t)b * nn + e] = fmaf(f, fmaf(f, fmaf(f, d, c), bb), a);
-    dA[(size_t)b * nn + e] = fmaf(f, fmaf(3.0f * f, d, 2.0f * c), bb);
-  }
-  if (e < (size_t)n) {
-    const float* tc = tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
-    tg[(size_t)b * n + e] = fmaf(f, fmaf(3.0f * f, tc[e], 2.0f * tc[n + e]), tc[2 * n + e]);
-  }
-}
-
-__global__ void v_reduce(int n, const float* __restrict__ A, const float* __restrict__ dA, float* __restrict__ red) {
-  const int b = blockIdx.x;
-  const size_t nn = (size_t)n * n;
-  const float* Ab = A + b * nn;
-  const float* dAb = dA + b * nn;
-  float* rb = red + (size_t)b * kRedStride * n;
-  __shared__ float part[2][256];
-  float ps = 0.f, psd = 0.f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    float r = 0.f, rd = 0.f, c = 0.f, cd = 0.f;
-    for (int k = 0; k < n; ++k) {
-      r += Ab[(size_t)i * n + k];
-      rd += dAb[(size_t)i * n + k];
-      c += Ab[(size_t)k * n + i];
-      cd += dAb[(size_t)k * n + i];
-    }
-    rb[i] = r;
-    rb[n + i] = rd;
-    rb[2 * n + i] = c;
-    rb[3 * n + i] = cd;
-    rb[4 * n + i] = Ab[(size_t)i * n + i];
-    rb[5 * n + i] = dAb[(size_t)i * n + i];
-    ps += r;
-    psd += rd;
-  }
-  part[0][threadIdx.x] = ps;
-  part[1][threadIdx.x] = psd;
-  __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      part[0][threadIdx.x] += part[0][threadIdx.x + s];
-      part[1][threadIdx.x] += part[1][threadIdx.x + s];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    rb[6 * n] = part[0][0];
-    rb[7 * n] = part[1][0];
-  }
-}
-
-// inv[b,i] = rsqrt(mean(z^2) + eps); m = (z*inv*rw + rb) W^T + bias.  z = relu(prev pre) if relu_in.
-__global__ void v_rms_linear(int n, int din, int dout, const float* __restrict__ Z, int relu_in,
-                             const float* __restrict__ rw, const float* __restrict__ rbias,
-                             const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ m,
-                             float* __restrict__ inv_out) {
-  const int b = blockIdx.y;
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (size_t)n * dout) return;
-  const int i = (int)(e / dout), o = (int)(e % dout);
-  const float* z = Z + ((size_t)b * n + i) * din;
-  float ss = 0.f;
-  for (int k = 0; k < din; ++k) {
-    const float v = relu_in ? fmaxf(z[k], 0.f) : z[k];
-    ss = fmaf(v, v, ss);
-  }
-  const float inv = 1.0f / sqrtf(ss / (float)din + 1e-5f);
-  float acc = bias[o];
-  const float* w = W + (size_t)o * din;
-  for (int k = 0; k < din; ++k) {
-    const float v = relu_in ? fmaxf(z[k], 0.f) : z[k];
-    acc = fmaf(fmaf(v * inv, rw[k], rbias[k]), w[k], acc);
-  }
-  m[((size_t)b * n + i) * dout + o] = acc;
-  if (o == 0) inv_out[(size_t)b * n + i] = inv;
-}
-
-__device__ __forceinline__ void row_terms(const float* fc, const float* rb, int n, int i, float& wi, float& ui) {
-  const float s = rb[6 * n], sd = rb[7 * n];
-  wi = fc[GNCDE_FC_WR_A] * rb[i] + fc[GNCDE_FC_WR_DA] * rb[n + i] + fc[GNCDE_FC_WC_A] * rb[2 * n + i] +
-       fc[GNCDE_FC_WC_DA] * rb[3 * n + i] + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
-  ui = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * rb[4 * n + i] + fc[GNCDE_FC_UD_DA] * rb[5 * n + i] +
-       fc[GNCDE_FC_UR_A] * rb[i] + fc[GNCDE_FC_UR_DA] * rb[n + i] + fc[GNCDE_FC_UC_A] * rb[2 * n + i] +
-       fc[GNCDE_FC_UC_DA] * rb[3 * n + i] + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
-}
-
-__device__ __forceinline__ float abar(const float* fc, const float* A, const float* dA, const float* rb, int n,
-                                      int i, int k) {
-  const float aik = A[(size_t)i * n + k], aki = A[(size_t)k * n + i];
-  const float dik = dA[(size_t)i * n + k], dki = dA[(size_t)k * n + i];
-  float wi, ui;
-  row_terms(fc, rb, n, i, wi, ui);
-  const float vk = fc[GNCDE_FC_VR_A] * rb[k] + fc[GNCDE_FC_VR_DA] * rb[n + k] + fc[GNCDE_FC_VC_A] * rb[2 * n + k] +
-                   fc[GNCDE_FC_VC_DA] * rb[3 * n + k];
-  float v = fc[GNCDE_FC_E_A] * aik + fc[GNCDE_FC_E_DA] * dik + fc[GNCDE_FC_ET_A] * aki + fc[GNCDE_FC_ET_DA] * dki;
-  v += wi + vk;
-  if (i == k) v += ui;
-  return v;
-}
-
-// out[b,i,o] = sum_k M[i,k] x[b,k,o] with M = (I+Abar) (trans=0) or its transpose (trans=1)
-__global__ void __launch_bounds__(256) v_prop(int n, int d, const float* __restrict__ fc, const float* __restrict__ A,
-                                              const float* __restrict__ dA, const float* __restrict__ red,
-                                              const float* __restrict__ x, float* __restrict__ out, int trans) {
-  const int b = blockIdx.z;
-  const int o0 = blockIdx.x * 16, i0 = blockIdx.y * 16;
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const size_t nn = (size_t)n * n;
-  const float* Ab = A + b * nn;
-  const float* dAb = dA + b * nn;
-  const float* rb = red + (size_t)b * kRedStride * n;
-  const float* xb = x + (size_t)b * n * d;
-  __shared__ float sA[16][17];
-  __shared__ float sX[16][17];
-  float acc = 0.f;
-  for (int k0 = 0; k0 < n; k0 += 16) {
-    const int i = i0 + ty, k = k0 + tx;
-    sA[ty][tx] = (i < n && k < n) ? (trans ? abar(fc, Ab, dAb, rb, n, k, i) : abar(fc, Ab, dAb, rb, n, i, k)) : 0.f;
-    const int kk = k0 + ty, o = o0 + tx;
-    sX[ty][tx] = (kk < n && o < d) ? xb[(size_t)kk * d + o] : 0.f;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc = fmaf(sA[ty][q], sX[q][tx], acc);
-    __syncthreads();
-  }
-  const int i = i0 + ty, o = o0 + tx;
-  if (i < n && o < d) out[((size_t)b * n + i) * d + o] = acc;
-}
-
 // ---- backward pieces ---------------------------------------------------------------------------------
 // gZ_{L-1}: ODE g = tg * gF; CDE g[i, (m*de+l)*2+k] = tg[i] gF[i,m] dX[i,l,k]
 __global__ void v_out_grad(int n, int dL, int h, int de, int T, const float* __restrict__ ts,
@@ -195,173 +53,172 @@ __global__ void v_relu_mask(size_t total, const float* __restrict__ pre, float* 
   if (e < total && !(pre[e] > 0.f)) g[e] = 0.f;
 }
 
-// column sums over nodes: out[b, o] = sum_i x[b, i, o]
-__global__ void v_colsum(int n, int d, const float* __restrict__ x, float* __restrict__ out) {
-  const int b = blockIdx.y;
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= d) return;
-  float s = 0.f;
-  for (int i = 0; i < n; ++i) s += x[((size_t)b * n + i) * d + o];
-  out[(size_t)b * d + o] = s;
+
+// ---- layer machinery on the MFMA GEMMs (gncde_gemm.hip) --------------------------------------------------
+__global__ void v_relu_copy(size_t total, const float* __restrict__ x, float* __restrict__ out) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < total) out[e] = fmaxf(x[e], 0.f);
 }
 
-// Fusion-table gradient of one layer for one sample.  With G = gpre m^T (G[i,k] = gpre[i].m[k]):
-//   g[E_A] = <G, A>, g[E_DA] = <G, dA>, g[ET_A] = <G, A^T>, g[ET_DA] = <G, dA^T>   (block partials here)
-// The row/column/diagonal families use R_i = gpre[i].colsum(m), C_k = m[k].colsum(gpre),
-// D_i = gpre[i].m[i] (v_fusion_rank) — no n x n intermediate is stored.
-__global__ void __launch_bounds__(256) v_fusion_dense(int n, int d, const float* __restrict__ A,
-                                                      const float* __restrict__ dA, const float* __restrict__ gpre,
-                                                      const float* __restrict__ m, float* __restrict__ part) {
-  const int b = blockIdx.y;
-  const int i = blockIdx.x;  // one row per block
+// zn = z * inv_row * rms_w + rms_b ; xh = z * inv_row (optional)
+__global__ void v_norm_rows(size_t rows, int d, const float* __restrict__ Z, const float* __restrict__ inv,
+                            const float* __restrict__ rw, const float* __restrict__ rb, float* __restrict__ zn,
+                            float* __restrict__ xh) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows * d) return;
+  const size_t r = e / d;
+  const int f = (int)(e % d);
+  const float x = Z[e] * inv[r];
+  if (zn) zn[e] = fmaf(x, rw[f], rb[f]);
+  if (xh) xh[e] = x;
+}
+
+// Column sums over `rows` rows, two passes with a fixed order: part[chunk][j], then out[j] (+)= sum_chunk.
+// mode 0: X; mode 1: X * Y (elementwise)
+constexpr int kChunk = 1024;
+__global__ void __launch_bounds__(256) v_colsum_part(size_t rows, int d, const float* __restrict__ X,
+                                                     const float* __restrict__ Y, float* __restrict__ part) {
+  const int j = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;  // 4 row groups
+  const size_t r0 = (size_t)blockIdx.y * kChunk;
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (j < d) {
+    for (size_t r = r0 + g; r < rows && r < r0 + kChunk; r += 4) {
+      const float x = X[r * d + j];
+      s += Y ? x * Y[r * d + j] : x;
+    }
+  }
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && j < d)
+    part[(size_t)blockIdx.y * d + j] = (red[0][threadIdx.x] + red[1][threadIdx.x]) +
+                                       (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+__global__ void v_colsum_final(int chunks, int d, const float* __restrict__ part, float* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= d) return;
+  float s = 0.f;
+  for (int c = 0; c < chunks; ++c) s += part[(size_t)c * d + j];
+  out[j] += s;
+}
+
+// RMSNorm backward per row (one wave): gz = inv (gxh - xh (xh . gxh) / d), gxh = gzn * rms_w
+__global__ void v_rms_bwd(size_t rows, int d, const float* __restrict__ Z, const float* __restrict__ inv,
+                          const float* __restrict__ rw, const float* __restrict__ gzn, float* __restrict__ gz) {
+  const size_t r = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float iv = inv[r];
+  const float* z = Z + r * d;
+  const float* g = gzn + r * d;
+  float dot = 0.f;
+  for (int f = lane; f < d; f += 64) dot = fmaf(g[f] * rw[f], z[f] * iv, dot);
+  for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+  const float c = dot / (float)d;
+  for (int f = lane; f < d; f += 64) gz[r * d + f] = iv * (g[f] * rw[f] - z[f] * iv * c);
+}
+
+// Dense fusion-table gradients from G = gpre m^T (materialised per sample): per 32x32 tile the partial sums of
+// G.*A, G.*dA, G.*A^T, G.*dA^T (the transposed tiles staged in LDS) -> part[b][tile][4]
+__global__ void __launch_bounds__(256) v_fusion_dense_G(int n, const float* __restrict__ A,
+                                                        const float* __restrict__ dA, const float* __restrict__ Gm,
+                                                        float* __restrict__ part) {
+  const int b = blockIdx.z;
+  const int i0 = blockIdx.y * 32, k0 = blockIdx.x * 32;
   const size_t nn = (size_t)n * n;
   const float* Ab = A + b * nn;
   const float* dAb = dA + b * nn;
-  const float* gi = gpre + ((size_t)b * n + i) * d;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    const float* mk = m + ((size_t)b * n + k) * d;
-    float G = 0.f;
-    for (int o = 0; o < d; ++o) G = fmaf(gi[o], mk[o], G);
-    s0 = fmaf(G, Ab[(size_t)i * n + k], s0);
-    s1 = fmaf(G, dAb[(size_t)i * n + k], s1);
-    s2 = fmaf(G, Ab[(size_t)k * n + i], s2);
-    s3 = fmaf(G, dAb[(size_t)k * n + i], s3);
-  }
+  const float* Gb = Gm + b * nn;
+  __shared__ float tA[32][33], tD[32][33];
   __shared__ float red[4][256];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = ty; y < 32; y += 8) {
+    const int k = k0 + y, i = i0 + tx;
+    const bool ok = k < n && i < n;
+    tA[y][tx] = ok ? Ab[(size_t)k * n + i] : 0.f;
+    tD[y][tx] = ok ? dAb[(size_t)k * n + i] : 0.f;
+  }
+  __syncthreads();
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (int y = ty; y < 32; y += 8) {
+    const int i = i0 + y, k = k0 + tx;
+    if (i >= n || k >= n) continue;
+    const float g = Gb[(size_t)i * n + k];
+    s0 = fmaf(g, Ab[(size_t)i * n + k], s0);
+    s1 = fmaf(g, dAb[(size_t)i * n + k], s1);
+    s2 = fmaf(g, tA[tx][y], s2);
+    s3 = fmaf(g, tD[tx][y], s3);
+  }
   red[0][threadIdx.x] = s0;
   red[1][threadIdx.x] = s1;
   red[2][threadIdx.x] = s2;
   red[3][threadIdx.x] = s3;
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s)
-      for (int q = 0; q < 4; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + s];
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st)
+      for (int q = 0; q < 4; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + st];
     __syncthreads();
   }
-  if (threadIdx.x < 4) part[((size_t)b * n + i) * 4 + threadIdx.x] = red[threadIdx.x][0];
+  const int tiles = gridDim.x * gridDim.y;
+  if (threadIdx.x < 4) part[((size_t)b * tiles + blockIdx.y * gridDim.x + blockIdx.x) * 4 + threadIdx.x] =
+      red[threadIdx.x][0];
 }
 
-// Per-sample accumulation of the 24 fusion-table gradients of layer l into gfc[b, l, :]
-__global__ void v_fusion_rank(int n, int d, int L, int l, const float* __restrict__ red,
-                              const float* __restrict__ gpre, const float* __restrict__ m,
-                              const float* __restrict__ cs_m, const float* __restrict__ cs_g,
-                              const float* __restrict__ part, float* __restrict__ gfc) {
+// Per sample: the 4 dense terms (tile partials in a fixed order) and the 20 rank-1 / diagonal families from
+// R_i = sum_k G[i][k], C_k = sum_i G[i][k], D_i = G[i][i] against the form's row/col/diag/total vectors.
+__global__ void __launch_bounds__(256) v_fusion_finish(int n, int L, int l, int tiles, const float* __restrict__ red,
+                                                       const float* __restrict__ Gm, const float* __restrict__ part,
+                                                       float* __restrict__ gfc) {
   const int b = blockIdx.x;
+  const size_t nn = (size_t)n * n;
+  const float* Gb = Gm + b * nn;
   const float* rb = red + (size_t)b * kRedStride * n;
   const float s = rb[6 * n], sd = rb[7 * n];
-  // one thread per accumulated quantity
-  const int q = threadIdx.x;
-  if (q >= GNCDE_FC) return;
-  float acc = 0.f;
-  for (int i = 0; i < n; ++i) {
-    const float* gi = gpre + ((size_t)b * n + i) * d;
-    const float* mi = m + ((size_t)b * n + i) * d;
-    float R = 0.f, C = 0.f, D = 0.f;
-    if (q >= GNCDE_FC_WR_A && q <= GNCDE_FC_WS_DA) {
-      for (int o = 0; o < d; ++o) R = fmaf(gi[o], cs_m[(size_t)b * d + o], R);
-    } else if (q >= GNCDE_FC_VR_A && q <= GNCDE_FC_VC_DA) {
-      for (int o = 0; o < d; ++o) C = fmaf(mi[o], cs_g[(size_t)b * d + o], C);
-    } else if ((q >= GNCDE_FC_UD_A && q <= GNCDE_FC_US_DA) || q == GNCDE_FC_IDC) {
-      for (int o = 0; o < d; ++o) D = fmaf(gi[o], mi[o], D);
-    }
-    float x = 0.f;
-    switch (q) {
-      case GNCDE_FC_E_A: case GNCDE_FC_E_DA: case GNCDE_FC_ET_A: case GNCDE_FC_ET_DA:
-        x = part[((size_t)b * n + i) * 4 + q];
-        break;
-      case GNCDE_FC_UD_A: x = D * rb[4 * n + i]; break;
-      case GNCDE_FC_UD_DA: x = D * rb[5 * n + i]; break;
-      case GNCDE_FC_UR_A: x = D * rb[i]; break;
-      case GNCDE_FC_UR_DA: x = D * rb[n + i]; break;
-      case GNCDE_FC_UC_A: x = D * rb[2 * n + i]; break;
-      case GNCDE_FC_UC_DA: x = D * rb[3 * n + i]; break;
-      case GNCDE_FC_US_A: x = D * s; break;
-      case GNCDE_FC_US_DA: x = D * sd; break;
-      case GNCDE_FC_WR_A: x = R * rb[i]; break;
-      case GNCDE_FC_WR_DA: x = R * rb[n + i]; break;
-      case GNCDE_FC_WC_A: x = R * rb[2 * n + i]; break;
-      case GNCDE_FC_WC_DA: x = R * rb[3 * n + i]; break;
-      case GNCDE_FC_WS_A: x = R * s; break;
-      case GNCDE_FC_WS_DA: x = R * sd; break;
-      case GNCDE_FC_VR_A: x = C * rb[i]; break;
-      case GNCDE_FC_VR_DA: x = C * rb[n + i]; break;
-      case GNCDE_FC_VC_A: x = C * rb[2 * n + i]; break;
-      case GNCDE_FC_VC_DA: x = C * rb[3 * n + i]; break;
-      case GNCDE_FC_IDC: x = D; break;
-      default: x = 0.f;
-    }
-    acc += x;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  float acc[GNCDE_FC];
+  for (int q = 0; q < GNCDE_FC; ++q) acc[q] = 0.f;
+  for (int k = tid; k < n; k += blockDim.x) {  // C_k: column sums (coalesced over threads)
+    float c = 0.f;
+    for (int i = 0; i < n; ++i) c += Gb[(size_t)i * n + k];
+    acc[GNCDE_FC_VR_A] += c * rb[k];
+    acc[GNCDE_FC_VR_DA] += c * rb[n + k];
+    acc[GNCDE_FC_VC_A] += c * rb[2 * n + k];
+    acc[GNCDE_FC_VC_DA] += c * rb[3 * n + k];
   }
-  gfc[((size_t)b * L + l) * GNCDE_FC + q] += acc;
-}
-
-// Linear + RMSNorm backward, per (b, i): gzn = gm W; gz = inv (gxh - xh (xh.gxh)/din), gxh = gzn*rw
-// (xh = z*inv).  Writes gZ_prev (layer input grad) and the per-node gzn for the parameter sums.
-__global__ void v_linear_input_grad(int n, int din, int dout, const float* __restrict__ Z, int relu_in,
-                                    const float* __restrict__ inv, const float* __restrict__ rw,
-                                    const float* __restrict__ W, const float* __restrict__ gm,
-                                    float* __restrict__ gzn, float* __restrict__ gz) {
-  const int b = blockIdx.y;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float* z = Z + ((size_t)b * n + i) * din;
-  const float* g = gm + ((size_t)b * n + i) * dout;
-  const float iv = inv[(size_t)b * n + i];
-  float dot = 0.f;
-  for (int f = 0; f < din; ++f) {
-    float acc = 0.f;
-    for (int o = 0; o < dout; ++o) acc = fmaf(g[o], W[(size_t)o * din + f], acc);
-    gzn[((size_t)b * n + i) * din + f] = acc;
-    const float xh = (relu_in ? fmaxf(z[f], 0.f) : z[f]) * iv;
-    dot = fmaf(acc * rw[f], xh, dot);
-  }
-  const float c = dot / (float)din;
-  for (int f = 0; f < din; ++f) {
-    const float zf = relu_in ? fmaxf(z[f], 0.f) : z[f];
-    const float xh = zf * iv;
-    const float gxh = gzn[((size_t)b * n + i) * din + f] * rw[f];
-    float v = iv * (gxh - xh * c);
-    if (relu_in && !(z[f] > 0.f)) v = 0.f;  // through the previous layer's ReLU
-    gz[((size_t)b * n + i) * din + f] = v;
-  }
-}
-
-// Per-sample parameter gradients of one layer (accumulated into gp[b, :] at the layer's offsets):
-//   bias += sum_i gm[i];  W[o,f] += sum_i gm[i,o] zn[i,f];  rms_w[f] += sum_i gzn[i,f] xh[i,f];
-//   rms_b[f] += sum_i gzn[i,f]
-__global__ void v_linear_param_grad(int n, int din, int dout, const float* __restrict__ Z, int relu_in,
-                                    const float* __restrict__ inv, const float* __restrict__ rw,
-                                    const float* __restrict__ rbias, const float* __restrict__ gm,
-                                    const float* __restrict__ gzn, size_t P, size_t off, float* __restrict__ gp) {
-  const int b = blockIdx.y;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nW = dout * din;
-  const int total = 2 * din + nW + dout;
-  if (e >= total) return;
-  float acc = 0.f;
-  if (e < din) {  // rms_w
-    const int f = e;
-    for (int i = 0; i < n; ++i) {
-      const float zf = Z[((size_t)b * n + i) * din + f];
-      const float xh = (relu_in ? fmaxf(zf, 0.f) : zf) * inv[(size_t)b * n + i];
-      acc = fmaf(gzn[((size_t)b * n + i) * din + f], xh, acc);
+  for (int i = w; i < n; i += 4) {  // R_i: row sums (one wave per row); D_i: diagonal
+    float r = 0.f;
+    for (int k = lane; k < n; k += 64) r += Gb[(size_t)i * n + k];
+    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+    if (lane == 0) {
+      const float D = Gb[(size_t)i * n + i];
+      acc[GNCDE_FC_WR_A] += r * rb[i];
+      acc[GNCDE_FC_WR_DA] += r * rb[n + i];
+      acc[GNCDE_FC_WC_A] += r * rb[2 * n + i];
+      acc[GNCDE_FC_WC_DA] += r * rb[3 * n + i];
+      acc[GNCDE_FC_WS_A] += r * s;
+      acc[GNCDE_FC_WS_DA] += r * sd;
+      acc[GNCDE_FC_UD_A] += D * rb[4 * n + i];
+      acc[GNCDE_FC_UD_DA] += D * rb[5 * n + i];
+      acc[GNCDE_FC_UR_A] += D * rb[i];
+      acc[GNCDE_FC_UR_DA] += D * rb[n + i];
+      acc[GNCDE_FC_UC_A] += D * rb[2 * n + i];
+      acc[GNCDE_FC_UC_DA] += D * rb[3 * n + i];
+      acc[GNCDE_FC_US_A] += D * s;
+      acc[GNCDE_FC_US_DA] += D * sd;
+      acc[GNCDE_FC_IDC] += D;
     }
-  } else if (e < 2 * din) {  // rms_b
-    const int f = e - din;
-    for (int i = 0; i < n; ++i) acc += gzn[((size_t)b * n + i) * din + f];
-  } else if (e < 2 * din + nW) {  // W
-    const int q = e - 2 * din, o = q / din, f = q % din;
-    for (int i = 0; i < n; ++i) {
-      const float zf = Z[((size_t)b * n + i) * din + f];
-      const float zn = fmaf((relu_in ? fmaxf(zf, 0.f) : zf) * inv[(size_t)b * n + i], rw[f], rbias[f]);
-      acc = fmaf(gm[((size_t)b * n + i) * dout + o], zn, acc);
-    }
-  } else {  // bias
-    const int o = e - 2 * din - nW;
-    for (int i = 0; i < n; ++i) acc += gm[((size_t)b * n + i) * dout + o];
   }
-  gp[(size_t)b * P + off + e] += acc;
+  if (tid < 4)
+    for (int t = 0; t < tiles; ++t) acc[tid] += part[((size_t)b * tiles + t) * 4 + tid];  // E_A, E_DA, ET_A, ET_DA
+  __shared__ float sred[GNCDE_FC][256];
+  for (int q = 0; q < GNCDE_FC; ++q) sred[q][tid] = acc[q];
+  __syncthreads();
+  if (tid < GNCDE_FC) {
+    float tot = 0.f;
+    for (int j = 0; j < (int)blockDim.x; ++j) tot += sred[tid][j];
+    gfc[((size_t)b * L + l) * GNCDE_FC + tid] += tot;
+  }
 }
 
 // out = sum over b of x[b, :]  (fixed order: deterministic)
@@ -428,14 +285,23 @@ __global__ void v_step_row(int B, size_t E, int G, int k, const float* __restric
 }
 
 // ---- workspace ----------------------------------------------------------------------------------------
+constexpr int kMinSplitRows = 1024;  // split-K chunk of the gW GEMM (rows of B*n), at most 64 chunks
+
+inline int split_rows(size_t rows) {
+  size_t ck = (rows + 63) / 64;
+  ck = (ck + 31) / 32 * 32;
+  return (int)(ck < (size_t)kMinSplitRows ? kMinSplitRows : ck);
+}
+
 struct VjpWs {
-  float *A, *dA, *red, *tg;
-  float* Zin[GNCDE_MAX_LAYERS];  // layer inputs (layer 0: stage input copy; l>0: pre of l-1)
-  float* M[GNCDE_MAX_LAYERS];
-  float* PRE[GNCDE_MAX_LAYERS];
-  float* INV[GNCDE_MAX_LAYERS];
-  float *g0, *g1, *gzn, *part, *csm, *csg;
-  float *gp, *gfc;               // per-sample accumulators [B, P], [B, L, 24]
+  float *A, *dA, *red, *tg, *abar, *G;
+  float* Z[GNCDE_MAX_LAYERS];    // layer inputs Z_l = relu(pre_{l-1}) for l >= 1 (Z_0 is the stage input)
+  float* M[GNCDE_MAX_LAYERS];    // m_l = Linear(RMSNorm(Z_l))
+  float* INV[GNCDE_MAX_LAYERS];  // 1 / rms of the rows of Z_l
+  float *wf, *bf;                // folded Linear weights / biases, all layers back to back
+  float *g0, *g1, *gm, *xh, *zn, *gzn;
+  float *cpart, *kpart, *dpart;  // column-sum, split-K and dense-fusion partials
+  float *gsum, *gfc;             // batch-summed parameter gradient [P]; per-sample fusion gradient [B, L, 24]
   float *y, *lam, *gyacc, *tmp;
   float* U[7];                   // stage inputs
   float* K[7];                   // stage values
@@ -455,26 +321,38 @@ struct Carver {
 
 void carve(const GncdeProblem& p, char* ws, VjpWs& w, size_t* bytes) {
   const size_t B = p.B, n = p.n, nn = n * n, D = max_dim(p), E = n * state_dim(p);
-  const size_t P = params_floats(p);
+  const size_t P = params_floats(p), R = B * n;
+  size_t WF = 0, BF = 0;
+  for (int l = 0; l < p.L; ++l) {
+    WF += (size_t)p.dims[l] * p.dims[l + 1];
+    BF += p.dims[l + 1];
+  }
+  const size_t tiles = (size_t)cdiv(n, 32) * cdiv(n, 32);
   Carver c{ws};
   auto tk = [&](size_t f) { return ws ? c.take(f) : (c.off += align_up(f * sizeof(float), 256), nullptr); };
   w.A = tk(B * nn);
   w.dA = tk(B * nn);
   w.red = tk(B * kRedStride * n);
   w.tg = tk(B * n);
+  w.abar = tk(B * nn);
+  w.G = tk(B * nn);
   for (int l = 0; l < p.L; ++l) {
-    w.Zin[l] = tk(B * n * D);
-    w.M[l] = tk(B * n * D);
-    w.PRE[l] = tk(B * n * D);
-    w.INV[l] = tk(B * n);
+    w.Z[l] = l > 0 ? tk(R * D) : nullptr;
+    w.M[l] = tk(R * D);
+    w.INV[l] = tk(R);
   }
-  w.g0 = tk(B * n * D);
-  w.g1 = tk(B * n * D);
-  w.gzn = tk(B * n * D);
-  w.part = tk(B * n * 4);
-  w.csm = tk(B * D);
-  w.csg = tk(B * D);
-  w.gp = tk(B * P);
+  w.wf = tk(WF);
+  w.bf = tk(BF);
+  w.g0 = tk(R * D);
+  w.g1 = tk(R * D);
+  w.gm = tk(R * D);
+  w.xh = tk(R * D);
+  w.zn = tk(R * D);
+  w.gzn = tk(R * D);
+  w.cpart = tk(cdiv(R, kChunk) * D);
+  w.kpart = tk(cdiv(R, split_rows(R)) * D * D);
+  w.dpart = tk(B * tiles * 4);
+  w.gsum = tk(P);
   w.gfc = tk(B * p.L * GNCDE_FC);
   w.y = tk(B * E);
   w.lam = tk(B * E);
@@ -491,23 +369,56 @@ void carve(const GncdeProblem& p, char* ws, VjpWs& w, size_t* bytes) {
   *bytes = c.off;
 }
 
-// The layer activations of F(t, u) kept in the workspace (layer inputs, m_l, pre-activations, 1/rms)
+// out[j] += column sums of X (or X .* Y) over `rows` rows (fixed order)
+void colsum(size_t rows, int d, const float* X, const float* Y, float* part, float* out, hipStream_t st) {
+  const unsigned chunks = cdiv(rows, kChunk);
+  hipLaunchKernelGGL(v_colsum_part, dim3(cdiv(d, 64), chunks), dim3(256), 0, st, rows, d, X, Y, part);
+  hipLaunchKernelGGL(v_colsum_final, dim3(cdiv(d, 256)), dim3(256), 0, st, (int)chunks, d, part, out);
+}
+
+// The layer activations of F(t, u) kept in the workspace: Z_l (l >= 1), m_l, 1/rms_l.  The last layer's
+// propagation is not needed by the reverse sweep and is skipped.
 void forward_keep(const GncdeProblem& p, const float* t, const float* u, VjpWs& w, hipStream_t st) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
-  hipLaunchKernelGGL(v_spline, dim3(cdiv(nn > (size_t)n ? nn : n, 256), B), dim3(256), 0, st, n, p.T, p.ts, p.coef,
-                     p.tcoef, t, w.A, w.dA, w.tg);
-  hipLaunchKernelGGL(v_reduce, dim3(B), dim3(256), 0, st, n, w.A, w.dA, w.red);
-  (void)hipMemcpyAsync(w.Zin[0], u, (size_t)B * n * p.dims[0] * sizeof(float), hipMemcpyDeviceToDevice, st);
+  vf_forms(p, t, w.A, w.dA, w.tg, w.red, st);
+  size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
-    const LayerOffsets o = layer_offsets(p, l);
-    const float* zin = l == 0 ? w.Zin[0] : w.PRE[l - 1];
-    hipLaunchKernelGGL(v_rms_linear, dim3(cdiv((size_t)n * dout, 256), B), dim3(256), 0, st, n, din, dout, zin,
-                       l > 0 ? 1 : 0, p.params + o.rms_w, p.params + o.rms_b, p.params + o.W, p.params + o.b, w.M[l],
-                       w.INV[l]);
-    hipLaunchKernelGGL(v_prop, dim3(cdiv(dout, 16), cdiv(n, 16), B), dim3(256), 0, st, n, dout,
-                       p.fusion + (size_t)l * GNCDE_FC, w.A, w.dA, w.red, w.M[l], w.PRE[l], 0);
+    const float* zin = l == 0 ? u : w.Z[l];
+    row_inv(B * n, din, zin, w.INV[l], st);
+    GemmArgs lin{};
+    lin.M = B * n;
+    lin.N = dout;
+    lin.K = din;
+    lin.A = zin;
+    lin.lda = din;
+    lin.B = w.wf + wo;
+    lin.ldb = din;
+    lin.C = w.M[l];
+    lin.ldc = dout;
+    lin.rowscale = w.INV[l];
+    lin.colbias = w.bf + bo;
+    gemm(lin, 1, true, st);
+    wo += (size_t)din * dout;
+    bo += dout;
+    if (l + 1 == p.L) break;
+    abar_full(B, n, p.fusion + (size_t)l * GNCDE_FC, w.A, w.dA, w.red, kRedStride, w.abar, st);
+    GemmArgs pr{};
+    pr.M = n;
+    pr.N = dout;
+    pr.K = n;
+    pr.A = w.abar;
+    pr.lda = n;
+    pr.sA = (long)nn;
+    pr.B = w.M[l];
+    pr.ldb = dout;
+    pr.sB = (long)n * dout;
+    pr.C = w.Z[l + 1];
+    pr.ldc = dout;
+    pr.sC = (long)n * dout;
+    pr.relu = 1;
+    gemm(pr, B, false, st);
   }
 }
 
@@ -523,48 +434,113 @@ size_t generic_vjp_workspace(const GncdeProblem& p, const GncdeSolver& s) {
 
 namespace {
 
-// VJP of F at (t, u) for cotangent gF (B x n x d_out); adds the input cotangent into gu (accumulate) and the
-// parameter / fusion gradients into w.gp / w.gfc.
+// VJP of F at (t, u) for cotangent gF (B x n x d_out); adds the input cotangent into gu and the parameter /
+// fusion gradients into w.gsum / w.gfc.  Per layer (pre = (I+Abar) m, gpre its cotangent):
+//   G = gpre m^T (per sample)            -> fusion-table gradient (dense terms + row/col/diag families)
+//   gm = (I+Abar)^T gpre                 -> g_bias = colsum(gm), g_W = gm^T zn (split-K), gzn = gm W
+//   g_rms_w = colsum(gzn .* xh), g_rms_b = colsum(gzn), gZ = RMSNorm^T(gzn)
 void vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* gF, float* gu, VjpWs& w,
             hipStream_t st) {
   const int B = p.B, n = p.n, L = p.L;
-  const size_t P = params_floats(p);
+  const size_t nn = (size_t)n * n, R = (size_t)B * n;
   forward_keep(p, t, u, w, st);
   const int dL = p.dims[L];
   hipLaunchKernelGGL(v_out_grad, dim3(cdiv((size_t)n * dL, 256), B), dim3(256), 0, st, n, dL, p.cde_hidden,
                      p.cde_embed, p.T, p.ts, p.data_coef, t, w.tg, gF, w.g0);
-  float* gZ = w.g0;   // cotangent of Z_l
-  float* gm = w.g1;   // cotangent of m_l
+  float* gcur = w.g0;  // cotangent of pre_l (after the mask)
+  float* gnext = w.g1;
+  const unsigned tiles1 = cdiv(n, 32);
+  const int ck = split_rows(R);
+  const int kchunks = (int)cdiv(R, ck);
   for (int l = L - 1; l >= 0; --l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
     const LayerOffsets o = layer_offsets(p, l);
+    const float* zin = l == 0 ? u : w.Z[l];
     if (l < L - 1)
-      hipLaunchKernelGGL(v_relu_mask, dim3(cdiv((size_t)B * n * dout, 256)), dim3(256), 0, st,
-                         (size_t)B * n * dout, w.PRE[l], gZ);
-    const float* fc = p.fusion + (size_t)l * GNCDE_FC;
-    // fusion-table gradient (needs gpre = gZ and m)
-    hipLaunchKernelGGL(v_fusion_dense, dim3(n, B), dim3(256), 0, st, n, dout, w.A, w.dA, gZ, w.M[l], w.part);
-    hipLaunchKernelGGL(v_colsum, dim3(cdiv(dout, 64), B), dim3(64), 0, st, n, dout, w.M[l], w.csm);
-    hipLaunchKernelGGL(v_colsum, dim3(cdiv(dout, 64), B), dim3(64), 0, st, n, dout, gZ, w.csg);
-    hipLaunchKernelGGL(v_fusion_rank, dim3(B), dim3(64), 0, st, n, dout, L, l, w.red, gZ, w.M[l], w.csm, w.csg,
-                       w.part, w.gfc);
+      hipLaunchKernelGGL(v_relu_mask, dim3(cdiv(R * dout, 256)), dim3(256), 0, st, R * dout, w.Z[l + 1], gcur);
+    abar_full(B, n, p.fusion + (size_t)l * GNCDE_FC, w.A, w.dA, w.red, kRedStride, w.abar, st);
+    // G = gpre m^T
+    GemmArgs gg{};
+    gg.M = n;
+    gg.N = n;
+    gg.K = dout;
+    gg.A = gcur;
+    gg.lda = dout;
+    gg.sA = (long)n * dout;
+    gg.B = w.M[l];
+    gg.ldb = dout;
+    gg.sB = (long)n * dout;
+    gg.C = w.G;
+    gg.ldc = n;
+    gg.sC = (long)nn;
+    gemm(gg, B, true, st);
+    hipLaunchKernelGGL(v_fusion_dense_G, dim3(tiles1, tiles1, B), dim3(256), 0, st, n, w.A, w.dA, w.G, w.dpart);
+    hipLaunchKernelGGL(v_fusion_finish, dim3(B), dim3(256), 0, st, n, L, l, (int)(tiles1 * tiles1), w.red, w.G,
+                       w.dpart, w.gfc);
     // gm = (I+Abar)^T gpre
-    hipLaunchKernelGGL(v_prop, dim3(cdiv(dout, 16), cdiv(n, 16), B), dim3(256), 0, st, n, dout, fc, w.A, w.dA,
-                       w.red, gZ, gm, 1);
-    // Linear + RMSNorm backward
-    const float* zin = l == 0 ? w.Zin[0] : w.PRE[l - 1];
-    const int relu_in = l > 0 ? 1 : 0;
-    float* gzprev = gZ;  // reuse: gZ is dead after gm is formed
-    hipLaunchKernelGGL(v_linear_input_grad, dim3(cdiv(n, 64), B), dim3(64), 0, st, n, din, dout, zin, relu_in,
-                       w.INV[l], p.params + o.rms_w, p.params + o.W, gm, w.gzn, gzprev);
-    const int tot = 2 * din + dout * din + dout;
-    hipLaunchKernelGGL(v_linear_param_grad, dim3(cdiv(tot, 128), B), dim3(128), 0, st, n, din, dout, zin, relu_in,
-                       w.INV[l], p.params + o.rms_w, p.params + o.rms_b, gm, w.gzn, P, o.rms_w, w.gp);
-    gZ = gzprev;
+    GemmArgs gmq{};
+    gmq.M = n;
+    gmq.N = dout;
+    gmq.K = n;
+    gmq.A = w.abar;
+    gmq.lda = n;
+    gmq.sA = (long)nn;
+    gmq.B = gcur;
+    gmq.ldb = dout;
+    gmq.sB = (long)n * dout;
+    gmq.C = w.gm;
+    gmq.ldc = dout;
+    gmq.sC = (long)n * dout;
+    gemm(gmq, B, false, st, true);
+    colsum(R, dout, w.gm, nullptr, w.cpart, w.gsum + o.b, st);
+    hipLaunchKernelGGL(v_norm_rows, dim3(cdiv(R * din, 256)), dim3(256), 0, st, R, din, zin, w.INV[l],
+                       p.params + o.rms_w, p.params + o.rms_b, w.zn, w.xh);
+    // g_W = gm^T zn, split over row chunks, chunk partials summed in order
+    GemmArgs gw{};
+    gw.M = dout;
+    gw.N = din;
+    gw.K = ck;
+    gw.A = w.gm;
+    gw.lda = dout;
+    gw.sA = (long)ck * dout;
+    gw.B = w.zn;
+    gw.ldb = din;
+    gw.sB = (long)ck * din;
+    gw.C = w.kpart;
+    gw.ldc = din;
+    gw.sC = (long)dout * din;
+    if (kchunks > 1) gemm(gw, kchunks - 1, false, st, true);
+    const size_t last = (size_t)(kchunks - 1) * ck;
+    gw.K = (int)(R - last);
+    gw.A = w.gm + last * dout;
+    gw.B = w.zn + last * din;
+    gw.C = w.kpart + (size_t)(kchunks - 1) * dout * din;
+    gemm(gw, 1, false, st, true);
+    hipLaunchKernelGGL(v_colsum_final, dim3(cdiv((size_t)dout * din, 256)), dim3(256), 0, st, kchunks, dout * din,
+                       w.kpart, w.gsum + o.W);
+    // gzn = gm W
+    GemmArgs gz{};
+    gz.M = (int)R;
+    gz.N = din;
+    gz.K = dout;
+    gz.A = w.gm;
+    gz.lda = dout;
+    gz.B = p.params + o.W;
+    gz.ldb = din;
+    gz.C = w.gzn;
+    gz.ldc = din;
+    gemm(gz, 1, false, st);
+    colsum(R, din, w.gzn, w.xh, w.cpart, w.gsum + o.rms_w, st);
+    colsum(R, din, w.gzn, nullptr, w.cpart, w.gsum + o.rms_b, st);
+    hipLaunchKernelGGL(v_rms_bwd, dim3(cdiv(R, 4)), dim3(256), 0, st, R, din, zin, w.INV[l], p.params + o.rms_w,
+                       w.gzn, gnext);
+    float* sw = gcur;
+    gcur = gnext;
+    gnext = sw;
   }
-  // gu += gZ (cotangent of the stage input)
+  // gu += cotangent of the stage input
   Lin lc{};
-  lc.x[0] = gZ;
+  lc.x[0] = gcur;
   lc.a[0] = 1.0f;
   lc.nx = 1;
   lc.scale_h = 0;
@@ -617,9 +593,20 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
   char* vf_ws = ws + bytes;
   const Tableau tab = s.method == GNCDE_RK4 ? rk4_tab() : tsit5_tab();
   generic_vf_prepare(p, vf_ws, st);
+  {
+    size_t wo = 0, bo = 0;
+    for (int l = 0; l < p.L; ++l) {
+      const int din = p.dims[l], dout = p.dims[l + 1];
+      const LayerOffsets o = layer_offsets(p, l);
+      fold_linear(din, dout, p.params + o.rms_w, p.params + o.rms_b, p.params + o.W, p.params + o.b, w.wf + wo,
+                  w.bf + bo, st);
+      wo += (size_t)din * dout;
+      bo += dout;
+    }
+  }
   const unsigned gb = cdiv(B, 256);
   const dim3 ge(cdiv(E, 256), B);
-  (void)hipMemsetAsync(w.gp, 0, (size_t)B * P * sizeof(float), st);
+  (void)hipMemsetAsync(w.gsum, 0, P * sizeof(float), st);
   (void)hipMemsetAsync(w.gfc, 0, (size_t)B * p.L * GNCDE_FC * sizeof(float), st);
   // lambda = cotangent of the final state (every saved state's cotangent is added as the sweep passes it)
   if (s.save_mode == GNCDE_SAVE_STEPS)
@@ -683,7 +670,7 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
       hipLaunchKernelGGL(v_step_row, ge, dim3(256), 0, st, B, E, G, k, gys, w.lam, 1);
   }
   (void)hipMemcpyAsync(gy0, w.lam, (size_t)B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
-  hipLaunchKernelGGL(v_batch_sum, dim3(cdiv(P, 256)), dim3(256), 0, st, B, P, w.gp, gparams);
+  (void)hipMemcpyAsync(gparams, w.gsum, P * sizeof(float), hipMemcpyDeviceToDevice, st);
   hipLaunchKernelGGL(v_batch_sum, dim3(cdiv((size_t)p.L * GNCDE_FC, 256)), dim3(256), 0, st, B,
                      (size_t)p.L * GNCDE_FC, w.gfc, gfusion);
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
