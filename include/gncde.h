@@ -160,6 +160,15 @@ int gncde_integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, con
                         float* gy0, float* gparams, float* gfusion, void* workspace, size_t workspace_bytes,
                         void* stream);
 
+/* gncde_integrate_vjp plus the cotangent of the CDE wrapper's data spline (CDE problems only): gdata_coef has the
+ * layout of prob->data_coef, [B, T-1, 4, n, de, 2]; the 'a' rows are zero (the wrapper reads dX/dt only,
+ * cde_wrapper_vector_field.py:25).  Chained with gncde_hermite_coefficients_vjp it gives the gradient of the
+ * data embedding that TGBGraphNeuralCDE rebuilds inside every forward (tgb_graph_neural_cde.py:118-130).
+ * Always takes the generic reverse sweep. */
+int gncde_integrate_vjp_data(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
+                             float* gy0, float* gparams, float* gfusion, float* gdata_coef, void* workspace,
+                             size_t workspace_bytes, void* stream);
+
 /* Per-node affine map out[r, :] = W @ x[r, :] + b for `rows` rows.  x: [rows, din], W: [dout, din],
  * b: [dout] (may be NULL), out: [rows, dout]. */
 int gncde_node_affine(int32_t rows, int32_t din, int32_t dout, const float* x, const float* W,
@@ -195,6 +204,11 @@ int gncde_graph_operator(int32_t kind, int32_t graphs, int32_t n, const float* A
  * layout).  dataset_configs.py:170, tgb_graph_neural_cde.py:130. */
 int gncde_hermite_coefficients(int32_t B, int32_t T, int32_t C, int32_t ncoef, const float* ts, const float* X,
                                float* out, void* stream);
+
+/* Reverse mode of gncde_hermite_coefficients with respect to X (the knots ts are data): gX [B, T, C] from
+ * gout [B, T-1, ncoef, C].  Overwrites gX. */
+int gncde_hermite_coefficients_vjp(int32_t B, int32_t T, int32_t C, int32_t ncoef, const float* ts,
+                                   const float* gout, float* gX, void* stream);
 
 /* idx[k] = clip(searchsorted(ts[b], t[k], 'left') - 1, 0, T-2) with b = sample[k].
  * ts: [B, T], t: [count], sample: [count] int32, idx: [count] int32. */

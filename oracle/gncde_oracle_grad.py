@@ -94,11 +94,49 @@ def vector_field_vjp(params: O.VFParams, t, y, control, g):
     return gZ, grads
 
 
-def cde_wrapper_vjp(params: O.VFParams, hidden_dim, data_embed_dim, t, y, control_adj, control_data, g):
-    """VJP of oracle.cde_wrapper: out[n,m] = sum_lk F[n,m,l,k] dX[n,l,k]."""
+def cde_wrapper_vjp(params: O.VFParams, hidden_dim, data_embed_dim, t, y, control_adj, control_data, g,
+                    data_grad=False):
+    """VJP of oracle.cde_wrapper: out[n,m] = sum_lk F[n,m,l,k] dX[n,l,k].
+
+    With ``data_grad`` the per-layer grads list gets one more entry, {"data_coef": [4, T-1, n, de, 2]}: the
+    cotangent of the data spline's (d, c, b, a) coefficients (dX = b + f (2c + 3f d) at the stage interval,
+    so the 'a' row stays zero).  It accumulates over stages like the parameter gradients."""
     dX = control_data.derivative(t)
-    gF = np.einsum("nm,nlk->nmlk", np.asarray(g, np.float64), dX).reshape(g.shape[0], -1)
-    return vector_field_vjp(params, t, y, control_adj, gF)
+    g = np.asarray(g, np.float64)
+    gF = np.einsum("nm,nlk->nmlk", g, dX).reshape(g.shape[0], -1)
+    gy, grads = vector_field_vjp(params, t, y, control_adj, gF)
+    if not data_grad:
+        return gy, grads
+    F = O.vector_field(params, t, y, control_adj).reshape(-1, hidden_dim, data_embed_dim, 2)
+    gdX = np.einsum("nm,nmlk->nlk", g, F)
+    ts = np.asarray(control_data.ts)
+    i = O.interval_index(ts, t)
+    f = t - ts[i]
+    gco = np.zeros((4, len(ts) - 1) + gdX.shape)
+    gco[0, i] = 3.0 * f * f * gdX
+    gco[1, i] = 2.0 * f * gdX
+    gco[2, i] = gdX
+    return gy, list(grads) + [{"data_coef": gco}]
+
+
+def hermite_jacobian(ts):
+    """J[q, i, j] = d coef_q(interval i) / d X[j] of backward_hermite_coefficients over knots ts (the map is
+    linear in X and acts on every channel alike), evaluated column by column on unit knot vectors."""
+    T = len(ts)
+    J = np.zeros((4, T - 1, T))
+    for j in range(T):
+        e = np.zeros((T, 1))
+        e[j, 0] = 1.0
+        co = O.backward_hermite_coefficients(np.asarray(ts, np.float64), e)
+        for q in range(4):
+            J[q, :, j] = co[q][:, 0]
+    return J
+
+
+def hermite_vjp(ts, gco):
+    """Cotangent of the knot values X [T, ...] from the coefficients' cotangent gco [4, T-1, ...]."""
+    J = hermite_jacobian(ts)
+    return np.einsum("qij,qi...->j...", J, np.asarray(gco, np.float64))
 
 
 def _tableau(method):

@@ -113,9 +113,10 @@ size_t gncde_vjp_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* so
   return generic_vjp_workspace(*prob, *solver);
 }
 
-int gncde_integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
-                        float* gy0, float* gparams, float* gfusion, void* workspace, size_t workspace_bytes,
-                        void* stream) {
+static int integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
+                         float* gy0, float* gparams, float* gfusion, float* gdata, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  using namespace gncde;
   int rc = validate_problem(prob);
   if (rc) return rc;
   rc = validate_solver(prob, solver);
@@ -123,6 +124,7 @@ int gncde_integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, con
   if (solver->controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
   if (solver->save_mode != GNCDE_SAVE_T1 && solver->save_mode != GNCDE_SAVE_STEPS) return GNCDE_ERR_UNSUPPORTED;
   if (!gparams || !gfusion) return GNCDE_ERR_ARG;
+  if (gdata && prob->cde_hidden <= 0) return GNCDE_ERR_ARG;  // only the CDE wrapper reads a data spline
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (prob->B == 0) {  // empty shard: zero gradients (an all-reduce still sees this rank's contribution)
     size_t P = params_floats(*prob);
@@ -131,12 +133,26 @@ int gncde_integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, con
     return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
   }
   if (!ys || !gys || !gy0) return GNCDE_ERR_ARG;
-  if (stage_vjp_supported(*prob, *solver)) {
+  if (!gdata && stage_vjp_supported(*prob, *solver)) {
     if (workspace_bytes < stage_vjp_workspace(*prob) || !workspace) return GNCDE_ERR_WORKSPACE;
     return stage_integrate_vjp(*prob, *solver, ys, gys, gy0, gparams, gfusion, static_cast<char*>(workspace), st);
   }
   if (workspace_bytes < generic_vjp_workspace(*prob, *solver) || !workspace) return GNCDE_ERR_WORKSPACE;
-  return generic_integrate_vjp(*prob, *solver, ys, gys, gy0, gparams, gfusion, static_cast<char*>(workspace), st);
+  return generic_integrate_vjp(*prob, *solver, ys, gys, gy0, gparams, gfusion, gdata, static_cast<char*>(workspace),
+                               st);
+}
+
+int gncde_integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
+                        float* gy0, float* gparams, float* gfusion, void* workspace, size_t workspace_bytes,
+                        void* stream) {
+  return integrate_vjp(prob, solver, ys, gys, gy0, gparams, gfusion, nullptr, workspace, workspace_bytes, stream);
+}
+
+int gncde_integrate_vjp_data(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
+                             float* gy0, float* gparams, float* gfusion, float* gdata_coef, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  if (!gdata_coef) return GNCDE_ERR_ARG;
+  return integrate_vjp(prob, solver, ys, gys, gy0, gparams, gfusion, gdata_coef, workspace, workspace_bytes, stream);
 }
 
 }  // extern "C"

@@ -72,6 +72,36 @@ __global__ void k_hermite(int T, int C, int ncoef, const float* __restrict__ ts,
   for (int j = 0; j < ncoef; ++j) o[(size_t)j * C] = q[j];
 }
 
+// Reverse of k_hermite.  With s_i the slope of interval i, r_i its left derivative (r_0 = s_0, r_i = s_{i-1}) and
+// e_i = s_i - r_i:  d = -e/dt^2, c = 2e/dt, b = r, a = y_i.  Cotangents: ge_i = -gd_i/dt_i^2 + 2 gc_i/dt_i,
+// gr_i = gb_i - ge_i, and the slope s_i collects ge_i + gr_{i+1} (+ gr_0 for i = 0).  Gathered per knot j:
+// gy_j = ga_j + gs_{j-1}/dt_{j-1} - gs_j/dt_j, so each thread writes one output and nothing is accumulated.
+__global__ void k_hermite_vjp(int T, int C, int ncoef, const float* __restrict__ ts, const float* __restrict__ g,
+                              float* __restrict__ gX) {
+  const int b = blockIdx.z, j = blockIdx.y;  // knot j in [0, T)
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float* tb = ts + (size_t)b * T;
+  const float* gb = g + (size_t)b * (T - 1) * ncoef * C + c;
+  auto gq = [&](int i, int q) { return gb[((size_t)i * ncoef + q) * C]; };
+  auto ge = [&](int i) {
+    const float dt = tb[i + 1] - tb[i];
+    return -gq(i, 0) / (dt * dt) + 2.0f * gq(i, 1) / dt;
+  };
+  auto gr = [&](int i) { return gq(i, 2) - ge(i); };
+  auto gs = [&](int i) {  // i in [0, T-2]
+    float v = ge(i);
+    if (i + 1 <= T - 2) v += gr(i + 1);
+    if (i == 0) v += gr(0);
+    return v;
+  };
+  float out = 0.f;
+  if (j <= T - 2 && ncoef == 4) out += gq(j, 3);
+  if (j >= 1) out += gs(j - 1) / (tb[j] - tb[j - 1]);
+  if (j <= T - 2) out -= gs(j) / (tb[j + 1] - tb[j]);
+  gX[((size_t)b * T + j) * C + c] = out;
+}
+
 }  // namespace
 }  // namespace gncde
 
@@ -105,6 +135,17 @@ int gncde_hermite_coefficients(int32_t B, int32_t T, int32_t C, int32_t ncoef, c
   if (!ts || !X || !out) return GNCDE_ERR_ARG;
   hipLaunchKernelGGL(k_hermite, dim3((unsigned)((C + 255) / 256), T - 1, B), dim3(256), 0,
                      static_cast<hipStream_t>(stream), T, C, ncoef, ts, X, out);
+  return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+}
+
+int gncde_hermite_coefficients_vjp(int32_t B, int32_t T, int32_t C, int32_t ncoef, const float* ts,
+                                   const float* gout, float* gX, void* stream) {
+  using namespace gncde;
+  if (B < 0 || T < 2 || C <= 0 || (ncoef != 3 && ncoef != 4)) return GNCDE_ERR_SHAPE;
+  if (B == 0) return GNCDE_OK;
+  if (!ts || !gout || !gX) return GNCDE_ERR_ARG;
+  hipLaunchKernelGGL(k_hermite_vjp, dim3((unsigned)((C + 255) / 256), T, B), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), T, C, ncoef, ts, gout, gX);
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }
 

@@ -140,8 +140,8 @@ int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const flo
 
 // reverse mode (discrete adjoint, GRID controller): gncde_vjp.hip
 size_t generic_vjp_workspace(const GncdeProblem& p, const GncdeSolver& s);
-int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys,
-                          float* gy0, float* gparams, float* gfusion, char* ws, hipStream_t st);
+int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys, float* gy0,
+                          float* gparams, float* gfusion, float* gdata, char* ws, hipStream_t st);
 
 // fused per-stage reverse sweep (H = 16, n <= 128, ODE): gncde_stage.hip
 bool stage_vjp_supported(const GncdeProblem& p, const GncdeSolver& s);

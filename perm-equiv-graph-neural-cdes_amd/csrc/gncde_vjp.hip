@@ -47,6 +47,33 @@ __global__ void v_out_grad(int n, int dL, int h, int de, int T, const float* __r
   gZ[((size_t)b * n + i) * dL + q] = g * gF[((size_t)b * n + i) * h + mo] * dX;
 }
 
+// Cotangent of the data spline (CDE wrapper): g_dX[i,l,k] = tg[i] sum_m gF[i,m] Z_L[i,(m*de+l)*2+k], scattered onto
+// the stage interval's (d, c, b) coefficients with dX/d(d,c,b) = (3f^2, 2f, 1).  One thread per (sample, element):
+// no two threads of a launch touch the same coefficient.
+__global__ void v_data_grad(int n, int dL, int h, int de, int T, const float* __restrict__ ts,
+                            const float* __restrict__ t, const float* __restrict__ tg, const float* __restrict__ gF,
+                            const float* __restrict__ ZL, float* __restrict__ gcoef) {
+  const int b = blockIdx.y;
+  const int E = n * de * 2;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int i = e / (de * 2), lk = e % (de * 2);
+  const float* z = ZL + ((size_t)b * n + i) * dL;
+  const float* g = gF + ((size_t)b * n + i) * h;
+  float s = 0.f;
+  for (int m = 0; m < h; ++m) s = fmaf(g[m], z[m * de * 2 + lk], s);
+  s *= tg[(size_t)b * n + i];
+  const float tb = t[b];
+  const float* tsb = ts + (size_t)b * T;
+  const int idx = interval_index(tsb, T, tb);
+  const float f = tb - tsb[idx];
+  const size_t blk = (size_t)E;
+  float* cb = gcoef + ((size_t)b * (T - 1) + idx) * 4 * blk + e;
+  cb[0] = fmaf(3.0f * f * f, s, cb[0]);
+  cb[blk] = fmaf(2.0f * f, s, cb[blk]);
+  cb[2 * blk] += s;
+}
+
 // gpre = gZ * 1[pre > 0] when the layer has a ReLU (l < L-1), else gZ
 __global__ void v_relu_mask(size_t total, const float* __restrict__ pre, float* __restrict__ g) {
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -300,6 +327,7 @@ struct VjpWs {
   float* INV[GNCDE_MAX_LAYERS];  // 1 / rms of the rows of Z_l
   float *wf, *bf;                // folded Linear weights / biases, all layers back to back
   float *g0, *g1, *gm, *xh, *zn, *gzn;
+  float* ZL;                     // last layer output (CDE data-spline cotangent only)
   float *cpart, *kpart, *dpart;  // column-sum, split-K and dense-fusion partials
   float *gsum, *gfc;             // batch-summed parameter gradient [P]; per-sample fusion gradient [B, L, 24]
   float *y, *lam, *gyacc, *tmp;
@@ -349,6 +377,7 @@ void carve(const GncdeProblem& p, char* ws, VjpWs& w, size_t* bytes) {
   w.xh = tk(R * D);
   w.zn = tk(R * D);
   w.gzn = tk(R * D);
+  w.ZL = p.cde_hidden > 0 ? tk(R * D) : nullptr;
   w.cpart = tk(cdiv(R, kChunk) * D);
   w.kpart = tk(cdiv(R, split_rows(R)) * D * D);
   w.dpart = tk(B * tiles * 4);
@@ -378,7 +407,7 @@ void colsum(size_t rows, int d, const float* X, const float* Y, float* part, flo
 
 // The layer activations of F(t, u) kept in the workspace: Z_l (l >= 1), m_l, 1/rms_l.  The last layer's
 // propagation is not needed by the reverse sweep and is skipped.
-void forward_keep(const GncdeProblem& p, const float* t, const float* u, VjpWs& w, hipStream_t st) {
+void forward_keep(const GncdeProblem& p, const float* t, const float* u, VjpWs& w, hipStream_t st, bool last) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
   vf_forms(p, t, w.A, w.dA, w.tg, w.red, st);
@@ -402,7 +431,7 @@ void forward_keep(const GncdeProblem& p, const float* t, const float* u, VjpWs& 
     gemm(lin, 1, true, st);
     wo += (size_t)din * dout;
     bo += dout;
-    if (l + 1 == p.L) break;
+    if (l + 1 == p.L && !last) break;
     abar_full(B, n, p.fusion + (size_t)l * GNCDE_FC, w.A, w.dA, w.red, kRedStride, w.abar, st);
     GemmArgs pr{};
     pr.M = n;
@@ -414,10 +443,10 @@ void forward_keep(const GncdeProblem& p, const float* t, const float* u, VjpWs& 
     pr.B = w.M[l];
     pr.ldb = dout;
     pr.sB = (long)n * dout;
-    pr.C = w.Z[l + 1];
+    pr.C = l + 1 < p.L ? w.Z[l + 1] : w.ZL;
     pr.ldc = dout;
     pr.sC = (long)n * dout;
-    pr.relu = 1;
+    pr.relu = l + 1 < p.L ? 1 : 0;
     gemm(pr, B, false, st);
   }
 }
@@ -439,12 +468,15 @@ namespace {
 //   G = gpre m^T (per sample)            -> fusion-table gradient (dense terms + row/col/diag families)
 //   gm = (I+Abar)^T gpre                 -> g_bias = colsum(gm), g_W = gm^T zn (split-K), gzn = gm W
 //   g_rms_w = colsum(gzn .* xh), g_rms_b = colsum(gzn), gZ = RMSNorm^T(gzn)
-void vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* gF, float* gu, VjpWs& w,
-            hipStream_t st) {
+void vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* gF, float* gu, float* gdata,
+            VjpWs& w, hipStream_t st) {
   const int B = p.B, n = p.n, L = p.L;
   const size_t nn = (size_t)n * n, R = (size_t)B * n;
-  forward_keep(p, t, u, w, st);
+  forward_keep(p, t, u, w, st, gdata != nullptr);
   const int dL = p.dims[L];
+  if (gdata)
+    hipLaunchKernelGGL(v_data_grad, dim3(cdiv((size_t)n * p.cde_embed * 2, 256), B), dim3(256), 0, st, n, dL,
+                       p.cde_hidden, p.cde_embed, p.T, p.ts, t, w.tg, gF, w.ZL, gdata);
   hipLaunchKernelGGL(v_out_grad, dim3(cdiv((size_t)n * dL, 256), B), dim3(256), 0, st, n, dL, p.cde_hidden,
                      p.cde_embed, p.T, p.ts, p.data_coef, t, w.tg, gF, w.g0);
   float* gcur = w.g0;  // cotangent of pre_l (after the mask)
@@ -582,7 +614,7 @@ Tableau tsit5_tab() {
 }  // namespace
 
 int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys, float* gy0,
-                          float* gparams, float* gfusion, char* ws, hipStream_t st) {
+                          float* gparams, float* gfusion, float* gdata, char* ws, hipStream_t st) {
   if (s.controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
   const int B = p.B, G = s.grid_len;
   const size_t E = (size_t)p.n * state_dim(p);
@@ -608,6 +640,8 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
   const dim3 ge(cdiv(E, 256), B);
   (void)hipMemsetAsync(w.gsum, 0, P * sizeof(float), st);
   (void)hipMemsetAsync(w.gfc, 0, (size_t)B * p.L * GNCDE_FC * sizeof(float), st);
+  if (gdata)
+    (void)hipMemsetAsync(gdata, 0, (size_t)B * (p.T - 1) * 4 * p.n * p.cde_embed * 2 * sizeof(float), st);
   // lambda = cotangent of the final state (every saved state's cotangent is added as the sweep passes it)
   if (s.save_mode == GNCDE_SAVE_STEPS)
     hipLaunchKernelGGL(v_step_row, ge, dim3(256), 0, st, B, E, G, G - 1, gys, w.lam, 0);
@@ -648,7 +682,7 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
       hipLaunchKernelGGL(v_stage_time, dim3(gb), dim3(256), 0, st, B, tab.c[i], w.tcur, w.hcur, w.tst);
       // tmp = cotangent of U_i
       (void)hipMemsetAsync(w.tmp, 0, (size_t)B * E * sizeof(float), st);
-      vf_vjp(p, w.tst, w.U[i], w.gK[i], w.tmp, w, st);
+      vf_vjp(p, w.tst, w.U[i], w.gK[i], w.tmp, gdata, w, st);
       // gy += tmp ; gK_j += h a_ij tmp
       Lin one{};
       one.x[0] = w.tmp;

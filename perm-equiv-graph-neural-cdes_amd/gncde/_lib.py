@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "gncde_integrate",
     "gncde_vjp_workspace_bytes",
     "gncde_integrate_vjp",
+    "gncde_integrate_vjp_data",
     "gncde_node_affine",
     "gncde_node_affine_grad",
     "gncde_adamw_workspace_bytes",
@@ -40,6 +41,7 @@ EXPORTED_SYMBOLS = (
     "gncde_interval_index",
     "gncde_graph_operator",
     "gncde_hermite_coefficients",
+    "gncde_hermite_coefficients_vjp",
 )
 
 
@@ -116,6 +118,9 @@ def load(path: str | None = None):
     lib.gncde_integrate_vjp.restype = c_int32
     lib.gncde_integrate_vjp.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver), c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    lib.gncde_integrate_vjp_data.restype = c_int32
+    lib.gncde_integrate_vjp_data.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver), c_void_p, c_void_p,
+                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
     lib.gncde_node_affine.restype = c_int32
     lib.gncde_node_affine.argtypes = [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p]
@@ -135,6 +140,9 @@ def load(path: str | None = None):
     lib.gncde_hermite_coefficients.restype = c_int32
     lib.gncde_hermite_coefficients.argtypes = [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                                c_void_p]
+    lib.gncde_hermite_coefficients_vjp.restype = c_int32
+    lib.gncde_hermite_coefficients_vjp.argtypes = [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                                   c_void_p, c_void_p]
     v = lib.gncde_abi_version()
     if v != ABI_VERSION:
         raise GncdeError(f"ABI mismatch: library {v}, bindings {ABI_VERSION}")

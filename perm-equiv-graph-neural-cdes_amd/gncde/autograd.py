@@ -19,9 +19,11 @@ from . import _lib, engine
 
 class _FixedGridSolve(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y0, params, fusion, prob, spec):
+    def forward(ctx, y0, params, fusion, data_coef, prob, spec):
         p = dataclasses.replace(prob, params=params.detach().to(torch.float32).contiguous(),
                                 fusion=fusion.detach().to(torch.float32).contiguous())
+        if data_coef is not None:
+            p = dataclasses.replace(p, data_coef=data_coef.detach().to(torch.float32).contiguous())
         steps = dataclasses.replace(spec, save_mode=_lib.SAVE_STEPS)
         ys = engine.integrate(p, steps, y0.detach())
         ctx.prob, ctx.spec = p, spec
@@ -34,16 +36,21 @@ class _FixedGridSolve(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (ys,) = ctx.saved_tensors
-        gy0, gp, gf = engine.integrate_vjp(ctx.prob, ctx.spec, ys, g)
+        gdata = None
+        if ctx.needs_input_grad[3]:
+            gy0, gp, gf, gdata = engine.integrate_vjp(ctx.prob, ctx.spec, ys, g, data_grad=True)
+        else:
+            gy0, gp, gf = engine.integrate_vjp(ctx.prob, ctx.spec, ys, g)
         d0, dp, df = ctx.dtypes
-        return gy0.to(d0), gp.to(dp), gf.to(df), None, None
+        return gy0.to(d0), gp.to(dp), gf.to(df), gdata, None, None
 
 
 def solve(prob: engine.Problem, spec: engine.SolverSpec, y0: torch.Tensor, params: torch.Tensor | None = None,
-          fusion: torch.Tensor | None = None) -> torch.Tensor:
+          fusion: torch.Tensor | None = None, data_coef: torch.Tensor | None = None) -> torch.Tensor:
     """Fixed-grid solve that records a backward.  ``spec.save_mode`` SAVE_T1 returns [B, n, d] (final
     state), SAVE_STEPS returns [B, G, n, d].  ``params`` / ``fusion`` default to the problem's own
-    (then only ``y0`` can carry gradients)."""
+    (then only ``y0`` can carry gradients).  ``data_coef`` (CDE problems) replaces the problem's data
+    spline with a differentiable one (TGBGraphNeuralCDE's in-forward spline of the embedded data)."""
     if spec.controller != _lib.CTRL_GRID:
         raise _lib.GncdeError("the differentiable solve needs a fixed grid (GRID controller); "
                               "adaptive PID solves are forward-only in this build")
@@ -51,7 +58,25 @@ def solve(prob: engine.Problem, spec: engine.SolverSpec, y0: torch.Tensor, param
         raise _lib.GncdeError("differentiable solve: save_mode must be SAVE_T1 or SAVE_STEPS")
     params = prob.params if params is None else params
     fusion = prob.fusion if fusion is None else fusion
-    return _FixedGridSolve.apply(y0, params, fusion, prob, spec)
+    return _FixedGridSolve.apply(y0, params, fusion, data_coef, prob, spec)
+
+
+class _Hermite(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ts, X, ncoef):
+        ctx.save_for_backward(ts)
+        ctx.ncoef = ncoef
+        return engine.hermite_coefficients(ts, X.detach(), ncoef)
+
+    @staticmethod
+    def backward(ctx, g):
+        (ts,) = ctx.saved_tensors
+        return None, engine.hermite_coefficients_vjp(ts, g, ctx.ncoef), None
+
+
+def hermite_coefficients(ts: torch.Tensor, X: torch.Tensor, ncoef: int = 4) -> torch.Tensor:
+    """Differentiable (w.r.t. X) backward-Hermite coefficients on gncde_hermite_coefficients(_vjp)."""
+    return _Hermite.apply(ts, X, ncoef)
 
 
 class _NodeAffine(torch.autograd.Function):

@@ -201,13 +201,15 @@ def integrate(prob: Problem, solver: SolverSpec, y0: torch.Tensor, stats: bool =
     return (ys, st) if stats else ys
 
 
-def integrate_vjp(prob: Problem, solver: SolverSpec, ys_steps: torch.Tensor, gys: torch.Tensor):
+def integrate_vjp(prob: Problem, solver: SolverSpec, ys_steps: torch.Tensor, gys: torch.Tensor,
+                  data_grad: bool = False):
     """Reverse mode of ``integrate`` for a fixed grid (the discrete adjoint ``jax.grad`` takes through
     diffrax's RecursiveCheckpointAdjoint, trainer.py:315).
 
     ys_steps: [B, G, n, d] the forward's SAVE_STEPS states; gys: cotangent of the forward output in
     ``solver.save_mode`` layout (SAVE_T1 [B, n, d] or SAVE_STEPS [B, G, n, d]).
-    Returns (gy0 [B, n, d], gparams [P] summed over samples, gfusion [L, 24] summed over samples).
+    Returns (gy0 [B, n, d], gparams [P] summed over samples, gfusion [L, 24] summed over samples), plus the
+    cotangent of ``prob.data_coef`` (layout of data_coef) when ``data_grad`` (CDE problems only).
     """
     _require_gpu()
     lib = _lib.load()
@@ -226,9 +228,17 @@ def integrate_vjp(prob: Problem, solver: SolverSpec, ys_steps: torch.Tensor, gys
     gfusion = torch.empty_like(prob.fusion)
     nbytes = lib.gncde_vjp_workspace_bytes(ctypes.byref(ps), ctypes.byref(ss))
     ws = _Workspace.get(nbytes) if nbytes else None
-    _lib.check(lib.gncde_integrate_vjp(ctypes.byref(ps), ctypes.byref(ss), _ptr(ys_steps), _ptr(gys), _ptr(gy0),
-                                       _ptr(gparams), _ptr(gfusion), _ptr(ws), nbytes, _stream()))
-    return gy0, gparams, gfusion
+    if not data_grad:
+        _lib.check(lib.gncde_integrate_vjp(ctypes.byref(ps), ctypes.byref(ss), _ptr(ys_steps), _ptr(gys),
+                                           _ptr(gy0), _ptr(gparams), _ptr(gfusion), _ptr(ws), nbytes, _stream()))
+        return gy0, gparams, gfusion
+    if prob.data_coef is None:
+        raise _lib.GncdeError("integrate_vjp(data_grad=True) needs a CDE problem")
+    gdata = torch.empty_like(prob.data_coef)
+    _lib.check(lib.gncde_integrate_vjp_data(ctypes.byref(ps), ctypes.byref(ss), _ptr(ys_steps), _ptr(gys),
+                                            _ptr(gy0), _ptr(gparams), _ptr(gfusion), _ptr(gdata), _ptr(ws),
+                                            nbytes, _stream()))
+    return gy0, gparams, gfusion, gdata
 
 
 def node_affine(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:
@@ -311,6 +321,19 @@ def hermite_coefficients(ts: torch.Tensor, X: torch.Tensor, ncoef: int = 4) -> t
     out = torch.empty((B, T - 1, ncoef) + tuple(X.shape[2:]), dtype=torch.float32, device=X.device)
     _lib.check(lib.gncde_hermite_coefficients(B, T, C, ncoef, _ptr(ts), _ptr(X), _ptr(out), _stream()))
     return out
+
+
+def hermite_coefficients_vjp(ts: torch.Tensor, gout: torch.Tensor, ncoef: int = 4) -> torch.Tensor:
+    """Reverse mode of ``hermite_coefficients`` w.r.t. X: gout [B, T-1, ncoef, ...] -> gX [B, T, ...]."""
+    _require_gpu()
+    lib = _lib.load()
+    gout = gout.to(device="cuda", dtype=torch.float32).contiguous()
+    ts = ts.to(device=gout.device, dtype=torch.float32).contiguous()
+    B, T = int(ts.shape[0]), int(ts.shape[1])
+    C = gout.numel() // max(B * (T - 1) * ncoef, 1)
+    gX = torch.empty((B, T) + tuple(gout.shape[3:]), dtype=torch.float32, device=gout.device)
+    _lib.check(lib.gncde_hermite_coefficients_vjp(B, T, C, ncoef, _ptr(ts), _ptr(gout), _ptr(gX), _stream()))
+    return gX
 
 
 def interval_index(ts: torch.Tensor, t: torch.Tensor, sample: torch.Tensor) -> torch.Tensor:

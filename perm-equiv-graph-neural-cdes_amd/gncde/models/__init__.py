@@ -267,15 +267,29 @@ class TGBGraphNeuralCDE(nn.Module):
         X = torch.stack([ts_d[:, :, None, None].expand_as(xd), xd], dim=-1)  # [B, T, n, de, 2]
         # the data spline rebuilt inside every forward (tgb_graph_neural_cde.py:118-130), on the GPU and
         # directly in the engine layout [B, T-1, 4, n, de, 2]
-        data_coef = engine.hermite_coefficients(ts_d, X.detach())
+        grad = torch.is_grad_enabled()
+        data_coef = autograd.hermite_coefficients(ts_d, X) if grad else engine.hermite_coefficients(ts_d, X)
         y0 = _affine(self.encoder, torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device))
-        prob = self.wrapped_vector_field.problem(control_adj, None, data_coef=data_coef)
+        prob = self.wrapped_vector_field.problem(control_adj, None, data_coef=data_coef.detach())
         grids = [layout.constant_step_grid(t[0], t[-1], self.dt0) for t in ts_d.cpu().numpy()]
         grid, ns = layout.stack_grids(grids, device=ts_d.device)
         spec = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_T1, grid=grid,
                                  nsteps=ns)
-        ys = engine.integrate(prob, spec, y0)
+        if grad:  # differentiable: discrete adjoint incl. the data spline -> data_encoder
+            params, fusion = self.vector_field.diff_tensors(prob.n, ts_d.device)
+            ys = autograd.solve(prob, spec, y0, params, fusion, data_coef=data_coef)
+        else:
+            ys = engine.integrate(prob, spec, y0)
         return _affine(self.decoder, ys)
+
+    def loss_terms(self, ts, coeffs_adj, x_data, x0, labels, source_mask):
+        """(sum of masked cross-entropies, number of unmasked rows) of trainer_tgb.cross_entropy_loss
+        (trainer_tgb.py:42-60): -sum(label * log_softmax(pred)) per node, rows where source_mask is True."""
+        pred = self.batched(ts, coeffs_adj, x_data, x0)
+        labels = torch.as_tensor(labels, dtype=torch.float32, device=pred.device).reshape(pred.shape)
+        mask = torch.as_tensor(source_mask, device=pred.device).reshape(pred.shape[:-1]).to(pred.dtype)
+        ce = -(labels * torch.log_softmax(pred, dim=-1)).sum(dim=-1)
+        return (ce * mask).sum(), mask.sum()
 
     def __call__(self, ts, coeffs_adj, x_data, x0, start_time=None, evolving_out=False):
         ts = torch.as_tensor(np.asarray(ts) if not torch.is_tensor(ts) else ts, dtype=torch.float32)

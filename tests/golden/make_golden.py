@@ -138,6 +138,8 @@ def pid_case(rng, name, B, n, T, kind, dims, rtol=1e-3, atol=1e-6, dt0=None, cde
                stats=np.array(st), rtol=np.array(rtol), atol=np.array(atol),
                dt0=np.array(np.nan if dt0 is None else dt0))
     if cde is not None:
+        if data_grad:
+            out.update(x=np.stack(xs), grad_x=np.stack(gxs))
         out.update(xd=np.stack([c[0] for c in dco]), xc=np.stack([c[1] for c in dco]),
                    xb=np.stack([c[2] for c in dco]), xa=np.stack([c[3] for c in dco]), h=np.array(h),
                    de=np.array(de))
@@ -168,7 +170,8 @@ def cde_case(rng, name, B, n, T, h, de, L):
     np.savez_compressed(os.path.join(HERE, name), **out)
 
 
-def grad_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None, cotangent="final", cde=None):
+def grad_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None, cotangent="final", cde=None,
+              data_grad=False):
     """Reverse mode of a fixed-grid solve (oracle/gncde_oracle_grad.py): expected dL/dy0 per sample and
     dL/dparams summed over samples for L = sum(g * y) with a random cotangent g."""
     if cde is not None:
@@ -187,7 +190,7 @@ def grad_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None, cot
             lay[nm] = lay[nm] * 3.0
     ds = dims[0]
     y0 = rng.standard_normal((B, n, ds))
-    grids, gys, gy0s, total, dco = [], [], [], None, []
+    grids, gys, gy0s, total, dco, gxs, xs = [], [], [], None, [], [], []
     for b in range(B):
         ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
         if cde is None:
@@ -195,12 +198,14 @@ def grad_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None, cot
             fv = lambda t, y, g, ctrl=ctrl: OG.vector_field_vjp(params, t, y, ctrl, g)  # noqa: E731
         else:
             x = rng.standard_normal((T, n, de))
+            xs.append(x)
             Xd = np.stack([np.broadcast_to(ts[b][:, None, None], x.shape), x], axis=-1)
             dc = O.backward_hermite_coefficients(ts[b], Xd)
             dco.append(dc)
             cx = O.CubicInterpolation(ts[b], dc)
             f = lambda t, y, ctrl=ctrl, cx=cx: O.cde_wrapper(params, h, de, t, y, ctrl, cx)  # noqa: E731
-            fv = lambda t, y, g, ctrl=ctrl, cx=cx: OG.cde_wrapper_vjp(params, h, de, t, y, ctrl, cx, g)  # noqa
+            fv = lambda t, y, g, ctrl=ctrl, cx=cx: OG.cde_wrapper_vjp(params, h, de, t, y, ctrl, cx, g,  # noqa
+                                                                      data_grad=data_grad)
         g = O.rk4_grid(ts[b, 0], ts[b, -1], nsteps) if method == "rk4" else O.constant_grid(ts[b, 0], ts[b, -1],
                                                                                              dt0)
         grids.append(g)
@@ -212,6 +217,8 @@ def grad_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None, cot
         for _ in range(20):
             gy0, gr = OG.solve_fixed_grid_vjp(f, fv, g, y0[b], method, **kw)
             gy0p, grp = OG.solve_fixed_grid_vjp(f, fv, g, y0[b] * (1 + 1e-6), method, **kw)
+            if data_grad:  # the data spline's cotangent -> the data knots' (channel 1; channel 0 is time)
+                gx, gr, grp = OG.hermite_vjp(ts[b], gr[-1]["data_coef"])[..., 1], gr[:-1], grp[:-1]
             va, vb = OG.grads_to_vector(gr, kind), OG.grads_to_vector(grp, kind)
             spread = max(np.max(np.abs(gy0p - gy0)) / np.max(np.abs(gy0)),
                          np.max(np.abs(vb - va)) / np.max(np.abs(va)))
@@ -222,6 +229,8 @@ def grad_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None, cot
             raise RuntimeError(f"{name}: no gradient-stable sample found")
         gys.append(gy)
         gy0s.append(gy0)
+        if data_grad:
+            gxs.append(gx)
         total = OG._acc(total, gr)
     G = max(len(g) for g in grids)
     grid = np.stack([np.concatenate([g, np.full(G - len(g), g[-1], np.float32)]) for g in grids])
@@ -231,6 +240,8 @@ def grad_case(rng, name, B, n, T, kind, dims, method, nsteps=None, dt0=None, cot
     out = dict(ts=ts, d=coeffs[0], c=coeffs[1], b=coeffs[2], a=coeffs[3], y0=y0, grid=grid, nsteps=nst,
                gys=np.stack(gys), gy0=np.stack(gy0s), method=np.array(method), cotangent=np.array(cotangent))
     if cde is not None:
+        if data_grad:
+            out.update(x=np.stack(xs), grad_x=np.stack(gxs))
         out.update(xd=np.stack([c[0] for c in dco]), xc=np.stack([c[1] for c in dco]),
                    xb=np.stack([c[2] for c in dco]), xa=np.stack([c[3] for c in dco]), h=np.array(h),
                    de=np.array(de))
@@ -273,6 +284,10 @@ def main():
     rng = np.random.default_rng(2468)
     pid_case(rng, "pid_undirected_n20_mixed.npz", 3, 20, 8, "undirected", [16, 24, 16])
     pid_case(rng, "pid_cde_n10_h8_de2.npz", 2, 10, 5, "undirected", [8, 8, 0], dt0=0.05, cde=(8, 2))
+    # the CDE data spline's cotangent (TGBGraphNeuralCDE trains its data encoder through it)
+    rng = np.random.default_rng(8642)
+    grad_case(rng, "grad_rk4_cde_data_n9_h4_de3.npz", 2, 9, 5, "undirected", [4, 6, 0], "rk4", nsteps=8,
+              cde=(4, 3), data_grad=True)
 
 
 if __name__ == "__main__":

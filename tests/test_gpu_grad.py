@@ -301,3 +301,87 @@ def test_stage_vjp_large_graphs_match_oracle(G, n, L, method):
     gparams_ref = np.stack([np.concatenate([total[l][nm] for nm in names]) for l in range(L)])
     mine = gf.double().cpu().numpy() @ M.numpy().T
     assert rel_err(mine, gparams_ref) <= RTOL_GRAD
+
+
+def test_data_spline_gradient_matches_golden(G, golden_dir):
+    """gncde_integrate_vjp_data + gncde_hermite_coefficients_vjp: the cotangent of the CDE wrapper's data knots
+    (TGBGraphNeuralCDE's data encoder trains through it, tgb_graph_neural_cde.py:118-130) vs the fp64 oracle
+    (pinned by finite differences in tests/test_oracle_grad.py)."""
+    z = np.load(os.path.join(golden_dir, "grad_rk4_cde_data_n9_h4_de3.npz"))
+    P = MG.load_layers(z)
+    prob = G.make_problem(z["ts"], (z["d"], z["c"], z["b"], z["a"]), P.kind, P.layers,
+                          data_coeffs=(z["xd"], z["xc"], z["xb"], z["xa"]), cde_hidden=int(z["h"]),
+                          cde_embed=int(z["de"]))
+    ts = torch.tensor(z["ts"], dtype=torch.float32, device="cuda")
+    x = _leaf(z["x"])
+    X = torch.stack([ts[:, :, None, None].expand_as(x), x], dim=-1)
+    dc = G.autograd.hermite_coefficients(ts, X)
+    assert dc.shape == prob.data_coef.shape
+    y0 = _leaf(z["y0"])
+    spec = G.SolverSpec(method=G._lib.RK4, save_mode=G._lib.SAVE_T1, grid=torch.tensor(z["grid"], device="cuda"),
+                        nsteps=torch.tensor(z["nsteps"], device="cuda"))
+    out = G.autograd.solve(prob, spec, y0, data_coef=dc)
+    (out.double() * torch.tensor(z["gys"], device="cuda")).sum().backward()
+    assert rel_err(y0.grad.cpu().numpy(), z["gy0"]) <= RTOL_GRAD
+    e = rel_err(x.grad.cpu().numpy(), z["grad_x"])
+    print(f"data-knot gradient rel err {e:.2e}")
+    assert e <= RTOL_GRAD
+
+
+def test_hermite_coefficients_vjp_matches_torch_autograd(G):
+    """The reverse of gncde_hermite_coefficients vs torch autograd of an fp64 restatement of the same map."""
+    rng = np.random.default_rng(21)
+    B, T, C = 3, 7, 10
+    ts = np.sort(rng.uniform(0, 4, (B, T)), axis=1)
+    ts[:, 0] = 0.0
+    X = torch.tensor(rng.standard_normal((B, T, C)), dtype=torch.float64, requires_grad=True)
+    tt = torch.tensor(ts, dtype=torch.float64)
+    dt = (tt[:, 1:] - tt[:, :-1])[..., None]
+    slope = (X[:, 1:] - X[:, :-1]) / dt
+    deriv = torch.cat([slope[:, :1], slope[:, :-1]], dim=1)
+    dd = slope - deriv
+    ref = torch.stack([-dd / (dt * dt), 2 * dd / dt, deriv, X[:, :-1]], dim=2)  # [B, T-1, 4, C]
+    g = torch.tensor(rng.standard_normal(ref.shape), dtype=torch.float64)
+    (ref * g).sum().backward()
+    for ncoef in (4, 3):
+        gX = G.engine.hermite_coefficients_vjp(torch.tensor(ts, dtype=torch.float32),
+                                               g[:, :, :ncoef].to(torch.float32), ncoef).cpu().double()
+        if ncoef == 4:
+            want = X.grad
+        else:
+            X2 = X.detach().clone().requires_grad_(True)
+            slope2 = (X2[:, 1:] - X2[:, :-1]) / dt
+            deriv2 = torch.cat([slope2[:, :1], slope2[:, :-1]], dim=1)
+            dd2 = slope2 - deriv2
+            ref2 = torch.stack([-dd2 / (dt * dt), 2 * dd2 / dt, deriv2], dim=2)
+            (ref2 * g[:, :, :3]).sum().backward()
+            want = X2.grad
+        assert torch.max(torch.abs(gX - want)) <= 1e-4 * torch.max(torch.abs(want))
+
+
+def test_tgb_model_trains_data_encoder(G):
+    """TGBGraphNeuralCDE's masked cross-entropy (trainer_tgb.py:42-60) back-propagates into every module,
+    the data encoder included, and a few ClipAdamW steps lower it."""
+    from gncde import synthetic, train
+    from gncde.models import TGBGraphNeuralCDE, vector_fields as V
+    rng = np.random.default_rng(5)
+    B, n, T, h, de = 4, 12, 3, 8, 2
+    ts, coeffs = _graph_controls(rng, B, n, T, irregular=False)
+    vf = V.PermEquivGraphVectorField(h, h, h * de * 2, 2, de, n, key=1)
+    model = TGBGraphNeuralCDE({"hidden_dim": h}, vf, "cubic", 3, dt0=0.25).to("cuda")
+    x_data = torch.tensor(rng.random((B, T, n, n)), dtype=torch.float32, device="cuda")
+    x0 = x_data[:, 0]
+    labels = torch.softmax(torch.tensor(rng.standard_normal((B, n, n)), dtype=torch.float32), dim=-1).cuda()
+    mask = torch.tensor(rng.random((B, n)) < 0.7, device="cuda")
+    args = (ts, coeffs, x_data, x0, labels, mask)
+    opt = train.ClipAdamW(model, learning_rate=3e-2)
+    opt.zero_grad()
+    ce, cnt = model.loss_terms(*args)
+    ce.backward()
+    for name, p in model.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all(), name
+    assert float(model.data_encoder.weight.grad.abs().max()) > 0
+    first = float(ce) / float(cnt)
+    for _ in range(8):
+        loss, _, _ = train.make_step(opt, model.loss_terms, *args)
+    assert float(loss) < first

@@ -98,3 +98,40 @@ def test_solve_vjp_matches_finite_differences(method, steps_mode):
         fd = _directional_fd(lambda s: loss(s, vy, vt), 0.0, 1.0)
         an = float(np.sum(gy0 * vy) + np.sum(gtheta * vt))
         assert abs(fd - an) <= 1e-6 * max(1.0, abs(an)), (fd, an)
+
+
+def test_data_spline_vjp_matches_finite_differences():
+    """Cotangent of the CDE wrapper's data knots (TGBGraphNeuralCDE's in-forward spline of the embedded data,
+    tgb_graph_neural_cde.py:118-130) through a whole RK4 solve: cde_wrapper_vjp(data_grad=True) + hermite_vjp."""
+    rng = np.random.default_rng(13)
+    n, T, h, de = 4, 4, 3, 2
+    ts = np.arange(T, dtype=np.float64)
+    _, X = O.make_graph_control(rng, n, T, irregular=False, t1=3.0)
+    ca = O.CubicInterpolation(ts, O.backward_hermite_coefficients(ts, X))
+    x = rng.standard_normal((T, n, de))
+    P = O.init_vf_params(rng, "undirected", [h, 4, h * de * 2])
+    y0 = rng.standard_normal((n, h))
+    g = rng.standard_normal((n, h))
+    grid = O.rk4_grid(ts[0], ts[-1], 5)
+
+    def spline(xv):
+        Xd = np.stack([np.broadcast_to(ts[:, None, None], xv.shape), xv], axis=-1)
+        return O.CubicInterpolation(ts, O.backward_hermite_coefficients(ts, Xd))
+
+    cx = spline(x)
+    f = lambda t, y: O.cde_wrapper(P, h, de, t, y, ca, cx)  # noqa: E731
+    fv = lambda t, y, gg: OG.cde_wrapper_vjp(P, h, de, t, y, ca, cx, gg, data_grad=True)  # noqa: E731
+    _, total = OG.solve_fixed_grid_vjp(f, fv, grid, y0, "rk4", g_final=g, time_dtype=None)
+    gX = OG.hermite_vjp(ts, total[-1]["data_coef"])[..., 1]  # channel 1 = data (channel 0 = time)
+
+    def loss(xv):
+        c = spline(xv)
+        yT, _ = O.solve_fixed_grid(lambda t, y: O.cde_wrapper(P, h, de, t, y, ca, c), grid, y0, "rk4",
+                                   time_dtype=None)
+        return float(np.sum(g * yT))
+
+    for _ in range(2):
+        v = rng.standard_normal(x.shape)
+        fd = _directional_fd(lambda s: loss(x + s * v), 0.0, 1.0)
+        an = float(np.sum(gX * v))
+        assert abs(fd - an) <= 1e-6 * max(1.0, abs(an)), (fd, an)
