@@ -240,3 +240,115 @@ class DynDataset:
         X = ops[:, torch.as_tensor(epoch, device=ops.device)]  # [B, K, n, n]
         coef, tcoef = layout.control_from_knots(ts, X)
         return ts, coef, tcoef
+
+
+# ------------------------------------------------------------------------------------------------------------
+# Snapshot-window datasets (PGT england-covid, TGB tgbn-trade shapes) — dataset_configs.py:461-815 (TGB),
+# :900-1135 (PGT)
+# ------------------------------------------------------------------------------------------------------------
+
+@dataclass
+class WindowDataCfg:
+    """The ``dataset:`` block of configs/pgt/*/*.yaml and configs/tgb/*/*.yaml (unknown keys ignored).
+
+    The reference reads england-covid from a JAX-era pickle and tgbn-trade through the tgb downloader; neither
+    can be used here (no unpickling of shipped files, no network), so ``synthetic_snapshots`` generates
+    snapshot sequences of the same shapes: england-covid n=129 with 8 node features (lagged case counts) and a
+    per-node target; tgbn-trade n=255 with node features = adjacency rows and next-period rows as targets."""
+
+    name: str = "england-covid"
+    window_size: int = 5
+    stride: int = 5
+    split_ratio: tuple = (0.6, 0.2, 0.2)
+    seed: int = 1234
+    normalise_features: bool = False
+    num_snapshots: int = 0  # 0: the dataset's own length (england-covid 61 days, tgbn-trade 32 years)
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "WindowDataCfg":
+        names = {f.name for f in fields(cls)}
+        return cls(**{k: v for k, v in (d or {}).items() if k in names})
+
+
+def synthetic_snapshots(name: str, rng: np.random.Generator, num_snapshots: int = 0):
+    """Snapshot sequence (list of dicts adj [n,n], x, y, src) shaped like the reference's datasets."""
+    if name.startswith("england"):
+        n, S, F = 129, num_snapshots or 61, 8
+        base = community_graph(n, rng)
+        signal = np.abs(rng.standard_normal(n)) * 10.0
+        hist = [signal.copy() for _ in range(F)]
+        snaps = []
+        for _ in range(S):
+            adj = base * rng.lognormal(3.0, 1.5, (n, n)) * (rng.random((n, n)) > 0.1)
+            deg = adj.sum(1, keepdims=True) + 1e-9
+            nxt = np.maximum(0.7 * signal + 0.3 * (adj / deg) @ signal + rng.standard_normal(n), 0.0)
+            x = np.stack(hist[-F:], axis=1)  # [n, 8] lagged values
+            snaps.append(dict(adj=adj, x=x, y=nxt, src=np.nonzero(adj.sum(1))[0]))
+            hist.append(nxt)
+            signal = nxt
+        return snaps
+    if name.startswith("tgbn-trade") or name.startswith("trade"):
+        n, S = 255, num_snapshots or 32
+        pattern = rng.random((n, n)) < 0.08
+        np.fill_diagonal(pattern, False)
+        vol = rng.lognormal(2.0, 2.0, (n, n))
+        snaps = []
+        for _ in range(S):
+            vol = vol * rng.lognormal(0.0, 0.2, (n, n))
+            active = pattern & (rng.random((n, n)) > 0.2)
+            adj = np.where(active, vol, 0.0)
+            snaps.append(dict(adj=adj, x=adj, src=np.nonzero(active.any(1))[0]))
+        return snaps
+    raise NotImplementedError(f"dataset {name}: england-covid and tgbn-trade shapes are generated here")
+
+
+def sample_disjoint_windows(rng: np.random.Generator, num_snapshots: int, window_size: int, stride: int,
+                            split_ratio):
+    """dataset_configs.py:692-735: shuffled window starts split into disjoint train / val / test."""
+    starts = np.arange(0, num_snapshots - window_size + 1, stride)
+    rng.shuffle(starts)
+    n_tr = int(len(starts) * split_ratio[0])
+    n_va = int(len(starts) * split_ratio[1])
+    return starts[:n_tr], starts[n_tr:n_tr + n_va], starts[n_tr + n_va:]
+
+
+class WindowDataset:
+    """Windows of ``window_size`` snapshots; the last snapshot of a window is its target (process_window,
+    dataset_configs.py:772-811 / :1103-1131), the rest become the graph path (raw adjacency knots, no operator)
+    and the node-data path, knots at t = 0 .. window_size-2."""
+
+    def __init__(self, cfg: WindowDataCfg, device="cuda"):
+        self.cfg, self.device = cfg, device
+        rng = np.random.default_rng(cfg.seed)
+        self.snaps = synthetic_snapshots(cfg.name, rng, cfg.num_snapshots)
+        self.n = self.snaps[0]["adj"].shape[0]
+        self.tgb = not cfg.name.startswith("england")
+        self.train, self.val, self.test = sample_disjoint_windows(rng, len(self.snaps), cfg.window_size, cfg.stride,
+                                                                  cfg.split_ratio)
+
+    def batch(self, starts):
+        """Model inputs for the windows starting at ``starts`` (engine layout, on the device):
+        PGT: (ts, control_adj, control_x, x0, y); TGB: (ts, control_adj, x_t, x0, y, source_mask)."""
+        from .interpolation import CubicInterpolation
+        w = self.cfg.window_size
+        dev = self.device
+        T = w - 1
+        wins = [self.snaps[s:s + w] for s in starts]
+        ts = torch.arange(T, dtype=torch.float32, device=dev).repeat(len(wins), 1)
+        A = torch.tensor(np.stack([[s["adj"] for s in win[:-1]] for win in wins]), dtype=torch.float32, device=dev)
+        coef, tcoef = layout.control_from_knots(ts, A)
+        adj = CubicInterpolation.from_layout(ts, coef=coef, tcoef=tcoef)
+        x_t = torch.tensor(np.stack([[s["x"] for s in win[:-1]] for win in wins]), dtype=torch.float32, device=dev)
+        if self.tgb and self.cfg.normalise_features:
+            x_t = torch.softmax(x_t, dim=-1)
+        x0 = torch.tensor(np.stack([win[0]["x"] for win in wins]), dtype=torch.float32, device=dev)
+        if not self.tgb:
+            X = torch.stack([ts[:, :, None, None].expand_as(x_t), x_t], dim=-1)
+            xc = CubicInterpolation.from_layout(ts, data_coef=engine.hermite_coefficients(ts, X))
+            y = torch.tensor(np.stack([win[-1]["y"] for win in wins]), dtype=torch.float32, device=dev)
+            return ts, adj, xc, x0, y
+        y = torch.tensor(np.stack([win[-1]["x"] for win in wins]), dtype=torch.float32, device=dev)
+        mask = torch.zeros(len(wins), self.n, dtype=torch.bool, device=dev)
+        for i, win in enumerate(wins):
+            mask[i, torch.as_tensor(win[-1]["src"], device=dev, dtype=torch.long)] = True
+        return ts, adj, x_t, x0, y, mask

@@ -28,6 +28,21 @@ class CubicInterpolation:
         self.coeffs = tuple(_tensor(c, device) for c in coeffs)  # (d, c, b, a)
         self._packed = {}
 
+    @classmethod
+    def from_layout(cls, ts, coef=None, tcoef=None, data_coef=None):
+        """A control already in the engine layout (e.g. from ``layout.control_from_knots`` /
+        ``engine.hermite_coefficients``): graph (ts [B,T], coef [B,T-1,4,n,n], tcoef [B,T-1,3,n]) or node data
+        (ts, data_coef [B,T-1,4,n,de,2]).  ``coeffs`` stays empty: evaluate/derivative are not available."""
+        self = cls.__new__(cls)
+        self.ts = _tensor(ts, "cuda").contiguous()
+        self.coeffs = ()
+        self._packed = {}
+        if coef is not None:
+            self._packed["graph"] = (self.ts, coef.contiguous(), tcoef.contiguous())
+        if data_coef is not None:
+            self._packed["data"] = data_coef.contiguous()
+        return self
+
     @property
     def batched(self) -> bool:
         return self.ts.dim() == 2

@@ -67,6 +67,11 @@ def _as_batched_coeffs(coeffs, batched):
                                         .unsqueeze(0) for c in coeffs)
 
 
+def _control(ts, coeffs):
+    """A reference-layout (d, c, b, a) tuple, or a control already packed (CubicInterpolation.from_layout)."""
+    return coeffs if isinstance(coeffs, CubicInterpolation) else CubicInterpolation(ts, coeffs)
+
+
 class GraphNeuralCDE(nn.Module):
     """``graph_neural_cde.py:12-113``: Linear(1->h) encoder, Tsit5 + PIDController(1e-3, 1e-6),
     dt0=None, SaveAt(ts) (evolving_out) or SaveAt(t1), Linear(h->1) read-out per node.
@@ -206,8 +211,8 @@ class PGTGraphNeuralCDE(nn.Module):
     def batched(self, ts, coeffs_adj, x_coeffs, x0, evolving_out=False, global_readout=True):
         if evolving_out:
             raise NotImplementedError("PGT drivers save at t1 (pgt_graph_neural_cde.py:116-117)")
-        control_adj = CubicInterpolation(ts, coeffs_adj)
-        control_data = CubicInterpolation(ts, x_coeffs)
+        control_adj = _control(ts, coeffs_adj)
+        control_data = _control(ts, x_coeffs)
         ts_d = control_adj.graph_layout()[0]
         y0 = self.encoder.run(torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device))
         prob = self.wrapped_vector_field.problem(control_adj, control_data)
@@ -225,10 +230,14 @@ class PGTGraphNeuralCDE(nn.Module):
 
     def loss_terms(self, ts, coeffs_adj, x_coeffs, x0, labels):
         """(sum of squared errors, count) of trainer_pgt.mse_loss (trainer_pgt.py:45-66) over the windows of
-        this shard: prediction = global read-out [B, feature_dim] vs labels."""
-        pred = self.batched(ts, coeffs_adj, x_coeffs, x0)
-        labels = torch.as_tensor(labels, dtype=torch.float32, device=pred.device).reshape(pred.shape)
-        return ((pred - labels) ** 2).sum(), pred.numel()
+        this shard.  The reference reshapes the global read-out to (feature_dim, 1) and subtracts the window's
+        label (last_snapshot.y, one value per node): broadcasting compares the read-out with every node's
+        label, and jnp.mean averages those feature_dim x n squares.  Same here, per window."""
+        pred = self.batched(ts, coeffs_adj, x_coeffs, x0)  # [B, feature_dim]
+        B = pred.shape[0]
+        labels = torch.as_tensor(labels, dtype=torch.float32, device=pred.device).reshape(B, 1, -1)
+        diff = pred.reshape(B, -1, 1) - labels
+        return (diff ** 2).sum(), diff[0].numel() * B
 
     def __call__(self, ts, coeffs_adj, x_coeffs, x0, evolving_out=False, global_readout=True):
         ts = torch.as_tensor(np.asarray(ts) if not torch.is_tensor(ts) else ts, dtype=torch.float32)
@@ -261,7 +270,7 @@ class TGBGraphNeuralCDE(nn.Module):
     def batched(self, ts, coeffs_adj, x_data, x0, start_time=None, evolving_out=False):
         if evolving_out:
             raise NotImplementedError("SaveAt(ts) with ConstantStepSize (dense output) is not implemented")
-        control_adj = CubicInterpolation(ts, coeffs_adj)
+        control_adj = _control(ts, coeffs_adj)
         ts_d = control_adj.graph_layout()[0]
         xd = _affine(self.data_encoder, torch.as_tensor(x_data, dtype=torch.float32, device=ts_d.device))
         X = torch.stack([ts_d[:, :, None, None].expand_as(xd), xd], dim=-1)  # [B, T, n, de, 2]

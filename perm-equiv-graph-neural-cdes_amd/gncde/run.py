@@ -1,6 +1,7 @@
-"""``single_run``-style entry point for the dynamical-systems workflow (the reference's
-``src/run/dyn/single_run.py`` -> ``engine.trainer.Trainer(**yaml).run()``), reading the same YAML schema
-(configs/dynamical_systems/*.yaml) and running it on this engine:
+"""``single_run``-style entry points: the reference's ``src/run/{dyn,pgt,tgb}/single_run.py`` ->
+``engine.trainer[_pgt|_tgb].Trainer(**yaml).run()``, reading the same YAML schema (configs/dynamical_systems,
+configs/pgt, configs/tgb) and running it on this engine.  ``Trainer`` drives graph_neural_cde (dynamical
+systems); ``WindowTrainer`` drives pgt_graph_neural_cde / tgb_graph_neural_cde over snapshot windows.
 
     python -m gncde.run --config <reference>/configs/dynamical_systems/perm_equiv_gncde_config.yaml \\
                         [--epochs N] [--steps-per-interval M] [--out metrics.jsonl]
@@ -28,7 +29,7 @@ import numpy as np
 import torch
 import yaml
 
-from . import _lib, data, engine, train
+from . import _lib, data, engine, metrics, train
 from .models import GraphNeuralCDE, vector_fields
 
 
@@ -130,16 +131,140 @@ class Trainer:
         return res
 
 
+class WindowTrainer:
+    """Mirror of trainer_pgt.Trainer (trainer_pgt.py:140-316) and trainer_tgb.Trainer (trainer_tgb.py:150-307)
+    for PGTGraphNeuralCDE / TGBGraphNeuralCDE over snapshot windows (gncde.data.WindowDataset).
+
+    As in the reference, every training window is one optimiser step (SlidingWindowTemporalLoader, batch_size
+    1); ``window_batch`` > 1 batches that many windows per step instead (one launch per step, gradients of the
+    summed per-window losses).  PGT: MSE of the global read-out against the window's node labels, best model by
+    validation loss.  TGB: masked cross-entropy, NDCG@10 on the masked rows (gncde.metrics), best model by
+    validation NDCG@10.  The solve is the reference's fixed-step Tsit5 (dt0 0.1 / 0.01) in both directions."""
+
+    def __init__(self, cfg: dict, epochs: int | None = None, out: str | None = None, window_batch: int = 1):
+        self.cfg = cfg
+        self.epochs = int(epochs if epochs is not None else cfg.get("epochs", 2000))
+        self.patience = int(cfg.get("patience", -1))
+        self.min_epochs = int(cfg.get("min_epochs", 100))
+        self.log_freq = int(cfg.get("log_freq", 10))
+        self.eval_freq = int(cfg.get("eval_freq", 10))
+        self.seed = int(cfg.get("seed", 1234))
+        self.out = out
+        self.window_batch = max(1, int(window_batch))
+        self.model_cfg = cfg.get("model", {})
+        name = self.model_cfg.get("name")
+        if name not in ("pgt_graph_neural_cde", "tgb_graph_neural_cde"):
+            raise NotImplementedError(f"model {name}: this runner drives pgt/tgb_graph_neural_cde")
+        self.tgb = name == "tgb_graph_neural_cde"
+
+    _log = Trainer._log
+
+    def build(self):
+        from .models import PGTGraphNeuralCDE, TGBGraphNeuralCDE
+        torch.manual_seed(self.seed)
+        np.random.seed(self.seed)
+        ds = data.WindowDataset(data.WindowDataCfg.from_dict(self.cfg.get("dataset", {})))
+        m, vfc = self.model_cfg, self.model_cfg.get("vector_field", {})
+        h = int(m.get("hidden_dim", 32))
+        de = int(vfc.get("data_embed_dim", 8))
+        cls = getattr(vector_fields, vfc.get("name", "PermEquivGraphVectorField"))
+        vf = cls(input_dim=h, hidden_dim=int(vfc.get("hidden_dim", h)), output_dim=h * de * 2,
+                 num_layers=int(vfc.get("num_layers", 2)), data_embed_dim=de, num_nodes=ds.n, key=self.seed)
+        if self.tgb:
+            model = TGBGraphNeuralCDE(m, vf, m.get("interpolation", "cubic"), self.seed)
+        else:
+            model = PGTGraphNeuralCDE(m, vf, m.get("interpolation", "cubic"), self.seed)
+        return ds, model.to("cuda")
+
+    def _chunks(self, starts, size):
+        return [starts[i:i + size] for i in range(0, len(starts), size)]
+
+    def _evaluate(self, model, ds, starts):
+        """(mean loss, mean NDCG@10 or nan) over windows, one window at a time like the reference loader."""
+        if len(starts) == 0:
+            return float("nan"), float("nan")
+        loss, ndcg = 0.0, 0.0
+        with torch.no_grad():
+            for s in starts:
+                b = ds.batch([s])
+                if self.tgb:
+                    ce, cnt = model.loss_terms(*b)
+                    loss += float(ce) / max(float(cnt), 1.0)
+                    pred = model.batched(*b[:4])[0]
+                    mask = b[5][0]
+                    ndcg += metrics.ndcg_at_k(b[4][0][mask], pred[mask], k=10)
+                else:
+                    sse, cnt = model.loss_terms(*b)
+                    loss += float(sse) / cnt
+        return loss / len(starts), (ndcg / len(starts) if self.tgb else float("nan"))
+
+    def run(self) -> dict:
+        from safetensors.torch import save_file
+        ds, model = self.build()
+        opt_cfg = self.cfg.get("optimiser", {})
+        sched = opt_cfg.get("schedule", {"name": "constant_schedule", "value": 1e-3})
+        if sched.get("name", "constant_schedule") != "constant_schedule":
+            raise NotImplementedError("only constant_schedule is wired (optimiser_configs.py)")
+        opt = train.ClipAdamW(model, learning_rate=float(sched.get("value", 1e-3)),
+                              weight_decay=float(opt_cfg.get("weight_decay", 0.0)),
+                              gradient_clipping=bool(opt_cfg.get("gradient_clipping", True)))
+        batches = [ds.batch(c) for c in self._chunks(list(ds.train), self.window_batch)]
+        best_val = -float("inf") if self.tgb else float("inf")
+        best_epoch, test_loss, test_ndcg, bad = -1, float("nan"), float("nan"), 0
+        ckpt_dir = self.cfg.get("checkpoint_dir", ".checkpoints/")
+        ckpt = os.path.join(ckpt_dir, self.cfg.get("checkpoint_name", "gncde") + ".safetensors")
+        for epoch in range(self.epochs):
+            t0 = time.time()
+            tot, mg, mu = 0.0, 0.0, 0.0
+            for b in batches:
+                loss, g, u = train.make_step(opt, model.loss_terms, *b)
+                tot += float(loss)
+                mg, mu = max(mg, float(g)), max(mu, float(u))
+            torch.cuda.synchronize()
+            rec = {"epoch": epoch + 1, "train_loss": tot / max(len(batches), 1), "train_step_time": time.time() - t0,
+                   "max_grad": mg, "max_update": mu}
+            if epoch == 0 or (epoch + 1) % self.log_freq == 0:
+                self._log(rec)
+            if (epoch + 1) % self.eval_freq == 0:
+                t0 = time.time()
+                vl, vn = self._evaluate(model, ds, ds.val)
+                rec = {"epoch": epoch + 1, "validation_loss": vl, "validation_step_time": time.time() - t0}
+                if self.tgb:
+                    rec["validation_ndcg@10"] = vn
+                self._log(rec)
+                better = vn > best_val if self.tgb else vl < best_val
+                if better:
+                    best_val, best_epoch, bad = (vn if self.tgb else vl), epoch, 0
+                    os.makedirs(ckpt_dir, exist_ok=True)
+                    save_file({k: v.detach().cpu().contiguous() for k, v in model.state_dict().items()}, ckpt)
+                    test_loss, test_ndcg = self._evaluate(model, ds, ds.test)
+                else:
+                    bad += 1
+                    if self.patience > 0 and bad * self.eval_freq >= self.patience and epoch > self.min_epochs:
+                        break
+        key = "best_validation_ndcg@10" if self.tgb else "best_validation_loss"
+        res = {key: best_val, "corr_test_loss": test_loss, "best_epoch": best_epoch, "checkpoint": ckpt}
+        if self.tgb:
+            res["corr_test_ndcg"] = test_ndcg
+        self._log(res)
+        return res
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--config", required=True)
     ap.add_argument("--epochs", type=int, default=None)
-    ap.add_argument("--steps-per-interval", type=int, default=2)
+    ap.add_argument("--steps-per-interval", type=int, default=2, help="dyn models: RK4 steps between knots")
+    ap.add_argument("--window-batch", type=int, default=1, help="pgt/tgb models: windows per optimiser step")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
     with open(args.config) as fh:
         cfg = yaml.safe_load(fh)
-    Trainer(cfg, args.epochs, args.steps_per_interval, args.out).run()
+    name = cfg.get("model", {}).get("name", "graph_neural_cde")
+    if name in ("pgt_graph_neural_cde", "tgb_graph_neural_cde"):
+        WindowTrainer(cfg, args.epochs, args.out, args.window_batch).run()
+    else:
+        Trainer(cfg, args.epochs, args.steps_per_interval, args.out).run()
 
 
 if __name__ == "__main__":

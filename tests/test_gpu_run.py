@@ -30,3 +30,29 @@ def test_dyn_single_run_small(tmp_path):
     lines = out.read_text().splitlines()
     losses = [yaml.safe_load(l)["train_loss"] for l in lines if "train_loss" in l]
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("config,metric", [("pgt_england_small.yaml", "best_validation_loss"),
+                                           ("tgb_trade_small.yaml", "best_validation_ndcg@10")])
+def test_window_single_run_small(tmp_path, config, metric):
+    """trainer_pgt / trainer_tgb flow: windows -> one optimiser step per window -> validation (MSE / NDCG@10)
+    -> checkpoint -> test metrics of the best model."""
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    from gncde import data, run
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "configs", config)) as fh:
+        cfg = yaml.safe_load(fh)
+    cfg["dataset"]["num_snapshots"] = 26 if "pgt" in config else 16
+    cfg["checkpoint_dir"] = str(tmp_path)
+    cfg["eval_freq"] = 2
+    ds = data.WindowDataset(data.WindowDataCfg.from_dict(cfg["dataset"]))
+    assert len(ds.train) >= 1 and len(ds.val) >= 1 and len(ds.test) >= 1
+    out = tmp_path / "metrics.jsonl"
+    res = run.WindowTrainer(cfg, epochs=4, out=str(out)).run()
+    assert res[metric] == res[metric] and res["best_epoch"] >= 0
+    assert os.path.exists(res["checkpoint"])
+    recs = [yaml.safe_load(l) for l in out.read_text().splitlines()]
+    assert all(r["train_loss"] == r["train_loss"] for r in recs if "train_loss" in r)
+    if "tgb" in config:
+        assert 0.0 <= res[metric] <= 1.0
