@@ -39,6 +39,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
   const int ar = TRANS_A ? (tid & 7) * 8 : tid >> 2, aq = TRANS_A ? tid >> 3 : (tid & 3) * 8;
   const int br = TRANS_B ? (tid >> 2) : (tid >> 3), bq = TRANS_B ? (tid & 3) * 8 : (tid & 7) * 8;
   float ra[8], rb[8];
+  float ss = 0.f;  // rownorm: this thread's share of sum_k A[row][k]^2
   auto fetch = [&](int k0) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -50,6 +51,9 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
         ra[q] = (r < g.M && kk < g.K) ? A[(size_t)r * g.lda + kk] : 0.f;
       }
     }
+    if (!TRANS_A && g.rownorm)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ss = fmaf(ra[q], ra[q], ss);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       if (TRANS_B) {  // B[k][j] = Bt[j][k]: row j = n0 + br, k = k0 + bq + q
@@ -91,6 +95,17 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
     }
     __syncthreads();
   }
+  __shared__ float sInv[64];
+  if (!TRANS_A && g.rownorm) {  // RMSNorm's 1/rms of the A rows (the whole row is this tile's K range)
+    ss += __shfl_xor(ss, 1);
+    ss += __shfl_xor(ss, 2);
+    if ((tid & 3) == 0) {
+      const float iv = 1.0f / sqrtf(ss / (float)g.K + 1e-5f);
+      sInv[ar] = iv;
+      if (g.inv_out && blockIdx.x == 0 && m0 + ar < g.M) g.inv_out[(size_t)b * g.sR + m0 + ar] = iv;
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -100,6 +115,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
         const int row = m0 + wm + 16 * i + 4 * hi + r, col = n0 + wn + 16 * j + lo;
         if (row < g.M && col < g.N) {
           float v = acc[i][j][r];
+          if (!TRANS_A && g.rownorm) v *= sInv[row - m0];
           if (g.rowscale) v *= g.rowscale[(size_t)b * g.sR + row];
           if (g.colbias) v += g.colbias[col];
           if (g.relu) v = fmaxf(v, 0.f);

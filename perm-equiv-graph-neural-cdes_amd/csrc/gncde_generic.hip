@@ -14,69 +14,119 @@ namespace {
 
 constexpr int kRedStride = 8;  // red[b][q][n]: r, rd, c, cd, diagA, diagdA, {s}, {sd}
 
-// ---- spline: A(t), dA(t), tg(t) -------------------------------------------------------------------
-__global__ void k_spline(int n, int T, const float* __restrict__ ts, const float* __restrict__ coef,
-                         const float* __restrict__ tcoef, const float* __restrict__ t,
-                         float* __restrict__ A, float* __restrict__ dA, float* __restrict__ tg) {
-  const int b = blockIdx.y;
+// ---- spline + reductions in one pass ------------------------------------------------------------------
+// grid (slabs of kSlab rows, B).  Thread j owns columns k = j, j+256, ...: for the slab's rows it evaluates A and
+// dA (coalesced along k), writes them, keeps the column partials and the diagonal, and accumulates per-row
+// partials that one block reduction turns into complete row sums (a slab holds whole rows).  Column partials
+// go to part[b][slab][2][n]; k_reduce_finish sums them over slabs (fixed order) and forms the totals.
+constexpr int kSlab = 16;
+
+__global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* __restrict__ ts,
+                                                     const float* __restrict__ coef, const float* __restrict__ tcoef,
+                                                     const float* __restrict__ t, float* __restrict__ A,
+                                                     float* __restrict__ dA, float* __restrict__ tg,
+                                                     float* __restrict__ red, float* __restrict__ part) {
+  const int b = blockIdx.y, slab = blockIdx.x;
+  const int i0 = slab * kSlab;
   const size_t nn = (size_t)n * n;
   const float tb = t[b];
   const float* tsb = ts + (size_t)b * T;
   const int idx = interval_index(tsb, T, tb);
   const float f = tb - tsb[idx];
+  const float f3 = 3.0f * f;
   const float* cb = coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < nn) {
-    const float d = cb[e], c = cb[nn + e], bb = cb[2 * nn + e], a = cb[3 * nn + e];
-    A[(size_t)b * nn + e] = fmaf(f, fmaf(f, fmaf(f, d, c), bb), a);
-    dA[(size_t)b * nn + e] = fmaf(f, fmaf(3.0f * f, d, 2.0f * c), bb);
+  float* Ab = A + (size_t)b * nn;
+  float* dAb = dA + (size_t)b * nn;
+  float* rb = red + (size_t)b * kRedStride * n;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rows = n - i0 < kSlab ? n - i0 : kSlab;
+  float ra[kSlab], rd[kSlab];
+#pragma unroll
+  for (int r = 0; r < kSlab; ++r) ra[r] = rd[r] = 0.f;
+  for (int k = tid; k < n; k += blockDim.x) {
+    float ca = 0.f, cd = 0.f;
+#pragma unroll
+    for (int r = 0; r < kSlab; ++r) {
+      if (r < rows) {
+        const size_t e = (size_t)(i0 + r) * n + k;
+        const float d = cb[e], c = cb[nn + e], bb = cb[2 * nn + e], a = cb[3 * nn + e];
+        const float va = fmaf(f, fmaf(f, fmaf(f, d, c), bb), a);
+        const float vd = fmaf(f, fmaf(f3, d, 2.0f * c), bb);
+        Ab[e] = va;
+        dAb[e] = vd;
+        ca += va;
+        cd += vd;
+        ra[r] += va;
+        rd[r] += vd;
+        if (k == i0 + r) {
+          rb[4 * n + k] = va;
+          rb[5 * n + k] = vd;
+        }
+      }
+    }
+    float* pb = part + ((size_t)b * gridDim.x + slab) * 2 * n;
+    pb[k] = ca;
+    pb[n + k] = cd;
   }
-  if (e < (size_t)n) {
+  __shared__ float sred[2][kSlab][4];
+#pragma unroll
+  for (int r = 0; r < kSlab; ++r) {
+    float x = ra[r], y = rd[r];
+    for (int o = 32; o > 0; o >>= 1) {
+      x += __shfl_xor(x, o);
+      y += __shfl_xor(y, o);
+    }
+    if (lane == 0) {
+      sred[0][r][w] = x;
+      sred[1][r][w] = y;
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * kSlab) {
+    const int q = tid / kSlab, r = tid % kSlab;
+    if (r < rows) rb[q * n + i0 + r] = (sred[q][r][0] + sred[q][r][1]) + (sred[q][r][2] + sred[q][r][3]);
+  }
+  if (slab == 0) {
     const float* tc = tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
-    tg[(size_t)b * n + e] = fmaf(f, fmaf(3.0f * f, tc[e], 2.0f * tc[n + e]), tc[2 * n + e]);
+    for (int e = tid; e < n; e += blockDim.x) tg[(size_t)b * n + e] = fmaf(f, fmaf(f3, tc[e], 2.0f * tc[n + e]), tc[2 * n + e]);
   }
 }
 
-// ---- row/col sums, diagonals, totals --------------------------------------------------------------
-// grid (B, 4): q = blockIdx.y selects row sums of A / dA (one wave per row, lanes along the row: coalesced;
-// these blocks also write the diagonals and the totals) or column sums of A / dA (one thread per column,
-// walking down the rows: coalesced across the threads).
-__global__ void __launch_bounds__(256) k_reduce(int n, const float* __restrict__ A, const float* __restrict__ dA,
-                                                float* __restrict__ red) {
-  const int b = blockIdx.x, q = blockIdx.y;
-  const size_t nn = (size_t)n * n;
-  const float* M = ((q & 1) ? dA : A) + b * nn;
+// column sums over slabs (fixed order) and the totals s = sum r, sd = sum rd
+__global__ void __launch_bounds__(256) k_reduce_finish(int n, int slabs, const float* __restrict__ part,
+                                                       float* __restrict__ red) {
+  const int b = blockIdx.x;
   float* rb = red + (size_t)b * kRedStride * n;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  if (q >= 2) {
-    for (int j = tid; j < n; j += blockDim.x) {
-      float c0 = 0.f, c1 = 0.f;
-      int k = 0;
-      for (; k + 1 < n; k += 2) {
-        c0 += M[(size_t)k * n + j];
-        c1 += M[(size_t)(k + 1) * n + j];
-      }
-      if (k < n) c0 += M[(size_t)k * n + j];
-      rb[q * n + j] = c0 + c1;
+  const float* pb = part + (size_t)b * slabs * 2 * n;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    float ca = 0.f, cd = 0.f;
+    for (int s = 0; s < slabs; ++s) {
+      ca += pb[(size_t)s * 2 * n + k];
+      cd += pb[(size_t)s * 2 * n + n + k];
     }
-    return;
+    rb[2 * n + k] = ca;
+    rb[3 * n + k] = cd;
   }
-  __shared__ float part[4];
-  float tot = 0.f;
-  for (int i = w; i < n; i += 4) {
-    const float* row = M + (size_t)i * n;
-    float s = 0.f;
-    for (int k = lane; k < n; k += 64) s += row[k];
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (lane == 0) {
-      rb[q * n + i] = s;
-      rb[(4 + q) * n + i] = row[i];
-    }
-    tot += s;
+  __shared__ float sp[2][4];
+  float x = 0.f, y = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    x += rb[i];
+    y += rb[n + i];
   }
-  if (lane == 0) part[w] = tot;
+  for (int o = 32; o > 0; o >>= 1) {
+    x += __shfl_xor(x, o);
+    y += __shfl_xor(y, o);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sp[0][w] = x;
+    sp[1][w] = y;
+  }
   __syncthreads();
-  if (tid == 0) rb[(6 + q) * n] = (part[0] + part[1]) + (part[2] + part[3]);
+  if (threadIdx.x == 0) {
+    rb[6 * n] = (sp[0][0] + sp[0][1]) + (sp[0][2] + sp[0][3]);
+    rb[7 * n] = (sp[1][0] + sp[1][1]) + (sp[1][2] + sp[1][3]);
+  }
 }
 
 // ---- epilogue: ODE dy = tg * Z; CDE dy[i,m] = tg[i] * sum_{l,k} Z[i,(m*de+l)*2+k] dX[i,l,k] --------
@@ -177,7 +227,7 @@ __global__ void k_grid_stats(int B, int method, const int32_t* __restrict__ nste
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
 struct VfWs {
-  float *A, *dA, *red, *tg, *Z0, *Z1, *m, *abar, *wf, *bf, *inv;
+  float *A, *dA, *red, *tg, *Z0, *Z1, *m, *abar, *wf, *bf, *inv, *part;
 };
 
 size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
@@ -204,6 +254,7 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.wf = take(wsum);  // W' = W diag(rms_w) per layer, back to back
   w.bf = take(bsum);  // bias' = bias + W rms_b per layer
   w.inv = take(B * n);
+  w.part = take(B * ((n + kSlab - 1) / kSlab) * 2 * n);
   return off;
 }
 
@@ -217,12 +268,15 @@ size_t generic_vf_workspace(const GncdeProblem& p) {
 // One evaluation = spline + reductions, then per layer two MFMA GEMMs (gncde_gemm.hip): the Linear over all
 // B*n node rows with RMSNorm folded in, and the per-sample (I + Abar) m with (I + Abar) materialised once.
 // Fold every layer's RMSNorm affine into its Linear (once per solve, not per evaluation).
-void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, hipStream_t st) {
+size_t vf_forms_scratch(const GncdeProblem& p) { return (size_t)p.B * cdiv(p.n, kSlab) * 2 * p.n; }
+
+void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, float* part,
+              hipStream_t st) {
   const int B = p.B, n = p.n;
-  const size_t nn = (size_t)n * n;
-  hipLaunchKernelGGL(k_spline, dim3(cdiv(nn > (size_t)n ? nn : n, 256), B), dim3(256), 0, st, n, p.T, p.ts, p.coef,
-                     p.tcoef, t, A, dA, tg);
-  hipLaunchKernelGGL(k_reduce, dim3(B, 4), dim3(256), 0, st, n, A, dA, red);
+  const unsigned slabs = cdiv(n, kSlab);
+  hipLaunchKernelGGL(k_spline_slab, dim3(slabs, B), dim3(256), 0, st, n, p.T, p.ts, p.coef, p.tcoef, t, A, dA, tg,
+                     red, part);
+  hipLaunchKernelGGL(k_reduce_finish, dim3(B), dim3(256), 0, st, n, (int)slabs, part, red);
 }
 
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
@@ -246,15 +300,12 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   VfWs w;
   carve_vf(p, ws, w);
   if (!prepared) generic_vf_prepare(p, ws, st);
-  hipLaunchKernelGGL(k_spline, dim3(cdiv(nn > (size_t)n ? nn : n, 256), B), dim3(256), 0, st, n, p.T,
-                     p.ts, p.coef, p.tcoef, t, w.A, w.dA, w.tg);
-  hipLaunchKernelGGL(k_reduce, dim3(B, 4), dim3(256), 0, st, n, w.A, w.dA, w.red);
+  vf_forms(p, t, w.A, w.dA, w.tg, w.red, w.part, st);
   const float* Zin = y;
   float* bufs[2] = {w.Z0, w.Z1};
   size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
-    row_inv(B * n, din, Zin, w.inv, st);
     GemmArgs lin{};
     lin.M = B * n;
     lin.N = dout;
@@ -265,7 +316,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     lin.ldb = din;
     lin.C = w.m;
     lin.ldc = dout;
-    lin.rowscale = w.inv;
+    lin.rownorm = 1;
     lin.colbias = w.bf + bo;
     gemm(lin, 1, true, st);
     wo += (size_t)din * dout;

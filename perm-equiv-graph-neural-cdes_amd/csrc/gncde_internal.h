@@ -113,6 +113,8 @@ struct GemmArgs {
   const float* colbias;  // optional [N]
   int relu;
   int accumulate;  // C += result
+  int rownorm;     // (NN/TRANS_B only) scale row r by 1/sqrt(mean_k A[r][k]^2 + 1e-5): RMSNorm folded into the GEMM
+  float* inv_out;  // optional with rownorm: those factors, [b * sR + r]
 };
 // TRANS_A: A[b] + k * lda + r (A^T stored row-major)
 void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st, bool trans_a = false);
@@ -126,7 +128,10 @@ void abar_full(int B, int n, const float* fc, const float* A, const float* dA, c
 size_t generic_vf_workspace(const GncdeProblem& p);
 size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s);
 // A(t), dA/dt(t), the time-channel derivative tg and the row/col/diag/total reductions (stride 8 n per sample)
-void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, hipStream_t st);
+// part: scratch of vf_forms_scratch(p) floats (per-slab column partials)
+size_t vf_forms_scratch(const GncdeProblem& p);
+void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, float* part,
+              hipStream_t st);
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st);
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared = false);

@@ -15,6 +15,8 @@ namespace gncde {
 namespace {
 
 constexpr int kPoll = 16;
+// one workgroup per sample: wide, so its element loops (E = n*h floats, 7 stage buffers) issue many loads at once
+constexpr int kAdvThreads = 1024;
 
 struct PidState {
   int phase, st, steps, rejects, evals, status, done, si;
@@ -99,8 +101,8 @@ __global__ void k_pid_init(PidArgs a, const float* __restrict__ y0) {
   }
 }
 
-__global__ void __launch_bounds__(256) k_pid_advance(PidArgs a) {
-  __shared__ float red[4];
+__global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
+  __shared__ float red[kAdvThreads / 64];
   __shared__ PidState sh;
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -314,7 +316,7 @@ int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const flo
     hipLaunchKernelGGL(k_pid_tst, dim3((B + 255) / 256), dim3(256), 0, st, B, a.state, tst, active);
     rc = generic_vf_eval(p, tst, a.yt, K, ws, st, true);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_pid_advance, dim3(B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_pid_advance, dim3(B), dim3(kAdvThreads), 0, st, a);
     if ((it + 1) % kPoll == 0) {
       int h_active = 0;
       (void)hipMemsetAsync(active, 0, sizeof(int), st);

@@ -328,7 +328,7 @@ struct VjpWs {
   float *wf, *bf;                // folded Linear weights / biases, all layers back to back
   float *g0, *g1, *gm, *xh, *zn, *gzn;
   float* ZL;                     // last layer output (CDE data-spline cotangent only)
-  float *cpart, *kpart, *dpart;  // column-sum, split-K and dense-fusion partials
+  float *cpart, *kpart, *dpart, *fpart;  // column-sum, split-K and dense-fusion partials
   float *gsum, *gfc;             // batch-summed parameter gradient [P]; per-sample fusion gradient [B, L, 24]
   float *y, *lam, *gyacc, *tmp;
   float* U[7];                   // stage inputs
@@ -381,6 +381,7 @@ void carve(const GncdeProblem& p, char* ws, VjpWs& w, size_t* bytes) {
   w.cpart = tk(cdiv(R, kChunk) * D);
   w.kpart = tk(cdiv(R, split_rows(R)) * D * D);
   w.dpart = tk(B * tiles * 4);
+  w.fpart = tk(vf_forms_scratch(p));
   w.gsum = tk(P);
   w.gfc = tk(B * p.L * GNCDE_FC);
   w.y = tk(B * E);
@@ -410,12 +411,11 @@ void colsum(size_t rows, int d, const float* X, const float* Y, float* part, flo
 void forward_keep(const GncdeProblem& p, const float* t, const float* u, VjpWs& w, hipStream_t st, bool last) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
-  vf_forms(p, t, w.A, w.dA, w.tg, w.red, st);
+  vf_forms(p, t, w.A, w.dA, w.tg, w.red, w.fpart, st);
   size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
     const float* zin = l == 0 ? u : w.Z[l];
-    row_inv(B * n, din, zin, w.INV[l], st);
     GemmArgs lin{};
     lin.M = B * n;
     lin.N = dout;
@@ -426,7 +426,8 @@ void forward_keep(const GncdeProblem& p, const float* t, const float* u, VjpWs& 
     lin.ldb = din;
     lin.C = w.M[l];
     lin.ldc = dout;
-    lin.rowscale = w.INV[l];
+    lin.rownorm = 1;
+    lin.inv_out = w.INV[l];
     lin.colbias = w.bf + bo;
     gemm(lin, 1, true, st);
     wo += (size_t)din * dout;
