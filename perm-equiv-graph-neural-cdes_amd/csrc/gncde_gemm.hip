@@ -25,87 +25,101 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
   const float* A = g.A + (size_t)b * g.sA;
   const float* B = g.B + (size_t)b * g.sB;
   float* C = g.C + (size_t)b * g.sC;
-  __shared__ float As[64][KC + 1];
-  __shared__ float Bs[KC][68];
+  __shared__ float As[64][KC + 1];  // As[r][k]
+  __shared__ float Bs[KC][68];      // Bs[k][j]
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  // which of the wave's 16x16 sub-tiles hold any valid row / column (padding tiles skip their MFMAs)
+  const bool mi0 = m0 + wm < g.M, mi1 = m0 + wm + 16 < g.M;
+  const bool nj0 = n0 + wn < g.N, nj1 = n0 + wn + 16 < g.N;
   floatx4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // per-thread slices of the next chunk, prefetched into registers while the current one is consumed
-  // A slice: 8 consecutive k of one row (row-major A) or 8 consecutive rows of one k (TRANS_A: At[k][r])
-  const int ar = TRANS_A ? (tid & 7) * 8 : tid >> 2, aq = TRANS_A ? tid >> 3 : (tid & 3) * 8;
-  const int br = TRANS_B ? (tid >> 2) : (tid >> 3), bq = TRANS_B ? (tid & 3) * 8 : (tid & 7) * 8;
+  // Per-thread slices of the next chunk (prefetched into registers while the current one is consumed), laid out
+  // so that consecutive lanes read consecutive addresses (coalesced 128-256 B per row per instruction):
+  //   A row-major (A[r][k]):  r = tid/32 + 8q,  k = tid%32          TRANS_A (At[k][r]): k = tid/64 + 4q, r = tid%64
+  //   B row-major (B[k][j]):  k = tid/64 + 4q,  j = tid%64          TRANS_B (Bt[j][k]): j = tid/32 + 8q, k = tid%32
   float ra[8], rb[8];
-  float ss = 0.f;  // rownorm: this thread's share of sum_k A[row][k]^2
+  float ss = 0.f;  // rownorm: sum of squares of this thread's A elements (row tid/32 + 8q)
+  float ssq[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) ssq[q] = 0.f;
   auto fetch = [&](int k0) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       if (TRANS_A) {
-        const int r = m0 + ar + q, kk = k0 + aq;
+        const int kk = k0 + (tid >> 6) + 4 * q, r = m0 + (tid & 63);
         ra[q] = (r < g.M && kk < g.K) ? A[(size_t)kk * g.lda + r] : 0.f;
       } else {
-        const int r = m0 + ar, kk = k0 + aq + q;
+        const int r = m0 + (tid >> 5) + 8 * q, kk = k0 + (tid & 31);
         ra[q] = (r < g.M && kk < g.K) ? A[(size_t)r * g.lda + kk] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (TRANS_B) {
+        const int j = n0 + (tid >> 5) + 8 * q, kk = k0 + (tid & 31);
+        rb[q] = (j < g.N && kk < g.K) ? B[(size_t)j * g.ldb + kk] : 0.f;
+      } else {
+        const int kk = k0 + (tid >> 6) + 4 * q, j = n0 + (tid & 63);
+        rb[q] = (kk < g.K && j < g.N) ? B[(size_t)kk * g.ldb + j] : 0.f;
       }
     }
     if (!TRANS_A && g.rownorm)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) ss = fmaf(ra[q], ra[q], ss);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      if (TRANS_B) {  // B[k][j] = Bt[j][k]: row j = n0 + br, k = k0 + bq + q
-        const int j = n0 + br, kk = k0 + bq + q;
-        rb[q] = (j < g.N && kk < g.K) ? B[(size_t)j * g.ldb + kk] : 0.f;
-      } else {        // row k = k0 + br, col j = n0 + bq + q
-        const int kk = k0 + br, j = n0 + bq + q;
-        rb[q] = (kk < g.K && j < g.N) ? B[(size_t)kk * g.ldb + j] : 0.f;
-      }
-    }
+      for (int q = 0; q < 8; ++q) ssq[q] = fmaf(ra[q], ra[q], ssq[q]);
   };
   fetch(0);
   for (int k0 = 0; k0 < g.K; k0 += KC) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       if (TRANS_A)
-        As[ar + q][aq] = ra[q];
+        As[tid & 63][(tid >> 6) + 4 * q] = ra[q];
       else
-        As[ar][aq + q] = ra[q];
+        As[(tid >> 5) + 8 * q][tid & 31] = ra[q];
       if (TRANS_B)
-        Bs[bq + q][br] = rb[q];
+        Bs[tid & 31][(tid >> 5) + 8 * q] = rb[q];
       else
-        Bs[br][bq + q] = rb[q];
+        Bs[(tid >> 6) + 4 * q][tid & 63] = rb[q];
     }
     __syncthreads();
+    const int ksteps = (g.K - k0 >= KC) ? KC / 4 : (g.K - k0 + 3) / 4;  // the K tail skips its zero steps
     if (k0 + KC < g.K) fetch(k0 + KC);
 #pragma unroll
     for (int kk = 0; kk < KC / 4; ++kk) {
-      float av[2], bv[2];
+      if (kk < ksteps) {
+        float av[2], bv[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        av[t] = As[wm + 16 * t + lo][4 * kk + hi];
-        bv[t] = Bs[4 * kk + hi][wn + 16 * t + lo];
+        for (int t = 0; t < 2; ++t) {
+          av[t] = As[wm + 16 * t + lo][4 * kk + hi];
+          bv[t] = Bs[4 * kk + hi][wn + 16 * t + lo];
+        }
+        if (mi0 && nj0) acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], acc[0][0], 0, 0, 0);
+        if (mi0 && nj1) acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[1], acc[0][1], 0, 0, 0);
+        if (mi1 && nj0) acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[0], acc[1][0], 0, 0, 0);
+        if (mi1 && nj1) acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], acc[1][1], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
   }
   __shared__ float sInv[64];
   if (!TRANS_A && g.rownorm) {  // RMSNorm's 1/rms of the A rows (the whole row is this tile's K range)
-    ss += __shfl_xor(ss, 1);
-    ss += __shfl_xor(ss, 2);
-    if ((tid & 3) == 0) {
-      const float iv = 1.0f / sqrtf(ss / (float)g.K + 1e-5f);
-      sInv[ar] = iv;
-      if (g.inv_out && blockIdx.x == 0 && m0 + ar < g.M) g.inv_out[(size_t)b * g.sR + m0 + ar] = iv;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float v = ssq[q];
+      for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);  // the 32 lanes of row tid/32 + 8q
+      if ((tid & 31) == 0) {
+        const int r = (tid >> 5) + 8 * q;
+        const float iv = 1.0f / sqrtf(v / (float)g.K + 1e-5f);
+        sInv[r] = iv;
+        if (g.inv_out && blockIdx.x == 0 && m0 + r < g.M) g.inv_out[(size_t)b * g.sR + m0 + r] = iv;
+      }
     }
     __syncthreads();
   }
+  (void)ss;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
