@@ -120,6 +120,36 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
     __syncthreads();
   }
   (void)ss;
+  if (!TRANS_A && g.cde_out) {  // CDE contraction: one 16x16 tile = 16 rows x one hidden channel's 16 columns
+    const float tb = g.cde_t[b];
+    const float* tsb = g.cde_ts + (size_t)b * g.cde_T;
+    const int idx = interval_index(tsb, g.cde_T, tb);
+    const float f = tb - tsb[idx];
+    const size_t blk = (size_t)g.M * 16;
+    const float* cb = g.cde_coef + ((size_t)b * (g.cde_T - 1) + idx) * 4 * blk;
+    const int hch = g.N / 16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + 4 * hi + r;
+        const int rr = row < g.M ? row : 0;
+        const float* c0 = cb + (size_t)rr * 16 + lo;
+        const float dX = fmaf(f, fmaf(3.0f * f, c0[0], 2.0f * c0[blk]), c0[2 * blk]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float v = acc[i][j][r] * dX;
+          v += __shfl_xor(v, 8);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 1);
+          const int ch = (n0 + wn + 16 * j) / 16;
+          if (lo == 0 && row < g.M && ch < hch)
+            g.cde_out[((size_t)b * g.M + row) * hch + ch] = g.cde_tg[(size_t)b * g.M + row] * v;
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll

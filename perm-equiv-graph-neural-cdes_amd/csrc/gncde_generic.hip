@@ -301,6 +301,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   carve_vf(p, ws, w);
   if (!prepared) generic_vf_prepare(p, ws, st);
   vf_forms(p, t, w.A, w.dA, w.tg, w.red, w.part, st);
+  const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
   const float* Zin = y;
   float* bufs[2] = {w.Z0, w.Z1};
   size_t wo = 0, bo = 0;
@@ -337,9 +338,24 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     pr.ldc = dout;
     pr.sC = (long)n * dout;
     pr.relu = l < p.L - 1 ? 1 : 0;
+    if (l == p.L - 1 && fused_out) {  // the VF epilogue in the GEMM: ODE dy = tg * Z, CDE contraction (de = 8)
+      if (p.cde_hidden > 0) {
+        pr.cde_out = dy;
+        pr.cde_coef = p.data_coef;
+        pr.cde_ts = p.ts;
+        pr.cde_t = t;
+        pr.cde_tg = w.tg;
+        pr.cde_T = p.T;
+      } else {
+        pr.C = dy;
+        pr.rowscale = w.tg;
+        pr.sR = n;
+      }
+    }
     gemm(pr, B, false, st);
     Zin = Zout;
   }
+  if (fused_out) return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
   const int dout = out_dim(p);
   hipLaunchKernelGGL(k_finalize, dim3(cdiv((size_t)n * dout, 256), B), dim3(256), 0, st, n,
                      p.dims[p.L], p.cde_hidden, p.cde_embed, p.T, p.ts, p.data_coef, t, w.tg, Zin,

@@ -115,6 +115,15 @@ struct GemmArgs {
   int accumulate;  // C += result
   int rownorm;     // (NN/TRANS_B only) scale row r by 1/sqrt(mean_k A[r][k]^2 + 1e-5): RMSNorm folded into the GEMM
   float* inv_out;  // optional with rownorm: those factors, [b * sR + r]
+  // CDE-wrapper epilogue (batched per-sample GEMM, de = 8 so that one 16-column MFMA tile is one hidden channel):
+  // instead of C, write cde_out[b][r][c/16] = cde_tg[b][r] * sum_{q<16} C[r][c+q] * dX_b[r][q], with dX the
+  // data spline's derivative at the sample's stage time (cde_wrapper_vector_field.py:19-26)
+  float* cde_out;
+  const float* cde_coef;  // [B, T-1, 4, M, 8, 2]
+  const float* cde_ts;    // [B, T]
+  const float* cde_t;     // [B]
+  const float* cde_tg;    // [B, M]
+  int cde_T;
 };
 // TRANS_A: A[b] + k * lda + r (A^T stored row-major)
 void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st, bool trans_a = false);

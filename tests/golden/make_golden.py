@@ -284,6 +284,9 @@ def main():
     rng = np.random.default_rng(2468)
     pid_case(rng, "pid_undirected_n20_mixed.npz", 3, 20, 8, "undirected", [16, 24, 16])
     pid_case(rng, "pid_cde_n10_h8_de2.npz", 2, 10, 5, "undirected", [8, 8, 0], dt0=0.05, cde=(8, 2))
+    # de = 8 (configs 3 / 5): the CDE contraction runs in the last GEMM's epilogue; n = 70 and h = 5 leave partial
+    # row and channel tiles
+    cde_case(np.random.default_rng(9753), "cde_n70_h5_de8.npz", 3, 70, 6, 5, 8, 3)
     # the CDE data spline's cotangent (TGBGraphNeuralCDE trains its data encoder through it)
     rng = np.random.default_rng(8642)
     grad_case(rng, "grad_rk4_cde_data_n9_h4_de3.npz", 2, 9, 5, "undirected", [4, 6, 0], "rk4", nsteps=8,

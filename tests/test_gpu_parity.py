@@ -62,8 +62,10 @@ def test_vf_eval_matches_golden(gncde, golden_dir, name):
     assert err <= RTOL_VF
 
 
-def test_cde_wrapper_vf_matches_golden(gncde, golden_dir):
-    z = np.load(os.path.join(golden_dir, "cde_n12_h8_de3.npz"))
+@pytest.mark.parametrize("name", ["cde_n12_h8_de3.npz", "cde_n70_h5_de8.npz"])
+def test_cde_wrapper_vf_matches_golden(gncde, golden_dir, name):
+    """de = 3: separate contraction kernel; de = 8: contraction fused into the last layer's GEMM epilogue."""
+    z = np.load(os.path.join(golden_dir, name))
     params = MG.load_layers(z)
     prob = problem_from(gncde, z, params, data=True)
     dy = gncde.vf_eval(prob, torch.tensor(z["t"], dtype=torch.float32, device="cuda"),
