@@ -196,45 +196,6 @@ __global__ void k_row_inv(int rows, int d, const float* __restrict__ Z, float* _
   if (lane == 0) inv[r] = 1.0f / sqrtf(ss / (float)d + 1e-5f);
 }
 
-// (I + Abar)[b, i, k] from the factored table; 32x32 tiles so both A[i][k] and A[k][i] are read coalesced
-__global__ void __launch_bounds__(256) k_abar_full(int n, const float* __restrict__ fc, const float* __restrict__ A,
-                                                   const float* __restrict__ dA, const float* __restrict__ red,
-                                                   int red_stride, float* __restrict__ out) {
-  const int b = blockIdx.z;
-  const int i0 = blockIdx.y * 32, k0 = blockIdx.x * 32;
-  const size_t nn = (size_t)n * n;
-  const float* Ab = A + b * nn;
-  const float* dAb = dA + b * nn;
-  const float* rb = red + (size_t)b * red_stride * n;
-  float* ob = out + b * nn;
-  __shared__ float tA[32][33], tD[32][33];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
-  for (int y = ty; y < 32; y += 8) {  // transposed block: rows k0.., cols i0..
-    const int k = k0 + y, i = i0 + tx;
-    const bool ok = k < n && i < n;
-    tA[y][tx] = ok ? Ab[(size_t)k * n + i] : 0.f;
-    tD[y][tx] = ok ? dAb[(size_t)k * n + i] : 0.f;
-  }
-  __syncthreads();
-  const float s = rb[6 * n], sd = rb[7 * n];
-  for (int y = ty; y < 32; y += 8) {
-    const int i = i0 + y, k = k0 + tx;
-    if (i >= n || k >= n) continue;
-    const float aik = Ab[(size_t)i * n + k], dik = dAb[(size_t)i * n + k];
-    const float aki = tA[tx][y], dki = tD[tx][y];
-    float v = fc[GNCDE_FC_E_A] * aik + fc[GNCDE_FC_E_DA] * dik + fc[GNCDE_FC_ET_A] * aki + fc[GNCDE_FC_ET_DA] * dki;
-    v += fc[GNCDE_FC_WR_A] * rb[i] + fc[GNCDE_FC_WR_DA] * rb[n + i] + fc[GNCDE_FC_WC_A] * rb[2 * n + i] +
-         fc[GNCDE_FC_WC_DA] * rb[3 * n + i] + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
-    v += fc[GNCDE_FC_VR_A] * rb[k] + fc[GNCDE_FC_VR_DA] * rb[n + k] + fc[GNCDE_FC_VC_A] * rb[2 * n + k] +
-         fc[GNCDE_FC_VC_DA] * rb[3 * n + k];
-    if (i == k)
-      v += fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * rb[4 * n + i] + fc[GNCDE_FC_UD_DA] * rb[5 * n + i] +
-           fc[GNCDE_FC_UR_A] * rb[i] + fc[GNCDE_FC_UR_DA] * rb[n + i] + fc[GNCDE_FC_UC_A] * rb[2 * n + i] +
-           fc[GNCDE_FC_UC_DA] * rb[3 * n + i] + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
-    ob[(size_t)i * n + k] = v;
-  }
-}
-
 }  // namespace
 
 void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st, bool trans_a) {
@@ -262,10 +223,5 @@ void row_inv(int rows, int d, const float* Z, float* inv, hipStream_t st) {
   hipLaunchKernelGGL(k_row_inv, dim3((rows + 3) / 4), dim3(256), 0, st, rows, d, Z, inv);
 }
 
-void abar_full(int B, int n, const float* fc, const float* A, const float* dA, const float* red, int red_stride,
-               float* out, hipStream_t st) {
-  const dim3 grid((n + 31) / 32, (n + 31) / 32, B);
-  hipLaunchKernelGGL(k_abar_full, grid, dim3(256), 0, st, n, fc, A, dA, red, red_stride, out);
-}
 
 }  // namespace gncde

@@ -18,7 +18,7 @@ constexpr int kRedStride = 8;  // red[b][q][n]: r, rd, c, cd, diagA, diagdA, {s}
 // grid (slabs of kSlab rows, B).  Thread j owns columns k = j, j+256, ...: for the slab's rows it evaluates A and
 // dA (coalesced along k), writes them, keeps the column partials and the diagonal, and accumulates per-row
 // partials that one block reduction turns into complete row sums (a slab holds whole rows).  Column partials
-// go to part[b][slab][2][n]; k_reduce_finish sums them over slabs (fixed order) and forms the totals.
+// go to part[b][slab][2][n]; k_abar_all sums them over slabs (fixed order) and forms the totals.
 constexpr int kSlab = 16;
 
 __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* __restrict__ ts,
@@ -92,40 +92,73 @@ __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* 
   }
 }
 
-// column sums over slabs (fixed order) and the totals s = sum r, sd = sum rd
-__global__ void __launch_bounds__(256) k_reduce_finish(int n, int slabs, const float* __restrict__ part,
-                                                       float* __restrict__ red) {
-  const int b = blockIdx.x;
+// (I + Abar_l)[b, i, k] for every layer l from one read of the A / dA tiles (32 x 32, the transposed tile staged in
+// LDS so both A[i][k] and A[k][i] are read coalesced).  The block also finishes the reductions it needs: column sums
+// of its i and k ranges from k_spline_slab's slab partials (fixed order) and the totals; blocks on the first tile
+// row / the first tile publish the column sums / totals into red (the reverse sweep reads them later).
+__global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const float* __restrict__ fus,
+                                                  const float* __restrict__ A, const float* __restrict__ dA,
+                                                  float* __restrict__ red, const float* __restrict__ part,
+                                                  float* __restrict__ out, size_t layer_stride) {
+  const int b = blockIdx.z;
+  const int i0 = blockIdx.y * 32, k0 = blockIdx.x * 32;
+  const size_t nn = (size_t)n * n;
+  const float* Ab = A + b * nn;
+  const float* dAb = dA + b * nn;
   float* rb = red + (size_t)b * kRedStride * n;
   const float* pb = part + (size_t)b * slabs * 2 * n;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    float ca = 0.f, cd = 0.f;
-    for (int s = 0; s < slabs; ++s) {
-      ca += pb[(size_t)s * 2 * n + k];
-      cd += pb[(size_t)s * 2 * n + n + k];
-    }
-    rb[2 * n + k] = ca;
-    rb[3 * n + k] = cd;
+  __shared__ float tA[32][33], tD[32][33];
+  __shared__ float cs[2][2][32];  // [i-range / k-range][A / dA][32]
+  __shared__ float tot[2][4];
+  const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;  // 32 x 8
+  for (int y = ty; y < 32; y += 8) {
+    const int k = k0 + y, i = i0 + tx;
+    const bool ok = k < n && i < n;
+    tA[y][tx] = ok ? Ab[(size_t)k * n + i] : 0.f;
+    tD[y][tx] = ok ? dAb[(size_t)k * n + i] : 0.f;
   }
-  __shared__ float sp[2][4];
-  float x = 0.f, y = 0.f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    x += rb[i];
-    y += rb[n + i];
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    x += __shfl_xor(x, o);
-    y += __shfl_xor(y, o);
-  }
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    sp[0][w] = x;
-    sp[1][w] = y;
+  if (tid < 128) {  // column sums of A / dA over the slabs for columns i0 + x and k0 + x
+    const int which = tid >> 6, q = (tid >> 5) & 1, x = tid & 31;
+    const int col = (which ? k0 : i0) + x;
+    float c = 0.f;
+    if (col < n)
+      for (int sl = 0; sl < slabs; ++sl) c += pb[(size_t)sl * 2 * n + q * n + col];
+    cs[which][q][x] = c;
+    if (which == 1 && blockIdx.y == 0 && col < n) rb[(2 + q) * n + col] = c;
+  } else {  // totals s = sum_i r_i, sd = sum_i rd_i (waves 2, 3)
+    const int w = (tid >> 6) - 2, lane = tid & 63;
+    float x = 0.f;
+    for (int i = lane; i < n; i += 64) x += rb[w * n + i];
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) tot[w][0] = x;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    rb[6 * n] = (sp[0][0] + sp[0][1]) + (sp[0][2] + sp[0][3]);
-    rb[7 * n] = (sp[1][0] + sp[1][1]) + (sp[1][2] + sp[1][3]);
+  const float s = tot[0][0], sd = tot[1][0];
+  if (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+    rb[6 * n] = s;
+    rb[7 * n] = sd;
+  }
+  for (int y = ty; y < 32; y += 8) {
+    const int i = i0 + y, k = k0 + tx;
+    if (i >= n || k >= n) continue;
+    const float aik = Ab[(size_t)i * n + k], dik = dAb[(size_t)i * n + k];
+    const float aki = tA[tx][y], dki = tD[tx][y];
+    const float ri = rb[i], rdi = rb[n + i], ci = cs[0][0][y], cdi = cs[0][1][y];
+    const float rk = rb[k], rdk = rb[n + k], ck = cs[1][0][tx], cdk = cs[1][1][tx];
+    const bool diag = i == k;
+    const float dgi = diag ? rb[4 * n + i] : 0.f, dgdi = diag ? rb[5 * n + i] : 0.f;
+    for (int l = 0; l < L; ++l) {
+      const float* fc = fus + l * GNCDE_FC;
+      float v = fc[GNCDE_FC_E_A] * aik + fc[GNCDE_FC_E_DA] * dik + fc[GNCDE_FC_ET_A] * aki + fc[GNCDE_FC_ET_DA] * dki;
+      v += fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci + fc[GNCDE_FC_WC_DA] * cdi +
+           fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
+      v += fc[GNCDE_FC_VR_A] * rk + fc[GNCDE_FC_VR_DA] * rdk + fc[GNCDE_FC_VC_A] * ck + fc[GNCDE_FC_VC_DA] * cdk;
+      if (diag)
+        v += fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dgi + fc[GNCDE_FC_UD_DA] * dgdi + fc[GNCDE_FC_UR_A] * ri +
+             fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci + fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s +
+             fc[GNCDE_FC_US_DA] * sd;
+      out[l * layer_stride + b * nn + (size_t)i * n + k] = v;
+    }
   }
 }
 
@@ -250,7 +283,7 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.Z0 = take(B * n * D);
   w.Z1 = take(B * n * D);
   w.m = take(B * n * D);
-  w.abar = take(B * nn);
+  w.abar = take((size_t)p.L * B * nn);  // (I + Abar_l) for every layer
   w.wf = take(wsum);  // W' = W diag(rms_w) per layer, back to back
   w.bf = take(bsum);  // bias' = bias + W rms_b per layer
   w.inv = take(B * n);
@@ -271,12 +304,14 @@ size_t generic_vf_workspace(const GncdeProblem& p) {
 size_t vf_forms_scratch(const GncdeProblem& p) { return (size_t)p.B * cdiv(p.n, kSlab) * 2 * p.n; }
 
 void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, float* part,
-              hipStream_t st) {
+              float* abar, hipStream_t st) {
   const int B = p.B, n = p.n;
   const unsigned slabs = cdiv(n, kSlab);
   hipLaunchKernelGGL(k_spline_slab, dim3(slabs, B), dim3(256), 0, st, n, p.T, p.ts, p.coef, p.tcoef, t, A, dA, tg,
                      red, part);
-  hipLaunchKernelGGL(k_reduce_finish, dim3(B), dim3(256), 0, st, n, (int)slabs, part, red);
+  const unsigned tiles = cdiv(n, 32);
+  hipLaunchKernelGGL(k_abar_all, dim3(tiles, tiles, B), dim3(256), 0, st, n, p.L, (int)slabs, p.fusion, A, dA, red,
+                     part, abar, (size_t)B * n * n);
 }
 
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
@@ -300,7 +335,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   VfWs w;
   carve_vf(p, ws, w);
   if (!prepared) generic_vf_prepare(p, ws, st);
-  vf_forms(p, t, w.A, w.dA, w.tg, w.red, w.part, st);
+  vf_forms(p, t, w.A, w.dA, w.tg, w.red, w.part, w.abar, st);
   const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
   const float* Zin = y;
   float* bufs[2] = {w.Z0, w.Z1};
@@ -322,13 +357,12 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     gemm(lin, 1, true, st);
     wo += (size_t)din * dout;
     bo += dout;
-    abar_full(B, n, p.fusion + (size_t)l * GNCDE_FC, w.A, w.dA, w.red, kRedStride, w.abar, st);
     float* Zout = bufs[l & 1];
     GemmArgs pr{};
     pr.M = n;
     pr.N = dout;
     pr.K = n;
-    pr.A = w.abar;
+    pr.A = w.abar + (size_t)l * B * nn;
     pr.lda = n;
     pr.sA = (long)nn;
     pr.B = w.m;

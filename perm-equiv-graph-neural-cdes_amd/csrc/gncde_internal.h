@@ -130,8 +130,6 @@ void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st, bool trans
 void fold_linear(int din, int dout, const float* rw, const float* rb, const float* W, const float* bias, float* Wf,
                  float* bf, hipStream_t st);
 void row_inv(int rows, int d, const float* Z, float* inv, hipStream_t st);
-void abar_full(int B, int n, const float* fc, const float* A, const float* dA, const float* red, int red_stride,
-               float* out, hipStream_t st);
 
 // generic (any-shape, multi-kernel) path: gncde_generic.hip
 size_t generic_vf_workspace(const GncdeProblem& p);
@@ -139,8 +137,9 @@ size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s);
 // A(t), dA/dt(t), the time-channel derivative tg and the row/col/diag/total reductions (stride 8 n per sample)
 // part: scratch of vf_forms_scratch(p) floats (per-slab column partials)
 size_t vf_forms_scratch(const GncdeProblem& p);
+// ... and (I + Abar_l) of every layer into abar [L, B, n, n] (red: stride 8 n per sample, completed here too)
 void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, float* part,
-              hipStream_t st);
+              float* abar, hipStream_t st);
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st);
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared = false);

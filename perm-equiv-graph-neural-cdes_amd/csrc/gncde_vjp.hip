@@ -362,7 +362,7 @@ void carve(const GncdeProblem& p, char* ws, VjpWs& w, size_t* bytes) {
   w.dA = tk(B * nn);
   w.red = tk(B * kRedStride * n);
   w.tg = tk(B * n);
-  w.abar = tk(B * nn);
+  w.abar = tk((size_t)p.L * B * nn);
   w.G = tk(B * nn);
   for (int l = 0; l < p.L; ++l) {
     w.Z[l] = l > 0 ? tk(R * D) : nullptr;
@@ -411,7 +411,7 @@ void colsum(size_t rows, int d, const float* X, const float* Y, float* part, flo
 void forward_keep(const GncdeProblem& p, const float* t, const float* u, VjpWs& w, hipStream_t st, bool last) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
-  vf_forms(p, t, w.A, w.dA, w.tg, w.red, w.fpart, st);
+  vf_forms(p, t, w.A, w.dA, w.tg, w.red, w.fpart, w.abar, st);
   size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
@@ -433,12 +433,11 @@ void forward_keep(const GncdeProblem& p, const float* t, const float* u, VjpWs& 
     wo += (size_t)din * dout;
     bo += dout;
     if (l + 1 == p.L && !last) break;
-    abar_full(B, n, p.fusion + (size_t)l * GNCDE_FC, w.A, w.dA, w.red, kRedStride, w.abar, st);
     GemmArgs pr{};
     pr.M = n;
     pr.N = dout;
     pr.K = n;
-    pr.A = w.abar;
+    pr.A = w.abar + (size_t)l * B * nn;
     pr.lda = n;
     pr.sA = (long)nn;
     pr.B = w.M[l];
@@ -491,7 +490,7 @@ void vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* 
     const float* zin = l == 0 ? u : w.Z[l];
     if (l < L - 1)
       hipLaunchKernelGGL(v_relu_mask, dim3(cdiv(R * dout, 256)), dim3(256), 0, st, R * dout, w.Z[l + 1], gcur);
-    abar_full(B, n, p.fusion + (size_t)l * GNCDE_FC, w.A, w.dA, w.red, kRedStride, w.abar, st);
+    const float* abar = w.abar + (size_t)l * B * nn;  // (I + Abar_l), formed by forward_keep
     // G = gpre m^T
     GemmArgs gg{};
     gg.M = n;
@@ -515,7 +514,7 @@ void vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* 
     gmq.M = n;
     gmq.N = dout;
     gmq.K = n;
-    gmq.A = w.abar;
+    gmq.A = abar;
     gmq.lda = n;
     gmq.sA = (long)nn;
     gmq.B = gcur;
