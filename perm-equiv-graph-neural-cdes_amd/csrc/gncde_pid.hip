@@ -36,6 +36,7 @@ struct PidArgs {
   float* kk;    // [7, B, E]
   const float* K;  // [B, E] value of the last evaluation
   float* ys;    // output: [B, S, E] (SAVE_TS) or [B, E]
+  float* tst;   // [B] time of each sample's next evaluation (written by init / advance)
 };
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
@@ -98,6 +99,7 @@ __global__ void k_pid_init(PidArgs a, const float* __restrict__ y0) {
     s.dt = a.auto_dt ? 0.f : a.dt0[b];
     s.si = si;
     a.state[b] = s;
+    a.tst[b] = s.tst;
   }
 }
 
@@ -225,7 +227,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
           for (int e = tid; e < E; e += blockDim.x) a.ys[((size_t)b * a.S + s.si) * E + e] = y[e];
       }
       s.done = 1;
-      if (tid == 0) a.state[b] = s;
+      if (tid == 0) a.state[b] = s;  // tst keeps its last value: finished samples' evaluations are ignored
       return;
     }
     s.tn = s.t + s.dt;
@@ -245,7 +247,10 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
     s.tst = ns1 >= 5 ? __fadd_rn(s.t, s.h) : stage_time(s.t, cst, s.h);
     s.st = ns1;
   }
-  if (tid == 0) a.state[b] = s;
+  if (tid == 0) {
+    a.state[b] = s;
+    a.tst[b] = s.tst;
+  }
 }
 
 __global__ void k_pid_tst(int B, const PidState* __restrict__ st, float* __restrict__ tst, int* __restrict__ active) {
@@ -307,13 +312,13 @@ int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const flo
   float* tst = reinterpret_cast<float*>(take(B * 4));
   int* active = reinterpret_cast<int*>(take(B * 4));
   a.ys = ys;
+  a.tst = tst;
   hipLaunchKernelGGL(k_pid_init, dim3(B), dim3(256), 0, st, a, y0);
   generic_vf_prepare(p, ws, st);
   // each sample needs at most 2 + 6 * max_steps + 1 evaluations
   const long max_iter = 3L + 6L * (long)s.max_steps;
   int rc = GNCDE_OK;
   for (long it = 0; it < max_iter; ++it) {
-    hipLaunchKernelGGL(k_pid_tst, dim3((B + 255) / 256), dim3(256), 0, st, B, a.state, tst, active);
     rc = generic_vf_eval(p, tst, a.yt, K, ws, st, true);
     if (rc) return rc;
     hipLaunchKernelGGL(k_pid_advance, dim3(B), dim3(kAdvThreads), 0, st, a);
