@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
   constexpr int PL = H + FB * FB * 4 * 64;  // bias', W' operands (RMSNorm affine folded)
 
   __shared__ __attribute__((aligned(16))) float sR0[R0];
-  __shared__ float sVec[(6 + L) * NP];
+  __shared__ __attribute__((aligned(16))) float sVec[(6 + L) * NP];
   __shared__ float sTs[kTMax];
   __shared__ __attribute__((aligned(16))) float sPar[L * PL];
   __shared__ float sFus[L * GNCDE_FC];
@@ -308,19 +308,35 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
         ec[l][q] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, fc[q])));
     }
     {
+      // Chunks of 4 slices: all 16 image reads and the L float4 reads of v_l are issued before the first
+      // use, so a chunk waits on LDS once; the pins at the end of a chunk keep the next chunk's loads
+      // from being hoisted (register pressure), not the loads of this one.
       int r0 = swz<NP>(i, hi * KS), c0 = swz<NP>(hi * KS, i), v0 = 6 * NP + hi * KS;
       asm volatile("" : "+v"(r0), "+v"(c0), "+v"(v0));
 #pragma unroll
-      for (int sl = 0; sl < KS; ++sl) {
-        const float ar = sR0[r0 + sl], dr = sR0[AS + r0 + sl];
-        const float ac = sR0[c0 + sl * (NP + 1)], dc = sR0[AS + c0 + sl * (NP + 1)];
+      for (int s4 = 0; s4 < KS; s4 += 4) {
+        float ar[4], dr[4], ac[4], dc[4];
+        floatx4 vv[L];
 #pragma unroll
-        for (int l = 0; l < L; ++l) {
-          Ab[l][sl] = fmaf(ec[l][0], ar, fmaf(ec[l][1], dr, fmaf(ec[l][2], ac, fmaf(ec[l][3], dc,
-                           wl[l] + sVec[v0 + l * NP + sl]))));
-          asm volatile("" : "+v"(Ab[l][sl]));
+        for (int j = 0; j < 4; ++j) {
+          ar[j] = sR0[r0 + s4 + j];
+          dr[j] = sR0[AS + r0 + s4 + j];
+          ac[j] = sR0[c0 + (s4 + j) * (NP + 1)];
+          dc[j] = sR0[AS + c0 + (s4 + j) * (NP + 1)];
         }
-        if ((sl & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int l = 0; l < L; ++l) vv[l] = *reinterpret_cast<const floatx4*>(sVec + v0 + l * NP + s4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int l = 0; l < L; ++l)
+            Ab[l][s4 + j] = fmaf(ec[l][0], ar[j], fmaf(ec[l][1], dr[j], fmaf(ec[l][2], ac[j], fmaf(ec[l][3], dc[j],
+                                 wl[l] + vv[l][j]))));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int l = 0; l < L; ++l) asm volatile("" : "+v"(Ab[l][s4 + j]));
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     tg = i < n ? fmaf(f, fmaf(f3, tc0, 2.0f * tc1), tc2) : 0.f;
@@ -346,9 +362,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       for (int fb = 0; fb < FB; ++fb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) ss = fmaf(Z[fb][r], Z[fb][r], ss);
-      ss += __shfl_xor(ss, 16);
-      ss += __shfl_xor(ss, 32);
-      const float inv = 1.0f / sqrtf(ss / (float)H + 1e-5f);
+      const float inv = rms_inv(xor_sum_rows4(ss), 1.0f / (float)H);
       float* Mb = sR0 + msel * (H * MS);
       msel ^= 1;
       floatx4 mown[FB];  // this lane's own m tile (T-layout), for the diagonal term u_l * m

@@ -49,6 +49,25 @@ __device__ __forceinline__ float stage_time(float t, float c, float h) {
   return __fadd_rn(t, __fmul_rn(c, h));
 }
 
+// Sum over the four 16-lane rows of a wave64 (lane ^ 16, lane ^ 32) on the gfx950 row-swap VALU ops:
+// no LDS round trip.  Written as asm because the clang builtins of this toolchain drop the second
+// (vsrc) result of the swap; the leading s_nop covers the VALU-write -> permlane-read hazard.
+__device__ __forceinline__ float xor_sum_rows4(float v) {
+  float x = v, y = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  v = x + y;  // lanes l and l^32 both hold v_l + v_{l^32}
+  x = v;
+  y = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  return x + y;
+}
+
+// equinox RMSNorm scale rsqrt(mean(x^2) + eps) on the hardware reciprocal square root (1 ulp; the
+// parity tolerances are fp32-accumulation bounds).
+__device__ __forceinline__ float rms_inv(float sumsq, float inv_d) {
+  return __builtin_amdgcn_rsqf(fmaf(sumsq, inv_d, 1e-5f));
+}
+
 // diffrax CubicInterpolation interval rule: clip(searchsorted(ts, t, 'left') - 1, 0, T-2).
 __device__ __forceinline__ int interval_index(const float* ts, int T, float t) {
   int lo = 0, hi = T;
