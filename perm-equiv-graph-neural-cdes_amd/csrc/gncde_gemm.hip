@@ -65,6 +65,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
       } else {
         const int kk = k0 + (tid >> 6) + 4 * q, j = n0 + (tid & 63);
         rb[q] = (kk < g.K && j < g.N) ? B[(size_t)kk * g.ldb + j] : 0.f;
+        if (g.kscale && kk < g.K) rb[q] *= g.kscale[(size_t)b * g.sK + kk];
       }
     }
     if (!TRANS_A && g.rownorm)
@@ -112,7 +113,7 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
       for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);  // the 32 lanes of row tid/32 + 8q
       if ((tid & 31) == 0) {
         const int r = (tid >> 5) + 8 * q;
-        const float iv = 1.0f / sqrtf(v / (float)g.K + 1e-5f);
+        const float iv = rms_inv(v, 1.0f / (float)g.K);
         sInv[r] = iv;
         if (g.inv_out && blockIdx.x == 0 && m0 + r < g.M) g.inv_out[(size_t)b * g.sR + m0 + r] = iv;
       }
@@ -121,31 +122,29 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
   }
   (void)ss;
   if (!TRANS_A && g.cde_out) {  // CDE contraction: one 16x16 tile = 16 rows x one hidden channel's 16 columns
-    const float tb = g.cde_t[b];
-    const float* tsb = g.cde_ts + (size_t)b * g.cde_T;
-    const int idx = interval_index(tsb, g.cde_T, tb);
-    const float f = tb - tsb[idx];
-    const size_t blk = (size_t)g.M * 16;
-    const float* cb = g.cde_coef + ((size_t)b * (g.cde_T - 1) + idx) * 4 * blk;
     const int hch = g.N / 16;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm + 16 * i + 4 * hi + r;
-        const int rr = row < g.M ? row : 0;
-        const float* c0 = cb + (size_t)rr * 16 + lo;
-        const float dX = fmaf(f, fmaf(3.0f * f, c0[0], 2.0f * c0[blk]), c0[2 * blk]);
+        const size_t grow = (size_t)b * g.M + (row < g.M ? row : 0);
+        const float dX = g.cde_dx[grow * 16 + lo];
+        const float qb = g.biasrow ? g.biasrow[(size_t)b * g.sR + (row < g.M ? row : 0)] : 1.0f;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          float v = acc[i][j][r] * dX;
+          float v = acc[i][j][r];
+          if (g.colbias) {
+            const int col = n0 + wn + 16 * j + lo;
+            v = fmaf(qb, col < g.N ? g.colbias[col] : 0.f, v);
+          }
+          v *= dX;
           v += __shfl_xor(v, 8);
           v += __shfl_xor(v, 4);
           v += __shfl_xor(v, 2);
           v += __shfl_xor(v, 1);
           const int ch = (n0 + wn + 16 * j) / 16;
-          if (lo == 0 && row < g.M && ch < hch)
-            g.cde_out[((size_t)b * g.M + row) * hch + ch] = g.cde_tg[(size_t)b * g.M + row] * v;
+          if (lo == 0 && row < g.M && ch < hch) g.cde_out[grow * hch + ch] = g.cde_tg[grow] * v;
         }
       }
     return;
@@ -160,13 +159,135 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
         if (row < g.M && col < g.N) {
           float v = acc[i][j][r];
           if (!TRANS_A && g.rownorm) v *= sInv[row - m0];
+          if (g.colbias) v = g.biasrow ? fmaf(g.biasrow[(size_t)b * g.sR + row], g.colbias[col], v) : v + g.colbias[col];
           if (g.rowscale) v *= g.rowscale[(size_t)b * g.sR + row];
-          if (g.colbias) v += g.colbias[col];
           if (g.relu) v = fmaxf(v, 0.f);
           if (g.accumulate) v += C[(size_t)row * g.ldc + col];
           C[(size_t)row * g.ldc + col] = v;
         }
       }
+}
+
+// ---- narrow GEMM (N <= 64): 32-row blocks, K split over the 4 waves ---------------------------------------
+// The n x n products of the narrow layers (N = d <= 64, K = n = 129 / 255) and the Linears of width <= 64 are
+// latency-bound on the 64x64 kernel: few workgroups and a serial K loop of one HBM round trip per 32-chunk.
+// Here a workgroup owns 32 rows x N columns; wave w takes the 16-wide K chunks w, w+4, ... and issues every load
+// of its round (up to 4 chunks = 64 K per wave, 256 per workgroup) before the first MFMA, straight into the MFMA
+// operand layout (MFMA step s of a chunk at k0: lane (lo, hi) holds A[row lo][k0 + 4s + hi] and
+// B[k0 + 4s + hi][col lo]; no LDS staging).  The four K partials meet once in LDS, summed in a fixed order.
+template <bool TRANS_B, int NB>
+__global__ void __launch_bounds__(256) k_gemm_narrow(GemmArgs g) {
+  constexpr int CPW = 4;  // chunks (16 K) per wave per round
+  const int b = blockIdx.z;
+  const int m0 = blockIdx.x * 32;
+  const float* A = g.A + (size_t)b * g.sA;
+  const float* B = g.B + (size_t)b * g.sB;
+  float* C = g.C + (size_t)b * g.sC;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
+  floatx4 acc[2][NB];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float ss[2] = {0.f, 0.f};  // rownorm: this lane's share of sum_k A[row][k]^2
+  const int rowA0 = m0 + lo, rowA1 = m0 + 16 + lo;
+  for (int kr = 0; kr < g.K; kr += 4 * 16 * CPW) {
+    float av[CPW][2][4], bv[CPW][4][NB];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      const int k0 = kr + 16 * (w + 4 * c);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int k = k0 + 4 * s4 + hi;
+        const bool kin = k < g.K;
+        av[c][0][s4] = (kin && rowA0 < g.M) ? A[(size_t)rowA0 * g.lda + k] : 0.f;
+        av[c][1][s4] = (kin && rowA1 < g.M) ? A[(size_t)rowA1 * g.lda + k] : 0.f;
+        const float ks = (g.kscale && kin) ? g.kscale[(size_t)b * g.sK + k] : 1.0f;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const int col = 16 * j + lo;
+          float v = 0.f;
+          if (kin && col < g.N) v = TRANS_B ? B[(size_t)col * g.ldb + k] : B[(size_t)k * g.ldb + col];
+          bv[c][s4][j] = v * ks;
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CPW; ++c)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        if (g.rownorm) {
+          ss[0] = fmaf(av[c][0][s4], av[c][0][s4], ss[0]);
+          ss[1] = fmaf(av[c][1][s4], av[c][1][s4], ss[1]);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int j = 0; j < NB; ++j)
+            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][t][s4], bv[c][s4][j], acc[t][j], 0, 0, 0);
+      }
+  }
+  // fixed-order reduction of the four wave partials; wave w then finishes tiles (t, j) with (t * NB + j) % 4 == w
+  __shared__ floatx4 red[4][2 * NB][64];
+  __shared__ float sInv[32];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) red[w][t * NB + j][lane] = acc[t][j];
+  if (g.rownorm) {
+    __shared__ float sSS[4][2][64];
+    sSS[w][0][lane] = ss[0];
+    sSS[w][1][lane] = ss[1];
+    __syncthreads();
+    if (tid < 32) {  // row tid: its 4 lanes (hi) of each of the 4 waves
+      const int t = tid >> 4, l16 = tid & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww)
+#pragma unroll
+        for (int h4 = 0; h4 < 4; ++h4) v += sSS[ww][t][l16 + 16 * h4];
+      const float iv = rms_inv(v, 1.0f / (float)g.K);
+      sInv[tid] = iv;
+      if (g.inv_out && m0 + tid < g.M) g.inv_out[(size_t)b * g.sR + m0 + tid] = iv;
+    }
+  }
+  __syncthreads();
+  const int hch = g.N / 16;
+  for (int tile = w; tile < 2 * NB; tile += 4) {
+    const int t = tile / NB, j = tile % NB;
+    floatx4 v4 = red[0][tile][lane];
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) {
+      const floatx4 o = red[ww][tile][lane];
+      v4 = floatx4{v4[0] + o[0], v4[1] + o[1], v4[2] + o[2], v4[3] + o[3]};
+    }
+    const int col = 16 * j + lo;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = 16 * t + 4 * hi + r, row = m0 + rl;
+      const bool rok = row < g.M;
+      const size_t rsafe = rok ? row : 0;
+      float v = v4[r];
+      if (g.rownorm) v *= sInv[rl];
+      if (g.colbias && col < g.N)
+        v = g.biasrow ? fmaf(g.biasrow[(size_t)b * g.sR + rsafe], g.colbias[col], v) : v + g.colbias[col];
+      if (g.cde_out) {  // one 16-column tile = one hidden channel (de = 8)
+        const size_t grow = (size_t)b * g.M + rsafe;
+        v *= g.cde_dx[grow * 16 + lo];
+        v += __shfl_xor(v, 8);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 1);
+        if (lo == 0 && rok && j < hch) g.cde_out[grow * hch + j] = g.cde_tg[grow] * v;
+        continue;
+      }
+      if (!rok || col >= g.N) continue;
+      if (g.rowscale) v *= g.rowscale[(size_t)b * g.sR + row];
+      if (g.relu) v = fmaxf(v, 0.f);
+      if (g.accumulate) v += C[(size_t)row * g.ldc + col];
+      C[(size_t)row * g.ldc + col] = v;
+    }
+  }
 }
 
 __global__ void k_fold(int din, int dout, const float* __restrict__ rw, const float* __restrict__ rb,
@@ -193,12 +314,29 @@ __global__ void k_row_inv(int rows, int d, const float* __restrict__ Z, float* _
   float ss = 0.f;
   for (int k = lane; k < d; k += 64) ss = fmaf(z[k], z[k], ss);
   for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
-  if (lane == 0) inv[r] = 1.0f / sqrtf(ss / (float)d + 1e-5f);
+  if (lane == 0) inv[r] = rms_inv(ss, 1.0f / (float)d);
 }
 
 }  // namespace
 
 void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st, bool trans_a) {
+  if (!trans_a && g.N <= 64) {
+    const dim3 gn((g.M + 31) / 32, 1, batch);
+    const int nb = (g.N + 15) / 16;
+#define GNCDE_NARROW(NB)                                                                                 \
+  if (nb == NB) {                                                                                        \
+    if (trans_b)                                                                                         \
+      hipLaunchKernelGGL((k_gemm_narrow<true, NB>), gn, dim3(256), 0, st, g);                            \
+    else                                                                                                 \
+      hipLaunchKernelGGL((k_gemm_narrow<false, NB>), gn, dim3(256), 0, st, g);                           \
+    return;                                                                                              \
+  }
+    GNCDE_NARROW(1)
+    GNCDE_NARROW(2)
+    GNCDE_NARROW(3)
+    GNCDE_NARROW(4)
+#undef GNCDE_NARROW
+  }
   const dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, batch);
   if (trans_a) {
     if (trans_b)

@@ -25,7 +25,9 @@ __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* 
                                                      const float* __restrict__ coef, const float* __restrict__ tcoef,
                                                      const float* __restrict__ t, float* __restrict__ A,
                                                      float* __restrict__ dA, float* __restrict__ tg,
-                                                     float* __restrict__ red, float* __restrict__ part) {
+                                                     float* __restrict__ red, float* __restrict__ part,
+                                                     const float* __restrict__ data_coef, int de2,
+                                                     float* __restrict__ dx) {
   const int b = blockIdx.y, slab = blockIdx.x;
   const int i0 = slab * kSlab;
   const size_t nn = (size_t)n * n;
@@ -90,6 +92,12 @@ __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* 
     const float* tc = tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
     for (int e = tid; e < n; e += blockDim.x) tg[(size_t)b * n + e] = fmaf(f, fmaf(f3, tc[e], 2.0f * tc[n + e]), tc[2 * n + e]);
   }
+  if (dx && slab == 1 % gridDim.x) {  // CDE wrapper: the data spline's derivative dX[i][q] at t (same knots)
+    const size_t blk = (size_t)n * de2;
+    const float* dc = data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk;
+    for (size_t e = tid; e < blk; e += blockDim.x)
+      dx[(size_t)b * blk + e] = fmaf(f, fmaf(f3, dc[e], 2.0f * dc[blk + e]), dc[2 * blk + e]);
+  }
 }
 
 // (I + Abar_l)[b, i, k] for every layer l from one read of the A / dA tiles (32 x 32, the transposed tile staged in
@@ -99,7 +107,8 @@ __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* 
 __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const float* __restrict__ fus,
                                                   const float* __restrict__ A, const float* __restrict__ dA,
                                                   float* __restrict__ red, const float* __restrict__ part,
-                                                  float* __restrict__ out, size_t layer_stride) {
+                                                  float* __restrict__ out, size_t layer_stride,
+                                                  float* __restrict__ qrow, int B) {
   const int b = blockIdx.z;
   const int i0 = blockIdx.y * 32, k0 = blockIdx.x * 32;
   const size_t nn = (size_t)n * n;
@@ -137,6 +146,24 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
   if (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
     rb[6 * n] = s;
     rb[7 * n] = sd;
+  }
+  if (qrow && blockIdx.x == 0 && tid < 32 && i0 + tid < n) {
+    // q_l[i] = sum_k (I + Abar_l)[i][k] from the reductions: the dense terms give their row / column sums, the
+    // w (row) family n copies, the v (column) family sum_k v_k (sum_k r_k = sum_k c_k = s), the diagonal once.
+    const int i = i0 + tid;
+    const float ri = rb[i], rdi = rb[n + i], ci = cs[0][0][tid], cdi = cs[0][1][tid];
+    const float dgi = rb[4 * n + i], dgdi = rb[5 * n + i], fn = (float)n;
+    for (int l = 0; l < L; ++l) {
+      const float* fc = fus + l * GNCDE_FC;
+      float q = fc[GNCDE_FC_E_A] * ri + fc[GNCDE_FC_E_DA] * rdi + fc[GNCDE_FC_ET_A] * ci + fc[GNCDE_FC_ET_DA] * cdi;
+      q += fn * (fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci + fc[GNCDE_FC_WC_DA] * cdi +
+                 fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd);
+      q += (fc[GNCDE_FC_VR_A] + fc[GNCDE_FC_VC_A]) * s + (fc[GNCDE_FC_VR_DA] + fc[GNCDE_FC_VC_DA]) * sd;
+      q += fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dgi + fc[GNCDE_FC_UD_DA] * dgdi + fc[GNCDE_FC_UR_A] * ri +
+           fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci + fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s +
+           fc[GNCDE_FC_US_DA] * sd;
+      qrow[((size_t)l * B + b) * n + i] = q;
+    }
   }
   for (int y = ty; y < 32; y += 8) {
     const int i = i0 + y, k = k0 + tx;
@@ -260,7 +287,7 @@ __global__ void k_grid_stats(int B, int method, const int32_t* __restrict__ nste
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
 struct VfWs {
-  float *A, *dA, *red, *tg, *Z0, *Z1, *m, *abar, *wf, *bf, *inv, *part;
+  float *A, *dA, *red, *tg, *Z0, *Z1, *m, *abar, *wf, *bf, *inv, *part, *q, *dx;
 };
 
 size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
@@ -288,6 +315,8 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.bf = take(bsum);  // bias' = bias + W rms_b per layer
   w.inv = take(B * n);
   w.part = take(B * ((n + kSlab - 1) / kSlab) * 2 * n);
+  w.q = take((size_t)p.L * B * n);                          // q_l = (I + Abar_l) 1
+  w.dx = take(B * n * (size_t)(p.cde_hidden > 0 ? 2 * p.cde_embed : 1));  // data-spline derivative at t
   return off;
 }
 
@@ -304,14 +333,14 @@ size_t generic_vf_workspace(const GncdeProblem& p) {
 size_t vf_forms_scratch(const GncdeProblem& p) { return (size_t)p.B * cdiv(p.n, kSlab) * 2 * p.n; }
 
 void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, float* part,
-              float* abar, hipStream_t st) {
+              float* abar, hipStream_t st, float* qrow, float* dx) {
   const int B = p.B, n = p.n;
   const unsigned slabs = cdiv(n, kSlab);
   hipLaunchKernelGGL(k_spline_slab, dim3(slabs, B), dim3(256), 0, st, n, p.T, p.ts, p.coef, p.tcoef, t, A, dA, tg,
-                     red, part);
+                     red, part, p.data_coef, 2 * p.cde_embed, p.cde_hidden > 0 ? dx : nullptr);
   const unsigned tiles = cdiv(n, 32);
   hipLaunchKernelGGL(k_abar_all, dim3(tiles, tiles, B), dim3(256), 0, st, n, p.L, (int)slabs, p.fusion, A, dA, red,
-                     part, abar, (size_t)B * n * n);
+                     part, abar, (size_t)B * n * n, qrow, B);
 }
 
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
@@ -335,58 +364,104 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   VfWs w;
   carve_vf(p, ws, w);
   if (!prepared) generic_vf_prepare(p, ws, st);
-  vf_forms(p, t, w.A, w.dA, w.tg, w.red, w.part, w.abar, st);
+  vf_forms(p, t, w.A, w.dA, w.tg, w.red, w.part, w.abar, st, w.q, w.dx);
   const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
   const float* Zin = y;
   float* bufs[2] = {w.Z0, w.Z1};
   size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
+    float* Zout = bufs[l & 1];
+    const bool last = l == p.L - 1;
+    // A widening layer (d_out > d_in: the CDE wrapper's h -> h*de*2 read-out layer) is evaluated in the
+    // reassociated order (I + Abar)(diag(inv) Z W'^T + 1 b'^T) = ((I + Abar) diag(inv) Z) W'^T + q b'^T with
+    // q = (I + Abar) 1: the n x n product runs at width d_in instead of d_out (configs 3 / 5: 16x / 16x fewer
+    // flops for that GEMM).  Exact algebra; only the fp32 summation order changes.
+    const bool reassoc = dout > din;
     GemmArgs lin{};
-    lin.M = B * n;
-    lin.N = dout;
-    lin.K = din;
-    lin.A = Zin;
-    lin.lda = din;
-    lin.B = w.wf + wo;
-    lin.ldb = din;
-    lin.C = w.m;
-    lin.ldc = dout;
-    lin.rownorm = 1;
-    lin.colbias = w.bf + bo;
-    gemm(lin, 1, true, st);
+    GemmArgs pr{};
+    float* m = w.m;
+    if (reassoc) {
+      row_inv(B * n, din, Zin, w.inv, st);
+      pr.M = n;
+      pr.N = din;
+      pr.K = n;
+      pr.A = w.abar + (size_t)l * B * nn;
+      pr.lda = n;
+      pr.sA = (long)nn;
+      pr.B = Zin;
+      pr.ldb = din;
+      pr.sB = (long)n * din;
+      pr.kscale = w.inv;
+      pr.sK = n;
+      pr.C = m;
+      pr.ldc = din;
+      pr.sC = (long)n * din;
+      gemm(pr, B, false, st);
+      lin.M = B * n;
+      lin.N = dout;
+      lin.K = din;
+      lin.A = m;
+      lin.lda = din;
+      lin.B = w.wf + wo;
+      lin.ldb = din;
+      lin.C = Zout;
+      lin.ldc = dout;
+      lin.colbias = w.bf + bo;
+      lin.biasrow = w.q + (size_t)l * B * n;
+      lin.relu = last ? 0 : 1;
+      if (last && fused_out) {  // the VF epilogue in the GEMM over all B*n rows
+        if (p.cde_hidden > 0) {
+          lin.cde_out = dy;
+          lin.cde_dx = w.dx;
+          lin.cde_tg = w.tg;
+        } else {
+          lin.C = dy;
+          lin.rowscale = w.tg;
+        }
+      }
+      gemm(lin, 1, true, st);
+    } else {
+      lin.M = B * n;
+      lin.N = dout;
+      lin.K = din;
+      lin.A = Zin;
+      lin.lda = din;
+      lin.B = w.wf + wo;
+      lin.ldb = din;
+      lin.C = m;
+      lin.ldc = dout;
+      lin.rownorm = 1;
+      lin.colbias = w.bf + bo;
+      gemm(lin, 1, true, st);
+      pr.M = n;
+      pr.N = dout;
+      pr.K = n;
+      pr.A = w.abar + (size_t)l * B * nn;
+      pr.lda = n;
+      pr.sA = (long)nn;
+      pr.B = m;
+      pr.ldb = dout;
+      pr.sB = (long)n * dout;
+      pr.C = Zout;
+      pr.ldc = dout;
+      pr.sC = (long)n * dout;
+      pr.relu = last ? 0 : 1;
+      if (last && fused_out) {  // the VF epilogue in the GEMM: ODE dy = tg * Z, CDE contraction (de = 8)
+        if (p.cde_hidden > 0) {
+          pr.cde_out = dy;
+          pr.cde_dx = w.dx;
+          pr.cde_tg = w.tg;
+        } else {
+          pr.C = dy;
+          pr.rowscale = w.tg;
+          pr.sR = n;
+        }
+      }
+      gemm(pr, B, false, st);
+    }
     wo += (size_t)din * dout;
     bo += dout;
-    float* Zout = bufs[l & 1];
-    GemmArgs pr{};
-    pr.M = n;
-    pr.N = dout;
-    pr.K = n;
-    pr.A = w.abar + (size_t)l * B * nn;
-    pr.lda = n;
-    pr.sA = (long)nn;
-    pr.B = w.m;
-    pr.ldb = dout;
-    pr.sB = (long)n * dout;
-    pr.C = Zout;
-    pr.ldc = dout;
-    pr.sC = (long)n * dout;
-    pr.relu = l < p.L - 1 ? 1 : 0;
-    if (l == p.L - 1 && fused_out) {  // the VF epilogue in the GEMM: ODE dy = tg * Z, CDE contraction (de = 8)
-      if (p.cde_hidden > 0) {
-        pr.cde_out = dy;
-        pr.cde_coef = p.data_coef;
-        pr.cde_ts = p.ts;
-        pr.cde_t = t;
-        pr.cde_tg = w.tg;
-        pr.cde_T = p.T;
-      } else {
-        pr.C = dy;
-        pr.rowscale = w.tg;
-        pr.sR = n;
-      }
-    }
-    gemm(pr, B, false, st);
     Zin = Zout;
   }
   if (fused_out) return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;

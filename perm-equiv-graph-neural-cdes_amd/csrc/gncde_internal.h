@@ -130,19 +130,20 @@ struct GemmArgs {
   const float* rowscale;  // optional: C = rowscale[b * sR + r] * acc
   long sR;
   const float* colbias;  // optional [N]
+  const float* biasrow;  // optional with colbias: C += biasrow[b * sR + r] * colbias[c] (rank-1 bias q b'^T)
+  const float* kscale;   // optional (NN only): B row k scaled by kscale[b * sK + k] (a diagonal left of B)
+  long sK;
   int relu;
   int accumulate;  // C += result
   int rownorm;     // (NN/TRANS_B only) scale row r by 1/sqrt(mean_k A[r][k]^2 + 1e-5): RMSNorm folded into the GEMM
   float* inv_out;  // optional with rownorm: those factors, [b * sR + r]
-  // CDE-wrapper epilogue (batched per-sample GEMM, de = 8 so that one 16-column MFMA tile is one hidden channel):
-  // instead of C, write cde_out[b][r][c/16] = cde_tg[b][r] * sum_{q<16} C[r][c+q] * dX_b[r][q], with dX the
-  // data spline's derivative at the sample's stage time (cde_wrapper_vector_field.py:19-26)
+  // CDE-wrapper epilogue (de = 8 so that one 16-column MFMA tile is one hidden channel): instead of C, write
+  // cde_out[b*M + r][c/16] = cde_tg[b*M + r] * sum_{q<16} C[r][c+q] * cde_dx[b*M + r][q], with dX the data
+  // spline's derivative at the row's stage time (cde_wrapper_vector_field.py:19-26).  Rows are global node
+  // rows, so the same epilogue serves a per-sample batched GEMM (M = n) and one GEMM over all B*n rows.
   float* cde_out;
-  const float* cde_coef;  // [B, T-1, 4, M, 8, 2]
-  const float* cde_ts;    // [B, T]
-  const float* cde_t;     // [B]
-  const float* cde_tg;    // [B, M]
-  int cde_T;
+  const float* cde_dx;  // [rows, 16]
+  const float* cde_tg;  // [rows]
 };
 // TRANS_A: A[b] + k * lda + r (A^T stored row-major)
 void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st, bool trans_a = false);
@@ -157,8 +158,10 @@ size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s);
 // part: scratch of vf_forms_scratch(p) floats (per-slab column partials)
 size_t vf_forms_scratch(const GncdeProblem& p);
 // ... and (I + Abar_l) of every layer into abar [L, B, n, n] (red: stride 8 n per sample, completed here too)
+// qrow (optional, [L, B, n]) receives q_l = (I + Abar_l) 1 (the row sums, from the reductions); dx (optional, CDE
+// wrapper, [B, n, 2 de]) the data spline's derivative at t.
 void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, float* part,
-              float* abar, hipStream_t st);
+              float* abar, hipStream_t st, float* qrow = nullptr, float* dx = nullptr);
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st);
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared = false);
