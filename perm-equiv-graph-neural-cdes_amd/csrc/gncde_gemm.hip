@@ -168,6 +168,16 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
       }
 }
 
+// Four consecutive K values p[0..3] of one row (the lane's 4 MFMA K steps of a 16-chunk): one dwordx4 when the row
+// is 16-byte aligned and the chunk is inside K, else four guarded scalars.
+__device__ __forceinline__ floatx4 load_k4(const float* p, bool vec, int k, int K) {
+  if (vec) return *reinterpret_cast<const floatx4*>(p);
+  floatx4 v;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) v[s] = k + s < K ? p[s] : 0.f;
+  return v;
+}
+
 // ---- narrow GEMM (N <= 64): 32-row blocks, K split over the 4 waves ---------------------------------------
 // The n x n products of the narrow layers (N = d <= 64, K = n = 129 / 255) and the Linears of width <= 64 are
 // latency-bound on the 64x64 kernel: few workgroups and a serial K loop of one HBM round trip per 32-chunk.
@@ -191,25 +201,32 @@ __global__ void __launch_bounds__(256) k_gemm_narrow(GemmArgs g) {
     for (int j = 0; j < NB; ++j) acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   float ss[2] = {0.f, 0.f};  // rownorm: this lane's share of sum_k A[row][k]^2
   const int rowA0 = m0 + lo, rowA1 = m0 + 16 + lo;
+  const bool avec = ((g.lda | g.sA) & 3) == 0 && ((uintptr_t)g.A & 15) == 0;
+  const bool bvec = TRANS_B && ((g.ldb | g.sB) & 3) == 0 && ((uintptr_t)g.B & 15) == 0;
   for (int kr = 0; kr < g.K; kr += 4 * 16 * CPW) {
-    float av[CPW][2][4], bv[CPW][4][NB];
+    floatx4 av[CPW][2], bv[CPW][NB];
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
-      const int k0 = kr + 16 * (w + 4 * c);
+      const int k = kr + 16 * (w + 4 * c) + 4 * hi;  // this lane's K steps k .. k+3 of chunk c
+      const bool kfull = k + 4 <= g.K;
+      av[c][0] = rowA0 < g.M ? load_k4(A + (size_t)rowA0 * g.lda + k, avec && kfull, k, g.K) : floatx4{0.f, 0.f, 0.f, 0.f};
+      av[c][1] = rowA1 < g.M ? load_k4(A + (size_t)rowA1 * g.lda + k, avec && kfull, k, g.K) : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int k = k0 + 4 * s4 + hi;
-        const bool kin = k < g.K;
-        av[c][0][s4] = (kin && rowA0 < g.M) ? A[(size_t)rowA0 * g.lda + k] : 0.f;
-        av[c][1][s4] = (kin && rowA1 < g.M) ? A[(size_t)rowA1 * g.lda + k] : 0.f;
-        const float ks = (g.kscale && kin) ? g.kscale[(size_t)b * g.sK + k] : 1.0f;
+      for (int j = 0; j < NB; ++j) {
+        const int col = 16 * j + lo;
+        floatx4 v = {0.f, 0.f, 0.f, 0.f};
+        if (col < g.N) {
+          if (TRANS_B) {
+            v = load_k4(B + (size_t)col * g.ldb + k, bvec && kfull, k, g.K);
+          } else {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          const int col = 16 * j + lo;
-          float v = 0.f;
-          if (kin && col < g.N) v = TRANS_B ? B[(size_t)col * g.ldb + k] : B[(size_t)k * g.ldb + col];
-          bv[c][s4][j] = v * ks;
+            for (int s4 = 0; s4 < 4; ++s4) v[s4] = k + s4 < g.K ? B[(size_t)(k + s4) * g.ldb + col] : 0.f;
+          }
         }
+        if (g.kscale)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) v[s4] *= k + s4 < g.K ? g.kscale[(size_t)b * g.sK + k + s4] : 0.f;
+        bv[c][j] = v;
       }
     }
 #pragma unroll
@@ -224,7 +241,7 @@ __global__ void __launch_bounds__(256) k_gemm_narrow(GemmArgs g) {
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int j = 0; j < NB; ++j)
-            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][t][s4], bv[c][s4][j], acc[t][j], 0, 0, 0);
+            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][t][s4], bv[c][j][s4], acc[t][j], 0, 0, 0);
       }
   }
   // fixed-order reduction of the four wave partials; wave w then finishes tiles (t, j) with (t * NB + j) % 4 == w
