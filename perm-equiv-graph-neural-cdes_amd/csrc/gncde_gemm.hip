@@ -183,8 +183,9 @@ __device__ __forceinline__ floatx4 load_k4(const float* p, bool vec, int k, int 
 // latency-bound on the 64x64 kernel: few workgroups and a serial K loop of one HBM round trip per 32-chunk.
 // Here a workgroup owns 32 rows x N columns; wave w takes the 16-wide K chunks w, w+4, ... and issues every load
 // of its round (up to 4 chunks = 64 K per wave, 256 per workgroup) before the first MFMA, straight into the MFMA
-// operand layout (MFMA step s of a chunk at k0: lane (lo, hi) holds A[row lo][k0 + 4s + hi] and
-// B[k0 + 4s + hi][col lo]; no LDS staging).  The four K partials meet once in LDS, summed in a fixed order.
+// operand layout (MFMA step s of a chunk at k0: lane (lo, hi) holds A[row lo][k0 + 4hi + s] and
+// B[k0 + 4hi + s][col lo], so a lane's four steps are one dwordx4 of an A row; no LDS staging).  The four K
+// partials meet once in LDS, summed in a fixed order.
 template <bool TRANS_B, int NB>
 __global__ void __launch_bounds__(256) k_gemm_narrow(GemmArgs g) {
   constexpr int CPW = 4;  // chunks (16 K) per wave per round
