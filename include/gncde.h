@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GNCDE_ABI_VERSION 1
+#define GNCDE_ABI_VERSION 2
 #define GNCDE_MAX_LAYERS 8
 #define GNCDE_FC 24
 
@@ -86,6 +86,17 @@ enum {
 };
 
 enum { GNCDE_RK4 = 0, GNCDE_TSIT5 = 1 };
+/* Arithmetic of the n x n stream (BASELINE config 5, "bf16 MFMA path").
+ *   FP32:         everything fp32 (the reference's arithmetic).
+ *   BF16:         the n x n products (I + Abar_l) Z run on v_mfma_f32_16x16x32_bf16 with both operands split into
+ *                 bf16 (hi, lo) pairs (three products, fp32 accumulation, ~2^-16 relative: fp32-class results and
+ *                 no rounding noise for the adaptive controller).  Inputs stay fp32.
+ *   BF16_STORAGE: as BF16, and `coef` holds bfloat16 values (same shape, uint16 storage): the operator spline's
+ *                 input is quantised to bf16, halving the dominant HBM stream.  Results equal the fp32 reference
+ *                 evaluated on the bf16-rounded coefficients.
+ * Splines, reductions, the Linears, solver and epilogues stay fp32.  The bf16 modes are forward only (the reverse
+ * entry points return GNCDE_ERR_UNSUPPORTED) and always take the generic path. */
+enum { GNCDE_COMPUTE_FP32 = 0, GNCDE_COMPUTE_BF16 = 1, GNCDE_COMPUTE_BF16_STORAGE = 2 };
 enum { GNCDE_CTRL_GRID = 0, GNCDE_CTRL_PID = 1 };
 enum { GNCDE_SAVE_T1 = 0, GNCDE_SAVE_STEPS = 1, GNCDE_SAVE_TS = 2 };
 /* stats[b*4 + k]: k=0 accepted steps, 1 rejected steps, 2 vector-field evaluations, 3 status
@@ -106,6 +117,7 @@ typedef struct GncdeProblem {
   const float* data_coef;
   const float* fusion;
   const float* params;
+  int32_t compute;                   /* GNCDE_COMPUTE_* (above) */
 } GncdeProblem;
 
 typedef struct GncdeSolver {

@@ -16,6 +16,7 @@ int validate_problem(const GncdeProblem* p) {
   for (int l = 0; l <= p->L; ++l)
     if (p->dims[l] <= 0) return GNCDE_ERR_SHAPE;
   if (!p->ts || !p->coef || !p->tcoef || !p->fusion || !p->params) return GNCDE_ERR_ARG;
+  if (p->compute < GNCDE_COMPUTE_FP32 || p->compute > GNCDE_COMPUTE_BF16_STORAGE) return GNCDE_ERR_ARG;
   if (p->cde_hidden > 0) {
     if (p->cde_embed <= 0 || !p->data_coef) return GNCDE_ERR_ARG;
     if (p->dims[p->L] != p->cde_hidden * p->cde_embed * 2) return GNCDE_ERR_SHAPE;
@@ -78,7 +79,8 @@ int gncde_integrate_path(const GncdeProblem* prob, const GncdeSolver* solver, ch
   rc = validate_solver(prob, solver);
   if (rc) return rc;
   if (!buf || buf_len == 0) return GNCDE_ERR_ARG;
-  if (!fused_supported(*prob, *solver, buf, buf_len)) snprintf(buf, buf_len, "generic");
+  if (!fused_supported(*prob, *solver, buf, buf_len))
+    snprintf(buf, buf_len, prob->compute != GNCDE_COMPUTE_FP32 ? "generic_bf16" : "generic");
   return GNCDE_OK;
 }
 
@@ -109,6 +111,7 @@ int gncde_integrate(const GncdeProblem* prob, const GncdeSolver* solver, const f
 
 size_t gncde_vjp_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* solver) {
   if (validate_problem(prob) != GNCDE_OK || validate_solver(prob, solver) != GNCDE_OK) return 0;
+  if (prob->compute != GNCDE_COMPUTE_FP32) return 0;
   if (stage_vjp_supported(*prob, *solver)) return stage_vjp_workspace(*prob);
   return generic_vjp_workspace(*prob, *solver);
 }
@@ -122,6 +125,7 @@ static int integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, co
   rc = validate_solver(prob, solver);
   if (rc) return rc;
   if (solver->controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
+  if (prob->compute != GNCDE_COMPUTE_FP32) return GNCDE_ERR_UNSUPPORTED;  // the bf16 path is forward-only
   if (solver->save_mode != GNCDE_SAVE_T1 && solver->save_mode != GNCDE_SAVE_STEPS) return GNCDE_ERR_UNSUPPORTED;
   if (!gparams || !gfusion) return GNCDE_ERR_ARG;
   if (gdata && prob->cde_hidden <= 0) return GNCDE_ERR_ARG;  // only the CDE wrapper reads a data spline

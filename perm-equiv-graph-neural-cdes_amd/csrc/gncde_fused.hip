@@ -764,7 +764,7 @@ const FusedEntry kFused[] = {
 };
 
 const FusedEntry* find_fused(const GncdeProblem& p, const GncdeSolver& s) {
-  if (p.cde_hidden != 0) return nullptr;
+  if (p.cde_hidden != 0 || p.compute != GNCDE_COMPUTE_FP32) return nullptr;
   int method = s.method;
   if (s.controller == GNCDE_CTRL_GRID) {
     if (s.save_mode != GNCDE_SAVE_T1 && s.save_mode != GNCDE_SAVE_STEPS) return nullptr;

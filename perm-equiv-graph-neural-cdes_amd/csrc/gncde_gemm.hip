@@ -178,6 +178,76 @@ __device__ __forceinline__ floatx4 load_k4(const float* p, bool vec, int k, int 
   return v;
 }
 
+// Fixed-order reduction of the four waves' K partials of a 32-row x 16*NB-column block, then the GEMM epilogue;
+// wave w finishes tiles (t, j) with (t * NB + j) % 4 == w.  ss: per-lane rownorm partials (row lo of each t).
+template <int NB>
+__device__ __forceinline__ void finish_split_k(const GemmArgs& g, const floatx4 (&acc)[2][NB], const float (&ss)[2],
+                                               int b, int m0, int n0, int w, int lane) {
+  const int tid = threadIdx.x, lo = lane & 15, hi = lane >> 4;
+  float* C = g.C + (size_t)b * g.sC;
+  __shared__ floatx4 red[4][2 * NB][64];
+  __shared__ float sInv[32];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) red[w][t * NB + j][lane] = acc[t][j];
+  if (g.rownorm) {
+    __shared__ float sSS[4][2][64];
+    sSS[w][0][lane] = ss[0];
+    sSS[w][1][lane] = ss[1];
+    __syncthreads();
+    if (tid < 32) {  // row tid: its 4 lanes (hi) of each of the 4 waves
+      const int t = tid >> 4, l16 = tid & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww)
+#pragma unroll
+        for (int h4 = 0; h4 < 4; ++h4) v += sSS[ww][t][l16 + 16 * h4];
+      const float iv = rms_inv(v, 1.0f / (float)g.K);
+      sInv[tid] = iv;
+      if (g.inv_out && n0 == 0 && m0 + tid < g.M) g.inv_out[(size_t)b * g.sR + m0 + tid] = iv;
+    }
+  }
+  __syncthreads();
+  const int hch = g.N / 16;
+  for (int tile = w; tile < 2 * NB; tile += 4) {
+    const int t = tile / NB, j = tile % NB;
+    floatx4 v4 = red[0][tile][lane];
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) {
+      const floatx4 o = red[ww][tile][lane];
+      v4 = floatx4{v4[0] + o[0], v4[1] + o[1], v4[2] + o[2], v4[3] + o[3]};
+    }
+    const int col = n0 + 16 * j + lo;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = 16 * t + 4 * hi + r, row = m0 + rl;
+      const bool rok = row < g.M;
+      const size_t rsafe = rok ? row : 0;
+      float v = v4[r];
+      if (g.rownorm) v *= sInv[rl];
+      if (g.colbias && col < g.N)
+        v = g.biasrow ? fmaf(g.biasrow[(size_t)b * g.sR + rsafe], g.colbias[col], v) : v + g.colbias[col];
+      if (g.cde_out) {  // one 16-column tile = one hidden channel (de = 8)
+        const size_t grow = (size_t)b * g.M + rsafe;
+        v *= g.cde_dx[grow * 16 + lo];
+        v += __shfl_xor(v, 8);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 1);
+        const int ch = (n0 + 16 * j) / 16;
+        if (lo == 0 && rok && ch < hch) g.cde_out[grow * hch + ch] = g.cde_tg[grow] * v;
+        continue;
+      }
+      if (!rok || col >= g.N) continue;
+      if (g.rowscale) v *= g.rowscale[(size_t)b * g.sR + row];
+      if (g.relu) v = fmaxf(v, 0.f);
+      if (g.accumulate) v += C[(size_t)row * g.ldc + col];
+      C[(size_t)row * g.ldc + col] = v;
+    }
+  }
+}
+
 // ---- narrow GEMM (N <= 64): 32-row blocks, K split over the 4 waves ---------------------------------------
 // The n x n products of the narrow layers (N = d <= 64, K = n = 129 / 255) and the Linears of width <= 64 are
 // latency-bound on the 64x64 kernel: few workgroups and a serial K loop of one HBM round trip per 32-chunk.
@@ -193,7 +263,6 @@ __global__ void __launch_bounds__(256) k_gemm_narrow(GemmArgs g) {
   const int m0 = blockIdx.x * 32;
   const float* A = g.A + (size_t)b * g.sA;
   const float* B = g.B + (size_t)b * g.sB;
-  float* C = g.C + (size_t)b * g.sC;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   floatx4 acc[2][NB];
 #pragma unroll
@@ -245,67 +314,94 @@ __global__ void __launch_bounds__(256) k_gemm_narrow(GemmArgs g) {
             acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c][t][s4], bv[c][j][s4], acc[t][j], 0, 0, 0);
       }
   }
-  // fixed-order reduction of the four wave partials; wave w then finishes tiles (t, j) with (t * NB + j) % 4 == w
-  __shared__ floatx4 red[4][2 * NB][64];
-  __shared__ float sInv[32];
+  finish_split_k<NB>(g, acc, ss, b, m0, 0, w, lane);
+}
+
+// ---- bf16 n x n products (GNCDE_COMPUTE_BF16*): C = A B on v_mfma_f32_16x16x32_bf16 -------------------------
+// A = (I + Abar) as bf16 (hi, lo) planes, B = the fp32 state split on load into hi = rne(x), lo = rne(x - hi);
+// C accumulates Ahi Bhi + Ahi Blo + Alo Bhi in fp32 (the dropped lo*lo term and the split residuals are ~2^-16
+// relative: the adaptive controller's error estimate does not see bf16 rounding noise).  Same split-K
+// organisation as the narrow kernel: a 32-deep chunk is one MFMA step per product, lane (lo, hi) holding
+// A[row lo][k0 + 8hi .. +7] (one 16-byte load per plane) and B[k0 + 8hi .. +7][col lo]; grid.y walks 16*NB-column
+// blocks so any N works.  fp32 epilogue.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ bf16x8 load_a8(const uint16_t* pa, bool vec, int k, int K) {
+  uint4 raw;
+  if (vec) {
+    raw = *reinterpret_cast<const uint4*>(pa);
+  } else {
+    uint16_t e[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) e[q] = k + q < K ? pa[q] : (uint16_t)0;
+    raw = uint4{e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16), e[4] | ((uint32_t)e[5] << 16),
+                e[6] | ((uint32_t)e[7] << 16)};
+  }
+  return __builtin_bit_cast(bf16x8, raw);
+}
+
+template <int NB>
+__global__ void __launch_bounds__(256) k_gemm_bf16(GemmArgs g) {
+  constexpr int CPW = 2;  // 32-deep chunks per wave per round
+  const int b = blockIdx.z;
+  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 16 * NB;
+  const uint16_t* A = reinterpret_cast<const uint16_t*>(g.A) + (size_t)b * g.sA;
+  const float* B = g.B + (size_t)b * g.sB;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
+  floatx4 acc[2][NB];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int j = 0; j < NB; ++j) red[w][t * NB + j][lane] = acc[t][j];
-  if (g.rownorm) {
-    __shared__ float sSS[4][2][64];
-    sSS[w][0][lane] = ss[0];
-    sSS[w][1][lane] = ss[1];
-    __syncthreads();
-    if (tid < 32) {  // row tid: its 4 lanes (hi) of each of the 4 waves
-      const int t = tid >> 4, l16 = tid & 15;
-      float v = 0.f;
+    for (int j = 0; j < NB; ++j) acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const bool avec = ((g.lda | g.sA | g.a_lo) & 7) == 0 && ((uintptr_t)g.A & 15) == 0;
+  for (int kr = 0; kr < g.K; kr += 4 * 32 * CPW) {
+    bf16x8 ah[CPW][2], al[CPW][2], bh[CPW][NB], bl[CPW][NB];
 #pragma unroll
-      for (int ww = 0; ww < 4; ++ww)
+    for (int c = 0; c < CPW; ++c) {
+      const int k = kr + 32 * (w + 4 * c) + 8 * hi;  // this lane's 8 K values
+      const bool vec = avec && k + 8 <= g.K;
 #pragma unroll
-        for (int h4 = 0; h4 < 4; ++h4) v += sSS[ww][t][l16 + 16 * h4];
-      const float iv = rms_inv(v, 1.0f / (float)g.K);
-      sInv[tid] = iv;
-      if (g.inv_out && m0 + tid < g.M) g.inv_out[(size_t)b * g.sR + m0 + tid] = iv;
-    }
-  }
-  __syncthreads();
-  const int hch = g.N / 16;
-  for (int tile = w; tile < 2 * NB; tile += 4) {
-    const int t = tile / NB, j = tile % NB;
-    floatx4 v4 = red[0][tile][lane];
-#pragma unroll
-    for (int ww = 1; ww < 4; ++ww) {
-      const floatx4 o = red[ww][tile][lane];
-      v4 = floatx4{v4[0] + o[0], v4[1] + o[1], v4[2] + o[2], v4[3] + o[3]};
-    }
-    const int col = 16 * j + lo;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rl = 16 * t + 4 * hi + r, row = m0 + rl;
-      const bool rok = row < g.M;
-      const size_t rsafe = rok ? row : 0;
-      float v = v4[r];
-      if (g.rownorm) v *= sInv[rl];
-      if (g.colbias && col < g.N)
-        v = g.biasrow ? fmaf(g.biasrow[(size_t)b * g.sR + rsafe], g.colbias[col], v) : v + g.colbias[col];
-      if (g.cde_out) {  // one 16-column tile = one hidden channel (de = 8)
-        const size_t grow = (size_t)b * g.M + rsafe;
-        v *= g.cde_dx[grow * 16 + lo];
-        v += __shfl_xor(v, 8);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 1);
-        if (lo == 0 && rok && j < hch) g.cde_out[grow * hch + j] = g.cde_tg[grow] * v;
-        continue;
+      for (int t = 0; t < 2; ++t) {
+        const int row = m0 + 16 * t + lo;
+        if (row < g.M) {
+          const uint16_t* pa = A + (size_t)row * g.lda + k;
+          ah[c][t] = load_a8(pa, vec, k, g.K);
+          al[c][t] = load_a8(pa + g.a_lo, vec, k, g.K);
+        } else {
+          ah[c][t] = al[c][t] = __builtin_bit_cast(bf16x8, uint4{0u, 0u, 0u, 0u});
+        }
       }
-      if (!rok || col >= g.N) continue;
-      if (g.rowscale) v *= g.rowscale[(size_t)b * g.sR + row];
-      if (g.relu) v = fmaxf(v, 0.f);
-      if (g.accumulate) v += C[(size_t)row * g.ldc + col];
-      C[(size_t)row * g.ldc + col] = v;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int col = n0 + 16 * j + lo;
+        bf16x8 vh, vl;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float x = 0.f;
+          if (k + q < g.K && col < g.N) {
+            x = B[(size_t)(k + q) * g.ldb + col];
+            if (g.kscale) x *= g.kscale[(size_t)b * g.sK + k + q];
+          }
+          vh[q] = (__bf16)x;
+          vl[q] = (__bf16)(x - (float)vh[q]);
+        }
+        bh[c][j] = vh;
+        bl[c][j] = vl;
+      }
     }
+#pragma unroll
+    for (int c = 0; c < CPW; ++c)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[c][t], bh[c][j], acc[t][j], 0, 0, 0);
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[c][t], bl[c][j], acc[t][j], 0, 0, 0);
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[c][t], bh[c][j], acc[t][j], 0, 0, 0);
+        }
   }
+  const float ss[2] = {0.f, 0.f};
+  finish_split_k<NB>(g, acc, ss, b, m0, n0, w, lane);
 }
 
 __global__ void k_fold(int din, int dout, const float* __restrict__ rw, const float* __restrict__ rb,
@@ -338,6 +434,17 @@ __global__ void k_row_inv(int rows, int d, const float* __restrict__ Z, float* _
 }  // namespace
 
 void gemm(const GemmArgs& g, int batch, bool trans_b, hipStream_t st, bool trans_a) {
+  if (g.a_bf16) {  // (I + Abar) in bf16 times the fp32 state: NN only
+    const int nb = g.N <= 16 ? 1 : (g.N <= 32 ? 2 : 4);
+    const dim3 gb((g.M + 31) / 32, (g.N + 16 * nb - 1) / (16 * nb), batch);
+    if (nb == 1)
+      hipLaunchKernelGGL((k_gemm_bf16<1>), gb, dim3(256), 0, st, g);
+    else if (nb == 2)
+      hipLaunchKernelGGL((k_gemm_bf16<2>), gb, dim3(256), 0, st, g);
+    else
+      hipLaunchKernelGGL((k_gemm_bf16<4>), gb, dim3(256), 0, st, g);
+    return;
+  }
   if (!trans_a && g.N <= 64) {
     const dim3 gn((g.M + 31) / 32, 1, batch);
     const int nb = (g.N + 15) / 16;

@@ -21,8 +21,15 @@ constexpr int kRedStride = 8;  // red[b][q][n]: r, rd, c, cd, diagA, diagdA, {s}
 // go to part[b][slab][2][n]; k_abar_all sums them over slabs (fixed order) and forms the totals.
 constexpr int kSlab = 16;
 
+// Coefficient storage: fp32, or bf16 (GNCDE_COMPUTE_BF16_STORAGE) widened on load.
+__device__ __forceinline__ float coef_at(const float* c, size_t e) { return c[e]; }
+__device__ __forceinline__ float coef_at(const uint16_t* c, size_t e) {
+  return __builtin_bit_cast(float, (uint32_t)c[e] << 16);
+}
+
+template <typename CT>
 __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* __restrict__ ts,
-                                                     const float* __restrict__ coef, const float* __restrict__ tcoef,
+                                                     const CT* __restrict__ coef, const float* __restrict__ tcoef,
                                                      const float* __restrict__ t, float* __restrict__ A,
                                                      float* __restrict__ dA, float* __restrict__ tg,
                                                      float* __restrict__ red, float* __restrict__ part,
@@ -36,7 +43,7 @@ __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* 
   const int idx = interval_index(tsb, T, tb);
   const float f = tb - tsb[idx];
   const float f3 = 3.0f * f;
-  const float* cb = coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
+  const CT* cb = coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
   float* Ab = A + (size_t)b * nn;
   float* dAb = dA + (size_t)b * nn;
   float* rb = red + (size_t)b * kRedStride * n;
@@ -51,7 +58,7 @@ __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* 
     for (int r = 0; r < kSlab; ++r) {
       if (r < rows) {
         const size_t e = (size_t)(i0 + r) * n + k;
-        const float d = cb[e], c = cb[nn + e], bb = cb[2 * nn + e], a = cb[3 * nn + e];
+        const float d = coef_at(cb, e), c = coef_at(cb, nn + e), bb = coef_at(cb, 2 * nn + e), a = coef_at(cb, 3 * nn + e);
         const float va = fmaf(f, fmaf(f, fmaf(f, d, c), bb), a);
         const float vd = fmaf(f, fmaf(f3, d, 2.0f * c), bb);
         Ab[e] = va;
@@ -104,10 +111,20 @@ __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* 
 // LDS so both A[i][k] and A[k][i] are read coalesced).  The block also finishes the reductions it needs: column sums
 // of its i and k ranges from k_spline_slab's slab partials (fixed order) and the totals; blocks on the first tile
 // row / the first tile publish the column sums / totals into red (the reverse sweep reads them later).
+__device__ __forceinline__ void abar_store(float* o, size_t e, size_t, float v) { o[e] = v; }
+// bf16 pair: hi = rne(v) in the first plane, lo = rne(v - hi) in the second (planes `plane` elements apart);
+// hi + lo carries 16 significand bits, so the split products lose ~2^-16, far below the PID tolerances.
+__device__ __forceinline__ void abar_store(uint16_t* o, size_t e, size_t plane, float v) {
+  const __bf16 h = (__bf16)v;
+  o[e] = __builtin_bit_cast(uint16_t, h);
+  o[plane + e] = __builtin_bit_cast(uint16_t, (__bf16)(v - (float)h));
+}
+
+template <typename OT>
 __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const float* __restrict__ fus,
                                                   const float* __restrict__ A, const float* __restrict__ dA,
                                                   float* __restrict__ red, const float* __restrict__ part,
-                                                  float* __restrict__ out, size_t layer_stride,
+                                                  OT* __restrict__ out, size_t layer_stride,
                                                   float* __restrict__ qrow, int B) {
   const int b = blockIdx.z;
   const int i0 = blockIdx.y * 32, k0 = blockIdx.x * 32;
@@ -184,7 +201,7 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
         v += fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dgi + fc[GNCDE_FC_UD_DA] * dgdi + fc[GNCDE_FC_UR_A] * ri +
              fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci + fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s +
              fc[GNCDE_FC_US_DA] * sd;
-      out[l * layer_stride + b * nn + (size_t)i * n + k] = v;
+      abar_store(out, l * layer_stride + b * nn + (size_t)i * n + k, (size_t)L * layer_stride, v);
     }
   }
 }
@@ -286,6 +303,14 @@ __global__ void k_grid_stats(int B, int method, const int32_t* __restrict__ nste
 
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
+// (I + Abar_l) of layer l: [B, n, n] fp32, or the hi plane of its bf16 (hi, lo) pair (bf16 modes: planes
+// [L, B, n, n] of uint16 each, the lo plane L*B*n*n elements after the hi plane — the fp32 buffer's bytes)
+inline const float* abar_layer(const GncdeProblem& p, const float* abar, int l) {
+  const size_t off = (size_t)l * p.B * p.n * p.n;
+  if (p.compute != GNCDE_COMPUTE_FP32) return reinterpret_cast<const float*>(reinterpret_cast<const uint16_t*>(abar) + off);
+  return abar + off;
+}
+
 struct VfWs {
   float *A, *dA, *red, *tg, *Z0, *Z1, *m, *abar, *wf, *bf, *inv, *part, *q, *dx;
 };
@@ -336,11 +361,22 @@ void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float*
               float* abar, hipStream_t st, float* qrow, float* dx) {
   const int B = p.B, n = p.n;
   const unsigned slabs = cdiv(n, kSlab);
-  hipLaunchKernelGGL(k_spline_slab, dim3(slabs, B), dim3(256), 0, st, n, p.T, p.ts, p.coef, p.tcoef, t, A, dA, tg,
-                     red, part, p.data_coef, 2 * p.cde_embed, p.cde_hidden > 0 ? dx : nullptr);
+  const bool bf16 = p.compute != GNCDE_COMPUTE_FP32;
+  float* dxo = p.cde_hidden > 0 ? dx : nullptr;
+  if (p.compute == GNCDE_COMPUTE_BF16_STORAGE)
+    hipLaunchKernelGGL(k_spline_slab<uint16_t>, dim3(slabs, B), dim3(256), 0, st, n, p.T, p.ts,
+                       reinterpret_cast<const uint16_t*>(p.coef), p.tcoef, t, A, dA, tg, red, part, p.data_coef,
+                       2 * p.cde_embed, dxo);
+  else
+    hipLaunchKernelGGL(k_spline_slab<float>, dim3(slabs, B), dim3(256), 0, st, n, p.T, p.ts, p.coef, p.tcoef, t, A,
+                       dA, tg, red, part, p.data_coef, 2 * p.cde_embed, dxo);
   const unsigned tiles = cdiv(n, 32);
-  hipLaunchKernelGGL(k_abar_all, dim3(tiles, tiles, B), dim3(256), 0, st, n, p.L, (int)slabs, p.fusion, A, dA, red,
-                     part, abar, (size_t)B * n * n, qrow, B);
+  if (bf16)
+    hipLaunchKernelGGL(k_abar_all<uint16_t>, dim3(tiles, tiles, B), dim3(256), 0, st, n, p.L, (int)slabs, p.fusion,
+                       A, dA, red, part, reinterpret_cast<uint16_t*>(abar), (size_t)B * n * n, qrow, B);
+  else
+    hipLaunchKernelGGL(k_abar_all<float>, dim3(tiles, tiles, B), dim3(256), 0, st, n, p.L, (int)slabs, p.fusion, A,
+                       dA, red, part, abar, (size_t)B * n * n, qrow, B);
 }
 
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
@@ -386,7 +422,9 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
       pr.M = n;
       pr.N = din;
       pr.K = n;
-      pr.A = w.abar + (size_t)l * B * nn;
+      pr.A = abar_layer(p, w.abar, l);
+      pr.a_bf16 = p.compute != GNCDE_COMPUTE_FP32;
+      pr.a_lo = (long)p.L * B * nn;
       pr.lda = n;
       pr.sA = (long)nn;
       pr.B = Zin;
@@ -437,7 +475,9 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
       pr.M = n;
       pr.N = dout;
       pr.K = n;
-      pr.A = w.abar + (size_t)l * B * nn;
+      pr.A = abar_layer(p, w.abar, l);
+      pr.a_bf16 = p.compute != GNCDE_COMPUTE_FP32;
+      pr.a_lo = (long)p.L * B * nn;
       pr.lda = n;
       pr.sA = (long)nn;
       pr.B = m;

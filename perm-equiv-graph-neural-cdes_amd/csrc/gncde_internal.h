@@ -133,6 +133,8 @@ struct GemmArgs {
   const float* biasrow;  // optional with colbias: C += biasrow[b * sR + r] * colbias[c] (rank-1 bias q b'^T)
   const float* kscale;   // optional (NN only): B row k scaled by kscale[b * sK + k] (a diagonal left of B)
   long sK;
+  int a_bf16;      // (NN only) A holds bf16 (hi, lo) pairs: hi at the element offsets of A, lo a_lo elements later
+  long a_lo;
   int relu;
   int accumulate;  // C += result
   int rownorm;     // (NN/TRANS_B only) scale row r by 1/sqrt(mean_k A[r][k]^2 + 1e-5): RMSNorm folded into the GEMM

@@ -12,11 +12,12 @@ from ctypes import POINTER, c_char_p, c_float, c_int32, c_size_t, c_void_p
 
 MAX_LAYERS = 8
 FC = 24
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 RK4, TSIT5 = 0, 1
 CTRL_GRID, CTRL_PID = 0, 1
 SAVE_T1, SAVE_STEPS, SAVE_TS = 0, 1, 2
+COMPUTE_FP32, COMPUTE_BF16, COMPUTE_BF16_STORAGE = 0, 1, 2  # GncdeProblem.compute (gncde.h)
 STAT_STEPS, STAT_REJECTS, STAT_EVALS, STAT_STATUS = 0, 1, 2, 3
 OP_NORM_LAP, OP_NORM_ADJ, OP_KIPF, OP_NORMALIZED_PLUS = 0, 1, 2, 3
 
@@ -60,6 +61,7 @@ class GncdeProblem(ctypes.Structure):
         ("data_coef", c_void_p),
         ("fusion", c_void_p),
         ("params", c_void_p),
+        ("compute", c_int32),
     ]
 
 

@@ -42,6 +42,7 @@ class Problem:
     data_coef: torch.Tensor | None = None  # [B, T-1, 4, n, de, 2]
     cde_hidden: int = 0
     cde_embed: int = 0
+    compute: int = _lib.COMPUTE_FP32  # COMPUTE_BF16(_STORAGE): the generic bf16 MFMA path (forward only)
     _keep: list = field(default_factory=list)
 
     @property
@@ -63,8 +64,9 @@ class Problem:
     def c_struct(self) -> _lib.GncdeProblem:
         for name in ("ts", "coef", "tcoef", "fusion", "params"):
             t = getattr(self, name)
-            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
-                raise _lib.GncdeError(f"Problem.{name} must be a contiguous float32 CUDA tensor")
+            want = torch.bfloat16 if (name == "coef" and self.compute == _lib.COMPUTE_BF16_STORAGE) else torch.float32
+            if not (t.is_cuda and t.dtype == want and t.is_contiguous()):
+                raise _lib.GncdeError(f"Problem.{name} must be a contiguous {want} CUDA tensor")
         if len(self.dims) - 1 > _lib.MAX_LAYERS:
             raise _lib.GncdeError("too many layers")
         s = _lib.GncdeProblem()
@@ -75,6 +77,7 @@ class Problem:
         s.ts, s.coef, s.tcoef = _ptr(self.ts).value, _ptr(self.coef).value, _ptr(self.tcoef).value
         s.data_coef = _ptr(self.data_coef).value if self.data_coef is not None else None
         s.fusion, s.params = _ptr(self.fusion).value, _ptr(self.params).value
+        s.compute = int(self.compute)
         return s
 
     def shard(self, start: int, stop: int) -> "Problem":
@@ -82,12 +85,30 @@ class Problem:
         return Problem(ts=self.ts[start:stop], coef=self.coef[start:stop], tcoef=self.tcoef[start:stop],
                        fusion=self.fusion, params=self.params, dims=list(self.dims),
                        data_coef=None if self.data_coef is None else self.data_coef[start:stop],
-                       cde_hidden=self.cde_hidden, cde_embed=self.cde_embed)
+                       cde_hidden=self.cde_hidden, cde_embed=self.cde_embed, compute=self.compute)
+
+    def with_compute(self, compute: str) -> "Problem":
+        """The same problem in another arithmetic ("fp32" | "bf16" | "bf16_storage": coefficients cast here)."""
+        mode = COMPUTE_MODES[compute]
+        dt = torch.bfloat16 if mode == _lib.COMPUTE_BF16_STORAGE else torch.float32
+        return Problem(ts=self.ts, coef=self.coef.to(dt).contiguous(), tcoef=self.tcoef, fusion=self.fusion,
+                       params=self.params, dims=list(self.dims), data_coef=self.data_coef,
+                       cde_hidden=self.cde_hidden, cde_embed=self.cde_embed, compute=mode)
 
 
-def make_problem(ts, coeffs, kind, layers, data_coeffs=None, cde_hidden=0, cde_embed=0, device="cuda"):
-    """Build a Problem from reference-layout inputs (ts [B,T], coeffs (d,c,b,a) [B,T-1,n,n,2], layer dicts)."""
+COMPUTE_MODES = {"fp32": _lib.COMPUTE_FP32, "bf16": _lib.COMPUTE_BF16, "bf16_storage": _lib.COMPUTE_BF16_STORAGE}
+
+
+def make_problem(ts, coeffs, kind, layers, data_coeffs=None, cde_hidden=0, cde_embed=0, device="cuda",
+                 compute="fp32"):
+    """Build a Problem from reference-layout inputs (ts [B,T], coeffs (d,c,b,a) [B,T-1,n,n,2], layer dicts).
+
+    compute="bf16" runs the n x n products on bf16 MFMA (split pairs, fp32-class results); "bf16_storage" also
+    stores the operator coefficients in bfloat16 (BASELINE config 5; forward only, see gncde.h GNCDE_COMPUTE_*)."""
     coef, tcoef = layout.pack_control(coeffs, device=device)
+    mode = COMPUTE_MODES[compute]
+    if mode == _lib.COMPUTE_BF16_STORAGE:
+        coef = coef.to(torch.bfloat16).contiguous()
     ts = torch.as_tensor(ts, dtype=torch.float32)
     if ts.dim() == 1:
         ts = ts.unsqueeze(0)
@@ -96,7 +117,8 @@ def make_problem(ts, coeffs, kind, layers, data_coeffs=None, cde_hidden=0, cde_e
     params = layout.pack_params(layers, device=device)
     dc = layout.pack_data_control(data_coeffs, device=device) if data_coeffs is not None else None
     return Problem(ts=ts.to(device).contiguous(), coef=coef, tcoef=tcoef, fusion=fusion, params=params,
-                   dims=layout.layer_dims(layers), data_coef=dc, cde_hidden=cde_hidden, cde_embed=cde_embed)
+                   dims=layout.layer_dims(layers), data_coef=dc, cde_hidden=cde_hidden, cde_embed=cde_embed,
+                   compute=mode)
 
 
 class _Workspace:

@@ -29,7 +29,7 @@ def flops_per_eval(n, dims, de=0):
     return f + (4 * n * dims[-1] if de else 0)
 
 
-def run(name, prob, spec, y0, reps):
+def run(name, prob, spec, y0, reps, ref=None):
     import gncde
     path = gncde.integrate_path(prob, spec)
     ys, st = gncde.integrate(prob, spec, y0, stats=True)
@@ -46,7 +46,10 @@ def run(name, prob, spec, y0, reps):
            "tflops_algorithmic": round(evals * fpe / dt / 1e12, 3),
            "mfma_frac": round(evals * fpe / dt / 1e12 / FP32_PEAK, 4),
            "finite": bool(torch.isfinite(ys).all())}
+    if ref is not None:  # deviation of this arithmetic from the fp32 solve of the same problem
+        out["rel_dev_vs_fp32"] = float((ys - ref).abs().max() / ref.abs().max())
     print(json.dumps(out), flush=True)
+    return ys
 
 
 def main():
@@ -75,7 +78,9 @@ def main():
             spec = gncde.SolverSpec(method=L.TSIT5, controller=L.CTRL_PID, save_mode=L.SAVE_T1, rtol=1e-3, atol=1e-6,
                                     t0=torch.zeros(B, device="cuda"), t1=torch.ones(B, device="cuda"),
                                     dt0=torch.full((B,), 0.01, device="cuda"))
-            run("5_trade_n255_h32_de8_L4_tsit5pid", prob, spec, y0, args.reps)
+            ys = run("5_trade_n255_h32_de8_L4_tsit5pid", prob, spec, y0, args.reps)
+            # BASELINE config 5's bf16 MFMA path: bf16 coefficients and (I + Abar), bf16 n x n products
+            run("5_trade_n255_h32_de8_L4_tsit5pid_bf16", prob.with_compute("bf16"), spec, y0, args.reps, ref=ys)
 
 
 if __name__ == "__main__":
