@@ -28,6 +28,7 @@ namespace gncde {
 namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));  // v_pk_fma_f32 / v_pk_add_f32 operands
 
 constexpr int kTMax = 256;  // knots per sample held in LDS
 
@@ -326,12 +327,22 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
         }
 #pragma unroll
         for (int l = 0; l < L; ++l) vv[l] = *reinterpret_cast<const floatx4*>(sVec + v0 + l * NP + s4);
+        // two adjacent slices per packed op (v_pk_fma_f32 with the SGPR coefficient broadcast): half the
+        // VALU issue of the scalar chain, same operation order
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; j += 2)
 #pragma unroll
-          for (int l = 0; l < L; ++l)
-            Ab[l][s4 + j] = fmaf(ec[l][0], ar[j], fmaf(ec[l][1], dr[j], fmaf(ec[l][2], ac[j], fmaf(ec[l][3], dc[j],
-                                 wl[l] + vv[l][j]))));
+          for (int l = 0; l < L; ++l) {
+            const floatx2 a2 = {ar[j], ar[j + 1]}, d2 = {dr[j], dr[j + 1]};
+            const floatx2 at2 = {ac[j], ac[j + 1]}, dt2 = {dc[j], dc[j + 1]};
+            floatx2 x = floatx2{vv[l][j], vv[l][j + 1]} + floatx2{wl[l], wl[l]};
+            x = __builtin_elementwise_fma(floatx2{ec[l][3], ec[l][3]}, dt2, x);
+            x = __builtin_elementwise_fma(floatx2{ec[l][2], ec[l][2]}, at2, x);
+            x = __builtin_elementwise_fma(floatx2{ec[l][1], ec[l][1]}, d2, x);
+            x = __builtin_elementwise_fma(floatx2{ec[l][0], ec[l][0]}, a2, x);
+            Ab[l][s4 + j] = x.x;
+            Ab[l][s4 + j + 1] = x.y;
+          }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
