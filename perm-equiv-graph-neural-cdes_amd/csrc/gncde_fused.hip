@@ -173,6 +173,9 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
 
   // ---- (I + Abar_l) operands for stage time t --------------------------------------------------------
   auto form = [&](float t) __attribute__((always_inline)) {
+    // The form phase (HBM loads, VALU, LDS) runs at raised wave priority: the co-resident waves of the other
+    // samples on this SIMD are mostly in their MFMA-bound eval phase and fill the gaps (config 2: -6%).
+    __builtin_amdgcn_s_setprio(1);
     __syncthreads();  // readers of the aliased M buffers are done
     // Opaque per-call copy of the thread id: keeps this phase's per-lane LDS bases from being hoisted
     // out of the time loop (they would stay live in registers across the whole solve).
@@ -189,6 +192,9 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     }
     int idx = cnt - 1;
     idx = idx < 0 ? 0 : (idx > T - 2 ? T - 2 : idx);
+#if GNCDE_X_NOCOEF  // diagnostic build only: every form reads interval 0 (cache-resident coefficients)
+    idx = 0;
+#endif
     const float f = t - sTs[idx];
     const float f3 = 3.0f * f;
     const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
@@ -352,6 +358,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     }
     tg = i < n ? fmaf(f, fmaf(f3, tc0, 2.0f * tc1), tc2) : 0.f;
     __syncthreads();  // all A/dA reads done before the aliased M buffers are written
+    __builtin_amdgcn_s_setprio(0);
   };
 
   // ---- one vector-field evaluation: Kout = VF(Yin) at the formed time --------------------------------
@@ -422,7 +429,11 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
   bool have = false;
   float tcache = 0.f;
   auto vf = [&](float t, const float (&Yin)[FB][4], float (&Kout)[FB][4]) __attribute__((always_inline)) {
+#if GNCDE_X_NOFORM  // diagnostic build only: one form per solve (times the evaluations alone)
+    if (!have) {
+#else
     if (!have || t != tcache) {
+#endif
       form(t);
       tcache = t;
       have = true;

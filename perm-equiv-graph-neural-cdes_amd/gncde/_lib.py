@@ -22,7 +22,7 @@ STAT_STEPS, STAT_REJECTS, STAT_EVALS, STAT_STATUS = 0, 1, 2, 3
 OP_NORM_LAP, OP_NORM_ADJ, OP_KIPF, OP_NORMALIZED_PLUS = 0, 1, 2, 3
 
 LIB_NAME = "libgncde_hip.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("GNCDE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)  # GNCDE_LIB: an alternative build of the same library (kernel experiments)
 
 # Every symbol include/gncde.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
