@@ -30,6 +30,10 @@ namespace {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));  // v_pk_fma_f32 / v_pk_add_f32 operands
 
+#ifndef GNCDE_X_SKIP  // diagnostic builds only: 1/2/3 skip the operand build / the reductions / the Horner pass
+#define GNCDE_X_SKIP 0
+#endif
+
 constexpr int kTMax = 256;  // knots per sample held in LDS
 
 // Tsit5 row a[s][0..5] for stage s = 1..6 (row 6 = b_sol) and c[s], as compile-time immediates
@@ -207,7 +211,8 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       tc1 = tc[n + ii];
       tc2 = tc[2 * n + ii];
     }
-    if (n == NP) {
+    if (GNCDE_X_SKIP == 3) {
+    } else if (n == NP) {
       const float4* c4 = reinterpret_cast<const float4*>(cb);
       constexpr int NQ = NP * NP / 4;
       // fully unrolled: every coefficient load of the interval is in flight before the first use (one HBM
@@ -243,7 +248,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       }
     }
     __syncthreads();
-    {  // r, rd (row sums), c, cd (column sums), diagonals: 4 NP threads, one line each
+    if (GNCDE_X_SKIP != 2) {  // r, rd (row sums), c, cd (column sums), diagonals: 4 NP threads, one line each
       const int q = ftid / NP, j = ftid % NP;
       const float* M = (q & 1) ? sdA : sA;
       float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;  // 4 chains: latency, not adds, bound this
@@ -314,7 +319,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       for (int q = 0; q < 4; ++q)
         ec[l][q] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, fc[q])));
     }
-    {
+    if (GNCDE_X_SKIP != 1) {
       // Chunks of 4 slices: all 16 image reads and the L float4 reads of v_l are issued before the first
       // use, so a chunk waits on LDS once; the pins at the end of a chunk keep the next chunk's loads
       // from being hoisted (register pressure), not the loads of this one.
