@@ -312,7 +312,7 @@ inline const float* abar_layer(const GncdeProblem& p, const float* abar, int l) 
 }
 
 struct VfWs {
-  float *A, *dA, *red, *tg, *Z0, *Z1, *m, *abar, *wf, *bf, *inv, *part, *q, *dx;
+  float *A, *dA, *red, *tg, *Z0, *Z1, *m, *abar, *wf, *wp, *bf, *inv, *part, *q, *dx;
 };
 
 size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
@@ -337,6 +337,7 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.m = take(B * n * D);
   w.abar = take((size_t)p.L * B * nn);  // (I + Abar_l) for every layer
   w.wf = take(wsum);  // W' = W diag(rms_w) per layer, back to back
+  w.wp = take(wsum);  // W' in k_layer's operand order (layers with layer_mode >= 0)
   w.bf = take(bsum);  // bias' = bias + W rms_b per layer
   w.inv = take(B * n);
   w.part = take(B * ((n + kSlab - 1) / kSlab) * 2 * n);
@@ -388,6 +389,8 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
     const LayerOffsets o = layer_offsets(p, l);
     fold_linear(din, dout, p.params + o.rms_w, p.params + o.rms_b, p.params + o.W, p.params + o.b, w.wf + wo,
                 w.bf + bo, st);
+    const int mode = layer_mode(p, l);
+    if (mode >= 0) permute_linear(dout, din, mode == 2, w.wf + wo, w.wp + wo, st);
     wo += (size_t)din * dout;
     bo += dout;
   }
@@ -414,6 +417,16 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     // q = (I + Abar) 1: the n x n product runs at width d_in instead of d_out (configs 3 / 5: 16x / 16x fewer
     // flops for that GEMM).  Exact algebra; only the fp32 summation order changes.
     const bool reassoc = dout > din;
+    const int mode = layer_mode(p, l);
+    if (mode >= 0 && (mode != 2 || fused_out)) {  // one fused launch (gncde_layer.hip)
+      float* out = mode == 0 ? Zout : dy;
+      layer_fused(p, l, mode, abar_layer(p, w.abar, l), Zin, w.wp + wo, w.bf + bo, w.q + (size_t)l * B * n, out, w.tg,
+                  w.dx, st);
+      wo += (size_t)din * dout;
+      bo += dout;
+      Zin = Zout;
+      continue;
+    }
     GemmArgs lin{};
     GemmArgs pr{};
     float* m = w.m;

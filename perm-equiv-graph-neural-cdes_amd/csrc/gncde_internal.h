@@ -153,6 +153,13 @@ void fold_linear(int din, int dout, const float* rw, const float* rb, const floa
                  float* bf, hipStream_t st);
 void row_inv(int rows, int d, const float* Z, float* inv, hipStream_t st);
 
+// fused ConvLayer launch of the generic path: gncde_layer.hip.  layer_mode: -1 = not supported (two-GEMM path),
+// 0 hidden layer (ReLU), 1 ODE output layer (tg scaling), 2 CDE output layer (de = 8 contraction).
+int layer_mode(const GncdeProblem& p, int l);
+void permute_linear(int rows, int din, bool cde, const float* W, float* out, hipStream_t st);
+void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, const float* Z, const float* wperm,
+                 const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st);
+
 // generic (any-shape, multi-kernel) path: gncde_generic.hip
 size_t generic_vf_workspace(const GncdeProblem& p);
 size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s);

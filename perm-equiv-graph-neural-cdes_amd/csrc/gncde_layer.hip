@@ -1,0 +1,343 @@
+// One fused launch per ConvLayer for the generic (multi-kernel) vector field — configs 3 / 5 and every shape the
+// persistent kernel does not take (layers.py:36-48, ConvEquivFusionLayer.__call__ layers.py:162-177):
+//
+//   Z_next[R, :] = act( ((I + Abar) diag(inv) Z)[R, :] W'^T + q[R] b'^T )
+//
+// in the reassociated order: W' = W diag(rms_w), b' = b + W rms_b (RMSNorm's affine folded, once per solve),
+// inv = the RMSNorm factor of each node row, q = (I + Abar) 1.  A workgroup owns 32 node rows R of one sample, so
+// nothing crosses workgroups inside a layer (the Linear-first order needs every row of m before the n x n product):
+//
+//   1. Z[b] (n x d_in, HBM/L2) -> LDS, each row scaled by its RMSNorm factor (row sum of squares on lane shuffles).
+//   2. P = (I + Abar)[R, :] Zs on v_mfma_f32_16x16x4f32: A operand = rows R of (I + Abar) straight from HBM/L2
+//      (one dwordx4 per lane per 16-deep K chunk, K permuted so a lane's 4 steps are 4 consecutive columns),
+//      B operand = Zs from LDS.  d_in / 16 column tiles per wave, the K range split over the remaining waves.
+//   3. Z_next[R, :] = P W'^T on MFMA (P from LDS, W' pre-permuted into the lane order: one coalesced 1 KB load per
+//      wave per operand), epilogue q b'^T + ReLU, or tg * (.) for the ODE output layer.
+//   3'. The CDE-wrapper output layer (cde_wrapper_vector_field.py:19-26, de = 8) never forms the n x h*16 read-out:
+//      dZ[i, m] = tg_i sum_{c, j} P[i, c] dX[i, j] W'[16 m + j, c] + tg_i q_i sum_j b'[16 m + j] dX[i, j]
+//      is one GEMM with K = (j, c) whose A operand P[i, c] dX[i, j] is formed in registers (one multiply per MFMA
+//      step), so the 16-column contraction happens inside the MFMA accumulation.
+//
+// This replaces, per layer, two GEMM launches, the row-norm kernel and the read-out's 16-lane shuffle epilogue.
+#include "gncde_internal.h"
+
+namespace gncde {
+
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned rows (n = 129, 255)
+
+constexpr int kRows = 32;  // node rows per workgroup: two 16-row MFMA tiles
+
+struct LayerArgs {
+  int n;
+  const float* abar;   // (I + Abar_l) [B, n, n]
+  const float* Z;      // [B, n, DIN]
+  const float* wperm;  // W' in the lane order of the kernel (permute_linear)
+  const float* bf;     // b' [DOUT] (CDE: [16 H])
+  const float* q;      // q_l [B, n]
+  float* out;          // [B, n, DOUT] (CDE: dy [B, n, H])
+  const float* tg;     // [B n] time-channel derivative (MODE 1, 2)
+  const float* dx;     // [B n, 16] data-spline derivative (MODE 2)
+};
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int DIN>
+__host__ __device__ constexpr int zs_stride() {
+  return DIN + 4;  // row stride of Zs / Ps: 16-byte rows, hi-groups of a column read 16 banks apart
+}
+
+// MODE 0: hidden layer, ReLU.  MODE 1: ODE output layer, out = tg * Z_next.  MODE 2: CDE output layer (DOUT = h).
+template <int DIN, int DOUT, int MODE>
+__global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int ZS = zs_stride<DIN>();
+  constexpr int CTP = DIN / 16;  // product column tiles
+  constexpr int KPP = 4 / CTP;   // product K parts (waves per column tile)
+  constexpr int NCC = DIN / 16;  // 16-deep K chunks of the Linear
+  const int n = a.n;
+  const int nk = (n + 15) & ~15;
+  floatx4* red = reinterpret_cast<floatx4*>(smem);  // [4][2][64] K-part partials (MODE 2)
+  float* sDx = smem + 4 * 2 * 64 * 4;               // [32][17] (MODE 2)
+  float* Ps = sDx + kRows * 17 + 12;                // [KPP][32][ZS] (16-byte aligned: 2048 + 556 is a multiple of 4)
+  float* Zs = Ps + KPP * kRows * ZS;                // [nk][ZS]
+  const int b = blockIdx.y, r0 = blockIdx.x * kRows;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
+  const size_t nb = (size_t)b * n;
+
+  // ---- 1. Zs = diag(inv) Z[b], zero rows up to nk -------------------------------------------------------------
+  {
+    constexpr int G = DIN / 4;  // float4 per row: a row's lanes are G consecutive lanes (256 % G == 0)
+    const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.Z + nb * DIN);
+    for (int e = tid; e < nk * G; e += 256) {
+      const int row = e / G, cg = e % G;
+      floatx4 v = row < n ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
+      float ss = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, v.w * v.w)));
+#pragma unroll
+      for (int o = 1; o < G; o <<= 1) ss += __shfl_xor(ss, o);
+      const float inv = rms_inv(ss, 1.0f / (float)DIN);
+      *reinterpret_cast<floatx4*>(Zs + row * ZS + 4 * cg) = v * inv;
+    }
+    if (MODE == 2)
+      for (int e = tid; e < kRows * 16; e += 256) {
+        const int row = e >> 4, j = e & 15, R = r0 + row;
+        sDx[row * 17 + j] = R < n ? a.dx[(nb + R) * 16 + j] : 0.f;
+      }
+  }
+  __syncthreads();
+
+  const bool two = r0 + 16 < n;  // the second row tile holds a valid row (else its MFMAs are skipped)
+
+  // ---- 2. P = (I + Abar)[R, :] Zs -------------------------------------------------------------------------------
+  {
+    const int ct = w % CTP, kp = w / CTP;
+    const float* Ab = a.abar + nb * n;
+    const int nch = nk >> 4;
+    const int ra0 = r0 + lo < n ? r0 + lo : n - 1, ra1 = r0 + 16 + lo < n ? r0 + 16 + lo : n - 1;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    for (int kr = kp; kr < nch; kr += 4 * KPP) {  // rounds of up to 4 chunks (this wave's: kr, kr + KPP, ...)
+      floatx4 av[4][2];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int kc = kr + c * KPP;
+        const int k = 16 * kc + 4 * hi;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const float* pa = Ab + (size_t)(t ? ra1 : ra0) * n + k;
+          floatx4 v = {0.f, 0.f, 0.f, 0.f};
+          if (kc < nch) {
+            if (k + 4 <= n) {
+              const floatx4u u = *reinterpret_cast<const floatx4u*>(pa);
+              v = floatx4{u.x, u.y, u.z, u.w};
+            } else {
+#pragma unroll
+              for (int s = 0; s < 4; ++s) v[s] = k + s < n ? pa[s] : 0.f;
+            }
+          }
+          av[c][t] = v;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int kc = kr + c * KPP;
+        if (kc >= nch) break;
+        const float* zb = Zs + (16 * kc + 4 * hi) * ZS + 16 * ct + lo;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float bv = zb[s * ZS];
+          acc0 = mfma4(av[c][0][s], bv, acc0);
+          if (two) acc1 = mfma4(av[c][1][s], bv, acc1);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      Ps[(kp * kRows + 4 * hi + r) * ZS + 16 * ct + lo] = acc0[r];
+      Ps[(kp * kRows + 16 + 4 * hi + r) * ZS + 16 * ct + lo] = acc1[r];
+    }
+  }
+  __syncthreads();
+
+  // P row (16 t + lo), columns 16 cc + 4 hi .. +3, summed over the K parts in a fixed order
+  auto prow = [&](int t, int cc) -> floatx4 {
+    const float* p = Ps + (16 * t + lo) * ZS + 16 * cc + 4 * hi;
+    floatx4 v = *reinterpret_cast<const floatx4*>(p);
+#pragma unroll
+    for (int kp = 1; kp < KPP; ++kp) v += *reinterpret_cast<const floatx4*>(p + kp * kRows * ZS);
+    return v;
+  };
+  const floatx4* W4 = reinterpret_cast<const floatx4*>(a.wperm);
+
+  if constexpr (MODE != 2) {
+    // ---- 3. Z_next = P W'^T + q b'^T -------------------------------------------------------------------------
+    constexpr int CTO = DOUT / 16;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int tile = w + 4 * tt;
+      if (tile >= 2 * CTO) break;
+      const int rt = tile / CTO, ct = tile % CTO;
+      if (rt == 1 && !two) break;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int cc = 0; cc < NCC; ++cc) {
+        const floatx4 pv = prow(rt, cc);
+        const floatx4 wv = W4[(ct * NCC + cc) * 64 + lane];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma4(pv[s], wv[s], acc);
+      }
+      const int col = 16 * ct + lo;
+      const float bc = a.bf[col];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int R = r0 + 16 * rt + 4 * hi + r;
+        if (R >= n) continue;
+        float v = fmaf(a.q[nb + R], bc, acc[r]);
+        if (MODE == 0) v = fmaxf(v, 0.f);
+        if (MODE == 1) v *= a.tg[nb + R];
+        a.out[(nb + R) * DOUT + col] = v;
+      }
+    }
+  } else {
+    // ---- 3'. CDE output layer: dZ = tg * (sum_{c,j} P[., c] dX[., j] W'[16 m + j, c] + q sum_j b'[16 m + j] dX) --
+    constexpr int CT = DOUT / 16;  // output column tiles (channels m)
+    constexpr int KP = 4 / CT;     // waves per column tile, splitting j
+    constexpr int JP = 16 / KP;
+    const int ct = w % CT, kp = w / CT, j0 = kp * JP;
+    float dxr[2][JP];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < JP; ++j) dxr[t][j] = sDx[(16 * t + lo) * 17 + j0 + j];
+    floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int cc = 0; cc < NCC; ++cc) {
+      const floatx4 p0 = prow(0, cc), p1 = prow(1, cc);
+#pragma unroll 4
+      for (int j = 0; j < JP; ++j) {
+        const floatx4 wv = W4[((ct * 16 + j0 + j) * NCC + cc) * 64 + lane];
+        const floatx4 a0 = p0 * dxr[0][j], a1 = p1 * dxr[1][j];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          acc[0] = mfma4(a0[s], wv[s], acc[0]);
+          if (two) acc[1] = mfma4(a1[s], wv[s], acc[1]);
+        }
+      }
+    }
+    // bias term of this wave's j range; rows 16 t + 4 hi + r, channel m = 16 ct + lo
+    const int m = 16 * ct + lo;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = 16 * t + 4 * hi + r, R = r0 + rl;
+        float sb = 0.f;
+#pragma unroll
+        for (int j = 0; j < JP; ++j) sb = fmaf(a.bf[16 * m + j0 + j], sDx[rl * 17 + j0 + j], sb);
+        acc[t][r] = fmaf(R < n ? a.q[nb + R] : 0.f, sb, acc[t][r]);
+      }
+    if constexpr (KP > 1) {
+      red[(w * 2 + 0) * 64 + lane] = acc[0];
+      red[(w * 2 + 1) * 64 + lane] = acc[1];
+      __syncthreads();
+      if (kp == 0) {
+#pragma unroll
+        for (int p = 1; p < KP; ++p) {
+          acc[0] += red[((w + p * CT) * 2 + 0) * 64 + lane];
+          acc[1] += red[((w + p * CT) * 2 + 1) * 64 + lane];
+        }
+      }
+    }
+    if (kp == 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int R = r0 + 16 * t + 4 * hi + r;
+          if (R < n) a.out[(nb + R) * DOUT + m] = a.tg[nb + R] * acc[t][r];
+        }
+    }
+  }
+}
+
+// W' [rows, din] -> the lane order of k_layer's B operands:
+//   Linear (cde = 0): out[(ct NCC + cc) 64 + lane][s] = W'[16 ct + lo][16 cc + 4 hi + s]
+//   CDE    (cde = 1): out[((ct 16 + j) NCC + cc) 64 + lane][s] = W'[16 (16 ct + lo) + j][16 cc + 4 hi + s]
+__global__ void k_permute_linear(int rows, int din, int cde, const float* __restrict__ W, float* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows * din) return;
+  const int ncc = din / 16;
+  const int s = e & 3, lane = (e >> 2) & 63, lo = lane & 15, hi = lane >> 4;
+  int blk = e >> 8;
+  const int cc = blk % ncc;
+  blk /= ncc;
+  int row;
+  if (cde) {
+    const int j = blk % 16, ct = blk / 16;
+    row = 16 * (16 * ct + lo) + j;
+  } else {
+    row = 16 * blk + lo;
+  }
+  out[e] = W[(size_t)row * din + 16 * cc + 4 * hi + s];
+}
+
+template <int DIN>
+size_t layer_smem(int n) {
+  constexpr int ZS = zs_stride<DIN>();
+  const int nk = (n + 15) & ~15;
+  return sizeof(float) * (4 * 2 * 64 * 4 + kRows * 17 + 12 + (4 / (DIN / 16)) * kRows * ZS + (size_t)nk * ZS);
+}
+
+constexpr size_t kMaxSmem = 64 * 1024;  // the default dynamic-LDS limit of a launch
+
+template <int DIN, int DOUT, int MODE>
+void launch(const LayerArgs& a, int B, hipStream_t st) {
+  const size_t sm = layer_smem<DIN>(a.n);
+  hipLaunchKernelGGL((k_layer<DIN, DOUT, MODE>), dim3((a.n + kRows - 1) / kRows, B), dim3(256), sm, st, a);
+}
+
+template <int DIN>
+bool dispatch_dout(const LayerArgs& a, int B, int dout, int mode, hipStream_t st) {
+#define GNCDE_LAYER_CASE(D)                                      \
+  if (dout == D) {                                               \
+    if (mode == 0) launch<DIN, D, 0>(a, B, st);                  \
+    else if (mode == 1) launch<DIN, D, 1>(a, B, st);             \
+    else launch<DIN, D, 2>(a, B, st);                            \
+    return true;                                                 \
+  }
+  GNCDE_LAYER_CASE(16)
+  GNCDE_LAYER_CASE(32)
+  GNCDE_LAYER_CASE(64)
+#undef GNCDE_LAYER_CASE
+  return false;
+}
+
+bool width_ok(int d) { return d == 16 || d == 32 || d == 64; }
+
+}  // namespace
+
+int layer_mode(const GncdeProblem& p, int l) {
+  if (p.compute != GNCDE_COMPUTE_FP32) return -1;
+  const int din = p.dims[l], dout = p.dims[l + 1];
+  if (!width_ok(din)) return -1;
+  const bool last = l == p.L - 1;
+  int mode;
+  if (last && p.cde_hidden > 0) {
+    if (p.cde_embed != 8 || dout != 16 * p.cde_hidden || !width_ok(p.cde_hidden)) return -1;
+    mode = 2;
+  } else {
+    if (!width_ok(dout)) return -1;
+    mode = last ? 1 : 0;
+  }
+  size_t sm = din == 16 ? layer_smem<16>(p.n) : (din == 32 ? layer_smem<32>(p.n) : layer_smem<64>(p.n));
+  return sm <= kMaxSmem ? mode : -1;
+}
+
+void permute_linear(int rows, int din, bool cde, const float* W, float* out, hipStream_t st) {
+  const int tot = rows * din;
+  hipLaunchKernelGGL(k_permute_linear, dim3((tot + 255) / 256), dim3(256), 0, st, rows, din, cde ? 1 : 0, W, out);
+}
+
+void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, const float* Z, const float* wperm,
+                 const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st) {
+  LayerArgs a{};
+  a.n = p.n;
+  a.abar = abar;
+  a.Z = Z;
+  a.wperm = wperm;
+  a.bf = bf;
+  a.q = q;
+  a.out = out;
+  a.tg = tg;
+  a.dx = dx;
+  const int din = p.dims[l];
+  const int dout = mode == 2 ? p.cde_hidden : p.dims[l + 1];
+  if (din == 16) dispatch_dout<16>(a, p.B, dout, mode, st);
+  else if (din == 32) dispatch_dout<32>(a, p.B, dout, mode, st);
+  else dispatch_dout<64>(a, p.B, dout, mode, st);
+}
+
+}  // namespace gncde
