@@ -29,6 +29,10 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned rows (n = 129, 255)
 
 constexpr int kRows = 32;  // node rows per workgroup: two 16-row MFMA tiles
+#ifndef GNCDE_X_JUNROLL
+#define GNCDE_X_JUNROLL 4
+#endif
+constexpr int kJUnroll = GNCDE_X_JUNROLL;  // read-out K loop: W' operand loads in flight per wave
 
 struct LayerArgs {
   int n;
@@ -57,14 +61,14 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int ZS = zs_stride<DIN>();
   constexpr int CTP = DIN / 16;  // product column tiles
-  constexpr int KPP = 4 / CTP;   // product K parts (waves per column tile)
+  constexpr int KPP = 4;         // product K parts (one per wave)
   constexpr int NCC = DIN / 16;  // 16-deep K chunks of the Linear
   const int n = a.n;
   const int nk = (n + 15) & ~15;
   floatx4* red = reinterpret_cast<floatx4*>(smem);  // [4][2][64] K-part partials (MODE 2)
   float* sDx = smem + 4 * 2 * 64 * 4;               // [32][17] (MODE 2)
-  float* Ps = sDx + kRows * 17 + 12;                // [KPP][32][ZS] (16-byte aligned: 2048 + 556 is a multiple of 4)
-  float* Zs = Ps + KPP * kRows * ZS;                // [nk][ZS]
+  float* Zs = sDx + kRows * 17 + 12;                // [nk][ZS] (16-byte aligned: 2048 + 556 is a multiple of 4)
+  float* Ps = Zs;                                   // [KPP][32][ZS] after the product (max(nk, 128) rows reserved)
   const int b = blockIdx.y, r0 = blockIdx.x * kRows;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const size_t nb = (size_t)b * n;
@@ -92,18 +96,22 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
 
   const bool two = r0 + 16 < n;  // the second row tile holds a valid row (else its MFMAs are skipped)
 
-  // ---- 2. P = (I + Abar)[R, :] Zs -------------------------------------------------------------------------------
+  // ---- 2. P = (I + Abar)[R, :] Zs: wave w takes the 16-deep K chunks w, w + 4, ... for every column tile, so each
+  // (I + Abar) element is loaded once per workgroup; the four K partials meet in LDS (aliasing Zs) in a fixed order.
   {
-    const int ct = w % CTP, kp = w / CTP;
     const float* Ab = a.abar + nb * n;
     const int nch = nk >> 4;
     const int ra0 = r0 + lo < n ? r0 + lo : n - 1, ra1 = r0 + 16 + lo < n ? r0 + 16 + lo : n - 1;
-    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    for (int kr = kp; kr < nch; kr += 4 * KPP) {  // rounds of up to 4 chunks (this wave's: kr, kr + KPP, ...)
+    floatx4 acc[2][CTP];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ct = 0; ct < CTP; ++ct) acc[t][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int kr = w; kr < nch; kr += 16) {  // rounds of up to 4 chunks: kr, kr + 4, kr + 8, kr + 12
       floatx4 av[4][2];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int kc = kr + c * KPP;
+        const int kc = kr + 4 * c;
         const int k = 16 * kc + 4 * hi;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -123,22 +131,26 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int kc = kr + c * KPP;
+        const int kc = kr + 4 * c;
         if (kc >= nch) break;
-        const float* zb = Zs + (16 * kc + 4 * hi) * ZS + 16 * ct + lo;
+        const float* zb = Zs + (16 * kc + 4 * hi) * ZS + lo;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const float bv = zb[s * ZS];
-          acc0 = mfma4(av[c][0][s], bv, acc0);
-          if (two) acc1 = mfma4(av[c][1][s], bv, acc1);
-        }
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int ct = 0; ct < CTP; ++ct) {
+            const float bv = zb[s * ZS + 16 * ct];
+            acc[0][ct] = mfma4(av[c][0][s], bv, acc[0][ct]);
+            if (two) acc[1][ct] = mfma4(av[c][1][s], bv, acc[1][ct]);
+          }
       }
     }
+    __syncthreads();  // Zs reads done: the partials alias it
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      Ps[(kp * kRows + 4 * hi + r) * ZS + 16 * ct + lo] = acc0[r];
-      Ps[(kp * kRows + 16 + 4 * hi + r) * ZS + 16 * ct + lo] = acc1[r];
-    }
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ct = 0; ct < CTP; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ps[(w * kRows + 16 * t + 4 * hi + r) * ZS + 16 * ct + lo] = acc[t][ct][r];
   }
   __syncthreads();
 
@@ -196,7 +208,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
 #pragma unroll
     for (int cc = 0; cc < NCC; ++cc) {
       const floatx4 p0 = prow(0, cc), p1 = prow(1, cc);
-#pragma unroll 4
+#pragma unroll kJUnroll
       for (int j = 0; j < JP; ++j) {
         const floatx4 wv = W4[((ct * 16 + j0 + j) * NCC + cc) * 64 + lane];
         const floatx4 a0 = p0 * dxr[0][j], a1 = p1 * dxr[1][j];
@@ -268,7 +280,7 @@ template <int DIN>
 size_t layer_smem(int n) {
   constexpr int ZS = zs_stride<DIN>();
   const int nk = (n + 15) & ~15;
-  return sizeof(float) * (4 * 2 * 64 * 4 + kRows * 17 + 12 + (4 / (DIN / 16)) * kRows * ZS + (size_t)nk * ZS);
+  return sizeof(float) * (4 * 2 * 64 * 4 + kRows * 17 + 12 + (size_t)(nk > 4 * kRows ? nk : 4 * kRows) * ZS);
 }
 
 constexpr size_t kMaxSmem = 64 * 1024;  // the default dynamic-LDS limit of a launch
