@@ -77,24 +77,30 @@ __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* 
     pb[k] = ca;
     pb[n + k] = cd;
   }
-  __shared__ float sred[2][kSlab][4];
+  // Row sums: the 2 x kSlab per-thread partials go through LDS (stride 264: the reads below hit 64 distinct banks),
+  // then thread t sums partials t % 8, t % 8 + 8, ... of row-sum t / 8 and three lane swaps finish it: 32 LDS
+  // writes + 32 reads + 3 shuffles per thread instead of 2 kSlab wave reductions (6 shuffles each).
+  constexpr int kPs = 264;
+  __shared__ float sp[2 * kSlab][kPs];
 #pragma unroll
   for (int r = 0; r < kSlab; ++r) {
-    float x = ra[r], y = rd[r];
-    for (int o = 32; o > 0; o >>= 1) {
-      x += __shfl_xor(x, o);
-      y += __shfl_xor(y, o);
-    }
-    if (lane == 0) {
-      sred[0][r][w] = x;
-      sred[1][r][w] = y;
-    }
+    sp[r][tid] = ra[r];
+    sp[kSlab + r][tid] = rd[r];
   }
   __syncthreads();
-  if (tid < 2 * kSlab) {
-    const int q = tid / kSlab, r = tid % kSlab;
-    if (r < rows) rb[q * n + i0 + r] = (sred[q][r][0] + sred[q][r][1]) + (sred[q][r][2] + sred[q][r][3]);
+  {
+    const int q = tid >> 3, p0 = tid & 7;
+    float x = 0.f;
+#pragma unroll 8
+    for (int j = 0; j < 32; ++j) x += sp[q][p0 + 8 * j];
+    x += __shfl_xor(x, 1);
+    x += __shfl_xor(x, 2);
+    x += __shfl_xor(x, 4);
+    const int r = q % kSlab;
+    if (p0 == 0 && r < rows) rb[(q / kSlab) * n + i0 + r] = x;
   }
+  (void)lane;
+  (void)w;
   if (slab == 0) {
     const float* tc = tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
     for (int e = tid; e < n; e += blockDim.x) tg[(size_t)b * n + e] = fmaf(f, fmaf(f3, tc[e], 2.0f * tc[n + e]), tc[2 * n + e]);
@@ -182,25 +188,33 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
       qrow[((size_t)l * B + b) * n + i] = q;
     }
   }
+  // The rank-1 and diagonal families per layer, once per tile: w_l (row i), v_l (column k), u_l (diagonal).
+  __shared__ float sWv[GNCDE_MAX_LAYERS][3][32];
+  for (int e = tid; e < L * 32; e += 256) {
+    const int l = e >> 5, x = e & 31;
+    const float* fc = fus + l * GNCDE_FC;
+    const int i = i0 + x < n ? i0 + x : n - 1, k = k0 + x < n ? k0 + x : n - 1;
+    const float ri = rb[i], rdi = rb[n + i], ci = cs[0][0][x], cdi = cs[0][1][x];
+    const float rk = rb[k], rdk = rb[n + k], ck = cs[1][0][x], cdk = cs[1][1][x];
+    sWv[l][0][x] = fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci +
+                   fc[GNCDE_FC_WC_DA] * cdi + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
+    sWv[l][1][x] = fc[GNCDE_FC_VR_A] * rk + fc[GNCDE_FC_VR_DA] * rdk + fc[GNCDE_FC_VC_A] * ck + fc[GNCDE_FC_VC_DA] * cdk;
+    sWv[l][2][x] = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * rb[4 * n + i] + fc[GNCDE_FC_UD_DA] * rb[5 * n + i] +
+                   fc[GNCDE_FC_UR_A] * ri + fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci +
+                   fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
+  }
+  __syncthreads();
   for (int y = ty; y < 32; y += 8) {
     const int i = i0 + y, k = k0 + tx;
     if (i >= n || k >= n) continue;
     const float aik = Ab[(size_t)i * n + k], dik = dAb[(size_t)i * n + k];
     const float aki = tA[tx][y], dki = tD[tx][y];
-    const float ri = rb[i], rdi = rb[n + i], ci = cs[0][0][y], cdi = cs[0][1][y];
-    const float rk = rb[k], rdk = rb[n + k], ck = cs[1][0][tx], cdk = cs[1][1][tx];
     const bool diag = i == k;
-    const float dgi = diag ? rb[4 * n + i] : 0.f, dgdi = diag ? rb[5 * n + i] : 0.f;
     for (int l = 0; l < L; ++l) {
       const float* fc = fus + l * GNCDE_FC;
       float v = fc[GNCDE_FC_E_A] * aik + fc[GNCDE_FC_E_DA] * dik + fc[GNCDE_FC_ET_A] * aki + fc[GNCDE_FC_ET_DA] * dki;
-      v += fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci + fc[GNCDE_FC_WC_DA] * cdi +
-           fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
-      v += fc[GNCDE_FC_VR_A] * rk + fc[GNCDE_FC_VR_DA] * rdk + fc[GNCDE_FC_VC_A] * ck + fc[GNCDE_FC_VC_DA] * cdk;
-      if (diag)
-        v += fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dgi + fc[GNCDE_FC_UD_DA] * dgdi + fc[GNCDE_FC_UR_A] * ri +
-             fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci + fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s +
-             fc[GNCDE_FC_US_DA] * sd;
+      v += sWv[l][0][y] + sWv[l][1][tx];
+      if (diag) v += sWv[l][2][y];
       abar_store(out, l * layer_stride + b * nn + (size_t)i * n + k, (size_t)L * layer_stride, v);
     }
   }

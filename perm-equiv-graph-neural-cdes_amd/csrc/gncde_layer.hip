@@ -21,6 +21,8 @@
 // This replaces, per layer, two GEMM launches, the row-norm kernel and the read-out's 16-lane shuffle epilogue.
 #include "gncde_internal.h"
 
+#include <type_traits>
+
 namespace gncde {
 
 namespace {
@@ -33,6 +35,10 @@ constexpr int kRows = 32;  // node rows per workgroup: two 16-row MFMA tiles
 #define GNCDE_X_JUNROLL 4
 #endif
 constexpr int kJUnroll = GNCDE_X_JUNROLL;  // read-out K loop: W' operand loads in flight per wave
+#ifndef GNCDE_X_SPLIT
+#define GNCDE_X_SPLIT 2
+#endif
+constexpr int kSplit = GNCDE_X_SPLIT;  // CDE read-out: workgroups per row block (channel groups)
 
 struct LayerArgs {
   int n;
@@ -69,28 +75,49 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
   float* sDx = smem + 4 * 2 * 64 * 4;               // [32][17] (MODE 2)
   float* Zs = sDx + kRows * 17 + 12;                // [nk][ZS] (16-byte aligned: 2048 + 556 is a multiple of 4)
   float* Ps = Zs;                                   // [KPP][32][ZS] after the product (max(nk, 128) rows reserved)
-  const int b = blockIdx.y, r0 = blockIdx.x * kRows;
+  float* sInv = Zs + (nk > 4 * kRows ? nk : 4 * kRows) * ZS;  // [nk] RMSNorm factors of the Z rows
+  // MODE 2 splits the read-out's channels over kSplit workgroups per row block (each recomputes P: the product is
+  // 1/16 of the read-out's MFMA work) so that the grid balances over the 256 CUs.
+  constexpr int SPLIT = (MODE == 2 && DOUT / 16 >= kSplit) ? kSplit : 1;
+  const int b = blockIdx.y, r0 = (blockIdx.x / SPLIT) * kRows, ch = blockIdx.x % SPLIT;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const size_t nb = (size_t)b * n;
 
-  // ---- 1. Zs = diag(inv) Z[b], zero rows up to nk -------------------------------------------------------------
+  // ---- 1. Zs = Z[b] (zero rows up to nk), every load of a round in flight before the first store; then the
+  // RMSNorm factor of each row from LDS (diag(inv) is applied to the (I + Abar) operand of the product).
   {
-    constexpr int G = DIN / 4;  // float4 per row: a row's lanes are G consecutive lanes (256 % G == 0)
+    constexpr int G = DIN / 4;  // float4 per row
+    constexpr int U = 8;
     const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.Z + nb * DIN);
-    for (int e = tid; e < nk * G; e += 256) {
-      const int row = e / G, cg = e % G;
-      floatx4 v = row < n ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
-      float ss = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, v.w * v.w)));
+    const int tot = nk * G, valid = n * G;
+    for (int e0 = tid; e0 < tot; e0 += 256 * U) {
+      floatx4 v[U];
 #pragma unroll
-      for (int o = 1; o < G; o <<= 1) ss += __shfl_xor(ss, o);
-      const float inv = rms_inv(ss, 1.0f / (float)DIN);
-      *reinterpret_cast<floatx4*>(Zs + row * ZS + 4 * cg) = v * inv;
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + 256 * u;
+        v[u] = e < valid ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + 256 * u;
+        if (e < tot) *reinterpret_cast<floatx4*>(Zs + (e / G) * ZS + 4 * (e % G)) = v[u];
+      }
     }
     if (MODE == 2)
       for (int e = tid; e < kRows * 16; e += 256) {
         const int row = e >> 4, j = e & 15, R = r0 + row;
         sDx[row * 17 + j] = R < n ? a.dx[(nb + R) * 16 + j] : 0.f;
       }
+    __syncthreads();
+    for (int r = tid; r < nk; r += 256) {
+      float ss = 0.f;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const floatx4 z = *reinterpret_cast<const floatx4*>(Zs + r * ZS + 4 * g);
+        ss = fmaf(z.x, z.x, fmaf(z.y, z.y, fmaf(z.z, z.z, fmaf(z.w, z.w, ss))));
+      }
+      sInv[r] = r < n ? rms_inv(ss, 1.0f / (float)DIN) : 0.f;
+    }
   }
   __syncthreads();
 
@@ -130,19 +157,35 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         }
       }
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
+      for (int c = 0; c < 4; ++c) {  // (I + Abar) diag(inv): column k of the operand scaled by inv[k]
         const int kc = kr + 4 * c;
-        if (kc >= nch) break;
-        const float* zb = Zs + (16 * kc + 4 * hi) * ZS + lo;
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int ct = 0; ct < CTP; ++ct) {
-            const float bv = zb[s * ZS + 16 * ct];
-            acc[0][ct] = mfma4(av[c][0][s], bv, acc[0][ct]);
-            if (two) acc[1][ct] = mfma4(av[c][1][s], bv, acc[1][ct]);
-          }
+        if (kc < nch) {
+          const floatx4 iv = *reinterpret_cast<const floatx4*>(sInv + 16 * kc + 4 * hi);
+          av[c][0] *= iv;
+          av[c][1] *= iv;
+        }
       }
+      auto mm = [&](auto two_c) __attribute__((always_inline)) {
+        constexpr bool TWO = decltype(two_c)::value;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int kc = kr + 4 * c;
+          if (kc >= nch) break;
+          const float* zb = Zs + (16 * kc + 4 * hi) * ZS + lo;
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int ct = 0; ct < CTP; ++ct) {
+              const float bv = zb[s * ZS + 16 * ct];
+              acc[0][ct] = mfma4(av[c][0][s], bv, acc[0][ct]);
+              if constexpr (TWO) acc[1][ct] = mfma4(av[c][1][s], bv, acc[1][ct]);
+            }
+        }
+      };
+      if (two)
+        mm(std::true_type{});
+      else
+        mm(std::false_type{});
     }
     __syncthreads();  // Zs reads done: the partials alias it
 #pragma unroll
@@ -195,30 +238,38 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
     }
   } else {
     // ---- 3'. CDE output layer: dZ = tg * (sum_{c,j} P[., c] dX[., j] W'[16 m + j, c] + q sum_j b'[16 m + j] dX) --
-    constexpr int CT = DOUT / 16;  // output column tiles (channels m)
-    constexpr int KP = 4 / CT;     // waves per column tile, splitting j
+    constexpr int CT = DOUT / 16 / SPLIT;  // this workgroup's output column tiles (channels m)
+    constexpr int KP = 4 / CT;             // waves per column tile, splitting j
     constexpr int JP = 16 / KP;
-    const int ct = w % CT, kp = w / CT, j0 = kp * JP;
+    const int ct = ch * CT + w % CT, kp = w / CT, j0 = kp * JP;
     float dxr[2][JP];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int j = 0; j < JP; ++j) dxr[t][j] = sDx[(16 * t + lo) * 17 + j0 + j];
     floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    // one copy of the K loop per row-tile count (a per-MFMA branch on `two` costs a branch per MFMA)
+    auto kloop = [&](auto two_c) __attribute__((always_inline)) {
+      constexpr bool TWO = decltype(two_c)::value;
 #pragma unroll
-    for (int cc = 0; cc < NCC; ++cc) {
-      const floatx4 p0 = prow(0, cc), p1 = prow(1, cc);
+      for (int cc = 0; cc < NCC; ++cc) {
+        const floatx4 p0 = prow(0, cc), p1 = TWO ? prow(1, cc) : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll kJUnroll
-      for (int j = 0; j < JP; ++j) {
-        const floatx4 wv = W4[((ct * 16 + j0 + j) * NCC + cc) * 64 + lane];
-        const floatx4 a0 = p0 * dxr[0][j], a1 = p1 * dxr[1][j];
+        for (int j = 0; j < JP; ++j) {
+          const floatx4 wv = W4[((ct * 16 + j0 + j) * NCC + cc) * 64 + lane];
+          const floatx4 a0 = p0 * dxr[0][j], a1 = p1 * dxr[1][j];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          acc[0] = mfma4(a0[s], wv[s], acc[0]);
-          if (two) acc[1] = mfma4(a1[s], wv[s], acc[1]);
+          for (int s = 0; s < 4; ++s) {
+            acc[0] = mfma4(a0[s], wv[s], acc[0]);
+            if constexpr (TWO) acc[1] = mfma4(a1[s], wv[s], acc[1]);
+          }
         }
       }
-    }
+    };
+    if (two)
+      kloop(std::true_type{});
+    else
+      kloop(std::false_type{});
     // bias term of this wave's j range; rows 16 t + 4 hi + r, channel m = 16 ct + lo
     const int m = 16 * ct + lo;
 #pragma unroll
@@ -280,7 +331,7 @@ template <int DIN>
 size_t layer_smem(int n) {
   constexpr int ZS = zs_stride<DIN>();
   const int nk = (n + 15) & ~15;
-  return sizeof(float) * (4 * 2 * 64 * 4 + kRows * 17 + 12 + (size_t)(nk > 4 * kRows ? nk : 4 * kRows) * ZS);
+  return sizeof(float) * (4 * 2 * 64 * 4 + kRows * 17 + 12 + (size_t)(nk > 4 * kRows ? nk : 4 * kRows) * ZS + nk);
 }
 
 constexpr size_t kMaxSmem = 64 * 1024;  // the default dynamic-LDS limit of a launch
@@ -288,7 +339,8 @@ constexpr size_t kMaxSmem = 64 * 1024;  // the default dynamic-LDS limit of a la
 template <int DIN, int DOUT, int MODE>
 void launch(const LayerArgs& a, int B, hipStream_t st) {
   const size_t sm = layer_smem<DIN>(a.n);
-  hipLaunchKernelGGL((k_layer<DIN, DOUT, MODE>), dim3((a.n + kRows - 1) / kRows, B), dim3(256), sm, st, a);
+  const int split = (MODE == 2 && DOUT / 16 >= kSplit) ? kSplit : 1;
+  hipLaunchKernelGGL((k_layer<DIN, DOUT, MODE>), dim3((a.n + kRows - 1) / kRows * split, B), dim3(256), sm, st, a);
 }
 
 template <int DIN>
