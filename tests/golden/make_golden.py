@@ -291,6 +291,19 @@ def main():
     rng = np.random.default_rng(8642)
     grad_case(rng, "grad_rk4_cde_data_n9_h4_de3.npz", 2, 9, 5, "undirected", [4, 6, 0], "rk4", nsteps=8,
               cde=(4, 3), data_grad=True)
+    layer_cases()
+
+
+def layer_cases():
+    """Shapes of the fused generic layer kernel (csrc/gncde_layer.hip): widths 16 / 32 / 64, the CDE read-out with
+    de = 8 (one or two channel groups per row block), widening ODE layers, and n with a partial or single-row last
+    32-row block."""
+    rng = np.random.default_rng(1357)
+    cde_case(rng, "cde_n40_h16_de8.npz", 2, 40, 5, 16, 8, 2)
+    cde_case(rng, "cde_n33_h32_de8.npz", 2, 33, 5, 32, 8, 3)
+    cde_case(rng, "cde_n20_h64_de8.npz", 2, 20, 4, 64, 8, 2)
+    vf_case(rng, "vf_undirected_n65_w16_32_64.npz", 2, 65, 4, "undirected", [16, 32, 64])
+    vf_case(rng, "vf_directed_n48_h64_L2.npz", 2, 48, 4, "directed", [64, 64, 64])
 
 
 if __name__ == "__main__":

@@ -47,7 +47,10 @@ def problem_from(G, z, params, data=False):
 
 
 VF_FIXTURES = ["vf_undirected_n16_L3.npz", "vf_directed_n16_L2.npz", "vf_plain_n16_L2.npz",
-               "vf_undirected_n10_mixed.npz", "vf_undirected_n4_L2.npz"]
+               "vf_undirected_n10_mixed.npz", "vf_undirected_n4_L2.npz",
+               # k_layer (csrc/gncde_layer.hip): widening ODE layers 16 -> 32 -> 64 at n = 65 (single-row last row
+               # block), width 64 directed at n = 48 (partial second row tile)
+               "vf_undirected_n65_w16_32_64.npz", "vf_directed_n48_h64_L2.npz"]
 
 
 @pytest.mark.parametrize("name", VF_FIXTURES)
@@ -62,9 +65,12 @@ def test_vf_eval_matches_golden(gncde, golden_dir, name):
     assert err <= RTOL_VF
 
 
-@pytest.mark.parametrize("name", ["cde_n12_h8_de3.npz", "cde_n70_h5_de8.npz"])
+@pytest.mark.parametrize("name", ["cde_n12_h8_de3.npz", "cde_n70_h5_de8.npz", "cde_n40_h16_de8.npz",
+                                  "cde_n33_h32_de8.npz", "cde_n20_h64_de8.npz"])
 def test_cde_wrapper_vf_matches_golden(gncde, golden_dir, name):
-    """de = 3: separate contraction kernel; de = 8: contraction fused into the last layer's GEMM epilogue."""
+    """de = 3: separate contraction kernel; de = 8, h = 5: contraction in the last GEMM's epilogue; de = 8 with
+    h = 16 / 32 / 64: the read-out k_layer contracts dX inside its MFMA K loop (one or two channel groups per row
+    block)."""
     z = np.load(os.path.join(golden_dir, name))
     params = MG.load_layers(z)
     prob = problem_from(gncde, z, params, data=True)
