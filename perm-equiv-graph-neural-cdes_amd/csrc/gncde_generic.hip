@@ -9,6 +9,8 @@
 // (perm_equiv_graph_vector_field.py:122-128), CDE wrapper (cde_wrapper_vector_field.py:19-26).
 #include "gncde_internal.h"
 
+#include <utility>
+
 namespace gncde {
 namespace {
 
@@ -254,10 +256,10 @@ __global__ void k_finalize(int n, int dL, int h, int de, int T, const float* __r
 }
 
 // ---- solver helpers ---------------------------------------------------------------------------------
-// Per-sample step geometry for step k of the host-planned grid.
+// Per-sample step geometry for step k of the host-planned grid; tst = the first stage's time (c = 0).
 __global__ void k_grid_step(int B, int G, int k, const float* __restrict__ grid,
                             const int32_t* __restrict__ nsteps, float* __restrict__ tcur,
-                            float* __restrict__ hcur) {
+                            float* __restrict__ hcur, float* __restrict__ tst) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const float* g = grid + (size_t)b * G;
@@ -270,25 +272,24 @@ __global__ void k_grid_step(int B, int G, int k, const float* __restrict__ grid,
     tcur[b] = g[ns];
     hcur[b] = 0.f;
   }
+  tst[b] = tcur[b];
 }
 
-__global__ void k_stage_time(int B, float c, const float* __restrict__ tcur,
-                             const float* __restrict__ hcur, float* __restrict__ tst) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  tst[b] = stage_time(tcur[b], c, hcur[b]);
-}
-
-// out = y + h_b * sum_j a_j K_j   (up to 7 terms; K_j == nullptr terms skipped)
+// out = y + h_b * sum_j a_j K_j   (up to 7 terms; K_j == nullptr terms skipped), and (tst != nullptr) the next
+// stage's time t_b + c h_b (the stage-time launch folded in)
 struct Combo {
   const float* K[7];
   float a[7];
   int nk;
+  float c;
+  const float* tcur;
+  float* tst;
 };
 __global__ void k_combo(int B, size_t E, const float* __restrict__ y, Combo cb,
                         const float* __restrict__ hcur, float* __restrict__ out) {
   const int b = blockIdx.y;
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (cb.tst && e == 0) cb.tst[b] = stage_time(cb.tcur[b], cb.c, hcur[b]);
   if (e >= E) return;
   const size_t o = (size_t)b * E + e;
   float s = 0.f;
@@ -575,11 +576,10 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, 0, y, ys);
   generic_vf_prepare(p, ws, st);
 
-  auto eval = [&](float c, const float* yin, float* out) {
-    hipLaunchKernelGGL(k_stage_time, dim3(gb), dim3(256), 0, st, B, c, tcur, hcur, tst);
-    return generic_vf_eval(p, tst, yin, out, ws, st, true);
-  };
-  auto combo = [&](std::initializer_list<std::pair<int, float>> terms, float* out) {
+  // Every evaluation's stage time tst is written by the launch before it (k_grid_step for c = 0, k_combo for the
+  // others); the step's y <- y_{k+1} and Tsit5's FSAL k1 <- k7 are pointer swaps, not copies.
+  auto eval = [&](const float* yin, float* out) { return generic_vf_eval(p, tst, yin, out, ws, st, true); };
+  auto combo = [&](std::initializer_list<std::pair<int, float>> terms, float* out, float c_next, bool has_next) {
     Combo cb{};
     cb.nk = 0;
     for (auto& tr : terms) {
@@ -587,6 +587,9 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
       cb.a[cb.nk] = tr.second;
       cb.nk++;
     }
+    cb.c = c_next;
+    cb.tcur = tcur;
+    cb.tst = has_next ? tst : nullptr;
     hipLaunchKernelGGL(k_combo, ge, dim3(256), 0, st, B, E, y, cb, hcur, out);
   };
 
@@ -594,40 +597,40 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   const int steps = G - 1;
   if (s.method == GNCDE_RK4) {
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
-      hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur);
-      rc |= eval(0.0f, y, K[0]);
-      combo({{0, 0.5f}}, yt);
-      rc |= eval(0.5f, yt, K[1]);
-      combo({{1, 0.5f}}, yt);
-      rc |= eval(0.5f, yt, K[2]);
-      combo({{2, 1.0f}}, yt);
-      rc |= eval(1.0f, yt, K[3]);
+      hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst);
+      rc |= eval(y, K[0]);
+      combo({{0, 0.5f}}, yt, 0.5f, true);
+      rc |= eval(yt, K[1]);
+      combo({{1, 0.5f}}, yt, 0.5f, true);
+      rc |= eval(yt, K[2]);
+      combo({{2, 1.0f}}, yt, 1.0f, true);
+      rc |= eval(yt, K[3]);
       // y + h/6 (k1 + 2k2 + 2k3 + k4)
-      combo({{0, 1.0f / 6.0f}, {1, 2.0f / 6.0f}, {2, 2.0f / 6.0f}, {3, 1.0f / 6.0f}}, yt);
-      (void)hipMemcpyAsync(y, yt, B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
+      combo({{0, 1.0f / 6.0f}, {1, 2.0f / 6.0f}, {2, 2.0f / 6.0f}, {3, 1.0f / 6.0f}}, yt, 0.f, false);
+      std::swap(y, yt);
       if (s.save_mode == GNCDE_SAVE_STEPS)
         hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, k + 1, y, ys);
     }
   } else {  // Tsit5 on the grid (ConstantStepSize), FSAL
-    hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, 0, s.grid, s.nsteps, tcur, hcur);
-    rc |= eval(0.0f, y, K[0]);
+    hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, 0, s.grid, s.nsteps, tcur, hcur, tst);
+    rc |= eval(y, K[0]);
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
-      hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur);
-      combo({{0, TSIT5_A21}}, yt);
-      rc |= eval(TSIT5_C2, yt, K[1]);
-      combo({{0, TSIT5_A31}, {1, TSIT5_A32}}, yt);
-      rc |= eval(TSIT5_C3, yt, K[2]);
-      combo({{0, TSIT5_A41}, {1, TSIT5_A42}, {2, TSIT5_A43}}, yt);
-      rc |= eval(TSIT5_C4, yt, K[3]);
-      combo({{0, TSIT5_A51}, {1, TSIT5_A52}, {2, TSIT5_A53}, {3, TSIT5_A54}}, yt);
-      rc |= eval(TSIT5_C5, yt, K[4]);
-      combo({{0, TSIT5_A61}, {1, TSIT5_A62}, {2, TSIT5_A63}, {3, TSIT5_A64}, {4, TSIT5_A65}}, yt);
-      rc |= eval(1.0f, yt, K[5]);
-      combo({{0, TSIT5_B1}, {1, TSIT5_B2}, {2, TSIT5_B3}, {3, TSIT5_B4}, {4, TSIT5_B5}, {5, TSIT5_B6}},
-            yt);
-      rc |= eval(1.0f, yt, K[6]);
-      (void)hipMemcpyAsync(y, yt, B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
-      (void)hipMemcpyAsync(K[0], K[6], B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
+      hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst);
+      combo({{0, TSIT5_A21}}, yt, TSIT5_C2, true);
+      rc |= eval(yt, K[1]);
+      combo({{0, TSIT5_A31}, {1, TSIT5_A32}}, yt, TSIT5_C3, true);
+      rc |= eval(yt, K[2]);
+      combo({{0, TSIT5_A41}, {1, TSIT5_A42}, {2, TSIT5_A43}}, yt, TSIT5_C4, true);
+      rc |= eval(yt, K[3]);
+      combo({{0, TSIT5_A51}, {1, TSIT5_A52}, {2, TSIT5_A53}, {3, TSIT5_A54}}, yt, TSIT5_C5, true);
+      rc |= eval(yt, K[4]);
+      combo({{0, TSIT5_A61}, {1, TSIT5_A62}, {2, TSIT5_A63}, {3, TSIT5_A64}, {4, TSIT5_A65}}, yt, 1.0f, true);
+      rc |= eval(yt, K[5]);
+      combo({{0, TSIT5_B1}, {1, TSIT5_B2}, {2, TSIT5_B3}, {3, TSIT5_B4}, {4, TSIT5_B5}, {5, TSIT5_B6}}, yt, 1.0f,
+            true);
+      rc |= eval(yt, K[6]);
+      std::swap(y, yt);
+      std::swap(K[0], K[6]);
       if (s.save_mode == GNCDE_SAVE_STEPS)
         hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, k + 1, y, ys);
     }
