@@ -7,10 +7,12 @@
 // inv = the RMSNorm factor of each node row, q = (I + Abar) 1.  A workgroup owns 32 node rows R of one sample, so
 // nothing crosses workgroups inside a layer (the Linear-first order needs every row of m before the n x n product):
 //
-//   1. Z[b] (n x d_in, HBM/L2) -> LDS, each row scaled by its RMSNorm factor (row sum of squares on lane shuffles).
-//   2. P = (I + Abar)[R, :] Zs on v_mfma_f32_16x16x4f32: A operand = rows R of (I + Abar) straight from HBM/L2
-//      (one dwordx4 per lane per 16-deep K chunk, K permuted so a lane's 4 steps are 4 consecutive columns),
-//      B operand = Zs from LDS.  d_in / 16 column tiles per wave, the K range split over the remaining waves.
+//   1. Z[b] (n x d_in, HBM/L2) -> LDS with every load of a round in flight; each row's RMSNorm factor from LDS.
+//   2. P = (I + Abar)[R, :] diag(inv) Zs on v_mfma_f32_16x16x4f32: A operand = rows R of (I + Abar) straight from
+//      HBM/L2 (one dwordx4 per lane per 16-deep K chunk, K permuted so a lane's 4 steps are 4 consecutive columns)
+//      scaled by inv, B operand = Zs from LDS; the K range split over the four waves (each element loaded once per
+//      workgroup), the partials summed in LDS in a fixed order.  bf16 modes: v_mfma_f32_16x16x32_bf16 on the
+//      (hi, lo) planes of (I + Abar) against diag(inv) Zs split into (hi, lo) on the fly (three products).
 //   3. Z_next[R, :] = P W'^T on MFMA (P from LDS, W' pre-permuted into the lane order: one coalesced 1 KB load per
 //      wave per operand), epilogue q b'^T + ReLU, or tg * (.) for the ODE output layer.
 //   3'. The CDE-wrapper output layer (cde_wrapper_vector_field.py:19-26, de = 8) never forms the n x h*16 read-out:
@@ -29,6 +31,8 @@ namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned rows (n = 129, 255)
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x8u __attribute__((ext_vector_type(8), aligned(2)));  // 8 bf16 of an (I + Abar) plane row
 
 constexpr int kRows = 32;  // node rows per workgroup: two 16-row MFMA tiles
 #ifndef GNCDE_X_JUNROLL
@@ -43,6 +47,8 @@ constexpr int kSplit = GNCDE_X_SPLIT;  // CDE read-out: workgroups per row block
 struct LayerArgs {
   int n;
   const float* abar;   // (I + Abar_l) [B, n, n]
+  const uint16_t* abar16;  // bf16 modes: its hi plane [B, n, n] (lo plane a_lo elements later)
+  long a_lo;
   const float* Z;      // [B, n, DIN]
   const float* wperm;  // W' in the lane order of the kernel (permute_linear)
   const float* bf;     // b' [DOUT] (CDE: [16 H])
@@ -62,7 +68,9 @@ __host__ __device__ constexpr int zs_stride() {
 }
 
 // MODE 0: hidden layer, ReLU.  MODE 1: ODE output layer, out = tg * Z_next.  MODE 2: CDE output layer (DOUT = h).
-template <int DIN, int DOUT, int MODE>
+// BF: the n x n product on v_mfma_f32_16x16x32_bf16 (GNCDE_COMPUTE_BF16*): (I + Abar) from its bf16 (hi, lo) planes,
+// diag(inv) Z split into (hi, lo) on the fly, three products (hi hi, hi lo, lo hi) with fp32 accumulation.
+template <int DIN, int DOUT, int MODE, bool BF>
 __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int ZS = zs_stride<DIN>();
@@ -70,7 +78,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
   constexpr int KPP = 4;         // product K parts (one per wave)
   constexpr int NCC = DIN / 16;  // 16-deep K chunks of the Linear
   const int n = a.n;
-  const int nk = (n + 15) & ~15;
+  const int nk = BF ? (n + 31) & ~31 : (n + 15) & ~15;  // K rows of Zs: whole MFMA K chunks
   floatx4* red = reinterpret_cast<floatx4*>(smem);  // [4][2][64] K-part partials (MODE 2)
   float* sDx = smem + 4 * 2 * 64 * 4;               // [32][17] (MODE 2)
   float* Zs = sDx + kRows * 17 + 12;                // [nk][ZS] (16-byte aligned: 2048 + 556 is a multiple of 4)
@@ -125,7 +133,65 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
 
   // ---- 2. P = (I + Abar)[R, :] Zs: wave w takes the 16-deep K chunks w, w + 4, ... for every column tile, so each
   // (I + Abar) element is loaded once per workgroup; the four K partials meet in LDS (aliasing Zs) in a fixed order.
-  {
+  if constexpr (BF) {
+    // K chunks of 32: wave w takes chunks w, w + 4, ...; lane (lo, hi) holds A[row lo][32 kc + 8 hi .. +7] of each
+    // plane and B[32 kc + 8 hi + j][col lo], j < 8 (the MFMA 16x16x32 operand layout)
+    const uint16_t* Ab = a.abar16 + nb * n;
+    const int nch = nk >> 5;
+    const int ra0 = r0 + lo < n ? r0 + lo : n - 1, ra1 = r0 + 16 + lo < n ? r0 + 16 + lo : n - 1;
+    floatx4 acc[2][CTP];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ct = 0; ct < CTP; ++ct) acc[t][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+    auto ld8 = [&](const uint16_t* pa, int k) -> bf16x8 {
+      u16x8u u;
+      if (k + 8 <= n) {
+        u = *reinterpret_cast<const u16x8u*>(pa);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) u[j] = k + j < n ? pa[j] : (uint16_t)0;
+      }
+      return __builtin_bit_cast(bf16x8, u);
+    };
+    for (int kc = w; kc < nch; kc += 4) {
+      const int k = 32 * kc + 8 * hi;
+      bf16x8 ah[2], al[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const uint16_t* pa = Ab + (size_t)(t ? ra1 : ra0) * n + k;
+        ah[t] = ld8(pa, k);
+        al[t] = ld8(pa + a.a_lo, k);
+      }
+      float iv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) iv[j] = sInv[k + j];
+#pragma unroll
+      for (int ct = 0; ct < CTP; ++ct) {
+        bf16x8 bh, bl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = Zs[(k + j) * ZS + 16 * ct + lo] * iv[j];
+          bh[j] = (__bf16)x;
+          bl[j] = (__bf16)(x - (float)bh[j]);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (t == 1 && !two) break;
+          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[t], bh, acc[t][ct], 0, 0, 0);
+          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[t], bl, acc[t][ct], 0, 0, 0);
+          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[t], bh, acc[t][ct], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // Zs reads done: the partials alias it
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ct = 0; ct < CTP; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ps[(w * kRows + 16 * t + 4 * hi + r) * ZS + 16 * ct + lo] = acc[t][ct][r];
+  } else {
     const float* Ab = a.abar + nb * n;
     const int nch = nk >> 4;
     const int ra0 = r0 + lo < n ? r0 + lo : n - 1, ra1 = r0 + 16 + lo < n ? r0 + 16 + lo : n - 1;
@@ -328,28 +394,29 @@ __global__ void k_permute_linear(int rows, int din, int cde, const float* __rest
 }
 
 template <int DIN>
-size_t layer_smem(int n) {
+size_t layer_smem(int n, bool bf) {
   constexpr int ZS = zs_stride<DIN>();
-  const int nk = (n + 15) & ~15;
+  const int nk = bf ? (n + 31) & ~31 : (n + 15) & ~15;
   return sizeof(float) * (4 * 2 * 64 * 4 + kRows * 17 + 12 + (size_t)(nk > 4 * kRows ? nk : 4 * kRows) * ZS + nk);
 }
 
 constexpr size_t kMaxSmem = 64 * 1024;  // the default dynamic-LDS limit of a launch
 
-template <int DIN, int DOUT, int MODE>
+template <int DIN, int DOUT, int MODE, bool BF>
 void launch(const LayerArgs& a, int B, hipStream_t st) {
-  const size_t sm = layer_smem<DIN>(a.n);
+  const size_t sm = layer_smem<DIN>(a.n, BF);
   const int split = (MODE == 2 && DOUT / 16 >= kSplit) ? kSplit : 1;
-  hipLaunchKernelGGL((k_layer<DIN, DOUT, MODE>), dim3((a.n + kRows - 1) / kRows * split, B), dim3(256), sm, st, a);
+  hipLaunchKernelGGL((k_layer<DIN, DOUT, MODE, BF>), dim3((a.n + kRows - 1) / kRows * split, B), dim3(256), sm, st,
+                     a);
 }
 
-template <int DIN>
+template <int DIN, bool BF>
 bool dispatch_dout(const LayerArgs& a, int B, int dout, int mode, hipStream_t st) {
 #define GNCDE_LAYER_CASE(D)                                      \
   if (dout == D) {                                               \
-    if (mode == 0) launch<DIN, D, 0>(a, B, st);                  \
-    else if (mode == 1) launch<DIN, D, 1>(a, B, st);             \
-    else launch<DIN, D, 2>(a, B, st);                            \
+    if (mode == 0) launch<DIN, D, 0, BF>(a, B, st);              \
+    else if (mode == 1) launch<DIN, D, 1, BF>(a, B, st);         \
+    else launch<DIN, D, 2, BF>(a, B, st);                        \
     return true;                                                 \
   }
   GNCDE_LAYER_CASE(16)
@@ -364,7 +431,6 @@ bool width_ok(int d) { return d == 16 || d == 32 || d == 64; }
 }  // namespace
 
 int layer_mode(const GncdeProblem& p, int l) {
-  if (p.compute != GNCDE_COMPUTE_FP32) return -1;
   const int din = p.dims[l], dout = p.dims[l + 1];
   if (!width_ok(din)) return -1;
   const bool last = l == p.L - 1;
@@ -376,7 +442,8 @@ int layer_mode(const GncdeProblem& p, int l) {
     if (!width_ok(dout)) return -1;
     mode = last ? 1 : 0;
   }
-  size_t sm = din == 16 ? layer_smem<16>(p.n) : (din == 32 ? layer_smem<32>(p.n) : layer_smem<64>(p.n));
+  const bool bf = p.compute != GNCDE_COMPUTE_FP32;
+  size_t sm = din == 16 ? layer_smem<16>(p.n, bf) : (din == 32 ? layer_smem<32>(p.n, bf) : layer_smem<64>(p.n, bf));
   return sm <= kMaxSmem ? mode : -1;
 }
 
@@ -399,9 +466,17 @@ void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, cons
   a.dx = dx;
   const int din = p.dims[l];
   const int dout = mode == 2 ? p.cde_hidden : p.dims[l + 1];
-  if (din == 16) dispatch_dout<16>(a, p.B, dout, mode, st);
-  else if (din == 32) dispatch_dout<32>(a, p.B, dout, mode, st);
-  else dispatch_dout<64>(a, p.B, dout, mode, st);
+  if (p.compute != GNCDE_COMPUTE_FP32) {  // abar is the hi plane of the layer's bf16 (hi, lo) pair (abar_layer)
+    a.abar16 = reinterpret_cast<const uint16_t*>(abar);
+    a.a_lo = (long)p.L * p.B * p.n * p.n;
+    if (din == 16) dispatch_dout<16, true>(a, p.B, dout, mode, st);
+    else if (din == 32) dispatch_dout<32, true>(a, p.B, dout, mode, st);
+    else dispatch_dout<64, true>(a, p.B, dout, mode, st);
+    return;
+  }
+  if (din == 16) dispatch_dout<16, false>(a, p.B, dout, mode, st);
+  else if (din == 32) dispatch_dout<32, false>(a, p.B, dout, mode, st);
+  else dispatch_dout<64, false>(a, p.B, dout, mode, st);
 }
 
 }  // namespace gncde

@@ -24,7 +24,10 @@ RTOL_BF16_VF = 1e-4
 RTOL_BF16_SOLVE = 5e-4
 VF_CASES = [("vf_undirected_n16_L3.npz", False), ("vf_directed_n16_L2.npz", False),
             ("vf_undirected_n10_mixed.npz", False), ("vf_plain_n16_L2.npz", False),
-            ("cde_n70_h5_de8.npz", True), ("cde_n12_h8_de3.npz", True)]
+            ("cde_n70_h5_de8.npz", True), ("cde_n12_h8_de3.npz", True),
+            # the bf16 product inside k_layer (csrc/gncde_layer.hip): K chunks of 32 with n = 65 / 48 / 40 / 33
+            ("vf_undirected_n65_w16_32_64.npz", False), ("vf_directed_n48_h64_L2.npz", False),
+            ("cde_n40_h16_de8.npz", True), ("cde_n33_h32_de8.npz", True)]
 
 
 @pytest.fixture(scope="module")
