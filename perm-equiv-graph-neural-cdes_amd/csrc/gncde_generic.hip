@@ -145,17 +145,24 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
   __shared__ float cs[2][2][32];  // [i-range / k-range][A / dA][32]
   __shared__ float tot[2][4];
   const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;  // 32 x 8
-  for (int y = ty; y < 32; y += 8) {
-    const int k = k0 + y, i = i0 + tx;
-    const bool ok = k < n && i < n;
-    tA[y][tx] = ok ? Ab[(size_t)k * n + i] : 0.f;
-    tD[y][tx] = ok ? dAb[(size_t)k * n + i] : 0.f;
+  // Every tile load is issued before the first use (one HBM round trip): the transposed tile (for LDS) and this
+  // thread's own (i, k) elements, rows ty + 8 q.
+  float ta[4], td[4], aik[4], dik[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int y = ty + 8 * q;
+    const bool okt = k0 + y < n && i0 + tx < n, oko = i0 + y < n && k0 + tx < n;
+    ta[q] = okt ? Ab[(size_t)(k0 + y) * n + i0 + tx] : 0.f;
+    td[q] = okt ? dAb[(size_t)(k0 + y) * n + i0 + tx] : 0.f;
+    aik[q] = oko ? Ab[(size_t)(i0 + y) * n + k0 + tx] : 0.f;
+    dik[q] = oko ? dAb[(size_t)(i0 + y) * n + k0 + tx] : 0.f;
   }
   if (tid < 128) {  // column sums of A / dA over the slabs for columns i0 + x and k0 + x
     const int which = tid >> 6, q = (tid >> 5) & 1, x = tid & 31;
     const int col = (which ? k0 : i0) + x;
     float c = 0.f;
     if (col < n)
+#pragma unroll 8
       for (int sl = 0; sl < slabs; ++sl) c += pb[(size_t)sl * 2 * n + q * n + col];
     cs[which][q][x] = c;
     if (which == 1 && blockIdx.y == 0 && col < n) rb[(2 + q) * n + col] = c;
@@ -165,6 +172,11 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
     for (int i = lane; i < n; i += 64) x += rb[w * n + i];
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
     if (lane == 0) tot[w][0] = x;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    tA[ty + 8 * q][tx] = ta[q];
+    tD[ty + 8 * q][tx] = td[q];
   }
   __syncthreads();
   const float s = tot[0][0], sd = tot[1][0];
@@ -206,15 +218,17 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
                    fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
   }
   __syncthreads();
-  for (int y = ty; y < 32; y += 8) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int y = ty + 8 * q;
     const int i = i0 + y, k = k0 + tx;
     if (i >= n || k >= n) continue;
-    const float aik = Ab[(size_t)i * n + k], dik = dAb[(size_t)i * n + k];
     const float aki = tA[tx][y], dki = tD[tx][y];
     const bool diag = i == k;
     for (int l = 0; l < L; ++l) {
       const float* fc = fus + l * GNCDE_FC;
-      float v = fc[GNCDE_FC_E_A] * aik + fc[GNCDE_FC_E_DA] * dik + fc[GNCDE_FC_ET_A] * aki + fc[GNCDE_FC_ET_DA] * dki;
+      float v = fc[GNCDE_FC_E_A] * aik[q] + fc[GNCDE_FC_E_DA] * dik[q] + fc[GNCDE_FC_ET_A] * aki +
+                fc[GNCDE_FC_ET_DA] * dki;
       v += sWv[l][0][y] + sWv[l][1][tx];
       if (diag) v += sWv[l][2][y];
       abar_store(out, l * layer_stride + b * nn + (size_t)i * n + k, (size_t)L * layer_stride, v);
