@@ -238,13 +238,17 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
           const int kc = kr + 4 * c;
           if (kc >= nch) break;
           const float* zb = Zs + (16 * kc + 4 * hi) * ZS + lo;
+          float bv[4][CTP];  // the chunk's B operands: every LDS read issued before the first MFMA
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int ct = 0; ct < CTP; ++ct) bv[s][ct] = zb[s * ZS + 16 * ct];
 #pragma unroll
           for (int s = 0; s < 4; ++s)
 #pragma unroll
             for (int ct = 0; ct < CTP; ++ct) {
-              const float bv = zb[s * ZS + 16 * ct];
-              acc[0][ct] = mfma4(av[c][0][s], bv, acc[0][ct]);
-              if constexpr (TWO) acc[1][ct] = mfma4(av[c][1][s], bv, acc[1][ct]);
+              acc[0][ct] = mfma4(av[c][0][s], bv[s][ct], acc[0][ct]);
+              if constexpr (TWO) acc[1][ct] = mfma4(av[c][1][s], bv[s][ct], acc[1][ct]);
             }
         }
       };
@@ -315,19 +319,26 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
       for (int j = 0; j < JP; ++j) dxr[t][j] = sDx[(16 * t + lo) * 17 + j0 + j];
     floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     // one copy of the K loop per row-tile count (a per-MFMA branch on `two` costs a branch per MFMA)
+    // Per 16-deep c chunk: all JP W' operand loads are issued first (one L2 round trip per chunk), the next chunk's
+    // while this one's MFMAs run; the j loop is fully unrolled so dX stays in statically indexed registers.
     auto kloop = [&](auto two_c) __attribute__((always_inline)) {
       constexpr bool TWO = decltype(two_c)::value;
+      floatx4 wv[2][JP];
+#pragma unroll
+      for (int j = 0; j < JP; ++j) wv[0][j] = W4[((ct * 16 + j0 + j) * NCC + 0) * 64 + lane];
 #pragma unroll
       for (int cc = 0; cc < NCC; ++cc) {
+        if (cc + 1 < NCC)
+#pragma unroll
+          for (int j = 0; j < JP; ++j) wv[(cc + 1) & 1][j] = W4[((ct * 16 + j0 + j) * NCC + cc + 1) * 64 + lane];
         const floatx4 p0 = prow(0, cc), p1 = TWO ? prow(1, cc) : floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll kJUnroll
+#pragma unroll
         for (int j = 0; j < JP; ++j) {
-          const floatx4 wv = W4[((ct * 16 + j0 + j) * NCC + cc) * 64 + lane];
           const floatx4 a0 = p0 * dxr[0][j], a1 = p1 * dxr[1][j];
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
-            acc[0] = mfma4(a0[s], wv[s], acc[0]);
-            if constexpr (TWO) acc[1] = mfma4(a1[s], wv[s], acc[1]);
+            acc[0] = mfma4(a0[s], wv[cc & 1][j][s], acc[0]);
+            if constexpr (TWO) acc[1] = mfma4(a1[s], wv[cc & 1][j][s], acc[1]);
           }
         }
       }
