@@ -39,6 +39,9 @@ constexpr int kRows = 32;  // node rows per workgroup: two 16-row MFMA tiles
 #define GNCDE_X_JUNROLL 4
 #endif
 constexpr int kJUnroll = GNCDE_X_JUNROLL;  // read-out K loop: W' operand loads in flight per wave
+#ifndef GNCDE_X_LSKIP  // diagnostic builds only: 1/2/3 skip the product MFMAs / the read-out MFMAs / the Z loads
+#define GNCDE_X_LSKIP 0
+#endif
 #ifndef GNCDE_X_SPLIT
 #define GNCDE_X_SPLIT 2
 #endif
@@ -103,7 +106,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = e0 + 256 * u;
-        v[u] = e < valid ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
+        v[u] = (e < valid && GNCDE_X_LSKIP != 3) ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -252,7 +255,8 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
             }
         }
       };
-      if (two)
+      if (GNCDE_X_LSKIP == 1) {
+      } else if (two)
         mm(std::true_type{});
       else
         mm(std::false_type{});
@@ -343,7 +347,8 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         }
       }
     };
-    if (two)
+    if (GNCDE_X_LSKIP == 2) {
+    } else if (two)
       kloop(std::true_type{});
     else
       kloop(std::false_type{});
