@@ -277,3 +277,41 @@ def test_config2_full_batch_properties(gncde):
     err = rel_err(ysP.cpu().numpy(), ys1[:, P].cpu().numpy())
     print(f"permutation equivariance rel err {err:.3e}")
     assert err <= RTOL_SOLVE
+
+
+@pytest.mark.parametrize("B,n,T,h,L,t1,dt", [(64, 129, 4, 64, 3, 3.0, 0.1),    # BASELINE config 3 (England shape)
+                                             (16, 255, 3, 32, 4, 1.0, 0.05)])  # config 5 shape, fixed grid
+def test_generic_cde_full_size_properties(gncde, B, n, T, h, L, t1, dt):
+    """Full BASELINE sizes on the generic path (spline, (I+Abar), one k_layer per layer with the CDE read-out
+    contracted in the MFMA loop): run-to-run bitwise determinism (fixed-order sums, no atomics) and permutation
+    equivariance (permuting the nodes of the operator path, the data path and the state permutes the result) of one
+    evaluation and of a Tsit5 solve.  No oracle at this size: these properties are size-independent.  A permutation
+    changes the fp32 summation order, and this synthetic operator path (normalised Laplacians of log-normal weights)
+    amplifies rounding over a solve, so the solve's equivariance error is bounded by 10x the solve's own response to
+    a one-ulp perturbation of y0 (and by RTOL_SOLVE when that is larger)."""
+    from gncde import layout, synthetic
+    G = gncde
+    prob, y0 = synthetic.cde_batch(B, n, T, h, 8, L, t1, seed=5)
+    P = torch.randperm(n, generator=torch.Generator().manual_seed(1)).cuda()
+    probP = G.Problem(ts=prob.ts, coef=prob.coef[:, :, :, P][:, :, :, :, P].contiguous(),
+                      tcoef=prob.tcoef[..., P].contiguous(), fusion=prob.fusion, params=prob.params,
+                      dims=prob.dims, data_coef=prob.data_coef[:, :, :, P].contiguous(), cde_hidden=h, cde_embed=8)
+    t = (prob.ts[:, 0] + 0.37 * (prob.ts[:, 1] - prob.ts[:, 0])).contiguous()
+    dy = G.vf_eval(prob, t, y0)
+    dyP = G.vf_eval(probP, t, y0[:, P].contiguous())
+    err_vf = rel_err(dyP.cpu().numpy(), dy[:, P].cpu().numpy())
+    grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, t1, dt)] * B)
+    spec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=grid, nsteps=ns)
+    assert G.integrate_path(prob, spec) == "generic"
+    ys1 = G.integrate(prob, spec, y0)
+    ys2 = G.integrate(prob, spec, y0)
+    assert torch.equal(ys1, ys2)
+    assert torch.isfinite(ys1).all()
+    ysP = G.integrate(probP, spec, y0[:, P].contiguous())
+    err = rel_err(ysP.cpu().numpy(), ys1[:, P].cpu().numpy())
+    ulp = torch.where(torch.rand(y0.shape, generator=torch.Generator().manual_seed(2)) < 0.5, -1.0, 1.0).cuda()
+    y0e = y0 * (1.0 + ulp * 2.0 ** -24)
+    sens = rel_err(G.integrate(prob, spec, y0e).cpu().numpy(), ys1.cpu().numpy())
+    print(f"n={n}: equivariance one eval {err_vf:.3e}, solve {err:.3e} (solve response to a 1-ulp y0 change {sens:.3e})")
+    assert err_vf <= RTOL_VF
+    assert err <= max(RTOL_SOLVE, 10.0 * sens)
