@@ -56,6 +56,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="3,4,5")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--batch5", type=int, default=16, help="config 5 windows per launch (the TGB trainer uses 1)")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     import gncde
@@ -73,7 +74,7 @@ def main():
             spec = gncde.SolverSpec(method=L.RK4, save_mode=L.SAVE_T1, grid=grid, nsteps=ns)
             run("4_gene_n128_h16_L2_rk4x100", prob, spec, y0, args.reps)
         elif c == "5":  # TGB-trade-shaped: n=255, h=32, L=4, de=8, d_L=512, Tsit5 + PID on [0, 1], B=16
-            prob, y0 = synthetic.cde_batch(16, 255, 3, 32, 8, 4, 1.0)
+            prob, y0 = synthetic.cde_batch(args.batch5, 255, 3, 32, 8, 4, 1.0)
             B = prob.B
             spec = gncde.SolverSpec(method=L.TSIT5, controller=L.CTRL_PID, save_mode=L.SAVE_T1, rtol=1e-3, atol=1e-6,
                                     t0=torch.zeros(B, device="cuda"), t1=torch.ones(B, device="cuda"),
