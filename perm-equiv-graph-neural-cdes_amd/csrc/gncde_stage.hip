@@ -122,7 +122,7 @@ __global__ void k_stage_prep(const float* __restrict__ params, float* __restrict
   }
 }
 
-enum { kEval1 = 0, kEval2 = 1, kVjpMid = 2, kVjpPair = 3, kBoundary = 4 };
+enum { kEval1 = 0, kEval2 = 1, kVjpMid = 2, kVjpPair = 3, kBoundary = 4, kEvalRk4 = 5, kBoundaryPair = 6 };
 
 struct RevArgs {
   int n, T, G, k, S, stage, has_next, has_cur, write_next;
@@ -155,7 +155,7 @@ struct RevArgs {
 //             k and its last stage (has_cur) -> gyacc, gK_j.  has_cur == 0 writes gy0 = lambda_0.
 template <int NP, int L, int PROG>
 __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
-  constexpr bool VJP = PROG >= kVjpMid;
+  constexpr bool VJP = PROG == kVjpMid || PROG == kVjpPair || PROG == kBoundary || PROG == kBoundaryPair;
   constexpr int NT = NP * 4;
   constexpr int NW = NP / 16;
   constexpr int KS = NP / 4;
@@ -555,7 +555,8 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
   float tk = 0.f, hk = 0.f;
   if (k >= 0) geom(k, tk, hk);
 
-  if constexpr (PROG == kEval1) {
+  if constexpr (!VJP) {
+  if constexpr (PROG == kEval1 || PROG == kEvalRk4) {
     const int i = a.stage;
     float y[4], U[4];
     load4(a.ys, rowk(k), y);
@@ -592,8 +593,8 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       for (int r = 0; r < 4; ++r) Un[r] = fmaf(hk, Un[r], y[r]);
       store4(a.U[i + 1], rowoff, Un);
     }
-    return;
-  } else if constexpr (PROG == kEval2) {  // RK4: stages 1 and 2 share t + h/2
+  }
+  if constexpr (PROG == kEval2 || PROG == kEvalRk4) {  // RK4: stages 1 and 2 share t + h/2
     float y[4], K0[4], U[4], Kv[4];
     load4(a.ys, rowk(k), y);
     load4(a.K[0], rowoff, K0);
@@ -614,7 +615,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) U[r] = fmaf(hk, Kv[r], y[r]);
     store4(a.U[3], rowoff, U);
-    return;
+  }
   } else {
     if constexpr (PROG == kVjpMid) {
       const int i = a.stage;
@@ -636,33 +637,8 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         for (int r = 0; r < 4; ++r) acc[r] = fmaf(cf, gU[r], acc[r]);
         store4(a.gK[j], rowoff, acc);
       }
-    } else if constexpr (PROG == kVjpPair) {  // RK4 stages 2 then 1 at t + h/2
-      float U[4], gK[4], gU[4], gy[4], g1[4];
-      load4(a.U[2], rowoff, U);
-      load4(a.gK[2], rowoff, gK);
-      form(stage_time(tk, 0.5f, hk));
-      forward(U);
-      backward(gK, gU);
-      load4(a.gyacc, rowoff, gy);
-      load4(a.gK[1], rowoff, g1);
-      const float hh = 0.5f * hk;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        gy[r] += gU[r];
-        g1[r] = fmaf(hh, gU[r], g1[r]);  // a[2][1] = 1/2
-      }
-      load4(a.U[1], rowoff, U);
-      forward(U);
-      backward(g1, gU);
-      load4(a.gK[0], rowoff, g1);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        gy[r] += gU[r];
-        g1[r] = fmaf(hh, gU[r], g1[r]);  // a[1][0] = 1/2
-      }
-      store4(a.gyacc, rowoff, gy);
-      store4(a.gK[0], rowoff, g1);
-    } else {  // kBoundary
+    }
+    if constexpr (PROG == kBoundary || PROG == kBoundaryPair) {
       const int S = a.S;
       float lam[4];
       float tn = 0.f, hn = 0.f;
@@ -710,6 +686,35 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       } else {
         store4(a.gy0, rowoff, lam);
       }
+    }
+    // RK4 stages 2 then 1 at t + h/2 (kBoundaryPair: right after the boundary, one launch and one gradient
+    // reduction for both)
+    if constexpr (PROG == kVjpPair || PROG == kBoundaryPair) {
+      float U[4], gK[4], gU[4], gy[4], g1[4];
+      load4(a.U[2], rowoff, U);
+      load4(a.gK[2], rowoff, gK);
+      form(stage_time(tk, 0.5f, hk));
+      forward(U);
+      backward(gK, gU);
+      load4(a.gyacc, rowoff, gy);
+      load4(a.gK[1], rowoff, g1);
+      const float hh = 0.5f * hk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gy[r] += gU[r];
+        g1[r] = fmaf(hh, gU[r], g1[r]);  // a[2][1] = 1/2
+      }
+      load4(a.U[1], rowoff, U);
+      forward(U);
+      backward(g1, gU);
+      load4(a.gK[0], rowoff, g1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gy[r] += gU[r];
+        g1[r] = fmaf(hh, gU[r], g1[r]);  // a[1][0] = 1/2
+      }
+      store4(a.gyacc, rowoff, gy);
+      store4(a.gK[0], rowoff, g1);
     }
     // ---- cross-wave reduction of the gradient accumulators, += into this sample's block --------------
     __syncthreads();
@@ -765,12 +770,12 @@ __global__ void k_lam_init(size_t E, int G, int steps, const float* __restrict__
 typedef void (*RevFn)(RevArgs);
 struct RevEntry {
   int np, l;
-  RevFn fn[5];
+  RevFn fn[7];
 };
 
 #define GNCDE_REV(NP, L) \
   {NP, L, {k_rev<NP, L, kEval1>, k_rev<NP, L, kEval2>, k_rev<NP, L, kVjpMid>, k_rev<NP, L, kVjpPair>, \
-           k_rev<NP, L, kBoundary>}}
+           k_rev<NP, L, kBoundary>, k_rev<NP, L, kEvalRk4>, k_rev<NP, L, kBoundaryPair>}}
 const RevEntry kRev[] = {
     GNCDE_REV(16, 1),  GNCDE_REV(16, 2),  GNCDE_REV(16, 3),  GNCDE_REV(16, 4),
     GNCDE_REV(32, 1),  GNCDE_REV(32, 2),  GNCDE_REV(32, 3),  GNCDE_REV(32, 4),
@@ -901,8 +906,7 @@ int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float
     if (rk4) {
       a.stage = 0;
       a.write_next = 0;
-      hipLaunchKernelGGL(e->fn[kEval1], grid, wg, 0, st, a);
-      hipLaunchKernelGGL(e->fn[kEval2], grid, wg, 0, st, a);
+      hipLaunchKernelGGL(e->fn[kEvalRk4], grid, wg, 0, st, a);  // stage 0 at t, then stages 1, 2 at t + h/2
     } else {
       for (int i = 0; i + 1 < a.S; ++i) {
         a.stage = i;
@@ -912,10 +916,10 @@ int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float
     }
     a.has_next = (k + 1 <= G - 2) ? 1 : 0;
     a.has_cur = 1;
-    hipLaunchKernelGGL(e->fn[kBoundary], grid, wg, 0, st, a);
     if (rk4) {
-      hipLaunchKernelGGL(e->fn[kVjpPair], grid, wg, 0, st, a);
+      hipLaunchKernelGGL(e->fn[kBoundaryPair], grid, wg, 0, st, a);  // boundary at t_{k+1}, then stages 2, 1
     } else {
+      hipLaunchKernelGGL(e->fn[kBoundary], grid, wg, 0, st, a);
       for (int i = a.S - 2; i >= 1; --i) {
         a.stage = i;
         hipLaunchKernelGGL(e->fn[kVjpMid], grid, wg, 0, st, a);
