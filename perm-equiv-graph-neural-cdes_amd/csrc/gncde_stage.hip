@@ -122,7 +122,7 @@ __global__ void k_stage_prep(const float* __restrict__ params, float* __restrict
   }
 }
 
-enum { kEval1 = 0, kEval2 = 1, kVjpMid = 2, kVjpPair = 3, kBoundary = 4, kEvalRk4 = 5, kBoundaryPair = 6 };
+enum { kEval1 = 0, kEval2 = 1, kVjpMid = 2, kVjpPair = 3, kBoundary = 4, kEvalRk4 = 5, kBoundaryPair = 6, kStepRk4 = 7 };
 
 struct RevArgs {
   int n, T, G, k, S, stage, has_next, has_cur, write_next;
@@ -155,7 +155,9 @@ struct RevArgs {
 //             k and its last stage (has_cur) -> gyacc, gK_j.  has_cur == 0 writes gy0 = lambda_0.
 template <int NP, int L, int PROG>
 __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
-  constexpr bool VJP = PROG == kVjpMid || PROG == kVjpPair || PROG == kBoundary || PROG == kBoundaryPair;
+  constexpr bool EVAL_RK4 = PROG == kEvalRk4 || PROG == kStepRk4;  // stage 0 at t, then stages 1, 2 at t + h/2
+  constexpr bool BOUND_PAIR = PROG == kBoundaryPair || PROG == kStepRk4;  // boundary at t_{k+1}, then stages 2, 1
+  constexpr bool VJP = PROG == kVjpMid || PROG == kVjpPair || PROG == kBoundary || BOUND_PAIR;
   constexpr int NT = NP * 4;
   constexpr int NW = NP / 16;
   constexpr int KS = NP / 4;
@@ -555,8 +557,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
   float tk = 0.f, hk = 0.f;
   if (k >= 0) geom(k, tk, hk);
 
-  if constexpr (!VJP) {
-  if constexpr (PROG == kEval1 || PROG == kEvalRk4) {
+  if constexpr (PROG == kEval1 || EVAL_RK4) {
     const int i = a.stage;
     float y[4], U[4];
     load4(a.ys, rowk(k), y);
@@ -594,7 +595,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       store4(a.U[i + 1], rowoff, Un);
     }
   }
-  if constexpr (PROG == kEval2 || PROG == kEvalRk4) {  // RK4: stages 1 and 2 share t + h/2
+  if constexpr (PROG == kEval2 || EVAL_RK4) {  // RK4: stages 1 and 2 share t + h/2
     float y[4], K0[4], U[4], Kv[4];
     load4(a.ys, rowk(k), y);
     load4(a.K[0], rowoff, K0);
@@ -616,7 +617,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
     for (int r = 0; r < 4; ++r) U[r] = fmaf(hk, Kv[r], y[r]);
     store4(a.U[3], rowoff, U);
   }
-  } else {
+  if constexpr (VJP) {
     if constexpr (PROG == kVjpMid) {
       const int i = a.stage;
       float U[4], gK[4], gU[4], acc[4];
@@ -638,7 +639,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         store4(a.gK[j], rowoff, acc);
       }
     }
-    if constexpr (PROG == kBoundary || PROG == kBoundaryPair) {
+    if constexpr (PROG == kBoundary || BOUND_PAIR) {
       const int S = a.S;
       float lam[4];
       float tn = 0.f, hn = 0.f;
@@ -689,7 +690,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
     }
     // RK4 stages 2 then 1 at t + h/2 (kBoundaryPair: right after the boundary, one launch and one gradient
     // reduction for both)
-    if constexpr (PROG == kVjpPair || PROG == kBoundaryPair) {
+    if constexpr (PROG == kVjpPair || BOUND_PAIR) {
       float U[4], gK[4], gU[4], gy[4], g1[4];
       load4(a.U[2], rowoff, U);
       load4(a.gK[2], rowoff, gK);
@@ -770,12 +771,12 @@ __global__ void k_lam_init(size_t E, int G, int steps, const float* __restrict__
 typedef void (*RevFn)(RevArgs);
 struct RevEntry {
   int np, l;
-  RevFn fn[7];
+  RevFn fn[8];
 };
 
 #define GNCDE_REV(NP, L) \
   {NP, L, {k_rev<NP, L, kEval1>, k_rev<NP, L, kEval2>, k_rev<NP, L, kVjpMid>, k_rev<NP, L, kVjpPair>, \
-           k_rev<NP, L, kBoundary>, k_rev<NP, L, kEvalRk4>, k_rev<NP, L, kBoundaryPair>}}
+           k_rev<NP, L, kBoundary>, k_rev<NP, L, kEvalRk4>, k_rev<NP, L, kBoundaryPair>, k_rev<NP, L, kStepRk4>}}
 const RevEntry kRev[] = {
     GNCDE_REV(16, 1),  GNCDE_REV(16, 2),  GNCDE_REV(16, 3),  GNCDE_REV(16, 4),
     GNCDE_REV(32, 1),  GNCDE_REV(32, 2),  GNCDE_REV(32, 3),  GNCDE_REV(32, 4),
@@ -903,27 +904,23 @@ int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float
   const dim3 grid(B), wg(e->np * 4);
   for (int k = G - 2; k >= 0; --k) {
     a.k = k;
-    if (rk4) {
-      a.stage = 0;
-      a.write_next = 0;
-      hipLaunchKernelGGL(e->fn[kEvalRk4], grid, wg, 0, st, a);  // stage 0 at t, then stages 1, 2 at t + h/2
-    } else {
-      for (int i = 0; i + 1 < a.S; ++i) {
-        a.stage = i;
-        a.write_next = (i + 2 == a.S) ? 1 : 0;
-        hipLaunchKernelGGL(e->fn[kEval1], grid, wg, 0, st, a);
-      }
-    }
     a.has_next = (k + 1 <= G - 2) ? 1 : 0;
     a.has_cur = 1;
-    if (rk4) {
-      hipLaunchKernelGGL(e->fn[kBoundaryPair], grid, wg, 0, st, a);  // boundary at t_{k+1}, then stages 2, 1
-    } else {
-      hipLaunchKernelGGL(e->fn[kBoundary], grid, wg, 0, st, a);
-      for (int i = a.S - 2; i >= 1; --i) {
-        a.stage = i;
-        hipLaunchKernelGGL(e->fn[kVjpMid], grid, wg, 0, st, a);
-      }
+    if (rk4) {  // one launch per step: stage 0 at t, stages 1, 2 at t + h/2, boundary at t_{k+1}, stages 2, 1
+      a.stage = 0;
+      a.write_next = 0;
+      hipLaunchKernelGGL(e->fn[kStepRk4], grid, wg, 0, st, a);
+      continue;
+    }
+    for (int i = 0; i + 1 < a.S; ++i) {
+      a.stage = i;
+      a.write_next = (i + 2 == a.S) ? 1 : 0;
+      hipLaunchKernelGGL(e->fn[kEval1], grid, wg, 0, st, a);
+    }
+    hipLaunchKernelGGL(e->fn[kBoundary], grid, wg, 0, st, a);
+    for (int i = a.S - 2; i >= 1; --i) {
+      a.stage = i;
+      hipLaunchKernelGGL(e->fn[kVjpMid], grid, wg, 0, st, a);
     }
   }
   // stage 0 of step 0 closes lambda_0 = dL/dy0
