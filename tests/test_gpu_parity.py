@@ -315,3 +315,39 @@ def test_generic_cde_full_size_properties(gncde, B, n, T, h, L, t1, dt):
     print(f"n={n}: equivariance one eval {err_vf:.3e}, solve {err:.3e} (solve response to a 1-ulp y0 change {sens:.3e})")
     assert err_vf <= RTOL_VF
     assert err <= max(RTOL_SOLVE, 10.0 * sens)
+
+
+@pytest.mark.parametrize("n,dims,kind,cde", [(300, [32, 32, 32], "undirected", None),   # product K in two rounds
+                                             (272, [16, 16, 256], "directed", (16, 8))])  # + CDE read-out
+def test_generic_vf_large_n_vs_oracle(gncde, n, dims, kind, cde):
+    """n > 256: the fused layer kernel's product runs more than one round of K chunks per wave; one evaluation
+    against the fp64 oracle computed here (no fixture: the coefficients alone would be megabytes)."""
+    from tests.golden import make_golden as MG2
+    rng = np.random.default_rng(n)
+    B, T = 2, 4
+    ts, coeffs, params = MG2.problem(rng, B, n, T, kind, dims)
+    kw, dco = {}, None
+    if cde is not None:
+        h, de = cde
+        dco = []
+        for b in range(B):
+            x = rng.standard_normal((T, n, de))
+            X = np.stack([np.broadcast_to(ts[b][:, None, None], x.shape), x], axis=-1)
+            dco.append(O.backward_hermite_coefficients(ts[b], X))
+        dcoeffs = tuple(np.stack([c[q] for c in dco]) for q in range(4))
+        kw = dict(data_coeffs=dcoeffs, cde_hidden=h, cde_embed=de)
+    prob = gncde.make_problem(ts, coeffs, params.kind, params.layers, **kw)
+    y = rng.standard_normal((B, n, dims[0]))
+    t = np.array([rng.uniform(ts[b, 0], ts[b, -1]) for b in range(B)], dtype=np.float32).astype(np.float64)
+    dy = gncde.vf_eval(prob, torch.tensor(t, dtype=torch.float32, device="cuda"),
+                       torch.tensor(y, dtype=torch.float32, device="cuda")).cpu().numpy()
+    for b in range(B):
+        ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
+        if cde is None:
+            ref = O.vector_field(params, t[b], y[b], ctrl)
+        else:
+            cd = O.CubicInterpolation(ts[b], tuple(c[b] for c in dcoeffs))
+            ref = O.cde_wrapper(params, cde[0], cde[1], t[b], y[b], ctrl, cd)
+        err = rel_err(dy[b], ref)
+        print(f"n={n} sample {b}: rel err {err:.3e}")
+        assert err <= RTOL_VF
