@@ -107,10 +107,10 @@ __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* 
     const float* tc = tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
     for (int e = tid; e < n; e += blockDim.x) tg[(size_t)b * n + e] = fmaf(f, fmaf(f3, tc[e], 2.0f * tc[n + e]), tc[2 * n + e]);
   }
-  if (dx && slab == 1 % gridDim.x) {  // CDE wrapper: the data spline's derivative dX[i][q] at t (same knots)
+  if (dx) {  // CDE wrapper: the data spline's derivative dX[i][q] at t (same knots), spread over the sample's slabs
     const size_t blk = (size_t)n * de2;
     const float* dc = data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk;
-    for (size_t e = tid; e < blk; e += blockDim.x)
+    for (size_t e = (size_t)slab * blockDim.x + tid; e < blk; e += (size_t)gridDim.x * blockDim.x)
       dx[(size_t)b * blk + e] = fmaf(f, fmaf(f3, dc[e], 2.0f * dc[blk + e]), dc[2 * blk + e]);
   }
 }
