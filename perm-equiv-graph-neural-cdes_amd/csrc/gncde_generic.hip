@@ -148,6 +148,15 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
   // Every tile load is issued before the first use (one HBM round trip): the transposed tile (for LDS) and this
   // thread's own (i, k) elements, rows ty + 8 q.
   float ta[4], td[4], aik[4], dik[4];
+  // ... and the row reductions this tile reads later (r, rd, diagonals of its i range; r, rd of its k range)
+  __shared__ float sRb[6][32];
+  float rbv = 0.f;
+  if (tid < 192) {
+    const int q = tid >> 5, x = tid & 31;
+    const int idx = (q < 4 ? i0 : k0) + x;
+    const int plane = q == 0 ? 0 : (q == 1 ? 1 : (q == 2 ? 4 : (q == 3 ? 5 : q - 4)));
+    rbv = idx < n ? rb[plane * n + idx] : 0.f;
+  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int y = ty + 8 * q;
@@ -178,6 +187,7 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
     tA[ty + 8 * q][tx] = ta[q];
     tD[ty + 8 * q][tx] = td[q];
   }
+  if (tid < 192) sRb[tid >> 5][tid & 31] = rbv;
   __syncthreads();
   const float s = tot[0][0], sd = tot[1][0];
   if (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
@@ -188,8 +198,8 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
     // q_l[i] = sum_k (I + Abar_l)[i][k] from the reductions: the dense terms give their row / column sums, the
     // w (row) family n copies, the v (column) family sum_k v_k (sum_k r_k = sum_k c_k = s), the diagonal once.
     const int i = i0 + tid;
-    const float ri = rb[i], rdi = rb[n + i], ci = cs[0][0][tid], cdi = cs[0][1][tid];
-    const float dgi = rb[4 * n + i], dgdi = rb[5 * n + i], fn = (float)n;
+    const float ri = sRb[0][tid], rdi = sRb[1][tid], ci = cs[0][0][tid], cdi = cs[0][1][tid];
+    const float dgi = sRb[2][tid], dgdi = sRb[3][tid], fn = (float)n;
     for (int l = 0; l < L; ++l) {
       const float* fc = fus + l * GNCDE_FC;
       float q = fc[GNCDE_FC_E_A] * ri + fc[GNCDE_FC_E_DA] * rdi + fc[GNCDE_FC_ET_A] * ci + fc[GNCDE_FC_ET_DA] * cdi;
@@ -207,13 +217,12 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
   for (int e = tid; e < L * 32; e += 256) {
     const int l = e >> 5, x = e & 31;
     const float* fc = fus + l * GNCDE_FC;
-    const int i = i0 + x < n ? i0 + x : n - 1, k = k0 + x < n ? k0 + x : n - 1;
-    const float ri = rb[i], rdi = rb[n + i], ci = cs[0][0][x], cdi = cs[0][1][x];
-    const float rk = rb[k], rdk = rb[n + k], ck = cs[1][0][x], cdk = cs[1][1][x];
+    const float ri = sRb[0][x], rdi = sRb[1][x], ci = cs[0][0][x], cdi = cs[0][1][x];
+    const float rk = sRb[4][x], rdk = sRb[5][x], ck = cs[1][0][x], cdk = cs[1][1][x];
     sWv[l][0][x] = fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci +
                    fc[GNCDE_FC_WC_DA] * cdi + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
     sWv[l][1][x] = fc[GNCDE_FC_VR_A] * rk + fc[GNCDE_FC_VR_DA] * rdk + fc[GNCDE_FC_VC_A] * ck + fc[GNCDE_FC_VC_DA] * cdk;
-    sWv[l][2][x] = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * rb[4 * n + i] + fc[GNCDE_FC_UD_DA] * rb[5 * n + i] +
+    sWv[l][2][x] = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * sRb[2][x] + fc[GNCDE_FC_UD_DA] * sRb[3][x] +
                    fc[GNCDE_FC_UR_A] * ri + fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci +
                    fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
   }
