@@ -7,6 +7,7 @@
 // Reference semantics: spline (perm_equiv_graph_vector_field.py:98-102), fusion (layers.py:102-160,
 // :256-337 via the factored table of gncde.h), ConvLayer (layers.py:36-48), VF epilogue
 // (perm_equiv_graph_vector_field.py:122-128), CDE wrapper (cde_wrapper_vector_field.py:19-26).
+#include <cstdlib>
 #include "gncde_internal.h"
 
 #include <utility>
@@ -434,8 +435,15 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
   }
 }
 
+bool generic_vf_folds_combo(const GncdeProblem& p) {
+  const int mode = layer_mode(p, p.L - 1);
+  const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
+  return p.L >= 2 && (mode == 1 || (mode == 2 && fused_out));
+}
+
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st, bool prepared) {
+                    hipStream_t st, bool prepared, const StageCombo* cb) {
+  if (cb && !generic_vf_folds_combo(p)) return GNCDE_ERR_UNSUPPORTED;
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
   VfWs w;
@@ -459,7 +467,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     if (mode >= 0 && (mode != 2 || fused_out)) {  // one fused launch (gncde_layer.hip)
       float* out = mode == 0 ? Zout : dy;
       layer_fused(p, l, mode, abar_layer(p, w.abar, l), Zin, w.wp + wo, w.bf + bo, w.q + (size_t)l * B * n, out, w.tg,
-                  w.dx, st);
+                  w.dx, st, last ? cb : nullptr);
       wo += (size_t)din * dout;
       bo += dout;
       Zin = Zout;
@@ -616,20 +624,50 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     hipLaunchKernelGGL(k_combo, ge, dim3(256), 0, st, B, E, y, cb, hcur, out);
   };
 
+  // Stage j's evaluation into K[j] followed by the next stage's input out = y + h sum_i a_i K_i (terms end with
+  // K[j]).  Where the output layer is a fused k_layer launch, the combination (and the next stage time) is formed
+  // in its epilogue instead of a separate k_combo launch: same expression, same order, bit-equal.
   int rc = GNCDE_OK;
+  // Opt-in (GNCDE_STAGE_FOLD=1): measured at config 3 the fold is slower (15.8 ms vs 15.15 ms per solve) -- the
+  // epilogue's dependent K loads lengthen the read-out k_layer by more than the k_combo launch it saves.
+  const char* fold_env = std::getenv("GNCDE_STAGE_FOLD");
+  const bool fold = generic_vf_folds_combo(p) && fold_env && fold_env[0] == '1';
+  auto eval_combo = [&](const float* yin, int j, std::initializer_list<std::pair<int, float>> terms, float* out,
+                        float c_next, bool has_next) {
+    if (!fold) {
+      rc |= eval(yin, K[j]);
+      combo(terms, out, c_next, has_next);
+      return;
+    }
+    StageCombo cb{};
+    const int nt = (int)terms.size();
+    for (auto& tr : terms) {
+      if (cb.nk == nt - 1) {
+        cb.a_last = tr.second;  // tr.first == j
+        break;
+      }
+      cb.K[cb.nk] = K[tr.first];
+      cb.a[cb.nk] = tr.second;
+      cb.nk++;
+    }
+    cb.c = c_next;
+    cb.y = y;
+    cb.tcur = tcur;
+    cb.hcur = hcur;
+    cb.tst = has_next ? tst : nullptr;
+    cb.out = out;
+    rc |= generic_vf_eval(p, tst, yin, K[j], ws, st, true, &cb);
+  };
+
   const int steps = G - 1;
   if (s.method == GNCDE_RK4) {
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
       hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst);
-      rc |= eval(y, K[0]);
-      combo({{0, 0.5f}}, yt, 0.5f, true);
-      rc |= eval(yt, K[1]);
-      combo({{1, 0.5f}}, yt, 0.5f, true);
-      rc |= eval(yt, K[2]);
-      combo({{2, 1.0f}}, yt, 1.0f, true);
-      rc |= eval(yt, K[3]);
+      eval_combo(y, 0, {{0, 0.5f}}, yt, 0.5f, true);
+      eval_combo(yt, 1, {{1, 0.5f}}, yt, 0.5f, true);
+      eval_combo(yt, 2, {{2, 1.0f}}, yt, 1.0f, true);
       // y + h/6 (k1 + 2k2 + 2k3 + k4)
-      combo({{0, 1.0f / 6.0f}, {1, 2.0f / 6.0f}, {2, 2.0f / 6.0f}, {3, 1.0f / 6.0f}}, yt, 0.f, false);
+      eval_combo(yt, 3, {{0, 1.0f / 6.0f}, {1, 2.0f / 6.0f}, {2, 2.0f / 6.0f}, {3, 1.0f / 6.0f}}, yt, 0.f, false);
       std::swap(y, yt);
       if (s.save_mode == GNCDE_SAVE_STEPS)
         hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, k + 1, y, ys);
@@ -639,18 +677,14 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     rc |= eval(y, K[0]);
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
       hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst);
-      combo({{0, TSIT5_A21}}, yt, TSIT5_C2, true);
-      rc |= eval(yt, K[1]);
-      combo({{0, TSIT5_A31}, {1, TSIT5_A32}}, yt, TSIT5_C3, true);
-      rc |= eval(yt, K[2]);
-      combo({{0, TSIT5_A41}, {1, TSIT5_A42}, {2, TSIT5_A43}}, yt, TSIT5_C4, true);
-      rc |= eval(yt, K[3]);
-      combo({{0, TSIT5_A51}, {1, TSIT5_A52}, {2, TSIT5_A53}, {3, TSIT5_A54}}, yt, TSIT5_C5, true);
-      rc |= eval(yt, K[4]);
-      combo({{0, TSIT5_A61}, {1, TSIT5_A62}, {2, TSIT5_A63}, {3, TSIT5_A64}, {4, TSIT5_A65}}, yt, 1.0f, true);
-      rc |= eval(yt, K[5]);
-      combo({{0, TSIT5_B1}, {1, TSIT5_B2}, {2, TSIT5_B3}, {3, TSIT5_B4}, {4, TSIT5_B5}, {5, TSIT5_B6}}, yt, 1.0f,
-            true);
+      combo({{0, TSIT5_A21}}, yt, TSIT5_C2, true);  // K[0] is the FSAL value; k_grid_step set this step's h
+      eval_combo(yt, 1, {{0, TSIT5_A31}, {1, TSIT5_A32}}, yt, TSIT5_C3, true);
+      eval_combo(yt, 2, {{0, TSIT5_A41}, {1, TSIT5_A42}, {2, TSIT5_A43}}, yt, TSIT5_C4, true);
+      eval_combo(yt, 3, {{0, TSIT5_A51}, {1, TSIT5_A52}, {2, TSIT5_A53}, {3, TSIT5_A54}}, yt, TSIT5_C5, true);
+      eval_combo(yt, 4, {{0, TSIT5_A61}, {1, TSIT5_A62}, {2, TSIT5_A63}, {3, TSIT5_A64}, {4, TSIT5_A65}}, yt, 1.0f,
+                 true);
+      eval_combo(yt, 5, {{0, TSIT5_B1}, {1, TSIT5_B2}, {2, TSIT5_B3}, {3, TSIT5_B4}, {4, TSIT5_B5}, {5, TSIT5_B6}},
+                 yt, 1.0f, true);
       rc |= eval(yt, K[6]);
       std::swap(y, yt);
       std::swap(K[0], K[6]);

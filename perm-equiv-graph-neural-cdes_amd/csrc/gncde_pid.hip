@@ -17,6 +17,9 @@ namespace {
 constexpr int kPoll = 16;
 // one workgroup per sample: wide, so its element loops (E = n*h floats, 7 stage buffers) issue many loads at once
 constexpr int kAdvThreads = 1024;
+// The per-stage element loops run in passes of kAdvU elements per thread (E <= 8192 in one pass); a pass issues
+// all of its loads before the first use, so a loop costs about one memory round trip per pass, not per element.
+constexpr int kAdvU = 8;
 
 struct PidState {
   int phase, st, steps, rejects, evals, status, done, si;
@@ -122,6 +125,14 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
   float* yt = a.yt + base;
   const float* K = a.K + base;
   auto kk = [&](int j) { return a.kk + (size_t)j * BE + base; };
+  constexpr int U = kAdvU, P = kAdvThreads * kAdvU;
+  auto ldu = [&](const float* p, int e0, float(&v)[U]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * kAdvThreads;
+      v[u] = e < E ? p[e] : 0.f;
+    }
+  };
   s.evals++;
   bool start = false;
   if (s.phase == 0) {  // f(t0, y0): FSAL k1 and f0 of the initial-step heuristic
@@ -159,16 +170,36 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
     s.phase = 2;
     start = true;
   } else {
-    for (int e = tid; e < E; e += blockDim.x) kk(s.st)[e] = K[e];
-    if (s.st == 6) {  // attempt complete: yt = y1 candidate, kk6 = f(tn, y1)
+    float* kst = kk(s.st);
+    for (int e0 = tid; e0 < E; e0 += P) {
+      float v[U];
+      ldu(K, e0, v);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (e0 + u * kAdvThreads < E) kst[e0 + u * kAdvThreads] = v[u];
+    }
+    if (s.st == 6) {  // attempt complete: yt = y1 candidate, kk6 = f(tn, y1) (= K)
       float pe = 0.f;
-      for (int e = tid; e < E; e += blockDim.x) {
-        const float err = s.h * (TSIT5_E1 * kk(0)[e] + TSIT5_E2 * kk(1)[e] + TSIT5_E3 * kk(2)[e] +
-                                 TSIT5_E4 * kk(3)[e] + TSIT5_E5 * kk(4)[e] + TSIT5_E6 * kk(5)[e] +
-                                 TSIT5_E7 * kk(6)[e]);
-        const float sc = fmaf(fmaxf(fabsf(y[e]), fabsf(yt[e])), rtol, atol);
-        const float v = err / sc;
-        pe = fmaf(v, v, pe);
+      for (int e0 = tid; e0 < E; e0 += P) {
+        float k0[U], k1[U], k2[U], k3[U], k4[U], k5[U], k6[U], yv[U], ytv[U];
+        ldu(kk(0), e0, k0);
+        ldu(kk(1), e0, k1);
+        ldu(kk(2), e0, k2);
+        ldu(kk(3), e0, k3);
+        ldu(kk(4), e0, k4);
+        ldu(kk(5), e0, k5);
+        ldu(K, e0, k6);
+        ldu(y, e0, yv);
+        ldu(yt, e0, ytv);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (e0 + u * kAdvThreads >= E) break;
+          const float err = s.h * (TSIT5_E1 * k0[u] + TSIT5_E2 * k1[u] + TSIT5_E3 * k2[u] + TSIT5_E4 * k3[u] +
+                                   TSIT5_E5 * k4[u] + TSIT5_E6 * k5[u] + TSIT5_E7 * k6[u]);
+          const float sc = fmaf(fmaxf(fabsf(yv[u]), fabsf(ytv[u])), rtol, atol);
+          const float v = err / sc;
+          pe = fmaf(v, v, pe);
+        }
       }
       const float err = sqrtf(block_sum(pe, red) * inv_cnt);
       const bool finite = isfinite(err);
@@ -196,9 +227,18 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
           }
         }
         __syncthreads();  // every thread has read y / kk before they are overwritten
-        for (int e = tid; e < E; e += blockDim.x) {
-          y[e] = yt[e];
-          kk(0)[e] = kk(6)[e];
+        for (int e0 = tid; e0 < E; e0 += P) {
+          float yv[U], kv[U];
+          ldu(yt, e0, yv);
+          ldu(K, e0, kv);  // kk6
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int e = e0 + u * kAdvThreads;
+            if (e < E) {
+              y[e] = yv[u];
+              kk(0)[e] = kv[u];
+            }
+          }
         }
         s.t = s.tn;
         ++s.steps;
@@ -239,10 +279,22 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
     float ar[6], cst;
     stage_row(ns1, ar, cst);
     __syncthreads();
-    for (int e = tid; e < E; e += blockDim.x) {
-      float acc = 0.f;
-      for (int j = 0; j < ns1 && j < 6; ++j) acc = fmaf(ar[j], kk(j)[e], acc);
-      yt[e] = fmaf(s.h, acc, y[e]);
+    for (int e0 = tid; e0 < E; e0 += P) {
+      // every stage buffer's loads issued at once (the ones past ns1 are loaded and not used: allocated memory,
+      // possibly stale, so they are selected away rather than multiplied by a zero coefficient)
+      float kv[6][U], yv[U], acc[U];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) ldu(kk(j), e0, kv[j]);
+      ldu(y, e0, yv);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = j < ns1 ? fmaf(ar[j], kv[j][u], acc[u]) : acc[u];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (e0 + u * kAdvThreads < E) yt[e0 + u * kAdvThreads] = fmaf(s.h, acc[u], yv[u]);
     }
     s.tst = ns1 >= 5 ? __fadd_rn(s.t, s.h) : stage_time(s.t, cst, s.h);
     s.st = ns1;

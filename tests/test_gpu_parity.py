@@ -351,3 +351,42 @@ def test_generic_vf_large_n_vs_oracle(gncde, n, dims, kind, cde):
         err = rel_err(dy[b], ref)
         print(f"n={n} sample {b}: rel err {err:.3e}")
         assert err <= RTOL_VF
+
+
+@pytest.mark.parametrize("fold", ["0", "1"])
+@pytest.mark.parametrize("method", ["rk4", "tsit5"])
+def test_generic_cde_fixed_grid_solve_vs_oracle(gncde, method, fold, monkeypatch):
+    """A CDE-wrapper solve on a fixed grid (the PGT / TGB configuration) on the generic path, where the de = 8
+    read-out k_layer also forms the next RK stage's input and stage time in its epilogue (StageCombo, no separate
+    combination launch; opt-in, GNCDE_STAGE_FOLD=1) or in separate k_combo launches (the default).  Against the fp64
+    oracle solve computed here; every step state is compared."""
+    monkeypatch.setenv("GNCDE_STAGE_FOLD", fold)
+    from gncde import layout
+    rng = np.random.default_rng(77 if method == "rk4" else 78)
+    B, n, T, h, de = 2, 40, 4, 16, 8
+    dims = [h, 16, 16 * h]
+    ts, coeffs, params = MG.problem(rng, B, n, T, "undirected", dims)
+    dco = []
+    for b in range(B):
+        x = rng.standard_normal((T, n, de))
+        X = np.stack([np.broadcast_to(ts[b][:, None, None], x.shape), x], axis=-1)
+        dco.append(O.backward_hermite_coefficients(ts[b], X))
+    dcoeffs = tuple(np.stack([c[q] for c in dco]) for q in range(4))
+    prob = gncde.make_problem(ts, coeffs, params.kind, params.layers, data_coeffs=dcoeffs, cde_hidden=h,
+                              cde_embed=de)
+    y0 = rng.standard_normal((B, n, h))
+    grids = [O.rk4_grid(ts[b, 0], ts[b, -1], 6) if method == "rk4" else O.constant_grid(ts[b, 0], ts[b, -1], 0.7)
+             for b in range(B)]
+    grid, ns = layout.stack_grids(grids)
+    spec = gncde.SolverSpec(method=gncde._lib.RK4 if method == "rk4" else gncde._lib.TSIT5,
+                            save_mode=gncde._lib.SAVE_STEPS, grid=grid, nsteps=ns)
+    assert gncde.integrate_path(prob, spec) == "generic"
+    ys = gncde.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda")).cpu().numpy()
+    for b in range(B):
+        ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
+        cd = O.CubicInterpolation(ts[b], tuple(c[b] for c in dcoeffs))
+        f = lambda t, y, ctrl=ctrl, cd=cd: O.cde_wrapper(params, h, de, t, y, ctrl, cd)  # noqa: E731
+        ref, _ = O.solve_fixed_grid(f, grids[b], y0[b], method=method, save_every_step=True, time_dtype=np.float32)
+        err = rel_err(ys[b, :len(grids[b])], ref)
+        print(f"cde {method} fold={fold} sample {b}: {len(grids[b]) - 1} steps, rel err {err:.3e}")
+        assert err <= RTOL_SOLVE
