@@ -309,16 +309,34 @@ struct Combo {
   const float* tcur;
   float* tst;
 };
-__global__ void k_combo(int B, size_t E, const float* __restrict__ y, Combo cb,
-                        const float* __restrict__ hcur, float* __restrict__ out) {
+// kComboU elements per thread (strided by the block), each element's stage-buffer loads issued together before the
+// summation: the load latency is paid once per thread, not once per term.  Same summation order per element.
+constexpr int kComboU = 4;
+__global__ void __launch_bounds__(256) k_combo(int B, size_t E, const float* __restrict__ y, Combo cb,
+                                               const float* __restrict__ hcur, float* __restrict__ out) {
   const int b = blockIdx.y;
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (cb.tst && e == 0) cb.tst[b] = stage_time(cb.tcur[b], cb.c, hcur[b]);
-  if (e >= E) return;
-  const size_t o = (size_t)b * E + e;
-  float s = 0.f;
-  for (int j = 0; j < cb.nk; ++j) s = fmaf(cb.a[j], cb.K[j][o], s);
-  out[o] = fmaf(hcur[b], s, y[o]);
+  const size_t e0 = (size_t)blockIdx.x * (blockDim.x * kComboU) + threadIdx.x;
+  if (cb.tst && e0 == 0) cb.tst[b] = stage_time(cb.tcur[b], cb.c, hcur[b]);
+  const float hb = hcur[b];
+  float kv[7][kComboU], yv[kComboU];
+#pragma unroll
+  for (int u = 0; u < kComboU; ++u) {
+    const size_t e = e0 + (size_t)u * blockDim.x, o = (size_t)b * E + e;
+    const bool in = e < E;
+    yv[u] = in ? y[o] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) kv[j][u] = (in && j < cb.nk) ? cb.K[j][o] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < kComboU; ++u) {
+    const size_t e = e0 + (size_t)u * blockDim.x;
+    if (e >= E) break;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+      if (j < cb.nk) s = fmaf(cb.a[j], kv[j][u], s);
+    out[(size_t)b * E + e] = fmaf(hb, s, yv[u]);
+  }
 }
 
 __global__ void k_save_step(int B, size_t E, int G, int k, const float* __restrict__ y,
@@ -602,6 +620,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   const int G = s.grid_len;
   const unsigned gb = cdiv(B, 256);
   const dim3 ge(cdiv(E, 256), B);
+  const dim3 gc(cdiv(E, 256 * kComboU), B);
   (void)hipMemcpyAsync(y, y0, B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
   if (s.save_mode == GNCDE_SAVE_STEPS)
     hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, 0, y, ys);
@@ -621,7 +640,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     cb.c = c_next;
     cb.tcur = tcur;
     cb.tst = has_next ? tst : nullptr;
-    hipLaunchKernelGGL(k_combo, ge, dim3(256), 0, st, B, E, y, cb, hcur, out);
+    hipLaunchKernelGGL(k_combo, gc, dim3(256), 0, st, B, E, y, cb, hcur, out);
   };
 
   // Stage j's evaluation into K[j] followed by the next stage's input out = y + h sum_i a_i K_i (terms end with
