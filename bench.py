@@ -32,12 +32,6 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32 MFMA dense (= f32 vector peak)
 
 
-def algorithmic_bytes_per_eval(n, d0, dL):
-    """fp32 (d,c,b,a) operator-channel coefficients of the active interval + stage state
-    in + k out."""
-    return 16 * n * n + 4 * n * (d0 + dL)
-
-
 def algorithmic_flops_per_eval(n, dims):
     """19 n^2 (spline) + sum_l [22 n^2 + 2 n^2 d_l + 2 n d_{l-1} d_l + 6 n d_l]."""
     f = 19 * n * n
@@ -46,17 +40,64 @@ def algorithmic_flops_per_eval(n, dims):
     return f
 
 
-def load_traffic(workload):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+def algorithmic_bytes_per_sample(n, d0, dL, T, rk4_steps):
+    """HBM bytes one RK4 solve of one sample must move.  SURVEY §8(d) charges the active interval's fp32
+    (d, c, b, a) operator-channel coefficients (16 n^2 B) and the time-channel means (12 n B) per vector-field
+    evaluation; an RK4 step has only two DISTINCT stage times (k2/k3 share t + h/2, k4 shares t + h with the next
+    step's k1), so a solve needs them 2 S + 1 times, not 4 S.  Plus the state in / out and the knots."""
+    forms = 2 * rk4_steps + 1
+    return forms * (16 * n * n + 12 * n) + 4 * n * (d0 + dL) + 4 * T
+
+
+def source_sha16(rel):
+    import hashlib
+    with open(os.path.join(ROOT, rel), "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
+FUSED_SRC = "perm-equiv-graph-neural-cdes_amd/csrc/gncde_fused.hip"
+
+
+def load_traffic(workload, kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json), or None when
+    the file was measured on another workload, another kernel instance, or another revision of the kernel
+    source (keyed by the sha256 of gncde_fused.hip, so a stale measurement is refused)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as fh:
             d = json.load(fh)
-        if d.get("workload") == workload:
+        if (d.get("workload") == workload and d.get("kernel") == kernel
+                and d.get("source_sha16") == source_sha16(FUSED_SRC)):
             return float(d["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError):
         pass
     return None
+
+
+def roofline(bytes_per_launch, flops_per_launch, kernel_ms, traffic):
+    """Both bounds for the dominant kernel; the binding one is chosen by arithmetic intensity against the fp32
+    ridge point (peak flops / peak bandwidth), not by whichever fraction is larger."""
+    sec = kernel_ms * 1e-3
+    gbs = bytes_per_launch / sec / 1e9
+    tfs = flops_per_launch / sec / 1e12
+    hbm = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_per_launch": bytes_per_launch}
+    mfma = {"bound": "mfma", "achieved": round(tfs, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4), "algorithmic_per_launch": flops_per_launch}
+    intensity = flops_per_launch / bytes_per_launch
+    ridge = FP32_MFMA_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)
+    roof, alt = (mfma, hbm) if intensity >= ridge else (hbm, mfma)
+    for r in (roof, alt):
+        if r["frac"] > 1.0:  # physically impossible: the work model, not the kernel, is wrong
+            print(f"bench.py: roofline fraction {r['frac']} > 1 for bound {r['bound']}", file=sys.stderr)
+            r["valid"] = False
+    roof["traffic"] = traffic
+    roof["kernel_ms"] = round(kernel_ms, 4)
+    roof["intensity_flop_per_byte"] = round(intensity, 2)
+    roof["ridge_flop_per_byte"] = round(ridge, 2)
+    if traffic is not None:
+        alt["measured_hbm_GBs"] = round(traffic / sec / 1e9, 1)
+    return roof, alt
 
 
 def cpu_baseline(prob, spec, y0, layers, target_s):
@@ -155,20 +196,9 @@ def main():
 
     if rank == 0:
         n = prob.n
-        bpe = algorithmic_bytes_per_eval(n, hidden, hidden)
-        fpe = algorithmic_flops_per_eval(n, prob.dims)
-        gbs = evals_per_launch * bpe / (kernel_ms * 1e-3) / 1e9
-        tfs = evals_per_launch * fpe / (kernel_ms * 1e-3) / 1e12
-        hbm = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-               "frac": round(gbs / HBM_PEAK_GBS, 4)}
-        mfma = {"bound": "mfma", "achieved": round(tfs, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4)}
-        roof, alt = (hbm, mfma) if hbm["frac"] >= mfma["frac"] else (mfma, hbm)
-        traffic = load_traffic(workload)
-        roof["traffic"] = traffic
-        roof["kernel_ms"] = round(kernel_ms, 4)
-        roof["algorithmic_per_launch"] = (evals_per_launch * bpe if roof["bound"] == "hbm"
-                                          else evals_per_launch * fpe)
+        bytes_launch = B * algorithmic_bytes_per_sample(n, hidden, hidden, T, args.rk4_steps)
+        flops_launch = evals_per_launch * algorithmic_flops_per_eval(n, prob.dims)
+        roof, alt = roofline(bytes_launch, flops_launch, kernel_ms, load_traffic(workload, path))
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(prob, spec, y0, layers, args.cpu_seconds)

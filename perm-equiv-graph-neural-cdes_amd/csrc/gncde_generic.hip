@@ -7,7 +7,6 @@
 // Reference semantics: spline (perm_equiv_graph_vector_field.py:98-102), fusion (layers.py:102-160,
 // :256-337 via the factored table of gncde.h), ConvLayer (layers.py:36-48), VF epilogue
 // (perm_equiv_graph_vector_field.py:122-128), CDE wrapper (cde_wrapper_vector_field.py:19-26).
-#include <cstdlib>
 #include "gncde_internal.h"
 
 #include <utility>
@@ -453,15 +452,8 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
   }
 }
 
-bool generic_vf_folds_combo(const GncdeProblem& p) {
-  const int mode = layer_mode(p, p.L - 1);
-  const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
-  return p.L >= 2 && (mode == 1 || (mode == 2 && fused_out));
-}
-
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st, bool prepared, const StageCombo* cb) {
-  if (cb && !generic_vf_folds_combo(p)) return GNCDE_ERR_UNSUPPORTED;
+                    hipStream_t st, bool prepared) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
   VfWs w;
@@ -485,7 +477,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     if (mode >= 0 && (mode != 2 || fused_out)) {  // one fused launch (gncde_layer.hip)
       float* out = mode == 0 ? Zout : dy;
       layer_fused(p, l, mode, abar_layer(p, w.abar, l), Zin, w.wp + wo, w.bf + bo, w.q + (size_t)l * B * n, out, w.tg,
-                  w.dx, st, last ? cb : nullptr);
+                  w.dx, st);
       wo += (size_t)din * dout;
       bo += dout;
       Zin = Zout;
@@ -644,38 +636,13 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   };
 
   // Stage j's evaluation into K[j] followed by the next stage's input out = y + h sum_i a_i K_i (terms end with
-  // K[j]).  Where the output layer is a fused k_layer launch, the combination (and the next stage time) is formed
-  // in its epilogue instead of a separate k_combo launch: same expression, same order, bit-equal.
+  // K[j]).  (Folding the combination into the read-out k_layer's epilogue measured slower at config 3, 15.8 vs
+  // 15.15 ms per solve: the epilogue's dependent K loads lengthen the critical launch by more than k_combo costs.)
   int rc = GNCDE_OK;
-  // Opt-in (GNCDE_STAGE_FOLD=1): measured at config 3 the fold is slower (15.8 ms vs 15.15 ms per solve) -- the
-  // epilogue's dependent K loads lengthen the read-out k_layer by more than the k_combo launch it saves.
-  const char* fold_env = std::getenv("GNCDE_STAGE_FOLD");
-  const bool fold = generic_vf_folds_combo(p) && fold_env && fold_env[0] == '1';
   auto eval_combo = [&](const float* yin, int j, std::initializer_list<std::pair<int, float>> terms, float* out,
                         float c_next, bool has_next) {
-    if (!fold) {
-      rc |= eval(yin, K[j]);
-      combo(terms, out, c_next, has_next);
-      return;
-    }
-    StageCombo cb{};
-    const int nt = (int)terms.size();
-    for (auto& tr : terms) {
-      if (cb.nk == nt - 1) {
-        cb.a_last = tr.second;  // tr.first == j
-        break;
-      }
-      cb.K[cb.nk] = K[tr.first];
-      cb.a[cb.nk] = tr.second;
-      cb.nk++;
-    }
-    cb.c = c_next;
-    cb.y = y;
-    cb.tcur = tcur;
-    cb.hcur = hcur;
-    cb.tst = has_next ? tst : nullptr;
-    cb.out = out;
-    rc |= generic_vf_eval(p, tst, yin, K[j], ws, st, true, &cb);
+    rc |= eval(yin, K[j]);
+    combo(terms, out, c_next, has_next);
   };
 
   const int steps = G - 1;

@@ -158,25 +158,8 @@ void row_inv(int rows, int d, const float* Z, float* inv, hipStream_t st);
 int layer_mode(const GncdeProblem& p, int l);
 void permute_linear(int rows, int din, bool cde, const float* W, float* out, hipStream_t st);
 
-// The next RK stage's input, folded into the output layer's epilogue (fixed-grid solves):
-//   out = y + h_b (sum_{i < nk} a_i K_i + a_last dy)   summed in that order (k_combo's order, bit-equal),
-// and (tst != nullptr) the next stage time t_b + c h_b.  out must not alias the evaluation's own input.
-struct StageCombo {
-  const float* K[7];
-  float a[7];
-  int nk;
-  float a_last;
-  float c;
-  const float* y;
-  const float* tcur;
-  const float* hcur;
-  float* tst;
-  float* out;
-};
-
 void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, const float* Z, const float* wperm,
-                 const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st,
-                 const StageCombo* cb = nullptr);
+                 const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st);
 
 // generic (any-shape, multi-kernel) path: gncde_generic.hip
 size_t generic_vf_workspace(const GncdeProblem& p);
@@ -191,10 +174,7 @@ void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float*
               float* abar, hipStream_t st, float* qrow = nullptr, float* dx = nullptr);
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st);
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st, bool prepared = false, const StageCombo* cb = nullptr);
-// true when generic_vf_eval can fold a StageCombo into its output layer: a fused k_layer output launch that is not
-// also the first layer, so its epilogue never writes a buffer another workgroup of the same launch still reads
-bool generic_vf_folds_combo(const GncdeProblem& p);
+                    hipStream_t st, bool prepared = false);
 int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
                       int32_t* stats, char* ws, hipStream_t st);
 

@@ -59,17 +59,7 @@ struct LayerArgs {
   float* out;          // [B, n, DOUT] (CDE: dy [B, n, H])
   const float* tg;     // [B n] time-channel derivative (MODE 1, 2)
   const float* dx;     // [B n, 16] data-spline derivative (MODE 2)
-  int has_cb;          // MODE 1, 2: also form the next RK stage's input (StageCombo) from the output
-  StageCombo cb;
 };
-
-// The folded RK combination of one output element o of sample b (k_combo's summation order: bit-equal to it)
-__device__ __forceinline__ void combo_store(const StageCombo& c, int b, size_t o, float v) {
-  float s = 0.f;
-  for (int i = 0; i < c.nk; ++i) s = fmaf(c.a[i], c.K[i][o], s);
-  s = fmaf(c.a_last, v, s);
-  c.out[o] = fmaf(c.hcur[b], s, c.y[o]);
-}
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -103,9 +93,6 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
   const int b = blockIdx.y, r0 = (blockIdx.x / SPLIT) * kRows, ch = blockIdx.x % SPLIT;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const size_t nb = (size_t)b * n;
-  // the next stage's time (this evaluation's spline launch has read the current one)
-  if (MODE != 0 && a.has_cb && a.cb.tst && blockIdx.x == 0 && tid == 0)
-    a.cb.tst[b] = stage_time(a.cb.tcur[b], a.cb.c, a.cb.hcur[b]);
 
   // ---- 1. Zs = Z[b] (zero rows up to nk), every load of a round in flight before the first store; then the
   // RMSNorm factor of each row from LDS (diag(inv) is applied to the (I + Abar) operand of the product).
@@ -322,7 +309,6 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         if (MODE == 1) v *= a.tg[nb + R];
         const size_t o = (nb + R) * DOUT + col;
         a.out[o] = v;
-        if (MODE == 1 && a.has_cb) combo_store(a.cb, b, o, v);
       }
     }
   } else {
@@ -399,9 +385,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
           const int R = r0 + 16 * t + 4 * hi + r;
           if (R < n) {
             const size_t o = (nb + R) * DOUT + m;
-            const float v = a.tg[nb + R] * acc[t][r];
-            a.out[o] = v;
-            if (a.has_cb) combo_store(a.cb, b, o, v);
+            a.out[o] = a.tg[nb + R] * acc[t][r];
           }
         }
     }
@@ -489,13 +473,8 @@ void permute_linear(int rows, int din, bool cde, const float* W, float* out, hip
 }
 
 void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, const float* Z, const float* wperm,
-                 const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st,
-                 const StageCombo* cb) {
+                 const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st) {
   LayerArgs a{};
-  if (cb && mode != 0) {
-    a.has_cb = 1;
-    a.cb = *cb;
-  }
   a.n = p.n;
   a.abar = abar;
   a.Z = Z;

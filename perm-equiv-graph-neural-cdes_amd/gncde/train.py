@@ -7,8 +7,8 @@ ranks (SURVEY §8 a9 + e).
 
 Here one process owns one GPU and a contiguous shard of the samples (``shard_range``).  Each rank
 back-propagates the SUM of its squared errors through the GPU solve (autograd.solve -> gncde_integrate_vjp);
-``reduce_gradients`` all-reduces the flat gradient and the (sse, count) pair in one RCCL call each, and
-divides by the global element count, which is exactly the gradient of the reference's full-batch
+``reduce_gradients`` all-reduces the flat gradient and the (sse, count) pair as one fp64 bucket (one RCCL call
+per step), and divides by the global element count, which is exactly the gradient of the reference's full-batch
 ``jnp.mean`` (loss_configs.py:47).  The optimiser update runs on the GPU over one flat parameter buffer
 (gncde_clip_adamw): every rank applies the same update to the same parameters, so replicas stay identical
 without a parameter broadcast.
@@ -35,13 +35,17 @@ def reduce_gradients(flat_grad: torch.Tensor, sse: torch.Tensor, count: int):
     normalise to the gradient of the global mean.  Returns (mean-loss gradient, global mean loss).
     Works for any backend (RCCL for GPU ranks, gloo for the CPU tests); a no-op reduction when the
     process group is absent or has one rank."""
-    tot = torch.stack([sse.detach().to(torch.float64).reshape(()),
-                       torch.tensor(float(count), dtype=torch.float64, device=sse.device)])
+    P = flat_grad.numel()
+    # One fp64 bucket [grad..., sse, count]: a single collective per step, and the element count stays exact
+    # past 2^24 (config 4: 8192 x 80 x 128 targets).
+    bucket = torch.cat([flat_grad.detach().reshape(-1).to(torch.float64),
+                        sse.detach().to(device=flat_grad.device, dtype=torch.float64).reshape(1),
+                        torch.full((1,), float(count), dtype=torch.float64, device=flat_grad.device)])
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    flat_grad.div_(tot[1].to(flat_grad.dtype))
-    return flat_grad, tot[0] / tot[1]
+        dist.all_reduce(bucket, op=dist.ReduceOp.SUM)
+    total = bucket[P + 1]
+    flat_grad.copy_((bucket[:P] / total).to(flat_grad.dtype).view_as(flat_grad))
+    return flat_grad, bucket[P] / total
 
 
 class ClipAdamW:

@@ -140,7 +140,7 @@ def test_pgt_driver_matches_oracle(G):
         ref_nodes = mlp(model.decoder, yT)
         # this random-init CDE amplifies perturbations ~240x over the 30 steps (a 1e-7 change of y0 moves
         # yT by 2.4e-5), so an fp32 solve - GPU or the oracle's own fp32 emulation (1.4e-4) - sits ~1e-4
-        # from the fp64 oracle; tools/debug_pgt.py reproduces the analysis
+        # from the fp64 oracle
         assert rel_err(per_node[b], ref_nodes) <= 1e-3
         # the global read-out sums node outputs of mixed sign: judge it against the summed magnitudes
         assert abs(float(out[b, 0]) - ref_nodes.sum()) <= 1e-3 * np.abs(ref_nodes).sum()

@@ -353,14 +353,11 @@ def test_generic_vf_large_n_vs_oracle(gncde, n, dims, kind, cde):
         assert err <= RTOL_VF
 
 
-@pytest.mark.parametrize("fold", ["0", "1"])
 @pytest.mark.parametrize("method", ["rk4", "tsit5"])
-def test_generic_cde_fixed_grid_solve_vs_oracle(gncde, method, fold, monkeypatch):
-    """A CDE-wrapper solve on a fixed grid (the PGT / TGB configuration) on the generic path, where the de = 8
-    read-out k_layer also forms the next RK stage's input and stage time in its epilogue (StageCombo, no separate
-    combination launch; opt-in, GNCDE_STAGE_FOLD=1) or in separate k_combo launches (the default).  Against the fp64
-    oracle solve computed here; every step state is compared."""
-    monkeypatch.setenv("GNCDE_STAGE_FOLD", fold)
+def test_generic_cde_fixed_grid_solve_vs_oracle(gncde, method):
+    """A CDE-wrapper solve on a fixed grid (the PGT / TGB configuration) on the generic path, through the de = 8
+    read-out k_layer and the k_combo stage combinations.  Against the fp64 oracle solve computed here; every step
+    state is compared."""
     from gncde import layout
     rng = np.random.default_rng(77 if method == "rk4" else 78)
     B, n, T, h, de = 2, 40, 4, 16, 8
@@ -388,5 +385,5 @@ def test_generic_cde_fixed_grid_solve_vs_oracle(gncde, method, fold, monkeypatch
         f = lambda t, y, ctrl=ctrl, cd=cd: O.cde_wrapper(params, h, de, t, y, ctrl, cd)  # noqa: E731
         ref, _ = O.solve_fixed_grid(f, grids[b], y0[b], method=method, save_every_step=True, time_dtype=np.float32)
         err = rel_err(ys[b, :len(grids[b])], ref)
-        print(f"cde {method} fold={fold} sample {b}: {len(grids[b]) - 1} steps, rel err {err:.3e}")
+        print(f"cde {method} sample {b}: {len(grids[b]) - 1} steps, rel err {err:.3e}")
         assert err <= RTOL_SOLVE

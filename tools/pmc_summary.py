@@ -2,7 +2,7 @@
 """Summarise rocprofv3 outputs for the dominant kernel.
 
   tools/pmc_summary.py stats  gpurun_out/prof/run_kernel_stats.csv            -> top kernels table
-  tools/pmc_summary.py traffic gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE WORKLOAD OUT.json
+  tools/pmc_summary.py traffic gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE WORKLOAD KERNEL OUT.json
   tools/pmc_summary.py counters DIR...                                          -> mean per kernel/counter
 
 HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are collected in
@@ -46,7 +46,7 @@ def main():
         for (k, c), v in sorted(counters(sys.argv[2:], os.environ.get("MATCH", "k_fused")).items()):
             print(f"{c:32s} {v:16.1f}  {k}")
     elif mode == "traffic":
-        fetch_dir, write_dir, workload, out = sys.argv[2:6]
+        fetch_dir, write_dir, workload, kernel, out = sys.argv[2:7]
         f = counters([fetch_dir]).items()
         w = counters([write_dir]).items()
         fetch = [v for (k, c), v in f if c == "FETCH_SIZE"]
@@ -54,7 +54,12 @@ def main():
         if not fetch or not write:
             raise SystemExit("no FETCH_SIZE/WRITE_SIZE rows for the fused kernel")
         fkb, wkb = fetch[0], write[0]
-        d = {"workload": workload, "kernel": "k_fused", "fetch_size_kib": fkb, "write_size_kib": wkb,
+        import hashlib
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        src = os.path.join(root, "perm-equiv-graph-neural-cdes_amd", "csrc", "gncde_fused.hip")
+        with open(src, "rb") as fh:
+            sha = hashlib.sha256(fh.read()).hexdigest()[:16]
+        d = {"workload": workload, "kernel": kernel, "source_sha16": sha, "fetch_size_kib": fkb, "write_size_kib": wkb,
              "hbm_bytes_per_launch": (2.0 * fkb + wkb) * 1024.0,
              "correction": "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md §HBM)"}
         with open(out, "w") as fh:
