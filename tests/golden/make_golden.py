@@ -138,8 +138,6 @@ def pid_case(rng, name, B, n, T, kind, dims, rtol=1e-3, atol=1e-6, dt0=None, cde
                stats=np.array(st), rtol=np.array(rtol), atol=np.array(atol),
                dt0=np.array(np.nan if dt0 is None else dt0))
     if cde is not None:
-        if data_grad:
-            out.update(x=np.stack(xs), grad_x=np.stack(gxs))
         out.update(xd=np.stack([c[0] for c in dco]), xc=np.stack([c[1] for c in dco]),
                    xb=np.stack([c[2] for c in dco]), xa=np.stack([c[3] for c in dco]), h=np.array(h),
                    de=np.array(de))
@@ -306,5 +304,17 @@ def layer_cases():
     vf_case(rng, "vf_directed_n48_h64_L2.npz", 2, 48, 4, "directed", [64, 64, 64])
 
 
+def pid_cde8_cases():
+    """Tsit5 + PIDController through the de = 8 read-out k_layer (BASELINE config 5's adaptive CDE solve, the
+    contraction inside the read-out's MFMA K loop): h = 16 (L = 2) and h = 32 (L = 3) at n = 40."""
+    rng = np.random.default_rng(5151)
+    pid_case(rng, "pid_cde8_n40_h16_L2.npz", 2, 40, 3, "undirected", [16, 16, 0], cde=(16, 8))
+    pid_case(rng, "pid_cde8_n40_h32_L3.npz", 2, 40, 3, "undirected", [32, 32, 32, 0], cde=(32, 8))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["pid_cde8"]:  # the fixtures added in round 2 (earlier files stay byte-identical)
+        pid_cde8_cases()
+    else:
+        main()
+        pid_cde8_cases()
