@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GNCDE_ABI_VERSION 2
+#define GNCDE_ABI_VERSION 3
 #define GNCDE_MAX_LAYERS 8
 #define GNCDE_FC 24
 
@@ -100,7 +100,7 @@ enum { GNCDE_COMPUTE_FP32 = 0, GNCDE_COMPUTE_BF16 = 1, GNCDE_COMPUTE_BF16_STORAG
 enum { GNCDE_CTRL_GRID = 0, GNCDE_CTRL_PID = 1 };
 enum { GNCDE_SAVE_T1 = 0, GNCDE_SAVE_STEPS = 1, GNCDE_SAVE_TS = 2 };
 /* stats[b*4 + k]: k=0 accepted steps, 1 rejected steps, 2 vector-field evaluations, 3 status
- * (0 ok, 1 max_steps exceeded, 2 non-finite error estimate) */
+ * (0 ok, 1 max_steps exceeded, 2 non-finite error estimate, 3 step record (step_ts) too short) */
 enum { GNCDE_STAT_STEPS = 0, GNCDE_STAT_REJECTS = 1, GNCDE_STAT_EVALS = 2, GNCDE_STAT_STATUS = 3 };
 
 typedef struct GncdeProblem {
@@ -134,6 +134,13 @@ typedef struct GncdeSolver {
   const float* t1;                   /* [B] (PID) */
   const float* dt0;                  /* [B] (PID) initial step, or NULL for the Hairer heuristic */
   const float* save_ts;              /* [B, S] (SAVE_TS), increasing, within [t0, t1] */
+  /* PID only, optional OUTPUT (NULL = not recorded): the accepted step sequence of every sample,
+   * step_ts[b, 0] = t0 and step_ts[b, k] = the time reached by the k-th accepted step (k <= stats steps).  It is
+   * the grid on which the reverse mode differentiates an adaptive solve (the controller's step sizes are treated
+   * as constants, as RecursiveCheckpointAdjoint does through diffrax's while_loop).  A sample with more accepted
+   * steps than step_ts_len - 1 gets status 3. */
+  float* step_ts;                    /* [B, step_ts_len] */
+  int32_t step_ts_len;
 } GncdeSolver;
 
 /* Library / error helpers */
@@ -180,6 +187,18 @@ int gncde_integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, con
 int gncde_integrate_vjp_data(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
                              float* gy0, float* gparams, float* gfusion, float* gdata_coef, void* workspace,
                              size_t workspace_bytes, void* stream);
+
+/* gncde_integrate_vjp with two optional extras (NULL = absent):
+ *   gstage:     [B, G-1, S, n, d_s], S = 4 (RK4) or 6 (Tsit5): cotangents added to the stage VALUES of each step,
+ *               K_j = VF(t_k + c_j h_k, U_j).  This is the reverse mode of output maps that read the stages, above all
+ *               the Tsit5 dense interpolant of SaveAt(ts) (graph_neural_cde.py:89-104): y(t_k + th h_k) =
+ *               y_k + h_k sum_j b_j(th) K_j, where K_6 (the FSAL value f(t_{k+1}, y_{k+1})) is stage 0 of step k+1 --
+ *               so a caller whose last step's K_6 carries a cotangent leaves one padded step (nsteps < G-1) and puts
+ *               it on stage 0 of step nsteps.
+ *   gdata_coef: the CDE data spline's cotangent, as gncde_integrate_vjp_data. */
+int gncde_integrate_vjp_ex(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
+                           const float* gstage, float* gy0, float* gparams, float* gfusion, float* gdata_coef,
+                           void* workspace, size_t workspace_bytes, void* stream);
 
 /* Per-node affine map out[r, :] = W @ x[r, :] + b for `rows` rows.  x: [rows, din], W: [dout, din],
  * b: [dout] (may be NULL), out: [rows, dout]. */

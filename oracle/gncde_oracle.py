@@ -453,7 +453,8 @@ def solve_tsit5_pid(f, t0, t1, y0, rtol=1e-3, atol=1e-6, dt0=None, save_ts=None,
     """Tsit5 + PIDController(rtol, atol) with diffrax defaults (pcoeff=0, icoeff=1, dcoeff=0), FSAL,
     SaveAt(ts) via the Tsit5 dense interpolant (SaveAt(t1) if save_ts is None).
 
-    Returns (ys, stats) with stats = dict(steps, rejects, evals).
+    Returns (ys, stats) with stats = dict(steps, rejects, evals, grid): grid = the accepted step times
+    (t0 first), the sequence the reverse mode differentiates on.
     """
     evals = 0
     y = np.array(y0, dtype=np.float64)
@@ -473,6 +474,7 @@ def solve_tsit5_pid(f, t0, t1, y0, rtol=1e-3, atol=1e-6, dt0=None, save_ts=None,
     fk = f(t, y)
     evals += 1
     steps = rejects = 0
+    grid = [t]
     while t < t1:
         if steps + rejects >= max_steps:
             raise RuntimeError("max_steps exceeded")
@@ -501,11 +503,12 @@ def solve_tsit5_pid(f, t0, t1, y0, rtol=1e-3, atol=1e-6, dt0=None, save_ts=None,
             y = y1
             fk = ks[6] / h  # FSAL: stage 7 is f(t1, y1)
             t = tn
+            grid.append(t)
             steps += 1
         else:
             rejects += 1
         dt = factor * h
-    stats = dict(steps=steps, rejects=rejects, evals=evals)
+    stats = dict(steps=steps, rejects=rejects, evals=evals, grid=np.array(grid))
     if save_ts is None:
         return y, stats
     return np.stack(out), stats

@@ -14,6 +14,9 @@ What it is
       literal fusion with a unit parameter (the fusion is affine in its parameters).
     * the discrete adjoint of the fixed-grid RK4 / Tsit5 solve — what diffrax's default
       RecursiveCheckpointAdjoint differentiates (graph_neural_cde.py:94-104, pgt_graph_neural_cde.py:119-129).
+    * the adaptive Tsit5 + PIDController solve with SaveAt(ts) (graph_neural_cde.py:53-54,89-104) differentiated
+      on its accepted step sequence with the step sizes held constant (solve_grid_dense_vjp): the Tsit5 steps
+      of that grid plus the reverse mode of the dense interpolant at the save times.
 
 PARITY: jax is not installed, so this cannot be compared with jax.grad itself.  It is pinned instead by
 central finite differences of the fp64 forward oracle (tests/test_oracle_grad.py), which checks the
@@ -201,6 +204,107 @@ def solve_fixed_grid_vjp(f, f_vjp, grid, y0, method="rk4", g_final=None, g_steps
                 if a[i][j] != 0.0:
                     gK[j] = gK[j] + h * a[i][j] * gu
         lam = gy + (g_steps[k] if g_steps is not None else 0.0)
+    return lam, total
+
+
+def _locate(grid, ts):
+    """(k, theta) of a save time: t_k < ts <= t_{k+1} (k = -1: ts <= t0, the initial state)."""
+    if ts <= grid[0]:
+        return -1, 0.0
+    k = int(np.searchsorted(grid, ts, side="left")) - 1
+    k = min(max(k, 0), len(grid) - 2)
+    return k, (ts - grid[k]) / (grid[k + 1] - grid[k])
+
+
+def _grid_geometry(grid, time_dtype):
+    geo = []
+    for k in range(len(grid) - 1):
+        if time_dtype is None:
+            geo.append((float(grid[k]), float(grid[k + 1]) - float(grid[k])))
+        else:
+            t = float(time_dtype(grid[k]))
+            geo.append((t, float(time_dtype(time_dtype(grid[k + 1]) - time_dtype(grid[k])))))
+    return geo
+
+
+def _tsit5_stages(f, t, h, y, time_dtype):
+    """The 7 stage inputs / values of a Tsit5 step (stage 7: f(t + h, y1)) and y1."""
+    tst = O._stage_times(t, h, list(O.TSIT5_C), time_dtype)
+    U, K = [], []
+    for i in range(7):
+        if i < 6:
+            u = y + h * sum((O.TSIT5_A[i][j] * K[j] for j in range(i)), np.zeros_like(y))
+        else:
+            u = y + h * sum(O.TSIT5_B[j] * K[j] for j in range(6))
+        U.append(u)
+        K.append(f(tst[i], u))
+    return tst, U, K
+
+
+def solve_grid_dense(f, grid, y0, save_ts, time_dtype=np.float32):
+    """Tsit5 on the accepted step sequence ``grid`` with SaveAt(ts) through the dense interpolant: what an adaptive
+    solve outputs once its steps are fixed.  Returns [S, n, d]."""
+    y = np.asarray(y0, np.float64)
+    geo = _grid_geometry(grid, time_dtype)
+    ys, stages = [y], []
+    for t, h in geo:
+        _, _, K = _tsit5_stages(f, t, h, ys[-1], time_dtype)
+        stages.append(K)
+        ys.append(ys[-1] + h * sum(O.TSIT5_B[j] * K[j] for j in range(6)))
+    out = []
+    for ts in save_ts:
+        k, th = _locate(np.asarray(grid, np.float64), float(ts))
+        if k < 0:
+            out.append(ys[0])
+            continue
+        w = O.tsit5_dense_weights(th)
+        out.append(ys[k] + geo[k][1] * sum(w[j] * stages[k][j] for j in range(7)))
+    return np.stack(out)
+
+
+def solve_grid_dense_vjp(f, f_vjp, grid, y0, save_ts, g_saves, time_dtype=np.float32):
+    """Reverse mode of solve_grid_dense for cotangents g_saves [S, n, d]: (g_y0, summed parameter grads).
+
+    Per save point s in step k: y(ts) = y_k + h_k sum_j b_j(th) K_j, j = 0..6, K_6 = f(t_k + h_k, y_{k+1}).  Going
+    backwards over the steps, the cotangent of K_6 of step k is pulled back through f onto y_{k+1} first; then the
+    usual Tsit5 adjoint of step k runs with stage seeds h_k (b_j lambda_{k+1} + sum_s b_j(th_s) g_s)."""
+    y = np.asarray(y0, np.float64)
+    geo = _grid_geometry(grid, time_dtype)
+    gridd = np.asarray(grid, np.float64)
+    ys = [y]
+    for t, h in geo:
+        _, _, K = _tsit5_stages(f, t, h, ys[-1], time_dtype)
+        ys.append(ys[-1] + h * sum(O.TSIT5_B[j] * K[j] for j in range(6)))
+    N = len(geo)
+    dense = [np.zeros((7,) + y.shape) for _ in range(N)]   # sum_s b_j(th_s) g_s per step
+    direct = [np.zeros_like(y) for _ in range(N + 1)]      # cotangent straight onto y_k
+    for ts, g in zip(save_ts, g_saves):
+        k, th = _locate(gridd, float(ts))
+        if k < 0:
+            direct[0] = direct[0] + g
+            continue
+        direct[k] = direct[k] + g
+        dense[k] = dense[k] + O.tsit5_dense_weights(th)[:, None, None] * g
+    lam = direct[N].copy()
+    total = None
+    b = list(O.TSIT5_B[:6])
+    for k in range(N - 1, -1, -1):
+        t, h = geo[k]
+        tst, U, _ = _tsit5_stages(f, t, h, ys[k], time_dtype)
+        if np.any(dense[k][6]):  # K_6 = f(t + h, y_{k+1})
+            gu, gr = f_vjp(tst[6], U[6], h * dense[k][6])
+            total = _acc(total, gr)
+            lam = lam + gu
+        gK = [h * (b[i] * lam + dense[k][i]) for i in range(6)]
+        gy = lam + direct[k]
+        for i in range(5, -1, -1):
+            gu, gr = f_vjp(tst[i], U[i], gK[i])
+            total = _acc(total, gr)
+            gy = gy + gu
+            for j in range(i):
+                if O.TSIT5_A[i][j] != 0.0:
+                    gK[j] = gK[j] + h * O.TSIT5_A[i][j] * gu
+        lam = gy
     return lam, total
 
 

@@ -40,6 +40,7 @@ int validate_solver(const GncdeProblem* p, const GncdeSolver* s) {
     if (!(s->rtol >= 0.f) || !(s->atol > 0.f)) return GNCDE_ERR_ARG;
     if (s->save_mode == GNCDE_SAVE_STEPS) return GNCDE_ERR_UNSUPPORTED;
     if (s->save_mode == GNCDE_SAVE_TS && (!s->save_ts || s->n_save < 1)) return GNCDE_ERR_ARG;
+    if (s->step_ts && s->step_ts_len < 1) return GNCDE_ERR_ARG;
   } else {
     return GNCDE_ERR_ARG;
   }
@@ -117,7 +118,7 @@ size_t gncde_vjp_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* so
 }
 
 static int integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
-                         float* gy0, float* gparams, float* gfusion, float* gdata, void* workspace,
+                         const float* gstage, float* gy0, float* gparams, float* gfusion, float* gdata, void* workspace,
                          size_t workspace_bytes, void* stream) {
   using namespace gncde;
   int rc = validate_problem(prob);
@@ -139,24 +140,34 @@ static int integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, co
   if (!ys || !gys || !gy0) return GNCDE_ERR_ARG;
   if (!gdata && stage_vjp_supported(*prob, *solver)) {
     if (workspace_bytes < stage_vjp_workspace(*prob) || !workspace) return GNCDE_ERR_WORKSPACE;
-    return stage_integrate_vjp(*prob, *solver, ys, gys, gy0, gparams, gfusion, static_cast<char*>(workspace), st);
+    return stage_integrate_vjp(*prob, *solver, ys, gys, gstage, gy0, gparams, gfusion, static_cast<char*>(workspace),
+                               st);
   }
   if (workspace_bytes < generic_vjp_workspace(*prob, *solver) || !workspace) return GNCDE_ERR_WORKSPACE;
-  return generic_integrate_vjp(*prob, *solver, ys, gys, gy0, gparams, gfusion, gdata, static_cast<char*>(workspace),
-                               st);
+  return generic_integrate_vjp(*prob, *solver, ys, gys, gstage, gy0, gparams, gfusion, gdata,
+                               static_cast<char*>(workspace), st);
 }
 
 int gncde_integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
                         float* gy0, float* gparams, float* gfusion, void* workspace, size_t workspace_bytes,
                         void* stream) {
-  return integrate_vjp(prob, solver, ys, gys, gy0, gparams, gfusion, nullptr, workspace, workspace_bytes, stream);
+  return integrate_vjp(prob, solver, ys, gys, nullptr, gy0, gparams, gfusion, nullptr, workspace, workspace_bytes,
+                       stream);
 }
 
 int gncde_integrate_vjp_data(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
                              float* gy0, float* gparams, float* gfusion, float* gdata_coef, void* workspace,
                              size_t workspace_bytes, void* stream) {
   if (!gdata_coef) return GNCDE_ERR_ARG;
-  return integrate_vjp(prob, solver, ys, gys, gy0, gparams, gfusion, gdata_coef, workspace, workspace_bytes, stream);
+  return integrate_vjp(prob, solver, ys, gys, nullptr, gy0, gparams, gfusion, gdata_coef, workspace, workspace_bytes,
+                       stream);
+}
+
+int gncde_integrate_vjp_ex(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
+                           const float* gstage, float* gy0, float* gparams, float* gfusion, float* gdata_coef,
+                           void* workspace, size_t workspace_bytes, void* stream) {
+  return integrate_vjp(prob, solver, ys, gys, gstage, gy0, gparams, gfusion, gdata_coef, workspace, workspace_bytes,
+                       stream);
 }
 
 }  // extern "C"

@@ -74,6 +74,8 @@ struct FusedArgs {
   const float* save_ts;
   int n_save, max_steps;
   float rtol, atol;
+  float* step_ts;  // [B, step_len] accepted step times (GncdeSolver.step_ts) or nullptr
+  int step_len;
 };
 
 constexpr int kTsit5Pid = 2;  // internal METHOD id: Tsit5 + PIDController (diffrax defaults)
@@ -617,6 +619,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     float dt = auto_dt ? 0.f : a.dt0[b];
     float t = t0, tn = t0, h = 0.f, tst = t0, h0 = 0.f, d1 = 0.f;
     int phase = 0, st = 0, steps = 0, rejects = 0, evals = 0, status = 0;
+    if (a.step_ts && tid == 0) a.step_ts[(size_t)b * a.step_len] = t0;
     while (true) {
       vf(tst, yt, K);
       ++evals;
@@ -719,6 +722,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
                 y[fb][r] = yt[fb][r];
                 kk[0][fb][r] = kk[6][fb][r];
               }
+            if (a.step_ts && tid == 0 && steps + 1 < a.step_len) a.step_ts[(size_t)b * a.step_len + steps + 1] = tn;
             t = tn;
             ++steps;
           } else {
@@ -753,6 +757,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       tst = ns1 >= 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);
       st = ns1;
     }
+    if (a.step_ts && status == 0 && steps + 1 > a.step_len) status = 3;  // step record truncated
     if (S == 0) {
       store(ysb);
     } else {
@@ -855,6 +860,8 @@ int fused_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0
   a.max_steps = s.max_steps;
   a.rtol = s.rtol;
   a.atol = s.atol;
+  a.step_ts = s.controller == GNCDE_CTRL_PID ? s.step_ts : nullptr;
+  a.step_len = s.step_ts_len;
   hipLaunchKernelGGL(e->fn, dim3(p.B), dim3(e->np * 4), 0, st, a);
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }

@@ -185,14 +185,16 @@ int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const flo
 
 // reverse mode (discrete adjoint, GRID controller): gncde_vjp.hip
 size_t generic_vjp_workspace(const GncdeProblem& p, const GncdeSolver& s);
-int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys, float* gy0,
-                          float* gparams, float* gfusion, float* gdata, char* ws, hipStream_t st);
+// gstage (optional): [B, G-1, S, E] cotangents added to the stage values (gncde_integrate_vjp_ex)
+int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys,
+                          const float* gstage, float* gy0, float* gparams, float* gfusion, float* gdata, char* ws,
+                          hipStream_t st);
 
 // fused per-stage reverse sweep (H = 16, n <= 128, ODE): gncde_stage.hip
 bool stage_vjp_supported(const GncdeProblem& p, const GncdeSolver& s);
 size_t stage_vjp_workspace(const GncdeProblem& p);
-int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys, float* gy0,
-                        float* gparams, float* gfusion, char* ws, hipStream_t st);
+int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys,
+                        const float* gstage, float* gy0, float* gparams, float* gfusion, char* ws, hipStream_t st);
 
 // fused persistent path: gncde_fused.hip.  Returns GNCDE_ERR_UNSUPPORTED when no kernel fits.
 bool fused_supported(const GncdeProblem& p, const GncdeSolver& s, char* name, size_t name_len);

@@ -40,6 +40,8 @@ struct PidArgs {
   const float* K;  // [B, E] value of the last evaluation
   float* ys;    // output: [B, S, E] (SAVE_TS) or [B, E]
   float* tst;   // [B] time of each sample's next evaluation (written by init / advance)
+  float* step_ts;  // [B, step_len] accepted step times (GncdeSolver.step_ts) or nullptr
+  int step_len;
 };
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
@@ -97,6 +99,7 @@ __global__ void k_pid_init(PidArgs a, const float* __restrict__ y0) {
     }
   }
   if (threadIdx.x == 0) {
+    if (a.step_ts) a.step_ts[(size_t)b * a.step_len] = t0;
     PidState s{};
     s.t = s.tn = s.tst = t0;
     s.dt = a.auto_dt ? 0.f : a.dt0[b];
@@ -240,6 +243,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
             }
           }
         }
+        if (a.step_ts && tid == 0 && s.steps + 1 < a.step_len) a.step_ts[(size_t)b * a.step_len + s.steps + 1] = s.tn;
         s.t = s.tn;
         ++s.steps;
       } else {
@@ -259,6 +263,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
       finish = true;
     }
     if (finish) {
+      if (a.step_ts && s.status == 0 && s.steps + 1 > a.step_len) s.status = 3;  // step record truncated
       __syncthreads();
       if (a.S == 0) {
         for (int e = tid; e < E; e += blockDim.x) a.ys[base + e] = y[e];
@@ -365,6 +370,8 @@ int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const flo
   int* active = reinterpret_cast<int*>(take(B * 4));
   a.ys = ys;
   a.tst = tst;
+  a.step_ts = s.step_ts;
+  a.step_len = s.step_ts_len;
   hipLaunchKernelGGL(k_pid_init, dim3(B), dim3(256), 0, st, a, y0);
   generic_vf_prepare(p, ws, st);
   // each sample needs at most 2 + 6 * max_steps + 1 evaluations

@@ -135,6 +135,7 @@ struct RevArgs {
   const int32_t* nsteps;
   const float* ys;      // checkpoints [B, G, n, H]
   const float* gys;     // saved-state cotangents [B, G, n, H] (SAVE_STEPS) or nullptr
+  const float* gst;     // extra stage-value cotangents [B, G-1, S, n, H] (gncde_integrate_vjp_ex) or nullptr
   float* K[6];          // stage values      [B, n, H] each
   float* U[6];          // stage inputs
   float* gK[6];         // stage cotangents
@@ -186,6 +187,9 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
   const size_t E = (size_t)n * H;
   const size_t rowoff = (size_t)b * E + (size_t)(node_ok ? node : 0) * H + 4 * hi;
   auto rowk = [&](int k) -> size_t { return ((size_t)b * G + k) * E + (size_t)(node_ok ? node : 0) * H + 4 * hi; };
+  auto rowst = [&](int k, int j) -> size_t {
+    return (((size_t)b * (G - 1) + k) * a.S + j) * E + (size_t)(node_ok ? node : 0) * H + 4 * hi;
+  };
   float* sA = sR0;
   float* sdA = sR0 + AS;
   float* sW = sVec + 6 * NP;
@@ -668,10 +672,11 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       if (a.has_cur) {  // seeds of step k and its last stage
         const int il = S - 1;
         const float tl = stage_time(tk, a.c[il], hk);
-        float U[4], gK[4], gU[4];
+        float U[4], gK[4], gU[4], sd[4] = {0.f, 0.f, 0.f, 0.f};
         load4(a.U[il], rowoff, U);
+        if (a.gst) load4(a.gst, rowst(k, il), sd);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) gK[r] = hk * a.bw[il] * lam[r];
+        for (int r = 0; r < 4; ++r) gK[r] = hk * a.bw[il] * lam[r] + sd[r];
         if (!formed || tl != tn) form(tl);
         forward(U);
         backward(gK, gU);
@@ -680,8 +685,9 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         for (int r = 0; r < 4; ++r) acc[r] = lam[r] + gU[r];
         store4(a.gyacc, rowoff, acc);
         for (int j = 0; j < il; ++j) {
+          if (a.gst) load4(a.gst, rowst(k, j), sd);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[r] = hk * fmaf(a.a[il][j], gU[r], a.bw[j] * lam[r]);
+          for (int r = 0; r < 4; ++r) acc[r] = hk * fmaf(a.a[il][j], gU[r], a.bw[j] * lam[r]) + sd[r];
           store4(a.gK[j], rowoff, acc);
         }
       } else {
@@ -840,8 +846,8 @@ size_t stage_vjp_workspace(const GncdeProblem& p) {
 //   kBoundary  at t_{k+1}: stage 0 of step k+1 closes lambda_{k+1}; seeds + last stage of step k
 //   middle     RK4: kVjpPair (stages 2, 1);  Tsit5: kVjpMid for stages 4..1
 // and a final kBoundary (stage 0 of step 0 -> gy0).
-int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys, float* gy0,
-                        float* gparams, float* gfusion, char* ws, hipStream_t st) {
+int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys,
+                        const float* gstage, float* gy0, float* gparams, float* gfusion, char* ws, hipStream_t st) {
   const RevEntry* e = find_rev(p);
   if (!e || s.controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
   const int B = p.B, G = s.grid_len;
@@ -867,6 +873,7 @@ int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float
   a.nsteps = s.nsteps;
   a.ys = ys;
   a.gys = steps ? gys : nullptr;
+  a.gst = gstage;
   for (int i = 0; i < 6; ++i) {
     a.K[i] = w.K[i];
     a.U[i] = w.U[i];

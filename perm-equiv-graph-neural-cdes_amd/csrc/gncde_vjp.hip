@@ -301,6 +301,18 @@ __global__ void v_lincomb(int B, size_t E, const float* __restrict__ base, Lin l
   out[o] = fmaf(hb, s, b0);
 }
 
+// gK_i = h_b b_i lam (+ gstage[b, k, i], the extra cotangent of stage i of step k: [B, G1, S, E])
+__global__ void v_seed(int B, size_t E, int G1, int S, int k, int i, float bi, const float* __restrict__ lam,
+                       const float* __restrict__ hcur, const float* __restrict__ gst, float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const size_t o = (size_t)b * E + e;
+  float v = hcur[b] * (bi * lam[o]);
+  if (gst) v += gst[(((size_t)b * G1 + k) * S + i) * E + e];
+  out[o] = v;
+}
+
 // row k of a per-step trajectory [B, G, E]: out = (accumulate ? out : 0) + traj[:, k]
 __global__ void v_step_row(int B, size_t E, int G, int k, const float* __restrict__ traj, float* __restrict__ out,
                            int accumulate) {
@@ -613,8 +625,9 @@ Tableau tsit5_tab() {
 
 }  // namespace
 
-int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys, float* gy0,
-                          float* gparams, float* gfusion, float* gdata, char* ws, hipStream_t st) {
+int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float* ys, const float* gys,
+                          const float* gstage, float* gy0, float* gparams, float* gfusion, float* gdata, char* ws,
+                          hipStream_t st) {
   if (s.controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
   const int B = p.B, G = s.grid_len;
   const size_t E = (size_t)p.n * state_dim(p);
@@ -668,15 +681,10 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
         if (rc) return rc;
       }
     }
-    // reverse: gK_i = h b_i lam ; gy = lam
-    for (int i = 0; i < tab.stages; ++i) {
-      Lin lc{};
-      lc.x[0] = w.lam;
-      lc.a[0] = tab.b[i];
-      lc.nx = 1;
-      lc.scale_h = 1;
-      hipLaunchKernelGGL(v_lincomb, ge, dim3(256), 0, st, B, E, nullptr, lc, w.hcur, w.gK[i], 0);
-    }
+    // reverse: gK_i = h b_i lam (+ the stage's extra cotangent) ; gy = lam
+    for (int i = 0; i < tab.stages; ++i)
+      hipLaunchKernelGGL(v_seed, ge, dim3(256), 0, st, B, E, G - 1, tab.stages, k, i, tab.b[i], w.lam, w.hcur,
+                         gstage, w.gK[i]);
     (void)hipMemcpyAsync(w.gyacc, w.lam, (size_t)B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
     for (int i = tab.stages - 1; i >= 0; --i) {
       hipLaunchKernelGGL(v_stage_time, dim3(gb), dim3(256), 0, st, B, tab.c[i], w.tcur, w.hcur, w.tst);

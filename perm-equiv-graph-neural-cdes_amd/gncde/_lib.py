@@ -12,13 +12,14 @@ from ctypes import POINTER, c_char_p, c_float, c_int32, c_size_t, c_void_p
 
 MAX_LAYERS = 8
 FC = 24
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 RK4, TSIT5 = 0, 1
 CTRL_GRID, CTRL_PID = 0, 1
 SAVE_T1, SAVE_STEPS, SAVE_TS = 0, 1, 2
 COMPUTE_FP32, COMPUTE_BF16, COMPUTE_BF16_STORAGE = 0, 1, 2  # GncdeProblem.compute (gncde.h)
 STAT_STEPS, STAT_REJECTS, STAT_EVALS, STAT_STATUS = 0, 1, 2, 3
+STATUS_OK, STATUS_MAX_STEPS, STATUS_NONFINITE, STATUS_STEP_RECORD = 0, 1, 2, 3
 OP_NORM_LAP, OP_NORM_ADJ, OP_KIPF, OP_NORMALIZED_PLUS = 0, 1, 2, 3
 
 LIB_NAME = "libgncde_hip.so"
@@ -35,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "gncde_vjp_workspace_bytes",
     "gncde_integrate_vjp",
     "gncde_integrate_vjp_data",
+    "gncde_integrate_vjp_ex",
     "gncde_node_affine",
     "gncde_node_affine_grad",
     "gncde_adamw_workspace_bytes",
@@ -81,6 +83,8 @@ class GncdeSolver(ctypes.Structure):
         ("t1", c_void_p),
         ("dt0", c_void_p),
         ("save_ts", c_void_p),
+        ("step_ts", c_void_p),
+        ("step_ts_len", c_int32),
     ]
 
 
@@ -123,6 +127,10 @@ def load(path: str | None = None):
     lib.gncde_integrate_vjp_data.restype = c_int32
     lib.gncde_integrate_vjp_data.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver), c_void_p, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    lib.gncde_integrate_vjp_ex.restype = c_int32
+    lib.gncde_integrate_vjp_ex.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver), c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                           c_void_p]
     lib.gncde_node_affine.restype = c_int32
     lib.gncde_node_affine.argtypes = [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p]

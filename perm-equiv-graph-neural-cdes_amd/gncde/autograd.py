@@ -1,8 +1,13 @@
-"""Differentiable fixed-grid solve: ``torch.autograd`` over ``gncde_integrate`` / ``gncde_integrate_vjp``.
+"""Differentiable solves: ``torch.autograd`` over ``gncde_integrate`` / ``gncde_integrate_vjp_ex``.
 
 Replaces ``equinox.filter_value_and_grad`` through ``diffrax.diffeqsolve`` (trainer.py:315 over
-graph_neural_cde.py:94-104): the forward keeps every step state (SAVE_STEPS) as the checkpoints, and the
-backward is the discrete adjoint computed on the GPU (gncde_vjp.hip).  Parameters enter as the packed
+graph_neural_cde.py:94-104).  Fixed grids: the forward keeps every step state (SAVE_STEPS) as the checkpoints,
+and the backward is the discrete adjoint computed on the GPU (gncde_stage.hip / gncde_vjp.hip).  Adaptive
+Tsit5 + PIDController: the forward records each sample's accepted step sequence (GncdeSolver.step_ts); the
+backward replays that grid for the checkpoints and runs the same discrete adjoint over it, with the step sizes
+held constant (what RecursiveCheckpointAdjoint differentiates through diffrax's while_loop: rejected attempts
+leave no trace in the accepted solution) and SaveAt(ts)'s Tsit5 dense interpolant differentiated through
+its stage values.  Parameters enter as the packed
 buffer ``params`` (include/gncde.h layout) and the factored fusion table ``fusion`` [L, 24]; both are
 ordinary differentiable torch tensors, so gradients flow on to the reference-named module parameters
 through ``layout.fusion_table_torch`` (the linear map whose transpose turns table gradients into
@@ -45,19 +50,116 @@ class _FixedGridSolve(torch.autograd.Function):
         return gy0.to(d0), gp.to(dp), gf.to(df), gdata, None, None
 
 
+def tsit5_dense_weights(theta: torch.Tensor) -> torch.Tensor:
+    """Tsit5 free interpolant b_j(theta), j = 0..6, in fp32 with the kernels' formula (gncde_pid.hip
+    tsit5_dense_w; oracle/gncde_oracle.py tsit5_dense_weights): y(t + th h) = y + h sum_j b_j(th) K_j."""
+    th = theta.to(torch.float32)
+    t2 = th * th
+    return torch.stack([
+        -1.0530884977290216 * th * (th - 1.3299890189751412) * (t2 - 1.4364028541716351 * th + 0.7139816917074209),
+        0.1017 * t2 * (t2 - 2.1966568338249754 * th + 1.2949852507374631),
+        2.490627285651252793 * t2 * (t2 - 2.38535645472061657 * th + 1.57803468208092486),
+        -16.54810288924490272 * (th - 1.21712927295533244) * (th - 0.61620406037800089) * t2,
+        47.37952196281928122 * (th - 1.203071208372362603) * (th - 0.658047292653547382) * t2,
+        -34.87065786149660974 * (th - 1.2) * (th - 0.666666666666666667) * t2,
+        2.5 * (th - 1.0) * (th - 0.6) * t2], dim=-1)
+
+
+def pid_replay_grid(step_ts: torch.Tensor, nsteps: torch.Tensor, pad: int = 1):
+    """The accepted step sequences of a recorded PID solve as a fixed grid [B, max(nsteps) + 1 + pad]: sample b's
+    times step_ts[b, :nsteps[b] + 1], then its last time repeated (zero-length padded steps, identities)."""
+    G = int(nsteps.max().item()) + 1 + pad
+    cols = torch.arange(G, device=step_ts.device)
+    idx = torch.minimum(cols[None, :], nsteps.to(torch.long)[:, None])
+    return step_ts.gather(1, idx).contiguous(), nsteps.to(torch.int32).contiguous()
+
+
+def dense_output_cotangents(grid: torch.Tensor, nsteps: torch.Tensor, save_ts: torch.Tensor, g: torch.Tensor):
+    """Reverse mode of SaveAt(ts) through the Tsit5 dense interpolant on a (replayed) grid.
+
+    The save point s of sample b lies in step k (t_k < ts <= t_{k+1}; ts <= t0 returns y0), th = (ts - t_k) / h_k,
+    and y(ts) = y_k + h_k sum_j b_j(th) K_j with K_6 = f(t_{k+1}, y_{k+1}) = stage 0 of step k + 1 (FSAL).  Its
+    cotangent g_s therefore goes to y_k (returned as per-step cotangents gys [B, G, n, d]) and to the stage values
+    (gstage [B, G-1, 6, n, d]: h_k b_j(th) g_s on stage j < 6 of step k, h_k b_6(th) g_s on stage 0 of step k+1;
+    the grid carries a padded step after every sample's last one, so k + 1 is always a step index)."""
+    B, G = grid.shape
+    S = save_ts.shape[1]
+    E = g[0, 0].numel()
+    ns = nsteps.to(torch.long)
+    gf = g.reshape(B, S, E).to(torch.float32)
+    t0 = grid[:, :1]
+    # k: last grid index with t_k < ts among the sample's real knots (searchsorted 'left' - 1), clamped to a step
+    kk = torch.searchsorted(grid.contiguous(), save_ts.to(torch.float32).contiguous(), right=False) - 1
+    kk = torch.minimum(torch.clamp(kk, min=0), (ns - 1).clamp(min=0)[:, None])
+    direct = save_ts <= t0  # y0 itself
+    tk = grid.gather(1, kk)
+    hk = grid.gather(1, kk + 1) - tk
+    th = torch.where(direct | (hk == 0), torch.zeros_like(hk), (save_ts - tk) / torch.where(hk == 0, 1.0, hk))
+    w = tsit5_dense_weights(th) * hk[..., None]  # [B, S, 7] = h_k b_j(th)
+    w = torch.where(direct[..., None], torch.zeros_like(w), w)
+    gys = torch.zeros(B, G, E, dtype=torch.float32, device=g.device)
+    gys.scatter_add_(1, torch.where(direct, 0, kk)[..., None].expand(B, S, E), gf)
+    gst = torch.zeros(B, G - 1, 6, E, dtype=torch.float32, device=g.device)
+    flat = gst.view(B, (G - 1) * 6, E)
+    for j in range(6):
+        flat.scatter_add_(1, (kk * 6 + j)[..., None].expand(B, S, E), w[..., j, None] * gf)
+    flat.scatter_add_(1, ((kk + 1) * 6)[..., None].expand(B, S, E), w[..., 6, None] * gf)
+    shp = tuple(g.shape[2:])
+    return gys.view((B, G) + shp), gst.view((B, G - 1, 6) + shp)
+
+
+class _PidSolve(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y0, params, fusion, data_coef, prob, spec):
+        p = dataclasses.replace(prob, params=params.detach().to(torch.float32).contiguous(),
+                                fusion=fusion.detach().to(torch.float32).contiguous())
+        if data_coef is not None:
+            p = dataclasses.replace(p, data_coef=data_coef.detach().to(torch.float32).contiguous())
+        rec = torch.empty(prob.B, spec.max_steps + 1, dtype=torch.float32, device=y0.device)
+        ys, st = engine.integrate(p, dataclasses.replace(spec, step_ts=rec), y0.detach(), stats=True)
+        if torch.any(st[:, _lib.STAT_STATUS] != 0):
+            raise _lib.GncdeError("adaptive solve failed (max_steps reached or non-finite error estimate)")
+        ctx.prob, ctx.spec = p, spec
+        ctx.dtypes = (y0.dtype, params.dtype, fusion.dtype)
+        ctx.save_for_backward(y0.detach().to(torch.float32).contiguous(), rec, st[:, _lib.STAT_STEPS].contiguous())
+        return ys
+
+    @staticmethod
+    def backward(ctx, g):
+        y0, rec, ns = ctx.saved_tensors
+        spec = ctx.spec
+        dense = spec.save_mode == _lib.SAVE_TS
+        grid, nst = pid_replay_grid(rec, ns, pad=1 if dense else 0)
+        steps = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_STEPS, grid=grid,
+                                  nsteps=nst)
+        ys = engine.integrate(ctx.prob, steps, y0)  # the checkpoints: the accepted steps replayed
+        want_data = ctx.needs_input_grad[3]
+        if dense:
+            gys, gst = dense_output_cotangents(grid, nst, spec.save_ts, g)
+            res = engine.integrate_vjp(ctx.prob, steps, ys, gys, data_grad=want_data, gstage=gst)
+        else:
+            t1 = dataclasses.replace(steps, save_mode=_lib.SAVE_T1)
+            res = engine.integrate_vjp(ctx.prob, t1, ys, g, data_grad=want_data)
+        gy0, gp, gf = res[:3]
+        d0, dp, df = ctx.dtypes
+        return gy0.to(d0), gp.to(dp), gf.to(df), (res[3] if want_data else None), None, None
+
+
 def solve(prob: engine.Problem, spec: engine.SolverSpec, y0: torch.Tensor, params: torch.Tensor | None = None,
           fusion: torch.Tensor | None = None, data_coef: torch.Tensor | None = None) -> torch.Tensor:
-    """Fixed-grid solve that records a backward.  ``spec.save_mode`` SAVE_T1 returns [B, n, d] (final
-    state), SAVE_STEPS returns [B, G, n, d].  ``params`` / ``fusion`` default to the problem's own
-    (then only ``y0`` can carry gradients).  ``data_coef`` (CDE problems) replaces the problem's data
-    spline with a differentiable one (TGBGraphNeuralCDE's in-forward spline of the embedded data)."""
-    if spec.controller != _lib.CTRL_GRID:
-        raise _lib.GncdeError("the differentiable solve needs a fixed grid (GRID controller); "
-                              "adaptive PID solves are forward-only in this build")
-    if spec.save_mode not in (_lib.SAVE_T1, _lib.SAVE_STEPS):
-        raise _lib.GncdeError("differentiable solve: save_mode must be SAVE_T1 or SAVE_STEPS")
+    """A solve that records a backward.  Fixed grid (GRID controller): SAVE_T1 returns [B, n, d] (final state),
+    SAVE_STEPS [B, G, n, d].  Tsit5 + PIDController: SAVE_T1 [B, n, d] or SAVE_TS [B, S, n, d] (the dense output at
+    spec.save_ts).  ``params`` / ``fusion`` default to the problem's own (then only ``y0`` can carry gradients).
+    ``data_coef`` (CDE problems) replaces the problem's data spline with a differentiable one (TGBGraphNeuralCDE's
+    in-forward spline of the embedded data)."""
     params = prob.params if params is None else params
     fusion = prob.fusion if fusion is None else fusion
+    if spec.controller == _lib.CTRL_PID:
+        if spec.method != _lib.TSIT5 or spec.save_mode not in (_lib.SAVE_T1, _lib.SAVE_TS):
+            raise _lib.GncdeError("differentiable adaptive solve: Tsit5 with SAVE_T1 or SAVE_TS")
+        return _PidSolve.apply(y0, params, fusion, data_coef, prob, spec)
+    if spec.save_mode not in (_lib.SAVE_T1, _lib.SAVE_STEPS):
+        raise _lib.GncdeError("differentiable fixed-grid solve: save_mode must be SAVE_T1 or SAVE_STEPS")
     return _FixedGridSolve.apply(y0, params, fusion, data_coef, prob, spec)
 
 

@@ -169,6 +169,7 @@ class SolverSpec:
     t1: torch.Tensor | None = None
     dt0: torch.Tensor | None = None
     save_ts: torch.Tensor | None = None
+    step_ts: torch.Tensor | None = None  # PID: OUTPUT [B, cap] accepted step times (t0 first), filled by integrate
 
     def c_struct(self) -> _lib.GncdeSolver:
         s = _lib.GncdeSolver()
@@ -183,13 +184,18 @@ class SolverSpec:
         s.t1 = _ptr(self.t1).value if self.t1 is not None else None
         s.dt0 = _ptr(self.dt0).value if self.dt0 is not None else None
         s.save_ts = _ptr(self.save_ts).value if self.save_ts is not None else None
+        if self.step_ts is not None:
+            if not (self.step_ts.is_cuda and self.step_ts.dtype == torch.float32 and self.step_ts.is_contiguous()):
+                raise _lib.GncdeError("SolverSpec.step_ts must be a contiguous fp32 CUDA tensor [B, cap]")
+            s.step_ts = _ptr(self.step_ts).value
+            s.step_ts_len = int(self.step_ts.shape[1])
         return s
 
     def shard(self, start, stop):
         cut = lambda x: None if x is None else x[start:stop]  # noqa: E731
         return SolverSpec(self.method, self.controller, self.save_mode, cut(self.grid), cut(self.nsteps),
                           self.rtol, self.atol, self.max_steps, cut(self.t0), cut(self.t1), cut(self.dt0),
-                          cut(self.save_ts))
+                          cut(self.save_ts), cut(self.step_ts))
 
 
 def integrate_path(prob: Problem, solver: SolverSpec) -> str:
@@ -224,12 +230,13 @@ def integrate(prob: Problem, solver: SolverSpec, y0: torch.Tensor, stats: bool =
 
 
 def integrate_vjp(prob: Problem, solver: SolverSpec, ys_steps: torch.Tensor, gys: torch.Tensor,
-                  data_grad: bool = False):
+                  data_grad: bool = False, gstage: torch.Tensor | None = None):
     """Reverse mode of ``integrate`` for a fixed grid (the discrete adjoint ``jax.grad`` takes through
     diffrax's RecursiveCheckpointAdjoint, trainer.py:315).
 
     ys_steps: [B, G, n, d] the forward's SAVE_STEPS states; gys: cotangent of the forward output in
-    ``solver.save_mode`` layout (SAVE_T1 [B, n, d] or SAVE_STEPS [B, G, n, d]).
+    ``solver.save_mode`` layout (SAVE_T1 [B, n, d] or SAVE_STEPS [B, G, n, d]); gstage (optional):
+    [B, G-1, S, n, d] extra cotangents of the stage values (S = 4 RK4 / 6 Tsit5; gncde_integrate_vjp_ex).
     Returns (gy0 [B, n, d], gparams [P] summed over samples, gfusion [L, 24] summed over samples), plus the
     cotangent of ``prob.data_coef`` (layout of data_coef) when ``data_grad`` (CDE problems only).
     """
@@ -244,23 +251,25 @@ def integrate_vjp(prob: Problem, solver: SolverSpec, ys_steps: torch.Tensor, gys
     want = (B, n, ds) if solver.save_mode == _lib.SAVE_T1 else (B, ss.grid_len, n, ds)
     if gys.shape != want:
         raise _lib.GncdeError(f"integrate_vjp: gys shape {tuple(gys.shape)} != {want}")
+    if gstage is not None:
+        S = 4 if solver.method == _lib.RK4 else 6
+        gstage = gstage.to(torch.float32).contiguous()
+        if gstage.shape != (B, ss.grid_len - 1, S, n, ds):
+            raise _lib.GncdeError(f"integrate_vjp: gstage shape {tuple(gstage.shape)} != "
+                                  f"{(B, ss.grid_len - 1, S, n, ds)}")
+    if data_grad and prob.data_coef is None:
+        raise _lib.GncdeError("integrate_vjp(data_grad=True) needs a CDE problem")
     dev = prob.params.device
     gy0 = torch.empty(B, n, ds, dtype=torch.float32, device=dev)
     gparams = torch.empty_like(prob.params)
     gfusion = torch.empty_like(prob.fusion)
+    gdata = torch.empty_like(prob.data_coef) if data_grad else None
     nbytes = lib.gncde_vjp_workspace_bytes(ctypes.byref(ps), ctypes.byref(ss))
     ws = _Workspace.get(nbytes) if nbytes else None
-    if not data_grad:
-        _lib.check(lib.gncde_integrate_vjp(ctypes.byref(ps), ctypes.byref(ss), _ptr(ys_steps), _ptr(gys),
-                                           _ptr(gy0), _ptr(gparams), _ptr(gfusion), _ptr(ws), nbytes, _stream()))
-        return gy0, gparams, gfusion
-    if prob.data_coef is None:
-        raise _lib.GncdeError("integrate_vjp(data_grad=True) needs a CDE problem")
-    gdata = torch.empty_like(prob.data_coef)
-    _lib.check(lib.gncde_integrate_vjp_data(ctypes.byref(ps), ctypes.byref(ss), _ptr(ys_steps), _ptr(gys),
-                                            _ptr(gy0), _ptr(gparams), _ptr(gfusion), _ptr(gdata), _ptr(ws),
-                                            nbytes, _stream()))
-    return gy0, gparams, gfusion, gdata
+    _lib.check(lib.gncde_integrate_vjp_ex(ctypes.byref(ps), ctypes.byref(ss), _ptr(ys_steps), _ptr(gys),
+                                          _ptr(gstage), _ptr(gy0), _ptr(gparams), _ptr(gfusion), _ptr(gdata),
+                                          _ptr(ws), nbytes, _stream()))
+    return (gy0, gparams, gfusion, gdata) if data_grad else (gy0, gparams, gfusion)
 
 
 def node_affine(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:

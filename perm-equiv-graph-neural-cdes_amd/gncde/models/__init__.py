@@ -133,16 +133,16 @@ class GraphNeuralCDE(nn.Module):
             ys, st = engine.integrate(prob, spec, y0, stats=True)
             if torch.any(st[:, _lib.STAT_STATUS] != 0):
                 raise RuntimeError("diffrax-equivalent failure: max_steps reached or non-finite state")
-            if spec.save_mode == _lib.SAVE_STEPS:
+            if spec.controller == _lib.CTRL_GRID and spec.save_mode == _lib.SAVE_STEPS:
                 ys = self._knot_states(ys, ts_d.shape[1])
             out = _affine(self.final_linear, ys)
         return (out, st) if return_stats else out
 
     def predict(self, ts, coeffs_adj, x0, evolving_out=True):
-        """Differentiable batched forward (fixed-grid ``solver`` only): the prediction of ``batched`` with
-        an autograd graph through the read-out, the GPU solve (discrete adjoint) and the encoder."""
-        if self.solver is None:
-            raise NotImplementedError("training needs a fixed-grid solver override (adaptive PID is forward-only)")
+        """Differentiable batched forward: the prediction of ``batched`` with an autograd graph through the
+        read-out, the GPU solve and the encoder.  The reference solve (Tsit5 + PIDController, SaveAt(ts)) is
+        differentiated on its accepted step sequence (autograd.solve); a fixed-grid ``solver`` override by its
+        discrete adjoint."""
         control = CubicInterpolation(ts, coeffs_adj)
         ts_d = control.graph_layout()[0]
         x0 = torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device)
@@ -170,7 +170,7 @@ class GraphNeuralCDE(nn.Module):
         y0 = _affine(self.initial_linear, x0)
         params, fusion = self.vector_field.diff_tensors(prob.n, x0.device)
         ys = autograd.solve(prob, spec, y0, params, fusion)
-        if spec.save_mode == _lib.SAVE_STEPS:
+        if spec.controller == _lib.CTRL_GRID and spec.save_mode == _lib.SAVE_STEPS:
             ys = self._knot_states(ys, prob.T)
         return _affine(self.final_linear, ys)
 

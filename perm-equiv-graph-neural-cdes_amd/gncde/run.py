@@ -12,10 +12,9 @@ Flow (trainer.py:88-285): build the dataset (gncde.data, f2), the vector field b
 interpolation / extrapolation MSE with the model's own solve (Tsit5 + PIDController, SaveAt(ts)); early
 stopping with ``patience`` / ``min_epochs``; the best model saved under ``checkpoint_dir`` (safetensors).
 
-One deliberate difference: training differentiates a fixed-grid solve (``--steps-per-interval`` RK4 steps
-between consecutive training knots, so every knot is a step state) instead of the adaptive Tsit5+PID
-solve — the engine's reverse mode covers fixed grids.  Evaluation uses the reference
-solve.  wandb is not used; metrics are printed (and appended to ``--out``) as JSON lines with the
+Training differentiates the reference's own solve (Tsit5 + PIDController, SaveAt(ts)) on each sample's
+accepted step sequence (autograd.solve).  ``--steps-per-interval M`` optionally replaces it with
+a fixed RK4 grid of M steps between consecutive knots (a build extension).  wandb is not used; metrics are printed (and appended to ``--out``) as JSON lines with the
 reference's names (train_loss, max_grad, max_update, validation_loss, test_loss_extra ...).
 """
 from __future__ import annotations
@@ -43,7 +42,8 @@ def _mse(pred, y, idx):
 class Trainer:
     """Mirror of the reference's dyn Trainer for GraphNeuralCDE models."""
 
-    def __init__(self, cfg: dict, epochs: int | None = None, steps_per_interval: int = 2, out: str | None = None):
+    def __init__(self, cfg: dict, epochs: int | None = None, steps_per_interval: int | None = None,
+                 out: str | None = None):
         self.cfg = cfg
         self.epochs = int(epochs if epochs is not None else cfg.get("epochs", 100))
         self.patience = int(cfg.get("patience", 10 ** 9))
@@ -74,7 +74,8 @@ class Trainer:
         vf = cls(input_dim=h, hidden_dim=int(vfc.get("hidden_dim", h)), output_dim=h,
                  num_layers=int(vfc.get("num_layers", 2)), data_embed_dim=1, num_nodes=ds.n, key=self.seed)
         model = GraphNeuralCDE(m, vf, m.get("interpolation", "cubic"), self.seed,
-                               solver={"method": "rk4", "steps_per_interval": self.steps_per_interval})
+                               solver=None if self.steps_per_interval is None else
+                               {"method": "rk4", "steps_per_interval": self.steps_per_interval})
         return ds, model.to("cuda")
 
     def run(self) -> dict:
@@ -254,7 +255,9 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--config", required=True)
     ap.add_argument("--epochs", type=int, default=None)
-    ap.add_argument("--steps-per-interval", type=int, default=2, help="dyn models: RK4 steps between knots")
+    ap.add_argument("--steps-per-interval", type=int, default=None,
+                    help="dyn models: train on a fixed RK4 grid of M steps between knots instead of the reference's "
+                         "adaptive Tsit5 + PID solve")
     ap.add_argument("--window-batch", type=int, default=1, help="pgt/tgb models: windows per optimiser step")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)

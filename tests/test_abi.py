@@ -44,15 +44,17 @@ def test_struct_layout_matches_c(tmp_path):
 #include <stddef.h>
 #include "{HEADER}"
 int main(void) {{
-  printf("%zu %zu %zu %zu %zu\\n", sizeof(GncdeProblem), offsetof(GncdeProblem, ts),
-         offsetof(GncdeProblem, params), sizeof(GncdeSolver), offsetof(GncdeSolver, save_ts));
+  printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(GncdeProblem), offsetof(GncdeProblem, ts),
+         offsetof(GncdeProblem, params), sizeof(GncdeSolver), offsetof(GncdeSolver, save_ts),
+         offsetof(GncdeSolver, step_ts), offsetof(GncdeSolver, step_ts_len));
   return 0;
 }}''')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-std=c99", str(src), "-o", str(exe)], check=True)
     vals = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
     P, S = _lib.GncdeProblem, _lib.GncdeSolver
-    assert vals == [ctypes.sizeof(P), P.ts.offset, P.params.offset, ctypes.sizeof(S), S.save_ts.offset]
+    assert vals == [ctypes.sizeof(P), P.ts.offset, P.params.offset, ctypes.sizeof(S), S.save_ts.offset,
+                    S.step_ts.offset, S.step_ts_len.offset]
 
 
 def _fake_problem(B=4, n=64, T=10, dims=(16, 16, 16, 16)):

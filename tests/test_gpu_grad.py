@@ -385,3 +385,117 @@ def test_tgb_model_trains_data_encoder(G):
     for _ in range(8):
         loss, _, _ = train.make_step(opt, model.loss_terms, *args)
     assert float(loss) < first
+
+
+def _pid_case(G, rng, B, n, kind, dims, cde=None):
+    """A small adaptive problem: (prob, params leaf, fusion leaves, fusion table, y0 leaf, oracle f/f_vjp per
+    sample).  cde = (h, de): the CDE wrapper against a random data spline."""
+    if cde is not None:
+        h, de = cde
+        dims = [h] + list(dims[1:-1]) + [h * de * 2]
+    T = 5
+    ts, coeffs, P = MG.problem(rng, B, n, T, kind, dims, irregular=cde is None)
+    for lay in P.layers:  # fusion terms large enough to matter
+        for nm in OG.FUSION_NAMES[kind]:
+            lay[nm] = lay[nm] * 3.0
+    kw, dco = {}, None
+    if cde is not None:
+        dco = []
+        for b in range(B):
+            x = rng.standard_normal((T, n, de))
+            X = np.stack([np.broadcast_to(ts[b][:, None, None], x.shape), x], axis=-1)
+            dco.append(O.backward_hermite_coefficients(ts[b], X))
+        dc = tuple(np.stack([c[q] for c in dco]) for q in range(4))
+        kw = dict(data_coeffs=dc, cde_hidden=h, cde_embed=de)
+    prob = G.make_problem(ts, coeffs, P.kind, P.layers, **kw)
+    fns = []
+    for b in range(B):
+        ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
+        if cde is None:
+            fns.append((lambda t, y, c=ctrl: O.vector_field(P, t, y, c),
+                        lambda t, y, g, c=ctrl: OG.vector_field_vjp(P, t, y, c, g)))
+        else:
+            cx = O.CubicInterpolation(ts[b], dco[b])
+            fns.append((lambda t, y, c=ctrl, x=cx: O.cde_wrapper(P, h, de, t, y, c, x),
+                        lambda t, y, g, c=ctrl, x=cx: OG.cde_wrapper_vjp(P, h, de, t, y, c, x, g)))
+    return ts, P, prob, fns, rng.standard_normal((B, n, dims[0]))
+
+
+@pytest.mark.parametrize("case,save", [("fused", "ts"), ("fused", "t1"), ("generic", "ts"), ("cde", "ts"),
+                                       ("cde", "t1")])
+def test_pid_solve_gradient_matches_oracle(G, case, save):
+    """Reverse mode of the adaptive Tsit5 + PIDController(1e-3, 1e-6) solve (graph_neural_cde.py:53-54,94-104,
+    differentiated by trainer.py:315) through autograd.solve: the forward records each sample's accepted steps
+    (GncdeSolver.step_ts), the backward replays them and runs the discrete adjoint with the dense-output stage
+    cotangents (gncde_integrate_vjp_ex).  Against the fp64 oracle's adjoint on the SAME step sequence
+    (solve_grid_dense_vjp, FD-pinned in tests/test_oracle_grad.py).  Paths: the fused PID forward + fused reverse
+    sweep (n = 16, h = 16), the generic PID forward + generic reverse (mixed widths), and the CDE wrapper (generic,
+    de = 2)."""
+    rng = np.random.default_rng({"fused": 31, "generic": 32, "cde": 33}[case])
+    if case == "fused":
+        ts, P, prob, fns, y0n = _pid_case(G, rng, 3, 16, "undirected", [16, 16, 16])
+    elif case == "generic":
+        ts, P, prob, fns, y0n = _pid_case(G, rng, 2, 12, "directed", [8, 12, 8])
+    else:
+        ts, P, prob, fns, y0n = _pid_case(G, rng, 2, 10, "undirected", [8, 8, 0], cde=(8, 2))
+    B = prob.B
+    tsd = torch.tensor(ts, dtype=torch.float32, device="cuda")
+    spec = G.SolverSpec(method=G._lib.TSIT5, controller=G._lib.CTRL_PID,
+                        save_mode=G._lib.SAVE_TS if save == "ts" else G._lib.SAVE_T1, rtol=1e-3, atol=1e-6,
+                        t0=tsd[:, 0].contiguous(), t1=tsd[:, -1].contiguous(),
+                        save_ts=tsd.contiguous() if save == "ts" else None)
+    path = G.integrate_path(prob, spec)
+    assert path.startswith("fused<") == (case == "fused"), path
+    names = OG.FUSION_NAMES[P.kind]
+    fus_leaves = [[_leaf(lay[nm]) for nm in names] for lay in P.layers]
+    fusion = G.layout.fusion_table_torch(P.kind, fus_leaves, prob.n).float()
+    # the step sequence the backward differentiates on (the autograd forward records the same one)
+    import dataclasses
+    rec = torch.empty(B, spec.max_steps + 1, device="cuda")
+    y0d = torch.tensor(y0n, dtype=torch.float32, device="cuda")
+    ys_rec, st = G.integrate(dataclasses.replace(prob, fusion=fusion.detach().contiguous()),
+                             dataclasses.replace(spec, step_ts=rec), y0d, stats=True)
+    st = st.cpu().numpy()
+    assert np.all(st[:, 3] == 0)
+    grids = [rec[b, :st[b, 0] + 1].cpu().numpy().astype(np.float64) for b in range(B)]
+    for b in range(B):
+        assert grids[b][0] == np.float32(ts[b, 0]) and grids[b][-1] == np.float32(ts[b, -1]), (grids[b], ts[b])
+        assert np.all(np.diff(grids[b]) > 0)
+    params = prob.params.clone().requires_grad_(True)
+    y0 = _leaf(y0n)
+    out = G.autograd.solve(prob, spec, y0, params, fusion)
+    assert torch.equal(out.detach(), ys_rec)
+    g = rng.standard_normal(tuple(out.shape))
+    (out.double() * torch.tensor(g, device="cuda")).sum().backward()
+    # the oracle's adjoint at y0 and at y0 (1 + 1e-6): ReLU networks have gradients that jump where a
+    # pre-activation crosses 0, so a sample whose gradient moves under that perturbation is judged against that
+    # spread (5x) instead of RTOL_GRAD (the fixtures instead redraw such samples, make_golden.grad_case)
+    refs = []
+    for scale in (1.0, 1.0 + 1e-6):
+        gy0_ref, total = [], None
+        for b in range(B):
+            f, fv = fns[b]
+            save_ts = ts[b] if save == "ts" else ts[b, -1:]
+            gb = g[b] if save == "ts" else g[b][None]
+            gy, gr = OG.solve_grid_dense_vjp(f, fv, grids[b], y0n[b] * scale, save_ts, gb, time_dtype=np.float32)
+            gy0_ref.append(gy)
+            total = OG._acc(total, gr)
+        refs.append((np.stack(gy0_ref), total))
+    (gy0_ref, total), (gy0_p, total_p) = refs
+    errs = {"y0": (rel_err(y0.grad.cpu().numpy(), gy0_ref), rel_err(gy0_p, gy0_ref))}
+    gp = params.grad.cpu().numpy()
+    off = 0
+    for l, lay in enumerate(P.layers):
+        for k in ("rms_w", "rms_b", "W", "b"):
+            sz = np.asarray(lay[k]).size
+            errs[f"l{l}.{k}"] = (rel_err(gp[off:off + sz].reshape(np.asarray(lay[k]).shape), total[l][k]),
+                                 rel_err(total_p[l][k], total[l][k]))
+            off += sz
+        for j, nm in enumerate(names):
+            errs[f"l{l}.{nm}"] = (rel_err(fus_leaves[l][j].grad.cpu().numpy(), total[l][nm]),
+                                  rel_err(total_p[l][nm], total[l][nm]))
+    worst = max(errs, key=lambda k: errs[k][0])
+    print(f"pid {case} save={save} [{path}]: steps {st[:, 0].tolist()} rejects {st[:, 1].tolist()}; worst {worst} "
+          f"{errs[worst][0]:.2e} (oracle spread under a 1e-6 change of y0: {errs[worst][1]:.2e})")
+    for k, (e, spread) in errs.items():
+        assert e <= max(RTOL_GRAD, 5.0 * spread), (k, e, spread)

@@ -10,7 +10,10 @@ import yaml
 pytestmark = pytest.mark.gpu
 
 
-def test_dyn_single_run_small(tmp_path):
+@pytest.mark.parametrize("spi", [None, 1])
+def test_dyn_single_run_small(tmp_path, spi):
+    """trainer.py flow on the dyn config: spi None trains on the reference's adaptive Tsit5 + PID solve (reverse mode
+    on the accepted steps), spi = 1 on the fixed RK4 grid override."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a HIP device")
     from gncde import data, run
@@ -24,7 +27,7 @@ def test_dyn_single_run_small(tmp_path):
     # heat diffusion conserves nothing special but must decay towards the mean: bounded by the initial max
     assert float(ds.true_y.abs().max()) <= float(ds.x0.abs().max()) * 1.0001
     out = tmp_path / "metrics.jsonl"
-    res = run.Trainer(cfg, epochs=12, steps_per_interval=1, out=str(out)).run()
+    res = run.Trainer(cfg, epochs=12, steps_per_interval=spi, out=str(out)).run()
     assert res["best_epoch"] > 0 and res["best_validation_loss"] == res["best_validation_loss"]
     assert os.path.exists(res["checkpoint"])
     lines = out.read_text().splitlines()

@@ -135,3 +135,39 @@ def test_data_spline_vjp_matches_finite_differences():
         fd = _directional_fd(lambda s: loss(x + s * v), 0.0, 1.0)
         an = float(np.sum(gX * v))
         assert abs(fd - an) <= 1e-6 * max(1.0, abs(an)), (fd, an)
+
+
+@pytest.mark.parametrize("kind,dims", [("undirected", [4, 4, 4]), ("directed", [3, 4, 3])])
+def test_adaptive_solve_dense_vjp_matches_finite_differences(kind, dims):
+    """Reverse mode of the reference's training solve, Tsit5 + PIDController(1e-3, 1e-6) with SaveAt(ts)
+    (graph_neural_cde.py:53-54,89-104 under trainer.py:315), on its accepted step sequence with the step sizes held
+    constant: solve_grid_dense_vjp against central differences of solve_grid_dense on that grid.  Save times include
+    t0 (the initial state itself), knots inside steps and t1."""
+    rng = np.random.default_rng(21)
+    ts, ctrl, P = _problem(rng, kind, dims)
+    n = 6
+    y0 = rng.standard_normal((n, dims[0]))
+
+    def f_of(theta):
+        Pt = OG.vector_to_params(theta, P)
+        return lambda t, y: O.vector_field(Pt, t, y, ctrl)
+
+    f = f_of(OG.params_to_vector(P))
+    ys, st = O.solve_tsit5_pid(f, ts[0], ts[-1], y0, save_ts=ts)
+    grid = st["grid"]
+    assert len(grid) == st["steps"] + 1 and st["rejects"] >= 0
+    # the dense forward on the recorded grid reproduces the adaptive solve's output
+    assert np.max(np.abs(OG.solve_grid_dense(f, grid, y0, ts, time_dtype=None) - ys)) <= 1e-12 * np.max(np.abs(ys))
+    g = rng.standard_normal(ys.shape)
+    fv = lambda t, y, gg: OG.vector_field_vjp(P, t, y, ctrl, gg)  # noqa: E731
+    gy0, grads = OG.solve_grid_dense_vjp(f, fv, grid, y0, ts, g)
+    theta, gtheta = OG.params_to_vector(P), OG.grads_to_vector(grads, kind)
+
+    def loss(s, vy, vt):
+        return float(np.sum(g * OG.solve_grid_dense(f_of(theta + s * vt), grid, y0 + s * vy, ts)))
+
+    for _ in range(2):
+        vy, vt = rng.standard_normal(y0.shape), rng.standard_normal(theta.shape)
+        fd = _directional_fd(lambda s: loss(s, vy, vt), 0.0, 1.0)
+        an = float(np.sum(gy0 * vy) + np.sum(gtheta * vt))
+        assert abs(fd - an) <= 1e-6 * max(1.0, abs(an)), (fd, an)
