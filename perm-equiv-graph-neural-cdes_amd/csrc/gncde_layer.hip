@@ -94,6 +94,37 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const size_t nb = (size_t)b * n;
 
+  const bool two = r0 + 16 < n;  // the second row tile holds a valid row (else its MFMAs are skipped)
+  // The fp32 product's first round of (I + Abar) operand loads is issued before Z is staged: the two HBM / L2 round
+  // trips overlap instead of following each other (the operand does not depend on Z; diag(inv) is applied later).
+  const int nch16 = nk >> 4;
+  const int ra0 = r0 + lo < n ? r0 + lo : n - 1, ra1 = r0 + 16 + lo < n ? r0 + 16 + lo : n - 1;
+  floatx4 av[4][2];
+  auto load_round = [&](int kr) __attribute__((always_inline)) {
+    const float* Ab = a.abar + nb * n;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int kc = kr + 4 * c;
+      const int k = 16 * kc + 4 * hi;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float* pa = Ab + (size_t)(t ? ra1 : ra0) * n + k;
+        floatx4 v = {0.f, 0.f, 0.f, 0.f};
+        if (kc < nch16) {
+          if (k + 4 <= n) {
+            const floatx4u u = *reinterpret_cast<const floatx4u*>(pa);
+            v = floatx4{u.x, u.y, u.z, u.w};
+          } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) v[s] = k + s < n ? pa[s] : 0.f;
+          }
+        }
+        av[c][t] = v;
+      }
+    }
+  };
+  if constexpr (!BF) load_round(w);
+
   // ---- 1. Zs = Z[b] (zero rows up to nk), every load of a round in flight before the first store; then the
   // RMSNorm factor of each row from LDS (diag(inv) is applied to the (I + Abar) operand of the product).
   {
@@ -132,8 +163,6 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
   }
   __syncthreads();
 
-  const bool two = r0 + 16 < n;  // the second row tile holds a valid row (else its MFMAs are skipped)
-
   // ---- 2. P = (I + Abar)[R, :] Zs: wave w takes the 16-deep K chunks w, w + 4, ... for every column tile, so each
   // (I + Abar) element is loaded once per workgroup; the four K partials meet in LDS (aliasing Zs) in a fixed order.
   if constexpr (BF) {
@@ -141,7 +170,6 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
     // plane and B[32 kc + 8 hi + j][col lo], j < 8 (the MFMA 16x16x32 operand layout)
     const uint16_t* Ab = a.abar16 + nb * n;
     const int nch = nk >> 5;
-    const int ra0 = r0 + lo < n ? r0 + lo : n - 1, ra1 = r0 + 16 + lo < n ? r0 + 16 + lo : n - 1;
     floatx4 acc[2][CTP];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -195,36 +223,14 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) Ps[(w * kRows + 16 * t + 4 * hi + r) * ZS + 16 * ct + lo] = acc[t][ct][r];
   } else {
-    const float* Ab = a.abar + nb * n;
-    const int nch = nk >> 4;
-    const int ra0 = r0 + lo < n ? r0 + lo : n - 1, ra1 = r0 + 16 + lo < n ? r0 + 16 + lo : n - 1;
+    const int nch = nch16;
     floatx4 acc[2][CTP];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int ct = 0; ct < CTP; ++ct) acc[t][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     for (int kr = w; kr < nch; kr += 16) {  // rounds of up to 4 chunks: kr, kr + 4, kr + 8, kr + 12
-      floatx4 av[4][2];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int kc = kr + 4 * c;
-        const int k = 16 * kc + 4 * hi;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const float* pa = Ab + (size_t)(t ? ra1 : ra0) * n + k;
-          floatx4 v = {0.f, 0.f, 0.f, 0.f};
-          if (kc < nch) {
-            if (k + 4 <= n) {
-              const floatx4u u = *reinterpret_cast<const floatx4u*>(pa);
-              v = floatx4{u.x, u.y, u.z, u.w};
-            } else {
-#pragma unroll
-              for (int s = 0; s < 4; ++s) v[s] = k + s < n ? pa[s] : 0.f;
-            }
-          }
-          av[c][t] = v;
-        }
-      }
+      if (kr != w) load_round(kr);  // the first round was issued before the Z staging
 #pragma unroll
       for (int c = 0; c < 4; ++c) {  // (I + Abar) diag(inv): column k of the operand scaled by inv[k]
         const int kc = kr + 4 * c;

@@ -14,7 +14,6 @@
 namespace gncde {
 namespace {
 
-constexpr int kPoll = 16;
 // one workgroup per sample: wide, so its element loops (E = n*h floats, 7 stage buffers) issue many loads at once
 constexpr int kAdvThreads = 1024;
 // The per-stage element loops run in passes of kAdvU elements per thread (E <= 8192 in one pass); a pass issues
@@ -336,8 +335,11 @@ size_t generic_pid_workspace(const GncdeProblem& p) {
   return sz;
 }
 
-int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
-                          char* ws, hipStream_t st) {
+// The PID solve as resumable pieces: pid_begin sets up and launches the init, pid_iterate enqueues one batched
+// evaluation + one controller stage, pid_poll_enqueue copies how many samples are still running to the host,
+// pid_end writes the stats.
+int pid_begin(PidRun& r, const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, char* ws,
+              hipStream_t st) {
   if (s.method != GNCDE_TSIT5) return GNCDE_ERR_UNSUPPORTED;
   const int B = p.B;
   const size_t E = (size_t)p.n * state_dim(p);
@@ -348,7 +350,9 @@ int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const flo
     cur += align_up(bytes, 256);
     return ptr;
   };
-  PidArgs a{};
+  PidArgs& a = *reinterpret_cast<PidArgs*>(r.args);
+  static_assert(sizeof(PidArgs) <= sizeof(r.args), "PidRun::args too small");
+  a = PidArgs{};
   a.B = B;
   a.E = (int)E;
   a.S = s.save_mode == GNCDE_SAVE_TS ? s.n_save : 0;
@@ -362,35 +366,62 @@ int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const flo
   a.save_ts = s.save_ts;
   a.y = reinterpret_cast<float*>(take(B * E * 4));
   a.yt = reinterpret_cast<float*>(take(B * E * 4));
-  float* K = reinterpret_cast<float*>(take(B * E * 4));
-  a.K = K;
+  r.K = reinterpret_cast<float*>(take(B * E * 4));
+  a.K = r.K;
   a.kk = reinterpret_cast<float*>(take(7 * B * E * 4));
   a.state = reinterpret_cast<PidState*>(take(B * sizeof(PidState)));
-  float* tst = reinterpret_cast<float*>(take(B * 4));
-  int* active = reinterpret_cast<int*>(take(B * 4));
+  r.tst = reinterpret_cast<float*>(take(B * 4));
+  r.active = reinterpret_cast<int*>(take(B * 4));
   a.ys = ys;
-  a.tst = tst;
+  a.tst = r.tst;
   a.step_ts = s.step_ts;
   a.step_len = s.step_ts_len;
+  r.p = p;
+  r.ws = ws;
+  r.st = st;
+  r.h_active = 1;
   hipLaunchKernelGGL(k_pid_init, dim3(B), dim3(256), 0, st, a, y0);
   generic_vf_prepare(p, ws, st);
+  return GNCDE_OK;
+}
+
+int pid_iterate(PidRun& r) {
+  const PidArgs& a = *reinterpret_cast<const PidArgs*>(r.args);
+  const int rc = generic_vf_eval(r.p, r.tst, a.yt, r.K, r.ws, r.st, true);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_pid_advance, dim3(a.B), dim3(kAdvThreads), 0, r.st, a);
+  return GNCDE_OK;
+}
+
+void pid_poll_enqueue(PidRun& r) {
+  const PidArgs& a = *reinterpret_cast<const PidArgs*>(r.args);
+  (void)hipMemsetAsync(r.active, 0, sizeof(int), r.st);
+  hipLaunchKernelGGL(k_pid_tst, dim3((a.B + 255) / 256), dim3(256), 0, r.st, a.B, a.state, r.tst, r.active);
+  (void)hipMemcpyAsync(&r.h_active, r.active, sizeof(int), hipMemcpyDeviceToHost, r.st);
+}
+
+void pid_end(PidRun& r, int32_t* stats) {
+  const PidArgs& a = *reinterpret_cast<const PidArgs*>(r.args);
+  if (stats) hipLaunchKernelGGL(k_pid_stats, dim3((a.B + 255) / 256), dim3(256), 0, r.st, a.B, a.state, stats);
+}
+
+int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
+                          char* ws, hipStream_t st) {
+  PidRun r;
+  int rc = pid_begin(r, p, s, y0, ys, ws, st);
+  if (rc) return rc;
   // each sample needs at most 2 + 6 * max_steps + 1 evaluations
-  const long max_iter = 3L + 6L * (long)s.max_steps;
-  int rc = GNCDE_OK;
+  const long max_iter = pid_max_iterations(s);
   for (long it = 0; it < max_iter; ++it) {
-    rc = generic_vf_eval(p, tst, a.yt, K, ws, st, true);
+    rc = pid_iterate(r);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_pid_advance, dim3(B), dim3(kAdvThreads), 0, st, a);
-    if ((it + 1) % kPoll == 0) {
-      int h_active = 0;
-      (void)hipMemsetAsync(active, 0, sizeof(int), st);
-      hipLaunchKernelGGL(k_pid_tst, dim3((B + 255) / 256), dim3(256), 0, st, B, a.state, tst, active);
-      (void)hipMemcpyAsync(&h_active, active, sizeof(int), hipMemcpyDeviceToHost, st);
+    if ((it + 1) % kPidPoll == 0) {
+      pid_poll_enqueue(r);
       if (hipStreamSynchronize(st) != hipSuccess) return GNCDE_ERR_HIP;
-      if (h_active == 0) break;
+      if (r.h_active == 0) break;
     }
   }
-  if (stats) hipLaunchKernelGGL(k_pid_stats, dim3((B + 255) / 256), dim3(256), 0, st, B, a.state, stats);
+  pid_end(r, stats);
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }
 

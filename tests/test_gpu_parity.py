@@ -477,3 +477,4 @@ def test_generic_cde_fixed_grid_solve_vs_oracle(gncde, method):
         err = rel_err(ys[b, :len(grids[b])], ref)
         print(f"cde {method} sample {b}: {len(grids[b]) - 1} steps, rel err {err:.3e}")
         assert err <= RTOL_SOLVE
+
