@@ -4,9 +4,12 @@ graphs whose edges change at random events, sampled at equal or irregular times 
 graph-path preparation of ``src/configs/dataset_configs.py:107-199`` (padding by events, graph operator,
 backward-Hermite coefficients).
 
-The trajectories are integrated on the GPU with torch (batched RK4 with at most ``max_dt`` sub-steps
-between samples; the reference integrates with diffrax ``cfg.method`` — this is data generation, not the
-hot path).  The graph operators and spline coefficients go through the engine's kernels
+The ground truth restates the reference's solve (ode_dataset.py:251-300, gen_all_data :388-470):
+``diffrax.diffeqsolve(ODETerm, cfg.method (Tsit5 | Dopri5), dt0=cfg.dt0, SaveAt(ts=t))`` with diffrax's default
+ConstantStepSize controller, per sample, one solve per event segment of the time axis, each segment starting from
+the previous segment's LAST saved state (gen_all_data's hand-over: the state jumps unchanged across the gap between
+the last time of one segment and the first of the next).  It runs batched in float64 torch on the device (data
+generation, not the hot path).  The graph operators and spline coefficients go through the engine's kernels
 (``gncde_graph_operator``, ``gncde_hermite_coefficients``) straight into the engine layout.  networkx is not
 installed: the community graph is a 4-block stochastic block model with the reference's block sizes
 (n/3, n/3, n/4, rest) and probabilities (0.25 inside, 0.01 across), ode_dataset.py:189-202.
@@ -36,13 +39,13 @@ class DynDataCfg:
     final_time: float = 5.0
     time_tick: int = 100
     sampling_type: str = "irregular"
-    method: str = "Tsit5"
+    method: str = "Dopri5"  # dataset_configs.py:70-73 default; the dyn YAMLs set Tsit5
     operator_type: str = "norm_lap"
     seed: int = 1234
     padding_mode: str = "same"
     interpolation: str = "cubic"
     amp_range: tuple = (1.0, 1.0)
-    max_dt: float = 0.01
+    dt0: float = 0.01  # dataset_configs.py:74 (ConstantStepSize step of the ground-truth solve)
 
     @classmethod
     def from_dict(cls, d: dict) -> "DynDataCfg":
@@ -119,6 +122,98 @@ def padding_by_time(num_knots: int, events_indices: np.ndarray) -> np.ndarray:
     mark = np.zeros(num_knots, dtype=np.int64)
     mark[visible] = 1
     return np.cumsum(mark)
+
+
+# ---- diffrax.diffeqsolve(ODETerm, Tsit5 | Dopri5, ConstantStepSize(dt0), SaveAt(ts)) restated (data side) ------------
+_TSIT5_C = (0.0, 0.161, 0.327, 0.9, 0.9800255409045097, 1.0, 1.0)
+_TSIT5_A = ((), (0.161,), (-0.008480655492356989, 0.335480655492357),
+            (2.897153057105493, -6.359448489975075, 4.3622954328695815),
+            (5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525),
+            (5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401, -0.028269050394068383),
+            (0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081, 2.324710524099774))
+_DOPRI5_C = (0.0, 0.2, 0.3, 0.8, 8.0 / 9.0, 1.0, 1.0)
+_DOPRI5_A = ((), (0.2,), (3.0 / 40.0, 9.0 / 40.0), (44.0 / 45.0, -56.0 / 15.0, 32.0 / 9.0),
+             (19372.0 / 6561.0, -25360.0 / 2187.0, 64448.0 / 6561.0, -212.0 / 729.0),
+             (9017.0 / 3168.0, -355.0 / 33.0, 46732.0 / 5247.0, 49.0 / 176.0, -5103.0 / 18656.0),
+             (35.0 / 384.0, 0.0, 500.0 / 1113.0, 125.0 / 192.0, -2187.0 / 6784.0, 11.0 / 84.0))
+# Dopri5 dense output: the midpoint y(t + h/2) from these weights, then the quartic through y0, y1, y_mid, f0, f1
+_DOPRI5_CMID = (6025192743.0 / 30085553152.0 / 2, 0.0, 51252292925.0 / 65400821598.0 / 2,
+                -2691868925.0 / 45128329728.0 / 2, 187940372067.0 / 1594534317056.0 / 2,
+                -1776094331.0 / 19743644256.0 / 2, 11237099.0 / 235043384.0 / 2)
+
+
+def _tsit5_dense(th):
+    t2 = th * th
+    return torch.stack([
+        -1.0530884977290216 * th * (th - 1.3299890189751412) * (t2 - 1.4364028541716351 * th + 0.7139816917074209),
+        0.1017 * t2 * (t2 - 2.1966568338249754 * th + 1.2949852507374631),
+        2.490627285651252793 * t2 * (t2 - 2.38535645472061657 * th + 1.57803468208092486),
+        -16.54810288924490272 * (th - 1.21712927295533244) * (th - 0.61620406037800089) * t2,
+        47.37952196281928122 * (th - 1.203071208372362603) * (th - 0.658047292653547382) * t2,
+        -34.87065786149660974 * (th - 1.2) * (th - 0.666666666666666667) * t2,
+        2.5 * (th - 1.0) * (th - 0.6) * t2], dim=-1)
+
+
+def _dense(method, th, h, y0, y1, K):
+    """y(t + th h) inside one step from its start / end states and its 7 stage values K [7, ...]."""
+    if method == "tsit5":
+        w = _tsit5_dense(th.reshape(-1))  # [m, 7]
+        return y0 + h * torch.einsum("mj,jm...->m...", w, K)
+    ymid = y0 + h * sum(c * K[j] for j, c in enumerate(_DOPRI5_CMID) if c != 0.0)
+    f0, f1 = h * K[0], h * K[6]
+    a = 2.0 * (f1 - f0) - 8.0 * (y1 + y0) + 16.0 * ymid
+    b = 5.0 * f0 - 3.0 * f1 + 18.0 * y0 + 14.0 * y1 - 32.0 * ymid
+    c = f1 - 4.0 * f0 - 11.0 * y0 - 5.0 * y1 + 16.0 * ymid
+    return y0 + th * (f0 + th * (c + th * (b + th * a)))
+
+
+def diffeqsolve_constant(f, ts: np.ndarray, y0: torch.Tensor, method: str = "Tsit5", dt0: float = 0.01):
+    """Per sample b: diffrax.diffeqsolve(ODETerm(f), method, t0=ts[b, 0], t1=ts[b, -1], dt0, y0[b],
+    SaveAt(ts=ts[b])) with the default ConstantStepSize (ode_dataset.py:279-293).  f is autonomous (heat / gene,
+    batched over samples); the step grids follow ConstantStepSize (t + dt0 in fp32, snapped to t1 within 1e-6) and
+    the save times are read off the solver's dense interpolant (Tsit5: its free interpolant; Dopri5: the quartic
+    through y0, y1, f0, f1 and the Dopri5 midpoint).  ts [B, S] (numpy), y0 [B, ...] -> [B, S, ...]."""
+    m = method.lower()
+    if m not in ("tsit5", "dopri5"):
+        raise NotImplementedError(f"ground-truth solver {method}: Tsit5 and Dopri5 are restated")
+    A = _TSIT5_A if m == "tsit5" else _DOPRI5_A
+    B, S = ts.shape
+    dev = y0.device
+    grids = [layout.constant_step_grid(float(ts[b, 0]), float(ts[b, -1]), dt0).astype(np.float64) for b in range(B)]
+    ns = np.array([len(g) - 1 for g in grids])
+    G = int(ns.max()) + 1
+    grid = np.stack([np.concatenate([g, np.full(G - len(g), g[-1])]) for g in grids])
+    # the step of every save time: t_k < ts <= t_{k+1} (k = -1: ts <= t0, the initial state)
+    kk = np.full((B, S), -1, dtype=np.int64)
+    th = np.zeros((B, S))
+    for b in range(B):
+        tsb = np.asarray(ts[b], np.float64)
+        for s_ in range(S):
+            if tsb[s_] <= grid[b, 0] or ns[b] == 0:
+                continue
+            k = min(max(int(np.searchsorted(grid[b, :ns[b] + 1], tsb[s_], side="left")) - 1, 0), ns[b] - 1)
+            kk[b, s_] = k
+            th[b, s_] = (tsb[s_] - grid[b, k]) / (grid[b, k + 1] - grid[b, k])
+    out = torch.empty((B, S) + tuple(y0.shape[1:]), dtype=y0.dtype, device=dev)
+    out[torch.as_tensor(kk < 0, device=dev)] = y0.unsqueeze(1).expand_as(out)[torch.as_tensor(kk < 0, device=dev)]
+    hs = torch.tensor(np.diff(grid, axis=1), dtype=y0.dtype, device=dev)  # [B, G-1]; 0 on padded steps
+    bshape = (B,) + (1,) * (y0.dim() - 1)
+    y, k0 = y0, f(y0)
+    for k in range(G - 1):
+        h = hs[:, k].reshape(bshape)
+        K = [k0]
+        for i in range(1, 7):
+            K.append(f(y + h * sum(a * K[j] for j, a in enumerate(A[i]) if a != 0.0)))
+        y1 = y + h * sum(a * K[j] for j, a in enumerate(A[6]) if a != 0.0)  # stage 7 input = y1 (FSAL)
+        sel = np.nonzero(kk == k)
+        if len(sel[0]):
+            bi = torch.as_tensor(sel[0], device=dev)
+            si = torch.as_tensor(sel[1], device=dev)
+            thv = torch.as_tensor(th[sel], dtype=y0.dtype, device=dev).reshape((-1,) + (1,) * (y0.dim() - 1))
+            Ks = torch.stack([Kj[bi] for Kj in K])
+            out[bi, si] = _dense(m, thv, hs[bi, k].reshape(thv.shape), y[bi], y1[bi], Ks)
+        y, k0 = y1, K[6]
+    return out
 
 
 class DynDataset:
@@ -208,25 +303,24 @@ class DynDataset:
         raise NotImplementedError(f"dataset {self.cfg.name}: heat and gene are generated here")
 
     def _solve(self, device) -> torch.Tensor:
+        """gen_all_data (ode_dataset.py:388-470): static graph -> one solve over every time; dynamic graph -> one
+        solve per event segment t[:, :e_0], t[:, e_0:e_1], ..., t[:, e_last:] on graph A_k, segment k + 1 started
+        from segment k's last saved state."""
         t = torch.tensor(self.t, dtype=torch.float64, device=device)
         A_all = torch.tensor(self.A, dtype=torch.float64, device=device)
-        epoch = padding_by_time(self.t.shape[1], self.events_indices) if self.cfg.dynamic_graph else \
-            np.zeros(self.t.shape[1], dtype=np.int64)
         x = self.x0.to(torch.float64)
-        out = [x[..., 0].clone()]
-        for j in range(1, self.t.shape[1]):
-            f = self._rhs(A_all[:, int(epoch[j - 1])])
-            span = t[:, j] - t[:, j - 1]  # [B]
-            steps = max(1, int(math.ceil(float(span.max()) / self.cfg.max_dt)))
-            h = (span / steps)[:, None, None]
-            for _ in range(steps):
-                k1 = f(x)
-                k2 = f(x + 0.5 * h * k1)
-                k3 = f(x + 0.5 * h * k2)
-                k4 = f(x + h * k3)
-                x = x + h / 6.0 * (k1 + 2 * k2 + 2 * k3 + k4)
-            out.append(x[..., 0].clone())
-        return torch.stack(out, dim=1).to(torch.float32)  # [B, Tt, n]
+        T = self.t.shape[1]
+        if not self.cfg.dynamic_graph:
+            bounds = [0, T]
+        else:
+            bounds = [0] + [int(e) for e in np.sort(self.events_indices)] + [T]
+        outs = []
+        for k in range(len(bounds) - 1):
+            s0, s1 = bounds[k], bounds[k + 1]
+            ys = diffeqsolve_constant(self._rhs(A_all[:, k]), self.t[:, s0:s1], x, self.cfg.method, self.cfg.dt0)
+            outs.append(ys)
+            x = ys[:, -1]
+        return torch.cat(outs, dim=1)[..., 0].to(torch.float32)  # [B, Tt, n]
 
     def graph_path(self, idx):
         """Engine-layout control over the knots ``idx`` (dataset_configs.py:159-199): graph operator of every

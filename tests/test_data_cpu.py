@@ -41,3 +41,45 @@ def test_events_and_padding():
     A = np.zeros((2, 5, 5))
     stack = data.events_happen_graph(rng, A, 3, 0.5)
     assert stack.shape == (2, 4, 5, 5)
+
+
+def test_split_sizes_match_reference_test():
+    """test_ode_dataset.py:54-60 (irregular sampling, time_tick 100, split 0.8 / 0.2)."""
+    rng = np.random.default_rng(1234)
+    tr, extra, inter = data.split_indices(rng, "irregular", 100, (0.8, 0.2))
+    assert len(tr) == int(100 * 0.8)
+    assert len(extra) == 100 - len(tr)
+    assert inter is not None
+
+
+def test_ground_truth_solver_linear_known_answer():
+    """diffeqsolve(ODETerm, Tsit5 | Dopri5, ConstantStepSize(dt0), SaveAt(ts)) restated (ode_dataset.py:279-293):
+    dy/dt = lam y against exp(lam t) at irregular save times that fall between steps (dense output), per-sample
+    time grids of different lengths, and ts[0] returning y0 itself."""
+    import torch
+    lam = torch.tensor([-1.3, 0.4], dtype=torch.float64)
+    f = lambda y: lam[:, None, None] * y  # noqa: E731
+    ts = np.array([[0.0, 0.013, 0.4, 0.777, 1.0], [0.0, 0.25, 0.5, 1.31, 2.0]])
+    y0 = torch.tensor([[[1.0]], [[2.0]]], dtype=torch.float64)
+    for method in ("Tsit5", "Dopri5"):
+        ys = data.diffeqsolve_constant(f, ts, y0, method, dt0=0.05)
+        ref = y0[:, None] * torch.exp(lam[:, None, None, None] * torch.tensor(ts)[:, :, None, None])
+        err = float((ys - ref).abs().max() / ref.abs().max())
+        assert ys.shape == (2, 5, 1, 1) and torch.equal(ys[:, 0], y0)
+        assert err < 1e-7, (method, err)
+
+
+def test_dynamic_ground_truth_hands_over_between_event_segments():
+    """gen_all_data (ode_dataset.py:420-465): each event segment is its own solve started from the previous
+    segment's last saved state, so the state at a segment's first time equals the state at the previous segment's
+    last time (no evolution across that gap) -- the reference's hand-over, restated."""
+    cfg = data.DynDataCfg(name="heat", batch_size=2, num_nodes=9, time_tick=20, dynamic_graph=True,
+                          all_dynamic=True, sampling_type="irregular", method="Tsit5", seed=3)
+    ds = data.DynDataset(cfg, device="cpu")
+    y = ds.true_y.numpy()
+    ev = np.sort(ds.events_indices)
+    assert len(ev) > 0
+    for e in ev:
+        assert np.array_equal(y[:, e], y[:, e - 1])
+    inside = [j for j in range(1, y.shape[1]) if j not in set(ev)]
+    assert any(not np.array_equal(y[:, j], y[:, j - 1]) for j in inside)
