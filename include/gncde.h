@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GNCDE_ABI_VERSION 3
+#define GNCDE_ABI_VERSION 4
 #define GNCDE_MAX_LAYERS 8
 #define GNCDE_FC 24
 
@@ -141,6 +141,13 @@ typedef struct GncdeSolver {
    * steps than step_ts_len - 1 gets status 3. */
   float* step_ts;                    /* [B, step_ts_len] */
   int32_t step_ts_len;
+  /* GRID only, optional (NULL = not recorded / not used): the stage record, [B, G-1, S-1, n, d_s] with S = 4 (RK4)
+   * or 6 (Tsit5): every step's stage inputs U_1 .. U_{S-1} (U_0 is the step's starting state, already in ys).
+   * gncde_integrate WRITES it; gncde_integrate_vjp* READ it (the same forward's record), so the reverse sweep
+   * evaluates no stage twice: with 288 GB of HBM per GPU the forward stores what the reverse would recompute.
+   * Only for problems where gncde_stage_record_floats() is non-zero (fused forward and fused reverse sweep);
+   * gncde_integrate returns GNCDE_ERR_UNSUPPORTED for a record on a problem its fused path does not take. */
+  float* stage_rec;
 } GncdeSolver;
 
 /* Library / error helpers */
@@ -149,6 +156,11 @@ const char* gncde_strerror(int code);
 /* Name of the kernel path gncde_integrate would take for this problem ("fused<64,16,3,rk4>" or
  * "generic"), written into buf (NUL-terminated).  Returns GNCDE_OK or an error code. */
 int gncde_integrate_path(const GncdeProblem* prob, const GncdeSolver* solver, char* buf, size_t buf_len);
+
+/* Floats per sample of the stage record (GncdeSolver.stage_rec) that gncde_integrate_vjp would read for this
+ * problem and solver: (G-1)*(S-1)*n*d_s when the fused reverse sweep takes it, 0 when the reverse sweep ignores
+ * it (PID controller, the generic reverse sweep, the _data variant).  Never fails; 0 for invalid arguments. */
+size_t gncde_stage_record_floats(const GncdeProblem* prob, const GncdeSolver* solver);
 
 /* Workspace bytes needed by gncde_vf_eval (solver == NULL) or gncde_integrate. */
 size_t gncde_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* solver);

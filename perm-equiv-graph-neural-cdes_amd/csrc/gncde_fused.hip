@@ -76,6 +76,7 @@ struct FusedArgs {
   float rtol, atol;
   float* step_ts;  // [B, step_len] accepted step times (GncdeSolver.step_ts) or nullptr
   int step_len;
+  float* rec;      // GRID: stage record [B, G-1, S-1, n, H] (GncdeSolver.stage_rec) or nullptr
 };
 
 constexpr int kTsit5Pid = 2;  // internal METHOD id: Tsit5 + PIDController (diffrax defaults)
@@ -456,13 +457,14 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
 #pragma unroll
     for (int r = 0; r < 4; ++r) y[fb][r] = node_ok ? y0b[(size_t)node * H + 16 * fb + 4 * hi + r] : 0.f;
 
-  auto store = [&](float* dst) __attribute__((always_inline)) {
+  auto store_from = [&](float* dst, const float (&v)[FB][4]) __attribute__((always_inline)) {
     if (!node_ok) return;
 #pragma unroll
     for (int fb = 0; fb < FB; ++fb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dst[(size_t)node * H + 16 * fb + 4 * hi + r] = y[fb][r];
+      for (int r = 0; r < 4; ++r) dst[(size_t)node * H + 16 * fb + 4 * hi + r] = v[fb][r];
   };
+  auto store = [&](float* dst) __attribute__((always_inline)) { store_from(dst, y); };
 
   const size_t E = (size_t)n * H;
 
@@ -498,6 +500,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
             acc[fb][r] = st == 0 ? K[fb][r] : fmaf(wk, K[fb][r], acc[fb][r]);
             yt[fb][r] = fmaf(hn, K[fb][r], y[fb][r]);
           }
+        if (a.rec && st < 3) store_from(a.rec + (((size_t)b * (G - 1) + k) * 3 + st) * E, yt);  // U_{st+1}
       }
       const float h6 = h / 6.0f;
 #pragma unroll
@@ -564,6 +567,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
           for (int j = 0; j < 6; ++j) sacc = fmaf(arow[j], kk[j][fb][r], sacc);
           yt[fb][r] = fmaf(h, sacc, y[fb][r]);
         }
+      if (a.rec && ns1 <= 5) store_from(a.rec + (((size_t)b * (G - 1) + k) * 5 + ns1 - 1) * E, yt);  // U_ns1
       tst = ns1 >= 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);
       st = ns1;
     }
@@ -862,6 +866,7 @@ int fused_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0
   a.atol = s.atol;
   a.step_ts = s.controller == GNCDE_CTRL_PID ? s.step_ts : nullptr;
   a.step_len = s.step_ts_len;
+  a.rec = s.controller == GNCDE_CTRL_GRID && s.grid_len >= 2 ? s.stage_rec : nullptr;
   hipLaunchKernelGGL(e->fn, dim3(p.B), dim3(e->np * 4), 0, st, a);
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }

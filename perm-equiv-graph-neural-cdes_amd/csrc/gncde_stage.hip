@@ -136,6 +136,7 @@ struct RevArgs {
   const float* ys;      // checkpoints [B, G, n, H]
   const float* gys;     // saved-state cotangents [B, G, n, H] (SAVE_STEPS) or nullptr
   const float* gst;     // extra stage-value cotangents [B, G-1, S, n, H] (gncde_integrate_vjp_ex) or nullptr
+  const float* rec;     // the forward's stage record [B, G-1, S-1, n, H] (GncdeSolver.stage_rec) or nullptr
   float* K[6];          // stage values      [B, n, H] each
   float* U[6];          // stage inputs
   float* gK[6];         // stage cotangents
@@ -321,6 +322,10 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
 
   // ---- forward at the formed time, activations kept for the backward ----------------------------------
   float Zin[L][4], invl[L], ml[L][4], prel[L][4];
+  // K range of lane group hi: [hi*KS, hi*KS + KS), walked from offset kRot: at NP = 128 the groups hi = 0 / 1 (and
+  // 2 / 3) of one 32-lane half would otherwise hit the same banks (hi*KS = 32 = 0 mod 32) — 2-way conflicts on
+  // every operand-build read; rotating the odd groups by 16 puts them on the other 16 banks.
+  const int kRot = KS == 32 ? 16 * (hi & 1) : 0;
   const int oAr = swz<NP>(node, hi * KS), oAc = swz<NP>(hi * KS, node);
   auto forward = [&](float (&Z)[4]) __attribute__((always_inline)) {
 #pragma unroll
@@ -351,16 +356,18 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         const float wi = sW[l * NP + node];
         const float* vv = sV + l * NP + hi * KS;
 #pragma unroll
-        for (int sl = 0; sl < KS; ++sl)
-          Ab[sl] = fmaf(e0, sA[oAr + sl], fmaf(e1, sdA[oAr + sl], fmaf(e2, sA[oAc + sl * (NP + 1)],
-                        fmaf(e3, sdA[oAc + sl * (NP + 1)], wi + vv[sl]))));
+        for (int sl = 0; sl < KS; ++sl) {
+          const int kr = (sl + kRot) & (KS - 1);
+          Ab[sl] = fmaf(e0, sA[oAr + kr], fmaf(e1, sdA[oAr + kr], fmaf(e2, sA[oAc + kr * (NP + 1)],
+                        fmaf(e3, sdA[oAc + kr * (NP + 1)], wi + vv[kr]))));
+        }
       }
       __syncthreads();
       floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
       const float* mrow = sMb + lo * MS + hi * KS;
 #pragma unroll
       for (int q = 0; q < KS / 4; ++q) {
-        const float4 mv = *reinterpret_cast<const float4*>(mrow + 4 * q);
+        const float4 mv = *reinterpret_cast<const float4*>(mrow + ((4 * q + kRot) & (KS - 1)));
         c0 = mfma4(mv.x, Ab[4 * q + 0], c0);
         c1 = mfma4(mv.y, Ab[4 * q + 1], c1);
         c0 = mfma4(mv.z, Ab[4 * q + 2], c0);
@@ -550,6 +557,16 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = node_ok ? p[off + r] : 0.f;
   };
+  // stage input U_i (i >= 1) of step k: from the forward's record when there is one (steps past nsteps have h = 0,
+  // so their stage inputs are the checkpoint y_k, which the forward never recorded), else as recomputed above
+  auto loadU = [&](int kk, int i, float (&v)[4]) {
+    if (!a.rec)
+      load4(a.U[i], rowoff, v);
+    else if (kk < ns)
+      load4(a.rec, (((size_t)b * (G - 1) + kk) * (a.S - 1) + i - 1) * E + (size_t)(node_ok ? node : 0) * H + 4 * hi, v);
+    else
+      load4(a.ys, rowk(kk), v);
+  };
   auto store4 = [&](float* p, size_t off, const float (&v)[4]) {
     if (node_ok)
 #pragma unroll
@@ -625,7 +642,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
     if constexpr (PROG == kVjpMid) {
       const int i = a.stage;
       float U[4], gK[4], gU[4], acc[4];
-      load4(a.U[i], rowoff, U);
+      loadU(k, i, U);
       load4(a.gK[i], rowoff, gK);
       form(stage_time(tk, a.c[i], hk));
       forward(U);
@@ -673,7 +690,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         const int il = S - 1;
         const float tl = stage_time(tk, a.c[il], hk);
         float U[4], gK[4], gU[4], sd[4] = {0.f, 0.f, 0.f, 0.f};
-        load4(a.U[il], rowoff, U);
+        loadU(k, il, U);
         if (a.gst) load4(a.gst, rowst(k, il), sd);
 #pragma unroll
         for (int r = 0; r < 4; ++r) gK[r] = hk * a.bw[il] * lam[r] + sd[r];
@@ -698,7 +715,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
     // reduction for both)
     if constexpr (PROG == kVjpPair || BOUND_PAIR) {
       float U[4], gK[4], gU[4], gy[4], g1[4];
-      load4(a.U[2], rowoff, U);
+      loadU(k, 2, U);
       load4(a.gK[2], rowoff, gK);
       form(stage_time(tk, 0.5f, hk));
       forward(U);
@@ -711,7 +728,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         gy[r] += gU[r];
         g1[r] = fmaf(hh, gU[r], g1[r]);  // a[2][1] = 1/2
       }
-      load4(a.U[1], rowoff, U);
+      loadU(k, 1, U);
       forward(U);
       backward(g1, gU);
       load4(a.gK[0], rowoff, g1);
@@ -840,9 +857,11 @@ size_t stage_vjp_workspace(const GncdeProblem& p) {
   return carve_stage(p, nullptr, w);
 }
 
-// Reverse sweep, per step k = G-2 .. 0 (RK4: 4 launches, Tsit5: 10):
-//   recompute  RK4: kEval1 (stage 0, t_k), kEval2 (stages 1-2 at t_k + h/2, and U_3)
+// Reverse sweep, per step k = G-2 .. 0 (RK4: one kStepRk4 launch; Tsit5: 10 launches):
+//   recompute  RK4: stage 0 at t_k, stages 1-2 at t_k + h/2, and U_3 (inside kStepRk4)
 //              Tsit5: kEval1 for stages 0..4 (the last writes U_5)
+//              -- skipped when the forward left a stage record (RK4: kBoundaryPair; Tsit5: no kEval1): the
+//                 sweep then forms A(t) twice per RK4 step instead of four times and runs no forward-only stage
 //   kBoundary  at t_{k+1}: stage 0 of step k+1 closes lambda_{k+1}; seeds + last stage of step k
 //   middle     RK4: kVjpPair (stages 2, 1);  Tsit5: kVjpMid for stages 4..1
 // and a final kBoundary (stage 0 of step 0 -> gy0).
@@ -874,6 +893,7 @@ int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float
   a.ys = ys;
   a.gys = steps ? gys : nullptr;
   a.gst = gstage;
+  a.rec = G >= 2 ? s.stage_rec : nullptr;
   for (int i = 0; i < 6; ++i) {
     a.K[i] = w.K[i];
     a.U[i] = w.U[i];
@@ -913,13 +933,13 @@ int stage_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const float
     a.k = k;
     a.has_next = (k + 1 <= G - 2) ? 1 : 0;
     a.has_cur = 1;
-    if (rk4) {  // one launch per step: stage 0 at t, stages 1, 2 at t + h/2, boundary at t_{k+1}, stages 2, 1
+    if (rk4) {  // one launch per step: [stage 0 at t, stages 1, 2 at t + h/2,] boundary at t_{k+1}, stages 2, 1
       a.stage = 0;
       a.write_next = 0;
-      hipLaunchKernelGGL(e->fn[kStepRk4], grid, wg, 0, st, a);
+      hipLaunchKernelGGL(e->fn[a.rec ? kBoundaryPair : kStepRk4], grid, wg, 0, st, a);
       continue;
     }
-    for (int i = 0; i + 1 < a.S; ++i) {
+    for (int i = 0; i + 1 < a.S && !a.rec; ++i) {  // recompute (no stage record)
       a.stage = i;
       a.write_next = (i + 2 == a.S) ? 1 : 0;
       hipLaunchKernelGGL(e->fn[kEval1], grid, wg, 0, st, a);

@@ -12,7 +12,7 @@ from ctypes import POINTER, c_char_p, c_float, c_int32, c_size_t, c_void_p
 
 MAX_LAYERS = 8
 FC = 24
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 RK4, TSIT5 = 0, 1
 CTRL_GRID, CTRL_PID = 0, 1
@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "gncde_abi_version",
     "gncde_strerror",
     "gncde_integrate_path",
+    "gncde_stage_record_floats",
     "gncde_workspace_bytes",
     "gncde_vf_eval",
     "gncde_integrate",
@@ -85,6 +86,7 @@ class GncdeSolver(ctypes.Structure):
         ("save_ts", c_void_p),
         ("step_ts", c_void_p),
         ("step_ts_len", c_int32),
+        ("stage_rec", c_void_p),
     ]
 
 
@@ -111,6 +113,8 @@ def load(path: str | None = None):
     lib.gncde_strerror.argtypes = [c_int32]
     lib.gncde_integrate_path.restype = c_int32
     lib.gncde_integrate_path.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver), c_char_p, c_size_t]
+    lib.gncde_stage_record_floats.restype = c_size_t
+    lib.gncde_stage_record_floats.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver)]
     lib.gncde_workspace_bytes.restype = c_size_t
     lib.gncde_workspace_bytes.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver)]
     lib.gncde_vf_eval.restype = c_int32

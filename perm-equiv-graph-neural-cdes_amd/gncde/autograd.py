@@ -22,6 +22,25 @@ import torch
 from . import _lib, engine
 
 
+# Share of the free device memory a stage record may take (GncdeSolver.stage_rec: the forward stores every step's
+# stage inputs so the reverse sweep recomputes none; config 4 needs 2.5 GB of the 288 GB).
+STAGE_RECORD_SHARE = 0.25
+
+
+def with_stage_record(prob: engine.Problem, spec: engine.SolverSpec, want: bool = True) -> engine.SolverSpec:
+    """``spec`` with a freshly allocated stage record when the reverse sweep would read one and it fits."""
+    if not want:
+        return spec
+    floats = engine.stage_record_floats(prob, spec)
+    if floats == 0 or prob.B == 0:
+        return spec
+    free, _ = torch.cuda.mem_get_info()
+    if prob.B * floats * 4 > STAGE_RECORD_SHARE * free:
+        return spec
+    return dataclasses.replace(spec, stage_rec=torch.empty(prob.B, floats, dtype=torch.float32,
+                                                           device=prob.params.device))
+
+
 class _FixedGridSolve(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y0, params, fusion, data_coef, prob, spec):
@@ -29,9 +48,10 @@ class _FixedGridSolve(torch.autograd.Function):
                                 fusion=fusion.detach().to(torch.float32).contiguous())
         if data_coef is not None:
             p = dataclasses.replace(p, data_coef=data_coef.detach().to(torch.float32).contiguous())
-        steps = dataclasses.replace(spec, save_mode=_lib.SAVE_STEPS)
+        steps = with_stage_record(p, dataclasses.replace(spec, save_mode=_lib.SAVE_STEPS, stage_rec=None),
+                                  want=data_coef is None)
         ys = engine.integrate(p, steps, y0.detach())
-        ctx.prob, ctx.spec = p, spec
+        ctx.prob, ctx.spec = p, dataclasses.replace(spec, stage_rec=steps.stage_rec)
         ctx.dtypes = (y0.dtype, params.dtype, fusion.dtype)
         ctx.save_for_backward(ys)
         if spec.save_mode == _lib.SAVE_STEPS:
@@ -132,8 +152,9 @@ class _PidSolve(torch.autograd.Function):
         grid, nst = pid_replay_grid(rec, ns, pad=1 if dense else 0)
         steps = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_STEPS, grid=grid,
                                   nsteps=nst)
-        ys = engine.integrate(ctx.prob, steps, y0)  # the checkpoints: the accepted steps replayed
         want_data = ctx.needs_input_grad[3]
+        steps = with_stage_record(ctx.prob, steps, want=not want_data)
+        ys = engine.integrate(ctx.prob, steps, y0)  # the checkpoints (and stage inputs): the accepted steps replayed
         if dense:
             gys, gst = dense_output_cotangents(grid, nst, spec.save_ts, g)
             res = engine.integrate_vjp(ctx.prob, steps, ys, gys, data_grad=want_data, gstage=gst)

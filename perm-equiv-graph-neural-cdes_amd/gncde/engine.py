@@ -8,6 +8,7 @@ torch's current stream.  Errors from the library raise ``GncdeError``.
 from __future__ import annotations
 
 import ctypes
+import dataclasses
 from dataclasses import dataclass, field
 
 import torch
@@ -170,6 +171,8 @@ class SolverSpec:
     dt0: torch.Tensor | None = None
     save_ts: torch.Tensor | None = None
     step_ts: torch.Tensor | None = None  # PID: OUTPUT [B, cap] accepted step times (t0 first), filled by integrate
+    # GRID: stage record [B, stage_record_floats(prob, solver)] written by integrate, read by integrate_vjp
+    stage_rec: torch.Tensor | None = None
 
     def c_struct(self) -> _lib.GncdeSolver:
         s = _lib.GncdeSolver()
@@ -189,13 +192,25 @@ class SolverSpec:
                 raise _lib.GncdeError("SolverSpec.step_ts must be a contiguous fp32 CUDA tensor [B, cap]")
             s.step_ts = _ptr(self.step_ts).value
             s.step_ts_len = int(self.step_ts.shape[1])
+        if self.stage_rec is not None:
+            if not (self.stage_rec.is_cuda and self.stage_rec.dtype == torch.float32
+                    and self.stage_rec.is_contiguous() and self.stage_rec.dim() == 2):
+                raise _lib.GncdeError("SolverSpec.stage_rec must be a contiguous fp32 CUDA tensor [B, floats]")
+            s.stage_rec = _ptr(self.stage_rec).value
         return s
 
     def shard(self, start, stop):
         cut = lambda x: None if x is None else x[start:stop]  # noqa: E731
         return SolverSpec(self.method, self.controller, self.save_mode, cut(self.grid), cut(self.nsteps),
                           self.rtol, self.atol, self.max_steps, cut(self.t0), cut(self.t1), cut(self.dt0),
-                          cut(self.save_ts), cut(self.step_ts))
+                          cut(self.save_ts), cut(self.step_ts), cut(self.stage_rec))
+
+
+def stage_record_floats(prob: Problem, solver: SolverSpec) -> int:
+    """Floats per sample of the stage record the reverse sweep would read (0: it would ignore one)."""
+    lib = _lib.load()
+    ss = dataclasses.replace(solver, stage_rec=None).c_struct()
+    return int(lib.gncde_stage_record_floats(ctypes.byref(prob.c_struct()), ctypes.byref(ss)))
 
 
 def integrate_path(prob: Problem, solver: SolverSpec) -> str:

@@ -44,9 +44,9 @@ def test_struct_layout_matches_c(tmp_path):
 #include <stddef.h>
 #include "{HEADER}"
 int main(void) {{
-  printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(GncdeProblem), offsetof(GncdeProblem, ts),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(GncdeProblem), offsetof(GncdeProblem, ts),
          offsetof(GncdeProblem, params), sizeof(GncdeSolver), offsetof(GncdeSolver, save_ts),
-         offsetof(GncdeSolver, step_ts), offsetof(GncdeSolver, step_ts_len));
+         offsetof(GncdeSolver, step_ts), offsetof(GncdeSolver, step_ts_len), offsetof(GncdeSolver, stage_rec));
   return 0;
 }}''')
     exe = tmp_path / "layout"
@@ -54,7 +54,7 @@ int main(void) {{
     vals = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
     P, S = _lib.GncdeProblem, _lib.GncdeSolver
     assert vals == [ctypes.sizeof(P), P.ts.offset, P.params.offset, ctypes.sizeof(S), S.save_ts.offset,
-                    S.step_ts.offset, S.step_ts_len.offset]
+                    S.step_ts.offset, S.step_ts_len.offset, S.stage_rec.offset]
 
 
 def _fake_problem(B=4, n=64, T=10, dims=(16, 16, 16, 16)):
@@ -101,3 +101,20 @@ def test_argument_validation_error_codes(mutate, code):
     mutate(p, s)
     buf = ctypes.create_string_buffer(64)
     assert lib.gncde_integrate_path(ctypes.byref(p), ctypes.byref(s), buf, 64) == code
+
+
+def test_stage_record_floats():
+    """gncde_stage_record_floats: (G-1)(S-1) n d_s where the fused reverse sweep reads a record, else 0."""
+    lib = _lib.load()
+    p = _fake_problem()
+    f = lambda p, s: lib.gncde_stage_record_floats(ctypes.byref(p), ctypes.byref(s))  # noqa: E731
+    assert f(p, _fake_solver(_lib.RK4)) == 100 * 3 * 64 * 16
+    assert f(p, _fake_solver(_lib.TSIT5)) == 100 * 5 * 64 * 16
+    s = _fake_solver(_lib.TSIT5)
+    s.controller, s.t0, s.t1, s.max_steps = _lib.CTRL_PID, 0x1000, 0x1000, 16
+    assert f(p, s) == 0                                            # PID: replayed as a grid by the reverse mode
+    assert f(_fake_problem(dims=(32, 32, 32)), _fake_solver()) == 0  # generic reverse sweep: no record
+    assert f(_fake_problem(n=200), _fake_solver()) == 0
+    bad = _fake_problem()
+    bad.T = 1
+    assert f(bad, _fake_solver()) == 0

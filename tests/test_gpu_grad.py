@@ -9,6 +9,7 @@ evaluation itself ill-conditioned (the same effect as tsit5c_plain in tests/test
 fixtures hold only gradient-stable samples (no ReLU pre-activation within fp32 reach of its kink, see
 make_golden.grad_case).
 """
+import dataclasses
 import os
 
 import numpy as np
@@ -249,10 +250,12 @@ def test_make_step_trains(G):
         assert p.untyped_storage().data_ptr() == opt.flat.untyped_storage().data_ptr()
 
 
+@pytest.mark.parametrize("rec", [False, True])
 @pytest.mark.parametrize("n,L,method", [(40, 2, "rk4"), (128, 2, "rk4"), (64, 3, "tsit5")])
-def test_stage_vjp_large_graphs_match_oracle(G, n, L, method):
+def test_stage_vjp_large_graphs_match_oracle(G, n, L, method, rec):
     """The fused per-stage reverse sweep (gncde_stage.hip) at padded and full workgroup sizes (NP 64 / 128)
-    against the fp64 reverse-mode oracle; the sample is re-drawn until its gradient is stable under a 1e-6
+    against the fp64 reverse-mode oracle, recomputing the stage inputs (rec False) or reading the forward's stage
+    record (rec True, GncdeSolver.stage_rec); the sample is re-drawn until its gradient is stable under a 1e-6
     perturbation (ReLU kinks, see make_golden.grad_case)."""
     rng = np.random.default_rng(100 + n)
     B, T, h = 2, 5, 16
@@ -285,7 +288,13 @@ def test_stage_vjp_large_graphs_match_oracle(G, n, L, method):
     grid, ns = G.layout.stack_grids(grids)
     spec = G.SolverSpec(method=G._lib.RK4 if method == "rk4" else G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS,
                         grid=grid, nsteps=ns)
+    if rec:
+        floats = G.engine.stage_record_floats(prob, spec)
+        assert floats == (grid.shape[1] - 1) * (3 if method == "rk4" else 5) * n * h
+        spec.stage_rec = torch.full((B, floats), float("nan"), device="cuda")
     ys = G.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda"))
+    if rec:
+        assert torch.isfinite(spec.stage_rec).all()  # every real step's stage inputs were written
     spec.save_mode = G._lib.SAVE_T1
     gy0, gp, gf = G.integrate_vjp(prob, spec, ys, torch.tensor(gfin, dtype=torch.float32, device="cuda"))
     assert rel_err(gy0.cpu().numpy(), np.stack(gy0_ref)) <= RTOL_GRAD
@@ -301,6 +310,43 @@ def test_stage_vjp_large_graphs_match_oracle(G, n, L, method):
     gparams_ref = np.stack([np.concatenate([total[l][nm] for nm in names]) for l in range(L)])
     mine = gf.double().cpu().numpy() @ M.numpy().T
     assert rel_err(mine, gparams_ref) <= RTOL_GRAD
+
+
+@pytest.mark.parametrize("method", ["rk4", "tsit5"])
+def test_stage_record_matches_recompute(G, method):
+    """The reverse sweep reading the forward's stage record equals the one recomputing the stage inputs (to fp32
+    rounding: the record holds the forward kernel's values), with ragged step counts (padded steps read the
+    checkpoint, never the unwritten record slots); a record on a problem the fused forward does not take is
+    refused (GNCDE_ERR_UNSUPPORTED), not left unwritten."""
+    rng = np.random.default_rng(7)
+    B, n, T, h, L = 3, 100, 5, 16, 2
+    ts, coeffs = _graph_controls(rng, B, n, T, irregular=False)
+    P = O.init_vf_params(rng, "undirected", [h] * (L + 1))
+    prob = G.make_problem(ts, coeffs, "undirected", P.layers)
+    grids = [O.rk4_grid(ts[b, 0], ts[b, -1], 4 + 2 * b) if method == "rk4" else
+             O.constant_grid(ts[b, 0], ts[b, -1], 0.5 - 0.1 * b) for b in range(B)]
+    grid, ns = G.layout.stack_grids(grids)
+    assert len(set(ns.tolist())) == B
+    spec = G.SolverSpec(method=G._lib.RK4 if method == "rk4" else G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS,
+                        grid=grid, nsteps=ns)
+    y0 = torch.tensor(rng.standard_normal((B, n, h)), dtype=torch.float32, device="cuda")
+    g = torch.tensor(rng.standard_normal((B, grid.shape[1], n, h)), dtype=torch.float32, device="cuda")
+    floats = G.engine.stage_record_floats(prob, spec)
+    assert floats == (grid.shape[1] - 1) * (3 if method == "rk4" else 5) * n * h
+    rec = torch.full((B, floats), float("nan"), device="cuda")
+    ys_r = G.integrate(prob, dataclasses.replace(spec, stage_rec=rec), y0)
+    ys = G.integrate(prob, spec, y0)
+    assert torch.equal(ys_r, ys)
+    a = G.integrate_vjp(prob, spec, ys, g)
+    b1 = G.integrate_vjp(prob, dataclasses.replace(spec, stage_rec=rec), ys, g)
+    b2 = G.integrate_vjp(prob, dataclasses.replace(spec, stage_rec=rec), ys, g)
+    for x, y, z in zip(a, b1, b2):
+        assert torch.equal(y, z)
+        assert rel_err(y.cpu().numpy(), x.cpu().numpy()) <= 1e-4
+    wide = G.make_problem(ts, coeffs, "undirected", O.init_vf_params(rng, "undirected", [h, 24, h]).layers)
+    assert G.engine.stage_record_floats(wide, spec) == 0
+    with pytest.raises(G._lib.GncdeError):
+        G.integrate(wide, dataclasses.replace(spec, stage_rec=rec), y0)
 
 
 def test_data_spline_gradient_matches_golden(G, golden_dir):
