@@ -25,6 +25,11 @@ namespace gncde {
 namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+
+// v_pk_fma_f32: two independent fp32 FMAs per VALU issue (same per-element operation order as fmaf)
+__device__ __forceinline__ floatx2 pkfma(floatx2 a, floatx2 b, floatx2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ floatx2 bc2(float v) { return floatx2{v, v}; }
 
 constexpr int H = 16;
 constexpr int kTMaxS = 256;
@@ -327,7 +332,9 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
   // every operand-build read; rotating the odd groups by 16 puts them on the other 16 banks.
   const int kRot = KS == 32 ? 16 * (hi & 1) : 0;
   const int oAr = swz<NP>(node, hi * KS), oAc = swz<NP>(hi * KS, node);
-  auto forward = [&](float (&Z)[4]) __attribute__((always_inline)) {
+  // full == false (a forward whose backward follows): the last layer's (I+Abar) m product is skipped — the
+  // backward needs only its m (and the earlier layers' pre-activations), never the stage value itself.
+  auto forward = [&](float (&Z)[4], bool full) __attribute__((always_inline)) {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       const float* op = a.ops + (size_t)l * kOpStride;
@@ -348,18 +355,28 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       for (int r = 0; r < 4; ++r) {
         mown[r] = fmaf(inv, acc[r], op[kOpBias + 4 * hi + r]);
         ml[l][r] = node_ok ? mown[r] : 0.f;
-        sMb[(4 * hi + r) * MS + node] = ml[l][r];
       }
+      if (!full && l == L - 1) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sMb[(4 * hi + r) * MS + node] = ml[l][r];
       float Ab[KS];
       {
         const float e0 = fc[GNCDE_FC_E_A], e1 = fc[GNCDE_FC_E_DA], e2 = fc[GNCDE_FC_ET_A], e3 = fc[GNCDE_FC_ET_DA];
         const float wi = sW[l * NP + node];
         const float* vv = sV + l * NP + hi * KS;
 #pragma unroll
-        for (int sl = 0; sl < KS; ++sl) {
+        for (int sl = 0; sl < KS; sl += 2) {  // slice pairs on packed FMAs
           const int kr = (sl + kRot) & (KS - 1);
-          Ab[sl] = fmaf(e0, sA[oAr + kr], fmaf(e1, sdA[oAr + kr], fmaf(e2, sA[oAc + kr * (NP + 1)],
-                        fmaf(e3, sdA[oAc + kr * (NP + 1)], wi + vv[kr]))));
+          const floatx2 ar = {sA[oAr + kr], sA[oAr + kr + 1]}, dr = {sdA[oAr + kr], sdA[oAr + kr + 1]};
+          const floatx2 ac = {sA[oAc + kr * (NP + 1)], sA[oAc + (kr + 1) * (NP + 1)]};
+          const floatx2 dc = {sdA[oAc + kr * (NP + 1)], sdA[oAc + (kr + 1) * (NP + 1)]};
+          floatx2 x = floatx2{vv[kr], vv[kr + 1]} + bc2(wi);
+          x = pkfma(bc2(e3), dc, x);
+          x = pkfma(bc2(e2), ac, x);
+          x = pkfma(bc2(e1), dr, x);
+          x = pkfma(bc2(e0), ar, x);
+          Ab[sl] = x.x;
+          Ab[sl + 1] = x.y;
         }
       }
       __syncthreads();
@@ -469,36 +486,52 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       fq[GNCDE_FC_VC_DA] = C * cdn;
       const float e0 = fc[GNCDE_FC_E_A], e1 = fc[GNCDE_FC_E_DA], e2 = fc[GNCDE_FC_ET_A], e3 = fc[GNCDE_FC_ET_DA];
       const float vk = sV[l * NP + node];
-      const float* wv = sW + l * NP + 4 * hi;
-      const int oCol = swz<NP>(4 * hi, node), oRow = swz<NP>(node, 4 * hi);
-      float q0 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;
+      // Row order of the G blocks: MFMA output row R = 4g + r (lane group g) stands for row base(it) + og(g) + r.
+      // Pairing blocks into 32-row windows puts lane groups 0 / 1 (2 / 3) of one 32-lane half 16 rows apart, so
+      // the A / dA reads of both the row (A[i][node]) and the column (A[node][i]) walk hit 32 distinct banks
+      // (with consecutive 16-row blocks they were 4 rows apart: 2-way conflicts).
+      constexpr bool PAIR = NW % 2 == 0;
+      auto og = [](int g) { return PAIR ? 16 * (g & 1) + 4 * (g >> 1) : 4 * g; };
+      auto base = [](int it) { return PAIR ? 32 * (it >> 1) + 8 * (it & 1) : 16 * it; };
+      const float* wv = sW + l * NP + og(hi);
+      const int oCol = swz<NP>(og(hi), node), oRow = swz<NP>(node, og(hi));
+      const int rA = og(lo >> 2) + (lo & 3);  // A-operand row of this lane
+      floatx2 q0 = {0.f, 0.f}, q1 = {0.f, 0.f}, q2 = {0.f, 0.f}, q3 = {0.f, 0.f};
       float AbT[KS];
 #pragma unroll
       for (int it = 0; it < NW; ++it) {
         floatx4 Gt = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Gt = mfma4(sGb[(4 * hi + j) * MS + 16 * it + lo], ml[l][j], Gt);
+        for (int j = 0; j < 4; ++j) Gt = mfma4(sGb[(4 * hi + j) * MS + base(it) + rA], ml[l][j], Gt);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int di = 16 * it + r;
-          const float aik = sA[oCol + di * (NP + 1)], dik = sdA[oCol + di * (NP + 1)];
-          const float aki = sA[oRow + di], dki = sdA[oRow + di];
-          q0 = fmaf(Gt[r], aik, q0);
-          q1 = fmaf(Gt[r], dik, q1);
-          q2 = fmaf(Gt[r], aki, q2);
-          q3 = fmaf(Gt[r], dki, q3);
-          AbT[4 * it + r] = fmaf(e0, aik, fmaf(e1, dik, fmaf(e2, aki, fmaf(e3, dki, wv[di] + vk))));
+        for (int r = 0; r < 4; r += 2) {  // row pairs on packed FMAs
+          const int di = base(it) + r;
+          const floatx2 g2 = {Gt[r], Gt[r + 1]};
+          const floatx2 aik = {sA[oCol + di * (NP + 1)], sA[oCol + (di + 1) * (NP + 1)]};
+          const floatx2 dik = {sdA[oCol + di * (NP + 1)], sdA[oCol + (di + 1) * (NP + 1)]};
+          const floatx2 aki = {sA[oRow + di], sA[oRow + di + 1]}, dki = {sdA[oRow + di], sdA[oRow + di + 1]};
+          q0 = pkfma(g2, aik, q0);
+          q1 = pkfma(g2, dik, q1);
+          q2 = pkfma(g2, aki, q2);
+          q3 = pkfma(g2, dki, q3);
+          floatx2 x = floatx2{wv[di], wv[di + 1]} + bc2(vk);
+          x = pkfma(bc2(e3), dki, x);
+          x = pkfma(bc2(e2), aki, x);
+          x = pkfma(bc2(e1), dik, x);
+          x = pkfma(bc2(e0), aik, x);
+          AbT[4 * it + r] = x.x;
+          AbT[4 * it + r + 1] = x.y;
         }
       }
-      fq[GNCDE_FC_E_A] = q0;
-      fq[GNCDE_FC_E_DA] = q1;
-      fq[GNCDE_FC_ET_A] = q2;
-      fq[GNCDE_FC_ET_DA] = q3;
+      fq[GNCDE_FC_E_A] = q0.x + q0.y;
+      fq[GNCDE_FC_E_DA] = q1.x + q1.y;
+      fq[GNCDE_FC_ET_A] = q2.x + q2.y;
+      fq[GNCDE_FC_ET_DA] = q3.x + q3.y;
       floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-      const float* grow = sGb + lo * MS + 4 * hi;
+      const float* grow = sGb + lo * MS + og(hi);
 #pragma unroll
       for (int it = 0; it < NW; ++it) {
-        const float4 gv = *reinterpret_cast<const float4*>(grow + 16 * it);
+        const float4 gv = *reinterpret_cast<const float4*>(grow + base(it));
         c0 = mfma4(gv.x, AbT[4 * it + 0], c0);
         c1 = mfma4(gv.y, AbT[4 * it + 1], c1);
         c0 = mfma4(gv.z, AbT[4 * it + 2], c0);
@@ -522,7 +555,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         zn[r] = node_ok ? fmaf(xh[r], rw4[r], op[kOpRb + 4 * hi + r]) : 0.f;
         sGb[(4 * hi + r) * MS + node] = gm[r];
         sMb[(4 * hi + r) * MS + node] = zn[r];
-        gbA[l][r] += xor_sum16(gm[r]);
+        gbA[l][r] += gm[r];  // lane partials: reduced over the wave's nodes once, at the end
       }
       __syncthreads();
       {
@@ -539,8 +572,8 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       float dot = 0.f, gxh[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        grwA[l][r] += xor_sum16(gz4[r] * xh[r]);
-        grbA[l][r] += xor_sum16(node_ok ? gz4[r] : 0.f);
+        grwA[l][r] = fmaf(gz4[r], xh[r], grwA[l][r]);
+        grbA[l][r] += node_ok ? gz4[r] : 0.f;
         gxh[r] = gz4[r] * rw4[r];
         dot = fmaf(gxh[r], xh[r], dot);
       }
@@ -594,7 +627,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
     for (int r = 0; r < 4; ++r) U[r] = fmaf(hk, U[r], y[r]);
     if (i > 0) store4(a.U[i], rowoff, U);
     form(stage_time(tk, a.c[i], hk));
-    forward(U);
+    forward(U, true);
     store4(a.K[i], rowoff, U);
     if (a.write_next) {  // input of stage i+1 (the last stage, whose value the sweep never needs)
       float Un[4];
@@ -627,13 +660,13 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
     form(stage_time(tk, 0.5f, hk));
 #pragma unroll
     for (int r = 0; r < 4; ++r) Kv[r] = U[r];
-    forward(Kv);
+    forward(Kv, true);
 #pragma unroll
     for (int r = 0; r < 4; ++r) U[r] = fmaf(hh, Kv[r], y[r]);
     store4(a.U[2], rowoff, U);
 #pragma unroll
     for (int r = 0; r < 4; ++r) Kv[r] = U[r];
-    forward(Kv);
+    forward(Kv, true);
 #pragma unroll
     for (int r = 0; r < 4; ++r) U[r] = fmaf(hk, Kv[r], y[r]);
     store4(a.U[3], rowoff, U);
@@ -645,7 +678,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       loadU(k, i, U);
       load4(a.gK[i], rowoff, gK);
       form(stage_time(tk, a.c[i], hk));
-      forward(U);
+      forward(U, false);
       backward(gK, gU);
       load4(a.gyacc, rowoff, acc);
 #pragma unroll
@@ -672,7 +705,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         load4(a.gK[0], rowoff, gK);
         form(tn);
         formed = true;
-        forward(U);
+        forward(U, false);
         backward(gK, gU);
         load4(a.gyacc, rowoff, lam);
 #pragma unroll
@@ -695,7 +728,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) gK[r] = hk * a.bw[il] * lam[r] + sd[r];
         if (!formed || tl != tn) form(tl);
-        forward(U);
+        forward(U, false);
         backward(gK, gU);
         float acc[4];
 #pragma unroll
@@ -718,7 +751,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       loadU(k, 2, U);
       load4(a.gK[2], rowoff, gK);
       form(stage_time(tk, 0.5f, hk));
-      forward(U);
+      forward(U, false);
       backward(gK, gU);
       load4(a.gyacc, rowoff, gy);
       load4(a.gK[1], rowoff, g1);
@@ -729,7 +762,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         g1[r] = fmaf(hh, gU[r], g1[r]);  // a[2][1] = 1/2
       }
       loadU(k, 1, U);
-      forward(U);
+      forward(U, false);
       backward(g1, gU);
       load4(a.gK[0], rowoff, g1);
 #pragma unroll
@@ -749,10 +782,11 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         blk[2 * H + (4 * hi + r) * H + lo] = gWacc[l][r];
+        const float rw = xor_sum16(grwA[l][r]), rb = xor_sum16(grbA[l][r]), bb = xor_sum16(gbA[l][r]);
         if (lo == 0) {
-          blk[4 * hi + r] = grwA[l][r];
-          blk[H + 4 * hi + r] = grbA[l][r];
-          blk[2 * H + H * H + 4 * hi + r] = gbA[l][r];
+          blk[4 * hi + r] = rw;
+          blk[H + 4 * hi + r] = rb;
+          blk[2 * H + H * H + 4 * hi + r] = bb;
         }
       }
       if (lane < GNCDE_FC) blk[kLayerP + lane] = gfA[l];
