@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
   __shared__ float sVec[(6 + 2 * L) * NP];
   __shared__ float sTs[kTMaxS];
   __shared__ float sFus[L * GNCDE_FC];
-  __shared__ float sCol[2][NW][H];
+  __shared__ float sCol[1][NW][H];
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -229,10 +229,23 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
     const float f = t - sTs[idx];
     const float f3 = 3.0f * f;
     const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
+    // time-channel coefficients first: their HBM round trip overlaps the interval's Horner pass
+    float tc0, tc1, tc2;
+    {
+      const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
+      const int ii = node_ok ? node : 0;
+      tc0 = tc[ii];
+      tc1 = tc[n + ii];
+      tc2 = tc[2 * n + ii];
+    }
     if (n == NP) {
       const float4* c4 = reinterpret_cast<const float4*>(cb);
       constexpr int NQ = NP * NP / 4;
-      for (int e4 = tid; e4 < NQ; e4 += NT) {
+      // fully unrolled: every coefficient load of the interval is in flight before the first use (one HBM
+      // round trip per form instead of NP/16 dependent ones; the form is the sweep's HBM-bound phase)
+#pragma unroll
+      for (int it = 0; it < NQ / NT; ++it) {
+        const int e4 = tid + it * NT;
         const float4 d = c4[e4], c = c4[NQ + e4], bb = c4[2 * NQ + e4], aa = c4[3 * NQ + e4];
         const int r = (e4 * 4) / NP, k = (e4 * 4) % NP;
         float* pa = sA + swz<NP>(r, k);
@@ -247,6 +260,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         pd[3] = fmaf(f, fmaf(f3, d.w, 2.0f * c.w), bb.w);
       }
     } else {
+#pragma unroll 8
       for (int e = tid; e < NP * NP; e += NT) {
         const int r = e / NP, k = e % NP;
         float va = 0.f, vd = 0.f;
@@ -267,6 +281,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
       if (q < 2) {
         const float* row = M + swz<NP>(j, 0);
+#pragma unroll 4
         for (int k = 0; k < NP; k += 4) {
           acc0 += row[k];
           acc1 += row[k + 1];
@@ -276,6 +291,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         sVec[(4 + q) * NP + j] = M[swz<NP>(j, j)];
       } else {
         const float* col = M + j;
+#pragma unroll 4
         for (int k = 0; k < NP; k += 4) {
           acc0 += col[swz<NP>(k, 0)];
           acc1 += col[swz<NP>(k + 1, 0)];
@@ -319,9 +335,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
               fc[GNCDE_FC_UR_DA] * rdn + fc[GNCDE_FC_UC_A] * cn + fc[GNCDE_FC_UC_DA] * cdn + fc[GNCDE_FC_US_A] * s +
               fc[GNCDE_FC_US_DA] * sd;
     }
-    const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
-    const int ii = node_ok ? node : 0;
-    tg = node_ok ? fmaf(f, fmaf(f3, tc[ii], 2.0f * tc[n + ii]), tc[2 * n + ii]) : 0.f;
+    tg = node_ok ? fmaf(f, fmaf(f3, tc0, 2.0f * tc1), tc2) : 0.f;
     __syncthreads();  // sW / sV visible
   };
 
@@ -430,38 +444,26 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         sMb[(4 * hi + r) * MS + node] = ml[l][r];
       }
       {
-        float cm[4], cg[4];
+        float cm[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          cm[r] = xor_sum16(ml[l][r]);
-          cg[r] = xor_sum16(gpre[r]);
-        }
-        if (lo == 0) {
+        for (int r = 0; r < 4; ++r) cm[r] = xor_sum16(ml[l][r]);
+        if (lo == 0)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            sCol[0][w][4 * hi + r] = cm[r];
-            sCol[1][w][4 * hi + r] = cg[r];
-          }
-        }
+          for (int r = 0; r < 4; ++r) sCol[0][w][4 * hi + r] = cm[r];
       }
       __syncthreads();
-      float colm[4], colg[4];
+      // R_i = gpre_i . colsum(m), D_i = gpre_i . m_i here; C_k = colsum(gpre) . m_k = sum_i G_ik comes from the
+      // G blocks below (no column sum of gpre needed)
+      float R = 0.f, D = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        colm[r] = xor_sum16(lo < NW ? sCol[0][lo < NW ? lo : 0][4 * hi + r] : 0.f);
-        colg[r] = xor_sum16(lo < NW ? sCol[1][lo < NW ? lo : 0][4 * hi + r] : 0.f);
-      }
-      float R = 0.f, C = 0.f, D = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        R = fmaf(gpre[r], colm[r], R);
-        C = fmaf(ml[l][r], colg[r], C);
+        const float colm = xor_sum16(lo < NW ? sCol[0][lo < NW ? lo : 0][4 * hi + r] : 0.f);
+        R = fmaf(gpre[r], colm, R);
         D = fmaf(gpre[r], ml[l][r], D);
       }
       R = xor_sum4(R);
-      C = xor_sum4(C);
       D = xor_sum4(D);
-      if (hi != 0) R = C = D = 0.f;  // every node once
+      if (hi != 0) R = D = 0.f;  // every node once
       float fq[GNCDE_FC];
 #pragma unroll
       for (int q = 0; q < GNCDE_FC; ++q) fq[q] = 0.f;
@@ -480,10 +482,6 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       fq[GNCDE_FC_WC_DA] = R * cdn;
       fq[GNCDE_FC_WS_A] = R * s;
       fq[GNCDE_FC_WS_DA] = R * sd;
-      fq[GNCDE_FC_VR_A] = C * rn;
-      fq[GNCDE_FC_VR_DA] = C * rdn;
-      fq[GNCDE_FC_VC_A] = C * cn;
-      fq[GNCDE_FC_VC_DA] = C * cdn;
       const float e0 = fc[GNCDE_FC_E_A], e1 = fc[GNCDE_FC_E_DA], e2 = fc[GNCDE_FC_ET_A], e3 = fc[GNCDE_FC_ET_DA];
       const float vk = sV[l * NP + node];
       // Row order of the G blocks: MFMA output row R = 4g + r (lane group g) stands for row base(it) + og(g) + r.
@@ -496,7 +494,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       const float* wv = sW + l * NP + og(hi);
       const int oCol = swz<NP>(og(hi), node), oRow = swz<NP>(node, og(hi));
       const int rA = og(lo >> 2) + (lo & 3);  // A-operand row of this lane
-      floatx2 q0 = {0.f, 0.f}, q1 = {0.f, 0.f}, q2 = {0.f, 0.f}, q3 = {0.f, 0.f};
+      floatx2 q0 = {0.f, 0.f}, q1 = {0.f, 0.f}, q2 = {0.f, 0.f}, q3 = {0.f, 0.f}, cs = {0.f, 0.f};
       float AbT[KS];
 #pragma unroll
       for (int it = 0; it < NW; ++it) {
@@ -514,6 +512,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
           q1 = pkfma(g2, dik, q1);
           q2 = pkfma(g2, aki, q2);
           q3 = pkfma(g2, dki, q3);
+          cs = cs + g2;
           floatx2 x = floatx2{wv[di], wv[di + 1]} + bc2(vk);
           x = pkfma(bc2(e3), dki, x);
           x = pkfma(bc2(e2), aki, x);
@@ -527,6 +526,14 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       fq[GNCDE_FC_E_DA] = q1.x + q1.y;
       fq[GNCDE_FC_ET_A] = q2.x + q2.y;
       fq[GNCDE_FC_ET_DA] = q3.x + q3.y;
+      {
+        float C = xor_sum4(cs.x + cs.y);
+        if (hi != 0) C = 0.f;
+        fq[GNCDE_FC_VR_A] = C * rn;
+        fq[GNCDE_FC_VR_DA] = C * rdn;
+        fq[GNCDE_FC_VC_A] = C * cn;
+        fq[GNCDE_FC_VC_DA] = C * cdn;
+      }
       floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
       const float* grow = sGb + lo * MS + og(hi);
 #pragma unroll
