@@ -7,7 +7,8 @@ for ctrs in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WA
             "SQ_INSTS_VALU_MFMA_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
             "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $ctrs --output-format csv -d "$ROOTDIR/gpurun_out/pmccfg_$i" -o run -- \
-     python3 "$ROOTDIR/tools/bench_configs.py" --configs "${CFGS:-3}" --reps 1 > "$ROOTDIR/gpurun_out/pmccfg_$i.log" 2>&1) || exit $?
+  out="$ROOTDIR/gpurun_out/pmccfg${CFGS:-3}_$i"
+  (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $ctrs --output-format csv -d "$out" -o run -- \
+     python3 "$ROOTDIR/tools/bench_configs.py" --configs "${CFGS:-3}" --reps 1 > "$out.log" 2>&1) || exit $?
 done
 echo done
