@@ -227,14 +227,21 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
         const int r = (e4 * 4) / NP, k = (e4 * 4) % NP;
         float* pa = sA + swz<NP>(r, k);
         float* pd = sdA + swz<NP>(r, k);
-        pa[0] = fmaf(f, fmaf(f, fmaf(f, d.x, c.x), bb.x), aa.x);
-        pa[1] = fmaf(f, fmaf(f, fmaf(f, d.y, c.y), bb.y), aa.y);
-        pa[2] = fmaf(f, fmaf(f, fmaf(f, d.z, c.z), bb.z), aa.z);
-        pa[3] = fmaf(f, fmaf(f, fmaf(f, d.w, c.w), bb.w), aa.w);
-        pd[0] = fmaf(f, fmaf(f3, d.x, 2.0f * c.x), bb.x);
-        pd[1] = fmaf(f, fmaf(f3, d.y, 2.0f * c.y), bb.y);
-        pd[2] = fmaf(f, fmaf(f3, d.z, 2.0f * c.z), bb.z);
-        pd[3] = fmaf(f, fmaf(f3, d.w, 2.0f * c.w), bb.w);
+        // element pairs on packed FMAs (same per-element Horner order as a scalar chain)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const floatx2 d2 = h2 ? floatx2{d.z, d.w} : floatx2{d.x, d.y};
+          const floatx2 c2 = h2 ? floatx2{c.z, c.w} : floatx2{c.x, c.y};
+          const floatx2 b2 = h2 ? floatx2{bb.z, bb.w} : floatx2{bb.x, bb.y};
+          const floatx2 a2 = h2 ? floatx2{aa.z, aa.w} : floatx2{aa.x, aa.y};
+          const floatx2 ff = {f, f}, f33 = {f3, f3}, two = {2.0f, 2.0f};
+          const floatx2 va = __builtin_elementwise_fma(ff, __builtin_elementwise_fma(ff, __builtin_elementwise_fma(ff, d2, c2), b2), a2);
+          const floatx2 vd = __builtin_elementwise_fma(ff, __builtin_elementwise_fma(f33, d2, two * c2), b2);
+          pa[2 * h2] = va.x;
+          pa[2 * h2 + 1] = va.y;
+          pd[2 * h2] = vd.x;
+          pd[2 * h2 + 1] = vd.y;
+        }
       }
     } else {  // padded image: rows/cols >= n are zero, so they add nothing to sums or operands
       for (int e = ftid; e < NP * NP; e += NT) {
