@@ -346,7 +346,8 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
   };
 
   // ---- forward at the formed time, activations kept for the backward ----------------------------------
-  float Zin[L][4], invl[L], ml[L][4], prel[L][4];
+  // activations of up to two stage evaluations at the formed time (slot 0 / 1; forward2 fills both)
+  float Zin[2][L][4], invl[2][L], ml[2][L][4], prel[2][L][4];
   // K range of lane group hi: [hi*KS, hi*KS + KS), walked from offset kRot: at NP = 128 the groups hi = 0 / 1 (and
   // 2 / 3) of one 32-lane half would otherwise hit the same banks (hi*KS = 32 = 0 mod 32) — 2-way conflicts on
   // every operand-build read; rotating the odd groups by 16 puts them on the other 16 banks.
@@ -360,13 +361,13 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       const float* op = a.ops + (size_t)l * kOpStride;
       const float* fc = sFus + l * GNCDE_FC;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Zin[l][r] = Z[r];
+      for (int r = 0; r < 4; ++r) Zin[0][l][r] = Z[r];
       float ss = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) ss = fmaf(Z[r], Z[r], ss);
       ss = xor_sum4(ss);
       const float inv = 1.0f / sqrtf(ss / (float)H + 1e-5f);
-      invl[l] = inv;
+      invl[0][l] = inv;
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc = mfma4(op[kOpWf + r * 64 + lane], Z[r], acc);
@@ -374,11 +375,11 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         mown[r] = fmaf(inv, acc[r], op[kOpBias + 4 * hi + r]);
-        ml[l][r] = node_ok ? mown[r] : 0.f;
+        ml[0][l][r] = node_ok ? mown[r] : 0.f;
       }
       if (!full && l == L - 1) break;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sMb[(4 * hi + r) * MS + node] = ml[l][r];
+      for (int r = 0; r < 4; ++r) sMb[(4 * hi + r) * MS + node] = ml[0][l][r];
       float Ab[KS];
       {
         const float e0 = fc[GNCDE_FC_E_A], e1 = fc[GNCDE_FC_E_DA], e2 = fc[GNCDE_FC_ET_A], e3 = fc[GNCDE_FC_ET_DA];
@@ -413,13 +414,99 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float z = fmaf(ul[l], mown[r], c0[r] + c1[r]);
-        prel[l][r] = z;
+        prel[0][l][r] = z;
         Z[r] = (l < L - 1) ? fmaxf(z, 0.f) : z;
       }
       __syncthreads();  // m^T reads done before sMb is rewritten
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) Z[r] = node_ok ? tg * Z[r] : 0.f;
+  };
+  // Two independent stage evaluations at the formed time (the boundary's stage 0 of step k+1 and last stage of step
+  // k; the pair's stages 2 and 1), forward only as far as their backwards need: each layer's operand slice Ab is
+  // built once for both, their m^T go to sMb / sGb (sGb is free until a backward), and their product MFMA chains
+  // interleave.
+  auto forward2 = [&](float (&Za)[4], float (&Zb)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      const float* op = a.ops + (size_t)l * kOpStride;
+      const float* fc = sFus + l * GNCDE_FC;
+      float mown[2][4];
+#pragma unroll
+      for (int sl2 = 0; sl2 < 2; ++sl2) {
+        float (&Z)[4] = sl2 ? Zb : Za;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Zin[sl2][l][r] = Z[r];
+        float ss = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ss = fmaf(Z[r], Z[r], ss);
+        ss = xor_sum4(ss);
+        const float inv = 1.0f / sqrtf(ss / (float)H + 1e-5f);
+        invl[sl2][l] = inv;
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = mfma4(op[kOpWf + r * 64 + lane], Z[r], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          mown[sl2][r] = fmaf(inv, acc[r], op[kOpBias + 4 * hi + r]);
+          ml[sl2][l][r] = node_ok ? mown[sl2][r] : 0.f;
+        }
+      }
+      if (l == L - 1) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sMb[(4 * hi + r) * MS + node] = ml[0][l][r];
+        sGb[(4 * hi + r) * MS + node] = ml[1][l][r];
+      }
+      float Ab[KS];
+      {
+        const float e0 = fc[GNCDE_FC_E_A], e1 = fc[GNCDE_FC_E_DA], e2 = fc[GNCDE_FC_ET_A], e3 = fc[GNCDE_FC_ET_DA];
+        const float wi = sW[l * NP + node];
+        const float* vv = sV + l * NP + hi * KS;
+#pragma unroll
+        for (int sl = 0; sl < KS; sl += 2) {
+          const int kr = (sl + kRot) & (KS - 1);
+          const floatx2 ar = {sA[oAr + kr], sA[oAr + kr + 1]}, dr = {sdA[oAr + kr], sdA[oAr + kr + 1]};
+          const floatx2 ac = {sA[oAc + kr * (NP + 1)], sA[oAc + (kr + 1) * (NP + 1)]};
+          const floatx2 dc = {sdA[oAc + kr * (NP + 1)], sdA[oAc + (kr + 1) * (NP + 1)]};
+          floatx2 x = floatx2{vv[kr], vv[kr + 1]} + bc2(wi);
+          x = pkfma(bc2(e3), dc, x);
+          x = pkfma(bc2(e2), ac, x);
+          x = pkfma(bc2(e1), dr, x);
+          x = pkfma(bc2(e0), ar, x);
+          Ab[sl] = x.x;
+          Ab[sl + 1] = x.y;
+        }
+      }
+      __syncthreads();
+      floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f}, d0 = c0, d1 = c0;
+      const float* mrow = sMb + lo * MS + hi * KS;
+      const float* grow = sGb + lo * MS + hi * KS;
+#pragma unroll
+      for (int q = 0; q < KS / 4; ++q) {
+        const int o = (4 * q + kRot) & (KS - 1);
+        const float4 mv = *reinterpret_cast<const float4*>(mrow + o);
+        const float4 gv = *reinterpret_cast<const float4*>(grow + o);
+        c0 = mfma4(mv.x, Ab[4 * q + 0], c0);
+        d0 = mfma4(gv.x, Ab[4 * q + 0], d0);
+        c1 = mfma4(mv.y, Ab[4 * q + 1], c1);
+        d1 = mfma4(gv.y, Ab[4 * q + 1], d1);
+        c0 = mfma4(mv.z, Ab[4 * q + 2], c0);
+        d0 = mfma4(gv.z, Ab[4 * q + 2], d0);
+        c1 = mfma4(mv.w, Ab[4 * q + 3], c1);
+        d1 = mfma4(gv.w, Ab[4 * q + 3], d1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float za = fmaf(ul[l], mown[0][r], c0[r] + c1[r]);
+        const float zb = fmaf(ul[l], mown[1][r], d0[r] + d1[r]);
+        prel[0][l][r] = za;
+        prel[1][l][r] = zb;
+        Za[r] = (l < L - 1) ? fmaxf(za, 0.f) : za;
+        Zb[r] = (l < L - 1) ? fmaxf(zb, 0.f) : zb;
+      }
+      __syncthreads();  // m^T reads done before sMb / sGb are rewritten
+    }
   };
 
   // ---- backward of the last forward: gU = J^T gK; gradients accumulated lane-distributed ---------------
@@ -434,7 +521,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       for (int r = 0; r < 4; ++r) gbA[l][r] = grwA[l][r] = grbA[l][r] = 0.f;
     }
   }
-  auto backward = [&](const float (&gK)[4], float (&gU)[4]) __attribute__((always_inline)) {
+  auto backward = [&](const float (&gK)[4], float (&gU)[4], const int slot) __attribute__((always_inline)) {
     float gZ[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) gZ[r] = node_ok ? tg * gK[r] : 0.f;
@@ -445,14 +532,14 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       float gpre[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        gpre[r] = (l < L - 1 && !(prel[l][r] > 0.f)) ? 0.f : gZ[r];
+        gpre[r] = (l < L - 1 && !(prel[slot][l][r] > 0.f)) ? 0.f : gZ[r];
         sGb[(4 * hi + r) * MS + node] = gpre[r];
-        sMb[(4 * hi + r) * MS + node] = ml[l][r];
+        sMb[(4 * hi + r) * MS + node] = ml[slot][l][r];
       }
       {
         float cm[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cm[r] = xor_sum16(ml[l][r]);
+        for (int r = 0; r < 4; ++r) cm[r] = xor_sum16(ml[slot][l][r]);
         if (lo == 0)
 #pragma unroll
           for (int r = 0; r < 4; ++r) sCol[0][w][4 * hi + r] = cm[r];
@@ -465,7 +552,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       for (int r = 0; r < 4; ++r) {
         const float colm = xor_sum16(lo < NW ? sCol[0][lo < NW ? lo : 0][4 * hi + r] : 0.f);
         R = fmaf(gpre[r], colm, R);
-        D = fmaf(gpre[r], ml[l][r], D);
+        D = fmaf(gpre[r], ml[slot][l][r], D);
       }
       R = xor_sum4(R);
       D = xor_sum4(D);
@@ -506,7 +593,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       for (int it = 0; it < NW; ++it) {
         floatx4 Gt = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Gt = mfma4(sGb[(4 * hi + j) * MS + base(it) + rA], ml[l][j], Gt);
+        for (int j = 0; j < 4; ++j) Gt = mfma4(sGb[(4 * hi + j) * MS + base(it) + rA], ml[slot][l][j], Gt);
 #pragma unroll
         for (int r = 0; r < 4; r += 2) {  // row pairs on packed FMAs
           const int di = base(it) + r;
@@ -564,7 +651,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         rw4[r] = op[kOpRw + 4 * hi + r];
-        xh[r] = Zin[l][r] * invl[l];
+        xh[r] = Zin[slot][l][r] * invl[slot][l];
         zn[r] = node_ok ? fmaf(xh[r], rw4[r], op[kOpRb + 4 * hi + r]) : 0.f;
         sGb[(4 * hi + r) * MS + node] = gm[r];
         sMb[(4 * hi + r) * MS + node] = zn[r];
@@ -592,7 +679,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       }
       dot = xor_sum4(dot);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) gZ[r] = node_ok ? invl[l] * (gxh[r] - xh[r] * dot * (1.0f / (float)H)) : 0.f;
+      for (int r = 0; r < 4; ++r) gZ[r] = node_ok ? invl[slot][l] * (gxh[r] - xh[r] * dot * (1.0f / (float)H)) : 0.f;
       __syncthreads();  // restaged buffers read before the next layer / form writes them
     }
 #pragma unroll
@@ -692,7 +779,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       load4(a.gK[i], rowoff, gK);
       form(stage_time(tk, a.c[i], hk));
       forward(U, false);
-      backward(gK, gU);
+      backward(gK, gU, 0);
       load4(a.gyacc, rowoff, acc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[r] += gU[r];
@@ -708,18 +795,26 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
     }
     if constexpr (PROG == kBoundary || BOUND_PAIR) {
       const int S = a.S;
-      float lam[4];
+      const int il = S - 1;
+      const float tl = stage_time(tk, a.c[il], hk);
+      float lam[4], Un[4], gKn[4], Uc[4];
       float tn = 0.f, hn = 0.f;
-      bool formed = false;
-      if (a.has_next) {  // stage 0 of step k+1 at t_{k+1}: lambda_{k+1} = gyacc + gU (+ gys[k+1])
+      if (a.has_next) {
         geom(k + 1, tn, hn);
-        float U[4], gK[4], gU[4];
-        load4(a.ys, rowk(k + 1), U);
-        load4(a.gK[0], rowoff, gK);
+        load4(a.ys, rowk(k + 1), Un);
+        load4(a.gK[0], rowoff, gKn);
+      }
+      if (a.has_cur) loadU(k, il, Uc);
+      // both evaluations at t_{k+1} in one two-stage forward when the last stage's time is that same float
+      const bool dual = a.has_next && a.has_cur && tl == tn;
+      if (a.has_next) {  // stage 0 of step k+1 at t_{k+1}: lambda_{k+1} = gyacc + gU (+ gys[k+1])
+        float gU[4];
         form(tn);
-        formed = true;
-        forward(U, false);
-        backward(gK, gU);
+        if (dual)
+          forward2(Un, Uc);
+        else
+          forward(Un, false);
+        backward(gKn, gU, 0);
         load4(a.gyacc, rowoff, lam);
 #pragma unroll
         for (int r = 0; r < 4; ++r) lam[r] += gU[r];
@@ -733,16 +828,17 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         load4(a.lam, rowoff, lam);
       }
       if (a.has_cur) {  // seeds of step k and its last stage
-        const int il = S - 1;
-        const float tl = stage_time(tk, a.c[il], hk);
-        float U[4], gK[4], gU[4], sd[4] = {0.f, 0.f, 0.f, 0.f};
-        loadU(k, il, U);
+        float gK[4], gU[4], sd[4] = {0.f, 0.f, 0.f, 0.f};
         if (a.gst) load4(a.gst, rowst(k, il), sd);
 #pragma unroll
         for (int r = 0; r < 4; ++r) gK[r] = hk * a.bw[il] * lam[r] + sd[r];
-        if (!formed || tl != tn) form(tl);
-        forward(U, false);
-        backward(gK, gU);
+        if (dual) {
+          backward(gK, gU, 1);
+        } else {
+          if (!a.has_next || tl != tn) form(tl);
+          forward(Uc, false);
+          backward(gK, gU, 0);
+        }
         float acc[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[r] = lam[r] + gU[r];
@@ -760,12 +856,13 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
     // RK4 stages 2 then 1 at t + h/2 (kBoundaryPair: right after the boundary, one launch and one gradient
     // reduction for both)
     if constexpr (PROG == kVjpPair || BOUND_PAIR) {
-      float U[4], gK[4], gU[4], gy[4], g1[4];
+      float U[4], U1[4], gK[4], gU[4], gy[4], g1[4];
       loadU(k, 2, U);
+      loadU(k, 1, U1);
       load4(a.gK[2], rowoff, gK);
       form(stage_time(tk, 0.5f, hk));
-      forward(U, false);
-      backward(gK, gU);
+      forward2(U, U1);  // stages 2 and 1 share t + h/2; stage 1's backward waits for stage 2's
+      backward(gK, gU, 0);
       load4(a.gyacc, rowoff, gy);
       load4(a.gK[1], rowoff, g1);
       const float hh = 0.5f * hk;
@@ -774,9 +871,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         gy[r] += gU[r];
         g1[r] = fmaf(hh, gU[r], g1[r]);  // a[2][1] = 1/2
       }
-      loadU(k, 1, U);
-      forward(U, false);
-      backward(g1, gU);
+      backward(g1, gU, 1);
       load4(a.gK[0], rowoff, g1);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
