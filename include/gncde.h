@@ -145,8 +145,8 @@ typedef struct GncdeSolver {
    * or 6 (Tsit5): every step's stage inputs U_1 .. U_{S-1} (U_0 is the step's starting state, already in ys).
    * gncde_integrate WRITES it; gncde_integrate_vjp* READ it (the same forward's record), so the reverse sweep
    * evaluates no stage twice: with 288 GB of HBM per GPU the forward stores what the reverse would recompute.
-   * Only for problems where gncde_stage_record_floats() is non-zero (fused forward and fused reverse sweep);
-   * gncde_integrate returns GNCDE_ERR_UNSUPPORTED for a record on a problem its fused path does not take. */
+   * Both forward paths (fused, generic) write it and both reverse sweeps (fused, generic, the _data variant)
+   * read it; size it with gncde_stage_record_floats(). */
   float* stage_rec;
 } GncdeSolver;
 
@@ -157,9 +157,9 @@ const char* gncde_strerror(int code);
  * "generic"), written into buf (NUL-terminated).  Returns GNCDE_OK or an error code. */
 int gncde_integrate_path(const GncdeProblem* prob, const GncdeSolver* solver, char* buf, size_t buf_len);
 
-/* Floats per sample of the stage record (GncdeSolver.stage_rec) that gncde_integrate_vjp would read for this
- * problem and solver: (G-1)*(S-1)*n*d_s when the fused reverse sweep takes it, 0 when the reverse sweep ignores
- * it (PID controller, the generic reverse sweep, the _data variant).  Never fails; 0 for invalid arguments. */
+/* Floats per sample of the stage record (GncdeSolver.stage_rec) for this problem and solver: (G-1)*(S-1)*n*d_s for
+ * an fp32 GRID solve with G >= 2, else 0 (PID controller: its reverse mode replays the accepted steps as a GRID
+ * solve, which takes the record; bf16 modes: no reverse mode).  Never fails; 0 for invalid arguments. */
 size_t gncde_stage_record_floats(const GncdeProblem* prob, const GncdeSolver* solver);
 
 /* Workspace bytes needed by gncde_vf_eval (solver == NULL) or gncde_integrate. */

@@ -70,10 +70,7 @@ const char* gncde_strerror(int code) {
 size_t gncde_stage_record_floats(const GncdeProblem* prob, const GncdeSolver* solver) {
   if (validate_problem(prob) != GNCDE_OK || validate_solver(prob, solver) != GNCDE_OK) return 0;
   if (solver->controller != GNCDE_CTRL_GRID || prob->compute != GNCDE_COMPUTE_FP32) return 0;
-  if (!stage_vjp_supported(*prob, *solver) || solver->grid_len < 2) return 0;
-  GncdeSolver fwd = *solver;  // the forward that writes the record: SAVE_STEPS checkpoints on the fused path
-  fwd.save_mode = GNCDE_SAVE_STEPS;
-  if (!fused_supported(*prob, fwd, nullptr, 0)) return 0;
+  if (solver->grid_len < 2) return 0;
   const size_t S = solver->method == GNCDE_RK4 ? 4 : 6;
   return (size_t)(solver->grid_len - 1) * (S - 1) * (size_t)prob->n * (size_t)prob->dims[0];
 }
@@ -117,8 +114,6 @@ int gncde_integrate(const GncdeProblem* prob, const GncdeSolver* solver, const f
   if (!y0 || !ys) return GNCDE_ERR_ARG;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (fused_supported(*prob, *solver, nullptr, 0)) return fused_integrate(*prob, *solver, y0, ys, stats, st);
-  // the stage record is written by the fused forward only (gncde_stage_record_floats is non-zero only there)
-  if (solver->controller == GNCDE_CTRL_GRID && solver->stage_rec) return GNCDE_ERR_UNSUPPORTED;
   if (workspace_bytes < generic_integrate_workspace(*prob, *solver) || !workspace) return GNCDE_ERR_WORKSPACE;
   return generic_integrate(*prob, *solver, y0, ys, stats, static_cast<char*>(workspace), st);
 }

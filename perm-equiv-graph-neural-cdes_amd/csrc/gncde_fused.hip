@@ -579,6 +579,11 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       st = ns1;
     }
   }
+  if (a.rec) {  // padded steps (h = 0): every stage input is the final state, as the generic forward records it
+    const int S1 = METHOD == GNCDE_RK4 ? 3 : 5;
+    for (int k = ns; k < G - 1; ++k)
+      for (int i = 0; i < S1; ++i) store(a.rec + (((size_t)b * (G - 1) + k) * S1 + i) * E);
+  }
   if (a.save_mode == GNCDE_SAVE_STEPS) {
     for (int k = ns + 1; k < G; ++k) store(a.ys + ((size_t)b * G + k) * E);
   } else {

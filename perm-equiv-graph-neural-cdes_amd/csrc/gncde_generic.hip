@@ -307,6 +307,8 @@ struct Combo {
   float c;
   const float* tcur;
   float* tst;
+  float* rec;         // stage record slot of this stage input ([B, G-1, S-1, E] at (k, i-1)) or nullptr
+  size_t rec_stride;  // floats between consecutive samples' slots: (G-1)*(S-1)*E
 };
 // kComboU elements per thread (strided by the block), each element's stage-buffer loads issued together before the
 // summation: the load latency is paid once per thread, not once per term.  Same summation order per element.
@@ -334,7 +336,9 @@ __global__ void __launch_bounds__(256) k_combo(int B, size_t E, const float* __r
 #pragma unroll
     for (int j = 0; j < 7; ++j)
       if (j < cb.nk) s = fmaf(cb.a[j], kv[j][u], s);
-    out[(size_t)b * E + e] = fmaf(hb, s, yv[u]);
+    const float v = fmaf(hb, s, yv[u]);
+    out[(size_t)b * E + e] = v;
+    if (cb.rec) cb.rec[(size_t)b * cb.rec_stride + e] = v;
   }
 }
 
@@ -630,8 +634,16 @@ int generic_integrate_one(const GncdeProblem& p, const GncdeSolver& s, const flo
   // Every evaluation's stage time tst is written by the launch before it (k_grid_step for c = 0, k_combo for the
   // others); the step's y <- y_{k+1} and Tsit5's FSAL k1 <- k7 are pointer swaps, not copies.
   auto eval = [&](const float* yin, float* out) { return generic_vf_eval(p, tst, yin, out, ws, st, true); };
+  // stage record (GncdeSolver.stage_rec): the stage input U_i of step k goes to slot (k, i-1) as it is formed
+  const int S = s.method == GNCDE_RK4 ? 4 : 6;
+  float* rec = G >= 2 ? s.stage_rec : nullptr;
+  int rec_k = 0, rec_i = 0;  // slot of the next combination's output (rec_i == 0: not recorded)
   auto combo = [&](std::initializer_list<std::pair<int, float>> terms, float* out, float c_next, bool has_next) {
     Combo cb{};
+    if (rec && rec_i > 0) {
+      cb.rec = rec + ((size_t)rec_k * (S - 1) + rec_i - 1) * E;
+      cb.rec_stride = (size_t)(G - 1) * (S - 1) * E;
+    }
     cb.nk = 0;
     for (auto& tr : terms) {
       cb.K[cb.nk] = K[tr.first];
@@ -658,9 +670,14 @@ int generic_integrate_one(const GncdeProblem& p, const GncdeSolver& s, const flo
   if (s.method == GNCDE_RK4) {
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
       hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst);
+      rec_k = k;
+      rec_i = 1;
       eval_combo(y, 0, {{0, 0.5f}}, yt, 0.5f, true);
+      rec_i = 2;
       eval_combo(yt, 1, {{1, 0.5f}}, yt, 0.5f, true);
+      rec_i = 3;
       eval_combo(yt, 2, {{2, 1.0f}}, yt, 1.0f, true);
+      rec_i = 0;
       // y + h/6 (k1 + 2k2 + 2k3 + k4)
       eval_combo(yt, 3, {{0, 1.0f / 6.0f}, {1, 2.0f / 6.0f}, {2, 2.0f / 6.0f}, {3, 1.0f / 6.0f}}, yt, 0.f, false);
       std::swap(y, yt);
@@ -672,12 +689,19 @@ int generic_integrate_one(const GncdeProblem& p, const GncdeSolver& s, const flo
     rc |= eval(y, K[0]);
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
       hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst);
+      rec_k = k;
+      rec_i = 1;
       combo({{0, TSIT5_A21}}, yt, TSIT5_C2, true);  // K[0] is the FSAL value; k_grid_step set this step's h
+      rec_i = 2;
       eval_combo(yt, 1, {{0, TSIT5_A31}, {1, TSIT5_A32}}, yt, TSIT5_C3, true);
+      rec_i = 3;
       eval_combo(yt, 2, {{0, TSIT5_A41}, {1, TSIT5_A42}, {2, TSIT5_A43}}, yt, TSIT5_C4, true);
+      rec_i = 4;
       eval_combo(yt, 3, {{0, TSIT5_A51}, {1, TSIT5_A52}, {2, TSIT5_A53}, {3, TSIT5_A54}}, yt, TSIT5_C5, true);
+      rec_i = 5;
       eval_combo(yt, 4, {{0, TSIT5_A61}, {1, TSIT5_A62}, {2, TSIT5_A63}, {3, TSIT5_A64}, {4, TSIT5_A65}}, yt, 1.0f,
                  true);
+      rec_i = 0;
       eval_combo(yt, 5, {{0, TSIT5_B1}, {1, TSIT5_B2}, {2, TSIT5_B3}, {3, TSIT5_B4}, {4, TSIT5_B5}, {5, TSIT5_B6}},
                  yt, 1.0f, true);
       rc |= eval(yt, K[6]);

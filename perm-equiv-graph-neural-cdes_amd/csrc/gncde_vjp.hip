@@ -664,8 +664,14 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
     hipLaunchKernelGGL(v_step_geom, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, w.tcur, w.hcur);
     // checkpoint y_k (the forward's SAVE_STEPS output)
     hipLaunchKernelGGL(v_step_row, ge, dim3(256), 0, st, B, E, G, k, ys, w.y, 0);
+    if (s.stage_rec) {  // the forward's stage record: U_0 = y_k, U_i (i >= 1) from slot (k, i-1); no recompute
+      (void)hipMemcpyAsync(w.U[0], w.y, (size_t)B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
+      for (int i = 1; i < tab.stages; ++i)
+        hipLaunchKernelGGL(v_step_row, ge, dim3(256), 0, st, B, E, (G - 1) * (tab.stages - 1),
+                           k * (tab.stages - 1) + i - 1, s.stage_rec, w.U[i], 0);
+    }
     // recompute stage inputs U_i and values K_i
-    for (int i = 0; i < tab.stages; ++i) {
+    for (int i = 0; i < tab.stages && !s.stage_rec; ++i) {
       Lin lc{};
       lc.nx = 0;
       lc.scale_h = 1;

@@ -48,8 +48,7 @@ class _FixedGridSolve(torch.autograd.Function):
                                 fusion=fusion.detach().to(torch.float32).contiguous())
         if data_coef is not None:
             p = dataclasses.replace(p, data_coef=data_coef.detach().to(torch.float32).contiguous())
-        steps = with_stage_record(p, dataclasses.replace(spec, save_mode=_lib.SAVE_STEPS, stage_rec=None),
-                                  want=data_coef is None)
+        steps = with_stage_record(p, dataclasses.replace(spec, save_mode=_lib.SAVE_STEPS, stage_rec=None))
         ys = engine.integrate(p, steps, y0.detach())
         ctx.prob, ctx.spec = p, dataclasses.replace(spec, stage_rec=steps.stage_rec)
         ctx.dtypes = (y0.dtype, params.dtype, fusion.dtype)
@@ -153,7 +152,7 @@ class _PidSolve(torch.autograd.Function):
         steps = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_STEPS, grid=grid,
                                   nsteps=nst)
         want_data = ctx.needs_input_grad[3]
-        steps = with_stage_record(ctx.prob, steps, want=not want_data)
+        steps = with_stage_record(ctx.prob, steps)
         ys = engine.integrate(ctx.prob, steps, y0)  # the checkpoints (and stage inputs): the accepted steps replayed
         if dense:
             gys, gst = dense_output_cotangents(grid, nst, spec.save_ts, g)

@@ -104,7 +104,7 @@ def test_argument_validation_error_codes(mutate, code):
 
 
 def test_stage_record_floats():
-    """gncde_stage_record_floats: (G-1)(S-1) n d_s where the fused reverse sweep reads a record, else 0."""
+    """gncde_stage_record_floats: (G-1)(S-1) n d_s for an fp32 GRID solve, else 0."""
     lib = _lib.load()
     p = _fake_problem()
     f = lambda p, s: lib.gncde_stage_record_floats(ctypes.byref(p), ctypes.byref(s))  # noqa: E731
@@ -113,8 +113,11 @@ def test_stage_record_floats():
     s = _fake_solver(_lib.TSIT5)
     s.controller, s.t0, s.t1, s.max_steps = _lib.CTRL_PID, 0x1000, 0x1000, 16
     assert f(p, s) == 0                                            # PID: replayed as a grid by the reverse mode
-    assert f(_fake_problem(dims=(32, 32, 32)), _fake_solver()) == 0  # generic reverse sweep: no record
-    assert f(_fake_problem(n=200), _fake_solver()) == 0
+    assert f(_fake_problem(dims=(32, 32, 32)), _fake_solver()) == 100 * 3 * 64 * 32  # generic reverse sweep too
+    assert f(_fake_problem(n=200), _fake_solver()) == 100 * 3 * 200 * 16
+    bf = _fake_problem()
+    bf.compute = _lib.COMPUTE_BF16
+    assert f(bf, _fake_solver()) == 0                               # bf16 modes: forward only
     bad = _fake_problem()
     bad.T = 1
     assert f(bad, _fake_solver()) == 0
