@@ -245,6 +245,202 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
   }
 }
 
+// ---- forward forms straight from the coefficients -----------------------------------------------------------
+// The fusion reads, per evaluation, the row sums, column sums, diagonals and totals of A(t) and dA/dt(t).  On an
+// interval A(t) = a + f (b + f (c + f d)) elementwise with one f per sample, so each of those reductions is the
+// same cubic of the matching reduction of the four coefficient planes (the time channel's tcoef uses the same
+// linearity).  k_coef_sums forms the plane reductions once per solve; an evaluation then evaluates O(n) cubics and
+// never sums n^2 values, so one launch (k_abar_direct) goes from the coefficients to every layer's (I + Abar_l)
+// with no A / dA round trip through HBM and no reduction pass in front of it.
+//
+// csum per (sample, interval): [plane q = d, c, b, a][kind = row sum, column sum, diagonal][n], then the 4 totals.
+__host__ __device__ inline size_t csum_stride(int n) { return (size_t)12 * n + 4; }
+
+// grid (4 planes, T-1 intervals, B).  Fixed summation orders (deterministic, no atomics).
+template <typename CT>
+__global__ void __launch_bounds__(256) k_coef_sums(int n, int T, const CT* __restrict__ coef, float* __restrict__ csum) {
+  const int q = blockIdx.x, iv = blockIdx.y, b = blockIdx.z;
+  const size_t nn = (size_t)n * n;
+  const CT* P = coef + (((size_t)b * (T - 1) + iv) * 4 + q) * nn;
+  float* o = csum + ((size_t)b * (T - 1) + iv) * csum_stride(n);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int j = tid; j < n; j += 256) {  // column j: one thread walks it (coalesced across the block)
+    float s = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < n; ++i) s += coef_at(P, (size_t)i * n + j);
+    o[(q * 3 + 1) * n + j] = s;
+    o[(q * 3 + 2) * n + j] = coef_at(P, (size_t)j * n + j);
+  }
+  float tot = 0.f;  // lane 0 of wave w: the sum of its rows' sums, in row order
+  for (int i = w; i < n; i += 4) {  // row i: wave w's lanes across it, one wave reduction
+    float s = 0.f;
+    for (int j = lane; j < n; j += 64) s += coef_at(P, (size_t)i * n + j);
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
+    if (lane == 0) o[(q * 3) * n + i] = s;
+    tot += s;
+  }
+  __shared__ float wt[4];
+  if (lane == 0) wt[w] = tot;
+  __syncthreads();
+  if (tid == 0) o[12 * n + q] = (wt[0] + wt[1]) + (wt[2] + wt[3]);
+}
+
+// grid (tile pairs I <= K of 32 x 32 tiles, B).  A block reads the coefficients of tile (I, K) and of its mirror
+// (K, I) once (the two tiles each need the other's transposed elements), evaluates A and dA/dt there, and writes
+// both tiles of every layer's (I + Abar_l); the node vectors of its two ranges are cubics of k_coef_sums' planes.
+// Diagonal blocks (I == K) also write q_l = (I + Abar_l) 1 for their rows, tg and the CDE data-spline derivative.
+template <typename CT, typename OT>
+__global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const float* __restrict__ ts,
+                                                     const CT* __restrict__ coef, const float* __restrict__ csum,
+                                                     const float* __restrict__ tcoef, const float* __restrict__ t,
+                                                     const float* __restrict__ fus, OT* __restrict__ out,
+                                                     size_t layer_stride, float* __restrict__ qrow,
+                                                     float* __restrict__ tg, const float* __restrict__ data_coef,
+                                                     int de2, float* __restrict__ dx, int B) {
+  const int b = blockIdx.y, nt = (n + 31) >> 5;
+  int I = 0, rem = blockIdx.x;
+  while (rem >= nt - I) {
+    rem -= nt - I;
+    ++I;
+  }
+  const int K = I + rem;
+  const bool dg = I == K;
+  const int i0 = I * 32, k0 = K * 32;
+  const size_t nn = (size_t)n * n;
+  const float tb = t[b];
+  const float* tsb = ts + (size_t)b * T;
+  const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;  // 32 x 8
+  const int idx = interval_index(tsb, T, tb);
+  const float f = tb - tsb[idx], f3 = 3.0f * f;
+  const CT* cb = coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
+  const float* cs = csum + ((size_t)b * (T - 1) + idx) * csum_stride(n);
+
+  // Every load of the block is issued before the first use (one memory round trip): the thread's elements of
+  // tile (I, K) and of the mirror (K, I), rows ty + 8 u; the node-vector planes; the totals.
+  float cx[4][4], cy[4][4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int y = ty + 8 * u;
+    const bool okx = i0 + y < n && k0 + tx < n, oky = !dg && k0 + y < n && i0 + tx < n;
+    const size_t ex = (size_t)(i0 + y) * n + k0 + tx, ey = (size_t)(k0 + y) * n + i0 + tx;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      cx[u][c] = okx ? coef_at(cb, c * nn + ex) : 0.f;
+      cy[u][c] = oky ? coef_at(cb, c * nn + ey) : 0.f;
+    }
+  }
+  // node vectors: thread (range r, kind k, node x) for tid < 192 evaluates value and derivative of one reduction
+  float pv[4] = {0.f, 0.f, 0.f, 0.f};
+  const int vr = tid / 96, vk = (tid / 32) % 3, vx = tid & 31, vnode = (vr ? k0 : i0) + vx;
+  if (tid < 192 && vnode < n)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) pv[c] = cs[(c * 3 + vk) * n + vnode];
+  float pt[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) pt[c] = cs[12 * n + c];
+
+  __shared__ float tX[32][33], tXd[32][33], tY[32][33], tYd[32][33];
+  __shared__ float sv[2][6][32];  // [range][r, rd, c, cd, diag, diag_d][node]
+  float ax[4], adx[4], ay[4], ady[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int y = ty + 8 * u;
+    ax[u] = fmaf(f, fmaf(f, fmaf(f, cx[u][0], cx[u][1]), cx[u][2]), cx[u][3]);
+    adx[u] = fmaf(f, fmaf(f3, cx[u][0], 2.0f * cx[u][1]), cx[u][2]);
+    ay[u] = fmaf(f, fmaf(f, fmaf(f, cy[u][0], cy[u][1]), cy[u][2]), cy[u][3]);
+    ady[u] = fmaf(f, fmaf(f3, cy[u][0], 2.0f * cy[u][1]), cy[u][2]);
+    tX[y][tx] = ax[u];
+    tXd[y][tx] = adx[u];
+    tY[y][tx] = ay[u];
+    tYd[y][tx] = ady[u];
+  }
+  if (tid < 192) {
+    sv[vr][2 * vk][vx] = fmaf(f, fmaf(f, fmaf(f, pv[0], pv[1]), pv[2]), pv[3]);
+    sv[vr][2 * vk + 1][vx] = fmaf(f, fmaf(f3, pv[0], 2.0f * pv[1]), pv[2]);
+  }
+  const float s = fmaf(f, fmaf(f, fmaf(f, pt[0], pt[1]), pt[2]), pt[3]);
+  const float sd = fmaf(f, fmaf(f3, pt[0], 2.0f * pt[1]), pt[2]);
+  __syncthreads();
+
+  // the rank-1 and diagonal families per layer: w_l over the rows, v_l over the columns of each range, u_l on
+  // the diagonal (diagonal blocks only)
+  __shared__ float sW[GNCDE_MAX_LAYERS][2][32], sV[GNCDE_MAX_LAYERS][2][32], sU[GNCDE_MAX_LAYERS][32];
+  for (int e = tid; e < L * 64; e += 256) {
+    const int l = e >> 6, r = (e >> 5) & 1, x = e & 31;
+    const float* fc = fus + l * GNCDE_FC;
+    const float ri = sv[r][0][x], rdi = sv[r][1][x], ci = sv[r][2][x], cdi = sv[r][3][x];
+    sW[l][r][x] = fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci +
+                  fc[GNCDE_FC_WC_DA] * cdi + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
+    sV[l][r][x] = fc[GNCDE_FC_VR_A] * ri + fc[GNCDE_FC_VR_DA] * rdi + fc[GNCDE_FC_VC_A] * ci + fc[GNCDE_FC_VC_DA] * cdi;
+    if (r == 0)
+      sU[l][x] = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * sv[0][4][x] + fc[GNCDE_FC_UD_DA] * sv[0][5][x] +
+                 fc[GNCDE_FC_UR_A] * ri + fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci +
+                 fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
+  }
+  if (dg) {
+    const int i = i0 + tid;
+    if (tid < 32 && i < n) {
+      // q_l[i] = sum_k (I + Abar_l)[i][k]: the dense terms give their row / column sums, the w (row) family n
+      // copies, the v (column) family sum_k v_k (sum_k r_k = sum_k c_k = s), the diagonal once.
+      const float ri = sv[0][0][tid], rdi = sv[0][1][tid], ci = sv[0][2][tid], cdi = sv[0][3][tid];
+      const float dgi = sv[0][4][tid], dgdi = sv[0][5][tid], fn = (float)n;
+      if (qrow)
+        for (int l = 0; l < L; ++l) {
+          const float* fc = fus + l * GNCDE_FC;
+          float q = fc[GNCDE_FC_E_A] * ri + fc[GNCDE_FC_E_DA] * rdi + fc[GNCDE_FC_ET_A] * ci + fc[GNCDE_FC_ET_DA] * cdi;
+          q += fn * (fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci +
+                     fc[GNCDE_FC_WC_DA] * cdi + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd);
+          q += (fc[GNCDE_FC_VR_A] + fc[GNCDE_FC_VC_A]) * s + (fc[GNCDE_FC_VR_DA] + fc[GNCDE_FC_VC_DA]) * sd;
+          q += fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dgi + fc[GNCDE_FC_UD_DA] * dgdi + fc[GNCDE_FC_UR_A] * ri +
+               fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci + fc[GNCDE_FC_UC_DA] * cdi +
+               fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
+          qrow[((size_t)l * B + b) * n + i] = q;
+        }
+      const float* tc = tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
+      tg[(size_t)b * n + i] = fmaf(f, fmaf(f3, tc[i], 2.0f * tc[n + i]), tc[2 * n + i]);
+    }
+    if (dx) {  // CDE wrapper: dX[i][q] at t for the block's rows (same knots)
+      const size_t blk = (size_t)n * de2;
+      const int rows = n - i0 < 32 ? n - i0 : 32;
+      const float* dc = data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)i0 * de2;
+      float* dxo = dx + (size_t)b * blk + (size_t)i0 * de2;
+      for (int e = tid; e < rows * de2; e += 256) dxo[e] = fmaf(f, fmaf(f3, dc[e], 2.0f * dc[blk + e]), dc[2 * blk + e]);
+    }
+  }
+  __syncthreads();
+  const float(*sX)[33] = dg ? tX : tY;  // transposed source of tile (I, K)
+  const float(*sXd)[33] = dg ? tXd : tYd;
+  const size_t plane = (size_t)L * layer_stride;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int y = ty + 8 * u;
+    if (i0 + y < n && k0 + tx < n) {  // tile (I, K): element (i0 + y, k0 + tx)
+      const float aki = sX[tx][y], dki = sXd[tx][y];
+      const size_t e = (size_t)b * nn + (size_t)(i0 + y) * n + k0 + tx;
+      for (int l = 0; l < L; ++l) {
+        const float* fc = fus + l * GNCDE_FC;
+        float v = fc[GNCDE_FC_E_A] * ax[u] + fc[GNCDE_FC_E_DA] * adx[u] + fc[GNCDE_FC_ET_A] * aki +
+                  fc[GNCDE_FC_ET_DA] * dki;
+        v += sW[l][0][y] + sV[l][1][tx];
+        if (dg && y == tx) v += sU[l][y];
+        abar_store(out, l * layer_stride + e, plane, v);
+      }
+    }
+    if (!dg && k0 + y < n && i0 + tx < n) {  // mirror tile (K, I): element (k0 + y, i0 + tx)
+      const float aik = tX[tx][y], dik = tXd[tx][y];
+      const size_t e = (size_t)b * nn + (size_t)(k0 + y) * n + i0 + tx;
+      for (int l = 0; l < L; ++l) {
+        const float* fc = fus + l * GNCDE_FC;
+        float v = fc[GNCDE_FC_E_A] * ay[u] + fc[GNCDE_FC_E_DA] * ady[u] + fc[GNCDE_FC_ET_A] * aik +
+                  fc[GNCDE_FC_ET_DA] * dik;
+        v += sW[l][1][y] + sV[l][0][tx];
+        abar_store(out, l * layer_stride + e, plane, v);
+      }
+    }
+  }
+}
+
 // ---- epilogue: ODE dy = tg * Z; CDE dy[i,m] = tg[i] * sum_{l,k} Z[i,(m*de+l)*2+k] dX[i,l,k] --------
 __global__ void k_finalize(int n, int dL, int h, int de, int T, const float* __restrict__ ts,
                            const float* __restrict__ data_coef, const float* __restrict__ t,
@@ -372,7 +568,7 @@ inline const float* abar_layer(const GncdeProblem& p, const float* abar, int l) 
 }
 
 struct VfWs {
-  float *A, *dA, *red, *tg, *Z0, *Z1, *m, *abar, *wf, *wp, *bf, *inv, *part, *q, *dx;
+  float *csum, *tg, *Z0, *Z1, *m, *abar, *wf, *wp, *bf, *inv, *q, *dx;
 };
 
 size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
@@ -388,9 +584,7 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
     off += align_up(floats * sizeof(float), 256);
     return ptr;
   };
-  w.A = take(B * nn);
-  w.dA = take(B * nn);
-  w.red = take(B * kRedStride * n);
+  w.csum = take(B * (size_t)(p.T - 1) * csum_stride(p.n));  // k_coef_sums' plane reductions, once per solve
   w.tg = take(B * n);
   w.Z0 = take(B * n * D);
   w.Z1 = take(B * n * D);
@@ -400,7 +594,6 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.wp = take(wsum);  // W' in k_layer's operand order (layers with layer_mode >= 0)
   w.bf = take(bsum);  // bias' = bias + W rms_b per layer
   w.inv = take(B * n);
-  w.part = take(B * ((n + kSlab - 1) / kSlab) * 2 * n);
   w.q = take((size_t)p.L * B * n);                          // q_l = (I + Abar_l) 1
   w.dx = take(B * n * (size_t)(p.cde_hidden > 0 ? 2 * p.cde_embed : 1));  // data-spline derivative at t
   return off;
@@ -440,9 +633,38 @@ void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float*
                        dA, red, part, abar, (size_t)B * n * n, qrow, B);
 }
 
+// The forward evaluation's forms: one k_abar_direct launch (every layer's (I + Abar_l), q_l, tg, dX) from the
+// coefficients and k_coef_sums' reductions.
+void vf_forms_direct(const GncdeProblem& p, const float* t, const float* csum, float* abar, float* qrow, float* tg,
+                     float* dx, hipStream_t st) {
+  const int B = p.B, n = p.n;
+  const unsigned nt = cdiv(n, 32);
+  const dim3 grid(nt * (nt + 1) / 2, B);
+  float* dxo = p.cde_hidden > 0 ? dx : nullptr;
+  const size_t ls = (size_t)B * n * n;
+  const bool bf16 = p.compute != GNCDE_COMPUTE_FP32;
+  if (p.compute == GNCDE_COMPUTE_BF16_STORAGE)
+    hipLaunchKernelGGL((k_abar_direct<uint16_t, uint16_t>), grid, dim3(256), 0, st, n, p.T, p.L, p.ts,
+                       reinterpret_cast<const uint16_t*>(p.coef), csum, p.tcoef, t, p.fusion,
+                       reinterpret_cast<uint16_t*>(abar), ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B);
+  else if (bf16)
+    hipLaunchKernelGGL((k_abar_direct<float, uint16_t>), grid, dim3(256), 0, st, n, p.T, p.L, p.ts, p.coef, csum,
+                       p.tcoef, t, p.fusion, reinterpret_cast<uint16_t*>(abar), ls, qrow, tg, p.data_coef,
+                       2 * p.cde_embed, dxo, B);
+  else
+    hipLaunchKernelGGL((k_abar_direct<float, float>), grid, dim3(256), 0, st, n, p.T, p.L, p.ts, p.coef, csum,
+                       p.tcoef, t, p.fusion, abar, ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B);
+}
+
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
   VfWs w;
   carve_vf(p, ws, w);
+  const dim3 gs(4, p.T - 1, p.B);
+  if (p.compute == GNCDE_COMPUTE_BF16_STORAGE)
+    hipLaunchKernelGGL(k_coef_sums<uint16_t>, gs, dim3(256), 0, st, p.n, p.T,
+                       reinterpret_cast<const uint16_t*>(p.coef), w.csum);
+  else
+    hipLaunchKernelGGL(k_coef_sums<float>, gs, dim3(256), 0, st, p.n, p.T, p.coef, w.csum);
   size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
@@ -463,7 +685,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   VfWs w;
   carve_vf(p, ws, w);
   if (!prepared) generic_vf_prepare(p, ws, st);
-  vf_forms(p, t, w.A, w.dA, w.tg, w.red, w.part, w.abar, st, w.q, w.dx);
+  vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st);
   const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
   const float* Zin = y;
   float* bufs[2] = {w.Z0, w.Z1};
