@@ -94,8 +94,10 @@ enum { GNCDE_RK4 = 0, GNCDE_TSIT5 = 1 };
  *   BF16_STORAGE: as BF16, and `coef` holds bfloat16 values (same shape, uint16 storage): the operator spline's
  *                 input is quantised to bf16, halving the dominant HBM stream.  Results equal the fp32 reference
  *                 evaluated on the bf16-rounded coefficients.
- * Splines, reductions, the Linears, solver and epilogues stay fp32.  The bf16 modes are forward only (the reverse
- * entry points return GNCDE_ERR_UNSUPPORTED) and always take the generic path. */
+ * Splines, reductions, the Linears, solver and epilogues stay fp32.  The bf16 modes always take the generic path.
+ * Their reverse mode (gncde_integrate_vjp*) is the fp32 discrete adjoint over the coefficients the forward read
+ * (BF16_STORAGE: the bf16 planes widened exactly into the workspace head, which gncde_vjp_workspace_bytes
+ * includes): the gradient of the bf16 solve to its own ~2^-16 product rounding. */
 enum { GNCDE_COMPUTE_FP32 = 0, GNCDE_COMPUTE_BF16 = 1, GNCDE_COMPUTE_BF16_STORAGE = 2 };
 enum { GNCDE_CTRL_GRID = 0, GNCDE_CTRL_PID = 1 };
 enum { GNCDE_SAVE_T1 = 0, GNCDE_SAVE_STEPS = 1, GNCDE_SAVE_TS = 2 };
@@ -159,7 +161,7 @@ int gncde_integrate_path(const GncdeProblem* prob, const GncdeSolver* solver, ch
 
 /* Floats per sample of the stage record (GncdeSolver.stage_rec) for this problem and solver: (G-1)*(S-1)*n*d_s for
  * an fp32 GRID solve with G >= 2, else 0 (PID controller: its reverse mode replays the accepted steps as a GRID
- * solve, which takes the record; bf16 modes: no reverse mode).  Never fails; 0 for invalid arguments. */
+ * solve, which takes the record; bf16 modes: their reverse sweep recomputes the stages, no record).  Never fails; 0 for invalid arguments. */
 size_t gncde_stage_record_floats(const GncdeProblem* prob, const GncdeSolver* solver);
 
 /* Workspace bytes needed by gncde_vf_eval (solver == NULL) or gncde_integrate. */

@@ -47,6 +47,31 @@ int validate_solver(const GncdeProblem* p, const GncdeSolver* s) {
   return GNCDE_OK;
 }
 
+// ---- reverse mode of the bf16 modes ---------------------------------------------------------------------
+// The bf16 modes' forward differs from the fp32 forward only in the n x n products, which run on split (hi, lo)
+// bf16 pairs with fp32 accumulation (~2^-16 relative per product), and, for BF16_STORAGE, in reading the operator
+// coefficients as bfloat16.  Their reverse mode is the fp32 discrete adjoint over the coefficients that forward
+// read: the fp32 planes themselves (BF16), or the bf16 planes widened exactly into the head of the workspace
+// (BF16_STORAGE).  It is the gradient of the bf16 solve to the forward's own product rounding.
+namespace {
+
+__global__ void k_widen_bf16(size_t N, const uint16_t* __restrict__ in, float* __restrict__ out) {
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += (size_t)gridDim.x * blockDim.x)
+    out[e] = __builtin_bit_cast(float, (uint32_t)in[e] << 16);
+}
+
+size_t coef_floats(const GncdeProblem& p) { return (size_t)p.B * (p.T - 1) * 4 * (size_t)p.n * p.n; }
+
+// the fp32 problem the reverse sweep runs on, and the workspace bytes it keeps in front for widened coefficients
+GncdeProblem fp32_view(const GncdeProblem& p, size_t& head) {
+  GncdeProblem q = p;
+  q.compute = GNCDE_COMPUTE_FP32;
+  head = p.compute == GNCDE_COMPUTE_BF16_STORAGE ? align_up(coef_floats(p) * sizeof(float), 256) : 0;
+  return q;
+}
+
+}  // namespace
+
 }  // namespace gncde
 
 using namespace gncde;
@@ -120,9 +145,10 @@ int gncde_integrate(const GncdeProblem* prob, const GncdeSolver* solver, const f
 
 size_t gncde_vjp_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* solver) {
   if (validate_problem(prob) != GNCDE_OK || validate_solver(prob, solver) != GNCDE_OK) return 0;
-  if (prob->compute != GNCDE_COMPUTE_FP32) return 0;
-  if (stage_vjp_supported(*prob, *solver)) return stage_vjp_workspace(*prob);
-  return generic_vjp_workspace(*prob, *solver);
+  size_t head = 0;
+  const GncdeProblem p = fp32_view(*prob, head);
+  if (stage_vjp_supported(p, *solver)) return head + stage_vjp_workspace(p);
+  return head + generic_vjp_workspace(p, *solver);
 }
 
 static int integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,
@@ -134,7 +160,6 @@ static int integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, co
   rc = validate_solver(prob, solver);
   if (rc) return rc;
   if (solver->controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
-  if (prob->compute != GNCDE_COMPUTE_FP32) return GNCDE_ERR_UNSUPPORTED;  // the bf16 path is forward-only
   if (solver->save_mode != GNCDE_SAVE_T1 && solver->save_mode != GNCDE_SAVE_STEPS) return GNCDE_ERR_UNSUPPORTED;
   if (!gparams || !gfusion) return GNCDE_ERR_ARG;
   if (gdata && prob->cde_hidden <= 0) return GNCDE_ERR_ARG;  // only the CDE wrapper reads a data spline
@@ -146,14 +171,22 @@ static int integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, co
     return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
   }
   if (!ys || !gys || !gy0) return GNCDE_ERR_ARG;
-  if (!gdata && stage_vjp_supported(*prob, *solver)) {
-    if (workspace_bytes < stage_vjp_workspace(*prob) || !workspace) return GNCDE_ERR_WORKSPACE;
-    return stage_integrate_vjp(*prob, *solver, ys, gys, gstage, gy0, gparams, gfusion, static_cast<char*>(workspace),
-                               st);
+  size_t head = 0;
+  GncdeProblem p = fp32_view(*prob, head);  // bf16 modes: the fp32 adjoint (see fp32_view)
+  char* ws = static_cast<char*>(workspace);
+  const bool stage = !gdata && stage_vjp_supported(p, *solver);
+  const size_t need = head + (stage ? stage_vjp_workspace(p) : generic_vjp_workspace(p, *solver));
+  if (workspace_bytes < need || !workspace) return GNCDE_ERR_WORKSPACE;
+  if (head) {
+    float* wide = reinterpret_cast<float*>(ws);
+    const size_t N = coef_floats(p);
+    hipLaunchKernelGGL(k_widen_bf16, dim3((unsigned)((N + 255) / 256 < 65536 ? (N + 255) / 256 : 65536)), dim3(256), 0,
+                       st, N, reinterpret_cast<const uint16_t*>(prob->coef), wide);
+    p.coef = wide;
+    ws += head;
   }
-  if (workspace_bytes < generic_vjp_workspace(*prob, *solver) || !workspace) return GNCDE_ERR_WORKSPACE;
-  return generic_integrate_vjp(*prob, *solver, ys, gys, gstage, gy0, gparams, gfusion, gdata,
-                               static_cast<char*>(workspace), st);
+  if (stage) return stage_integrate_vjp(p, *solver, ys, gys, gstage, gy0, gparams, gfusion, ws, st);
+  return generic_integrate_vjp(p, *solver, ys, gys, gstage, gy0, gparams, gfusion, gdata, ws, st);
 }
 
 int gncde_integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, const float* ys, const float* gys,

@@ -43,7 +43,7 @@ class Problem:
     data_coef: torch.Tensor | None = None  # [B, T-1, 4, n, de, 2]
     cde_hidden: int = 0
     cde_embed: int = 0
-    compute: int = _lib.COMPUTE_FP32  # COMPUTE_BF16(_STORAGE): the generic bf16 MFMA path (forward only)
+    compute: int = _lib.COMPUTE_FP32  # COMPUTE_BF16(_STORAGE): the generic bf16 MFMA path (reverse mode: fp32 adjoint)
     _keep: list = field(default_factory=list)
 
     @property
@@ -105,7 +105,7 @@ def make_problem(ts, coeffs, kind, layers, data_coeffs=None, cde_hidden=0, cde_e
     """Build a Problem from reference-layout inputs (ts [B,T], coeffs (d,c,b,a) [B,T-1,n,n,2], layer dicts).
 
     compute="bf16" runs the n x n products on bf16 MFMA (split pairs, fp32-class results); "bf16_storage" also
-    stores the operator coefficients in bfloat16 (BASELINE config 5; forward only, see gncde.h GNCDE_COMPUTE_*)."""
+    stores the operator coefficients in bfloat16 (BASELINE config 5; reverse mode = the fp32 adjoint over the coefficients read, see gncde.h GNCDE_COMPUTE_*)."""
     coef, tcoef = layout.pack_control(coeffs, device=device)
     mode = COMPUTE_MODES[compute]
     if mode == _lib.COMPUTE_BF16_STORAGE:

@@ -117,7 +117,7 @@ def test_stage_record_floats():
     assert f(_fake_problem(n=200), _fake_solver()) == 100 * 3 * 200 * 16
     bf = _fake_problem()
     bf.compute = _lib.COMPUTE_BF16
-    assert f(bf, _fake_solver()) == 0                               # bf16 modes: forward only
+    assert f(bf, _fake_solver()) == 0                               # bf16 modes: the sweep recomputes stages
     bad = _fake_problem()
     bad.T = 1
     assert f(bad, _fake_solver()) == 0

@@ -155,12 +155,38 @@ def test_bf16_config5_shape_vs_fp32(gncde, n):
     assert np.isfinite(yb).all() and np.isfinite(yq).all()
 
 
-def test_bf16_reverse_mode_unsupported(gncde, golden_dir):
-    z = np.load(os.path.join(golden_dir, "rk4_undirected_n12_mixed.npz"))
+# Reverse mode of the bf16 modes (gncde_abi.hip fp32_view): the fp32 discrete adjoint over the coefficients the
+# bf16 forward read.  It must equal, bit for bit, the fp32 adjoint called on those coefficients (BF16: the fp32
+# planes; BF16_STORAGE: the planes rounded to bf16 and widened) with the same checkpoints; fixtures cover the fused
+# stage sweep (n = 16, h = 16), the generic sweep (mixed widths) and the CDE wrapper with the data-spline cotangent.
+BF16_GRAD_CASES = [("rk4_undirected_n16_L2.npz", False), ("rk4_undirected_n12_mixed.npz", False),
+                   ("grad_rk4_cde_data_n9_h4_de3.npz", True)]
+RTOL_BF16_GRAD = 5e-4  # bf16 (split products) vs the fp32 solve's gradient: the forward's product rounding only
+
+
+@pytest.mark.parametrize("mode", ["bf16", "bf16_storage"])
+@pytest.mark.parametrize("name,data", BF16_GRAD_CASES)
+def test_bf16_reverse_mode_is_fp32_adjoint_of_read_coefficients(gncde, golden_dir, name, data, mode):
+    import dataclasses
+    z = np.load(os.path.join(golden_dir, name))
     params = MG.load_layers(z)
-    prob = problem_from(gncde, z, params).with_compute("bf16")
-    spec = gncde.SolverSpec(method=gncde._lib.RK4, save_mode=gncde._lib.SAVE_STEPS,
+    p32 = problem_from(gncde, z, params, data=data)
+    pb = p32.with_compute(mode)
+    spec = gncde.SolverSpec(method=gncde._lib.RK4 if str(z["method"]) == "rk4" else gncde._lib.TSIT5,
+                            save_mode=gncde._lib.SAVE_STEPS,
                             grid=torch.tensor(z["grid"], device="cuda"), nsteps=torch.tensor(z["nsteps"], device="cuda"))
-    ys = gncde.integrate(prob, spec, torch.tensor(z["y0"], dtype=torch.float32, device="cuda"))
-    with pytest.raises(gncde._lib.GncdeError):
-        gncde.integrate_vjp(prob, spec, ys, torch.ones_like(ys))
+    y0 = torch.tensor(z["y0"], dtype=torch.float32, device="cuda")
+    ys = gncde.integrate(pb, spec, y0)
+    gys = torch.randn(ys.shape, generator=torch.Generator().manual_seed(7)).to("cuda")
+    got = gncde.integrate_vjp(pb, spec, ys, gys, data_grad=data)
+    ref_prob = p32 if mode == "bf16" else dataclasses.replace(p32, coef=p32.coef.to(torch.bfloat16).float().contiguous())
+    ref = gncde.integrate_vjp(ref_prob, spec, ys, gys, data_grad=data)
+    assert len(got) == len(ref) == (4 if data else 3)
+    for g, r in zip(got, ref):
+        assert torch.isfinite(g).all()
+        assert torch.equal(g, r)
+    if mode == "bf16":  # against the fp32 solve's own gradient (its own checkpoints)
+        ys32 = gncde.integrate(p32, spec, y0)
+        full = gncde.integrate_vjp(p32, spec, ys32, gys, data_grad=data)
+        for g, r in zip(got, full):
+            assert rel_err(g.cpu().numpy(), r.cpu().numpy()) <= RTOL_BF16_GRAD
