@@ -173,6 +173,44 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
     start = true;
   } else {
     float* kst = kk(s.st);
+    if (s.st < 6 && E <= P) {
+      // A stage inside an attempt, one pass (e.g. config 5's 255 x 32): K, y and only the stage buffers the next
+      // input reads (j < st + 1, the current one taken from K in registers) in one round trip, instead of K, then
+      // all six buffers (the CU's load path, not HBM, bounds a one-workgroup-per-sample kernel).
+      const int ns1 = s.st + 1;
+      float ar[6], cst;
+      stage_row(ns1, ar, cst);
+      float kq[U], yv[U], kv[6][U];
+      ldu(K, tid, kq);
+      ldu(y, tid, yv);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        if (j < ns1 && j != s.st) {  // uniform: a scalar branch around the loads
+          ldu(kk(j), tid, kv[j]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u) kv[j][u] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + u * kAdvThreads;
+        float acc = 0.f;  // the memory path's summation order
+#pragma unroll
+        for (int j = 0; j < 6; ++j) acc = j < ns1 ? fmaf(ar[j], j == s.st ? kq[u] : kv[j][u], acc) : acc;
+        if (e < E) {
+          kst[e] = kq[u];
+          yt[e] = fmaf(s.h, acc, yv[u]);
+        }
+      }
+      s.tst = ns1 >= 5 ? __fadd_rn(s.t, s.h) : stage_time(s.t, cst, s.h);
+      s.st = ns1;
+      if (tid == 0) {
+        a.state[b] = s;
+        a.tst[b] = s.tst;
+      }
+      return;
+    }
     for (int e0 = tid; e0 < E; e0 += P) {
       float v[U];
       ldu(K, e0, v);
