@@ -339,6 +339,32 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
   float pt[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) pt[c] = cs[12 * n + c];
+  // the fusion table (to LDS) and, in diagonal blocks, the time-channel and data-spline coefficients of the
+  // block's rows: the same round trip, not one more after the first barrier
+  __shared__ float sF[GNCDE_MAX_LAYERS * GNCDE_FC];
+  const float fv = tid < L * GNCDE_FC ? fus[tid] : 0.f;
+  float tcv[3] = {0.f, 0.f, 0.f};
+  const size_t blk = (size_t)n * de2;
+  const int drows = n - i0 < 32 ? n - i0 : 32, dn = dx ? drows * de2 : 0;
+  const float* dc = dx ? data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)i0 * de2 : nullptr;
+  float dcv[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+  if (dg) {
+    if (tid < 32 && i0 + tid < n) {
+      const float* tc = tcoef + ((size_t)b * (T - 1) + idx) * 3 * n + i0 + tid;
+      tcv[0] = tc[0];
+      tcv[1] = tc[n];
+      tcv[2] = tc[2 * n];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = tid + 256 * h;
+      if (e < dn) {
+        dcv[h][0] = dc[e];
+        dcv[h][1] = dc[blk + e];
+        dcv[h][2] = dc[2 * blk + e];
+      }
+    }
+  }
 
   __shared__ float tX[32][33], tXd[32][33], tY[32][33], tYd[32][33];
   __shared__ float sv[2][6][32];  // [range][r, rd, c, cd, diag, diag_d][node]
@@ -361,6 +387,17 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
   }
   const float s = fmaf(f, fmaf(f, fmaf(f, pt[0], pt[1]), pt[2]), pt[3]);
   const float sd = fmaf(f, fmaf(f3, pt[0], 2.0f * pt[1]), pt[2]);
+  if (tid < L * GNCDE_FC) sF[tid] = fv;
+  if (dg) {
+    if (tid < 32 && i0 + tid < n) tg[(size_t)b * n + i0 + tid] = fmaf(f, fmaf(f3, tcv[0], 2.0f * tcv[1]), tcv[2]);
+    float* dxo = dx + (size_t)b * blk + (size_t)i0 * de2;  // CDE wrapper: dX[i][q] at t for the block's rows
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = tid + 256 * h;
+      if (e < dn) dxo[e] = fmaf(f, fmaf(f3, dcv[h][0], 2.0f * dcv[h][1]), dcv[h][2]);
+    }
+    for (int e = tid + 512; e < dn; e += 256) dxo[e] = fmaf(f, fmaf(f3, dc[e], 2.0f * dc[blk + e]), dc[2 * blk + e]);
+  }
   __syncthreads();
 
   // the rank-1 and diagonal families per layer: w_l over the rows, v_l over the columns of each range, u_l on
@@ -368,7 +405,7 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
   __shared__ float sW[GNCDE_MAX_LAYERS][2][32], sV[GNCDE_MAX_LAYERS][2][32], sU[GNCDE_MAX_LAYERS][32];
   for (int e = tid; e < L * 64; e += 256) {
     const int l = e >> 6, r = (e >> 5) & 1, x = e & 31;
-    const float* fc = fus + l * GNCDE_FC;
+    const float* fc = sF + l * GNCDE_FC;
     const float ri = sv[r][0][x], rdi = sv[r][1][x], ci = sv[r][2][x], cdi = sv[r][3][x];
     sW[l][r][x] = fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci +
                   fc[GNCDE_FC_WC_DA] * cdi + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
@@ -387,7 +424,7 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
       const float dgi = sv[0][4][tid], dgdi = sv[0][5][tid], fn = (float)n;
       if (qrow)
         for (int l = 0; l < L; ++l) {
-          const float* fc = fus + l * GNCDE_FC;
+          const float* fc = sF + l * GNCDE_FC;
           float q = fc[GNCDE_FC_E_A] * ri + fc[GNCDE_FC_E_DA] * rdi + fc[GNCDE_FC_ET_A] * ci + fc[GNCDE_FC_ET_DA] * cdi;
           q += fn * (fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci +
                      fc[GNCDE_FC_WC_DA] * cdi + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd);
@@ -397,15 +434,6 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
                fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
           qrow[((size_t)l * B + b) * n + i] = q;
         }
-      const float* tc = tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
-      tg[(size_t)b * n + i] = fmaf(f, fmaf(f3, tc[i], 2.0f * tc[n + i]), tc[2 * n + i]);
-    }
-    if (dx) {  // CDE wrapper: dX[i][q] at t for the block's rows (same knots)
-      const size_t blk = (size_t)n * de2;
-      const int rows = n - i0 < 32 ? n - i0 : 32;
-      const float* dc = data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)i0 * de2;
-      float* dxo = dx + (size_t)b * blk + (size_t)i0 * de2;
-      for (int e = tid; e < rows * de2; e += 256) dxo[e] = fmaf(f, fmaf(f3, dc[e], 2.0f * dc[blk + e]), dc[2 * blk + e]);
     }
   }
   __syncthreads();
@@ -419,7 +447,7 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
       const float aki = sX[tx][y], dki = sXd[tx][y];
       const size_t e = (size_t)b * nn + (size_t)(i0 + y) * n + k0 + tx;
       for (int l = 0; l < L; ++l) {
-        const float* fc = fus + l * GNCDE_FC;
+        const float* fc = sF + l * GNCDE_FC;
         float v = fc[GNCDE_FC_E_A] * ax[u] + fc[GNCDE_FC_E_DA] * adx[u] + fc[GNCDE_FC_ET_A] * aki +
                   fc[GNCDE_FC_ET_DA] * dki;
         v += sW[l][0][y] + sV[l][1][tx];
@@ -431,7 +459,7 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
       const float aik = tX[tx][y], dik = tXd[tx][y];
       const size_t e = (size_t)b * nn + (size_t)(k0 + y) * n + i0 + tx;
       for (int l = 0; l < L; ++l) {
-        const float* fc = fus + l * GNCDE_FC;
+        const float* fc = sF + l * GNCDE_FC;
         float v = fc[GNCDE_FC_E_A] * ay[u] + fc[GNCDE_FC_E_DA] * ady[u] + fc[GNCDE_FC_ET_A] * aik +
                   fc[GNCDE_FC_ET_DA] * dik;
         v += sW[l][1][y] + sV[l][0][tx];
