@@ -124,6 +124,38 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
     }
   };
   if constexpr (!BF) load_round(w);
+  // The epilogue's operands (W' B operands of the wave's output tiles, b', q, tg of its rows) do not depend on the
+  // product either: issued here, so the tail after the last barrier is MFMA + stores, not two more L2 round trips.
+  constexpr int CTO = MODE != 2 ? DOUT / 16 : 1;
+  constexpr int NCCE = MODE != 2 ? DIN / 16 : 1;
+  floatx4 wpre[2][NCCE];
+  float bpre[2], qpre[2][4], gpre[2][4];
+  if constexpr (MODE != 2) {
+    const floatx4* W4p = reinterpret_cast<const floatx4*>(a.wperm);
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int tile = w + 4 * tt, rt = tile / CTO, ct = tile % CTO;
+      const bool ok = tile < 2 * CTO;
+#pragma unroll
+      for (int cc = 0; cc < NCCE; ++cc) wpre[tt][cc] = ok ? W4p[(ct * NCCE + cc) * 64 + lane] : floatx4{0.f, 0.f, 0.f, 0.f};
+      bpre[tt] = ok ? a.bf[16 * ct + lo] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int R = r0 + 16 * rt + 4 * hi + r;
+        qpre[tt][r] = ok && R < n ? a.q[nb + R] : 0.f;
+        gpre[tt][r] = MODE == 1 && ok && R < n ? a.tg[nb + R] : 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int R = r0 + 16 * t + 4 * hi + r;
+        qpre[t][r] = R < n ? a.q[nb + R] : 0.f;
+        gpre[t][r] = R < n ? a.tg[nb + R] : 0.f;
+      }
+  }
 
   // ---- 1. Zs = Z[b] (zero rows up to nk), every load of a round in flight before the first store; then the
   // RMSNorm factor of each row from LDS (diag(inv) is applied to the (I + Abar) operand of the product).
@@ -300,19 +332,19 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
 #pragma unroll
       for (int cc = 0; cc < NCC; ++cc) {
         const floatx4 pv = prow(rt, cc);
-        const floatx4 wv = W4[(ct * NCC + cc) * 64 + lane];
+        const floatx4 wv = wpre[tt][cc];
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc = mfma4(pv[s], wv[s], acc);
       }
       const int col = 16 * ct + lo;
-      const float bc = a.bf[col];
+      const float bc = bpre[tt];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int R = r0 + 16 * rt + 4 * hi + r;
         if (R >= n) continue;
-        float v = fmaf(a.q[nb + R], bc, acc[r]);
+        float v = fmaf(qpre[tt][r], bc, acc[r]);
         if (MODE == 0) v = fmaxf(v, 0.f);
-        if (MODE == 1) v *= a.tg[nb + R];
+        if (MODE == 1) v *= gpre[tt][r];
         const size_t o = (nb + R) * DOUT + col;
         a.out[o] = v;
       }
@@ -369,7 +401,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         float sb = 0.f;
 #pragma unroll
         for (int j = 0; j < JP; ++j) sb = fmaf(a.bf[16 * m + j0 + j], sDx[rl * 17 + j0 + j], sb);
-        acc[t][r] = fmaf(R < n ? a.q[nb + R] : 0.f, sb, acc[t][r]);
+        acc[t][r] = fmaf(R < n ? qpre[t][r] : 0.f, sb, acc[t][r]);
       }
     if constexpr (KP > 1) {
       red[(w * 2 + 0) * 64 + lane] = acc[0];
@@ -391,7 +423,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
           const int R = r0 + 16 * t + 4 * hi + r;
           if (R < n) {
             const size_t o = (nb + R) * DOUT + m;
-            a.out[o] = a.tg[nb + R] * acc[t][r];
+            a.out[o] = gpre[t][r] * acc[t][r];
           }
         }
     }
