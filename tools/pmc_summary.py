@@ -45,6 +45,28 @@ def main():
     elif mode == "counters":
         for (k, c), v in sorted(counters(sys.argv[2:], os.environ.get("MATCH", "k_fused")).items()):
             print(f"{c:32s} {v:16.1f}  {k}")
+    elif mode == "table":  # one line per kernel over tools/pmc_configs.sh's pass directories (all kernels)
+        acc = defaultdict(lambda: defaultdict(list))
+        for d in sys.argv[2:]:
+            for r in _rows(d):
+                acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        g = lambda c, k: (sum(c[k]) / len(c[k])) if c.get(k) else 0.0  # noqa: E731
+        rows = []
+        for name, c in acc.items():
+            waves = g(c, "SQ_WAVES")
+            pw = lambda k: g(c, k) / waves if waves else 0.0  # noqa: E731
+            hbm = (2.0 * g(c, "FETCH_SIZE") + g(c, "WRITE_SIZE")) * 1024.0
+            short = name.replace("gncde::(anonymous namespace)::", "").replace("void ", "")[:60]
+            if "gncde" not in name:
+                continue
+            rows.append((hbm, f"{short:60s} dispatches={len(c.get('SQ_WAVES', [])):5d} waves={waves:8.0f} "
+                              f"VALU/wave={pw('SQ_INSTS_VALU'):8.1f} MFMA/wave={pw('SQ_INSTS_VALU_MFMA_F32'):6.1f} "
+                              f"LDS/wave={pw('SQ_INSTS_LDS'):6.1f} bank_conflict_cyc={g(c, 'SQ_LDS_BANK_CONFLICT'):10.0f} "
+                              f"mfma_busy={g(c, 'SQ_VALU_MFMA_BUSY_CYCLES'):10.0f} wait_any_per_wave={pw('SQ_WAIT_ANY'):9.0f} "
+                              f"busy_cyc={g(c, 'SQ_BUSY_CYCLES'):9.0f} hbm_bytes={hbm:12.0f} "
+                              f"fetch_kib={g(c, 'FETCH_SIZE'):9.1f} write_kib={g(c, 'WRITE_SIZE'):9.1f}"))
+        for _, line in sorted(rows, key=lambda x: -x[0]):
+            print(line)
     elif mode == "traffic":
         fetch_dir, write_dir, workload, kernel, out = sys.argv[2:7]
         f = counters([fetch_dir]).items()
