@@ -35,10 +35,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x8u __attribute__((ext_vector_type(8), aligned(2)));  // 8 bf16 of an (I + Abar) plane row
 
 constexpr int kRows = 32;  // node rows per workgroup: two 16-row MFMA tiles
-#ifndef GNCDE_X_JUNROLL
-#define GNCDE_X_JUNROLL 4
-#endif
-constexpr int kJUnroll = GNCDE_X_JUNROLL;  // read-out K loop: W' operand loads in flight per wave
 #ifndef GNCDE_X_LSKIP  // diagnostic builds only: 1/2/3 skip the product MFMAs / the read-out MFMAs / the Z loads
 #define GNCDE_X_LSKIP 0
 #endif

@@ -40,14 +40,18 @@ def main():
                                     t0=torch.zeros(B, device="cuda"), t1=torch.ones(B, device="cuda"),
                                     dt0=torch.full((B,), 0.01, device="cuda"))
             name = "5_trade_n255_h32_de8_L4_tsit5pid"
-        for share in (0.25, 0.0):
+        # config 5 also in BASELINE's bf16 mode (reverse mode: the fp32 adjoint over the coefficients read)
+        runs = [(prob, 0.25, "fp32"), (prob, 0.0, "fp32")]
+        if c == "5":
+            runs.append((prob.with_compute("bf16"), 0.25, "bf16"))
+        for pr, share, mode in runs:
             autograd.STAGE_RECORD_SHARE = share
             fw, bw = [], []
             for _ in range(args.reps + 1):
-                params = prob.params.clone().requires_grad_(True)
+                params = pr.params.clone().requires_grad_(True)
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                 e[0].record()
-                out = autograd.solve(prob, spec, y0, params)
+                out = autograd.solve(pr, spec, y0, params)
                 loss = out.square().sum()
                 e[1].record()
                 loss.backward()
@@ -55,7 +59,8 @@ def main():
                 torch.cuda.synchronize()
                 fw.append(e[0].elapsed_time(e[1]))
                 bw.append(e[1].elapsed_time(e[2]))
-            print(json.dumps({"config": name, "stage_record": share > 0, "forward_ms": round(min(fw[1:]), 3),
+            print(json.dumps({"config": name, "compute": mode, "stage_record": share > 0 and mode == "fp32",
+                              "grad_finite": bool(torch.isfinite(params.grad).all()), "forward_ms": round(min(fw[1:]), 3),
                               "backward_ms": round(min(bw[1:]), 3)}), flush=True)
     autograd.STAGE_RECORD_SHARE = 0.25
 

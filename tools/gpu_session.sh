@@ -51,6 +51,11 @@ for step in "$@"; do
            rc=$?; echo "proftrain rc=$rc"; tail -n 5 "$ROOTDIR/gpurun_out/proftrain.log"; \
            case $rc in 124|134|137|139) exit $rc;; esac) || exit $? ;;
     configs) run configs 900 python tools/bench_configs.py ;;
+    profgrad) (cd /tmp && run_dir="$ROOTDIR/gpurun_out/profgrad" && rm -rf "$run_dir" && \
+           timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$run_dir" -o run -- \
+             python3 "$ROOTDIR/tools/bench_grad_configs.py" --configs "${CFGS:-5}" --reps 1 > "$ROOTDIR/gpurun_out/profgrad.log" 2>&1; \
+           rc=$?; echo "profgrad rc=$rc"; tail -n 5 "$ROOTDIR/gpurun_out/profgrad.log"; \
+           case $rc in 124|134|137|139) exit $rc;; esac) || exit $? ;;
     pmcsq) i=0; for ctrs in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT" \
                           "SQ_INSTS_VALU_MFMA_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
                           "TCC_HIT_sum TCC_MISS_sum"; do
