@@ -101,8 +101,9 @@ __global__ void v_norm_rows(size_t rows, int d, const float* __restrict__ Z, con
 }
 
 // Column sums over `rows` rows, two passes with a fixed order: part[chunk][j], then out[j] (+)= sum_chunk.
-// mode 0: X; mode 1: X * Y (elementwise)
-constexpr int kChunk = 1024;
+// mode 0: X; mode 1: X * Y (elementwise).  Chunks of 128 rows, each thread's 32 rows loaded 8 at a time (all in
+// flight): with 1024-row chunks and a serial row loop a chunk was 256 dependent L2 round trips (55 us at config 5).
+constexpr int kChunk = 128;
 __global__ void __launch_bounds__(256) v_colsum_part(size_t rows, int d, const float* __restrict__ X,
                                                      const float* __restrict__ Y, float* __restrict__ part) {
   const int j = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -111,9 +112,17 @@ __global__ void __launch_bounds__(256) v_colsum_part(size_t rows, int d, const f
   __shared__ float red[4][64];
   float s = 0.f;
   if (j < d) {
-    for (size_t r = r0 + g; r < rows && r < r0 + kChunk; r += 4) {
-      const float x = X[r * d + j];
-      s += Y ? x * Y[r * d + j] : x;
+    for (int q0 = 0; q0 < kChunk / 4; q0 += 8) {
+      float x[8], y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const size_t r = r0 + g + 4 * (size_t)(q0 + u);
+        const bool ok = r < rows;
+        x[u] = ok ? X[r * d + j] : 0.f;
+        y[u] = (ok && Y) ? Y[r * d + j] : 1.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += Y ? x[u] * y[u] : x[u];
     }
   }
   red[g][threadIdx.x & 63] = s;
@@ -126,6 +135,7 @@ __global__ void v_colsum_final(int chunks, int d, const float* __restrict__ part
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= d) return;
   float s = 0.f;
+#pragma unroll 8
   for (int c = 0; c < chunks; ++c) s += part[(size_t)c * d + j];
   out[j] += s;
 }
@@ -150,7 +160,7 @@ __global__ void v_rms_bwd(size_t rows, int d, const float* __restrict__ Z, const
 // G.*A, G.*dA, G.*A^T, G.*dA^T (the transposed tiles staged in LDS) -> part[b][tile][4]
 __global__ void __launch_bounds__(256) v_fusion_dense_G(int n, const float* __restrict__ A,
                                                         const float* __restrict__ dA, const float* __restrict__ Gm,
-                                                        float* __restrict__ part) {
+                                                        float* __restrict__ part, float* __restrict__ rcpart) {
   const int b = blockIdx.z;
   const int i0 = blockIdx.y * 32, k0 = blockIdx.x * 32;
   const size_t nn = (size_t)n * n;
@@ -167,16 +177,30 @@ __global__ void __launch_bounds__(256) v_fusion_dense_G(int n, const float* __re
     tD[y][tx] = ok ? dAb[(size_t)k * n + i] : 0.f;
   }
   __syncthreads();
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, cs = 0.f;
+  // ... and the tile's partial row sums (over its 32 columns) and column sums (over its 32 rows) of G, so that
+  // v_fusion_finish sums tiles1 partials per node instead of walking a whole row / column of G
+  const int tiles1 = gridDim.x;
+  float* rowp = rcpart + (((size_t)b * tiles1 + blockIdx.x) * 2) * n;      // [b][K tile][0][i]
+  float* colp = rcpart + (((size_t)b * tiles1 + blockIdx.y) * 2 + 1) * n;  // [b][I tile][1][k]
   for (int y = ty; y < 32; y += 8) {
     const int i = i0 + y, k = k0 + tx;
-    if (i >= n || k >= n) continue;
-    const float g = Gb[(size_t)i * n + k];
-    s0 = fmaf(g, Ab[(size_t)i * n + k], s0);
-    s1 = fmaf(g, dAb[(size_t)i * n + k], s1);
-    s2 = fmaf(g, tA[tx][y], s2);
-    s3 = fmaf(g, tD[tx][y], s3);
+    const bool ok = i < n && k < n;
+    const float g = ok ? Gb[(size_t)i * n + k] : 0.f;
+    if (ok) {
+      s0 = fmaf(g, Ab[(size_t)i * n + k], s0);
+      s1 = fmaf(g, dAb[(size_t)i * n + k], s1);
+      s2 = fmaf(g, tA[tx][y], s2);
+      s3 = fmaf(g, tD[tx][y], s3);
+    }
+    cs += g;
+    float r = g;  // row i over the 32 lanes tx of this half-wave
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) r += __shfl_xor(r, o);
+    if (tx == 0 && i < n) rowp[i] = r;
   }
+  __shared__ float cpr[8][32];
+  cpr[ty][tx] = cs;
   red[0][threadIdx.x] = s0;
   red[1][threadIdx.x] = s1;
   red[2][threadIdx.x] = s2;
@@ -187,6 +211,12 @@ __global__ void __launch_bounds__(256) v_fusion_dense_G(int n, const float* __re
       for (int q = 0; q < 4; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + st];
     __syncthreads();
   }
+  if (threadIdx.x < 32 && k0 + threadIdx.x < n) {  // (the reduction loop's barriers order cpr)
+    float c = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) c += cpr[q][threadIdx.x];
+    colp[k0 + threadIdx.x] = c;
+  }
   const int tiles = gridDim.x * gridDim.y;
   if (threadIdx.x < 4) part[((size_t)b * tiles + blockIdx.y * gridDim.x + blockIdx.x) * 4 + threadIdx.x] =
       red[threadIdx.x][0];
@@ -196,7 +226,7 @@ __global__ void __launch_bounds__(256) v_fusion_dense_G(int n, const float* __re
 // R_i = sum_k G[i][k], C_k = sum_i G[i][k], D_i = G[i][i] against the form's row/col/diag/total vectors.
 __global__ void __launch_bounds__(256) v_fusion_finish(int n, int L, int l, int tiles, const float* __restrict__ red,
                                                        const float* __restrict__ Gm, const float* __restrict__ part,
-                                                       float* __restrict__ gfc) {
+                                                       const float* __restrict__ rcpart, float* __restrict__ gfc) {
   const int b = blockIdx.x;
   const size_t nn = (size_t)n * n;
   const float* Gb = Gm + b * nn;
@@ -205,19 +235,22 @@ __global__ void __launch_bounds__(256) v_fusion_finish(int n, int L, int l, int 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   float acc[GNCDE_FC];
   for (int q = 0; q < GNCDE_FC; ++q) acc[q] = 0.f;
-  for (int k = tid; k < n; k += blockDim.x) {  // C_k: column sums (coalesced over threads)
+  const int t1 = (n + 31) >> 5;
+  const float* rcb = rcpart + (size_t)b * t1 * 2 * n;
+  for (int k = tid; k < n; k += blockDim.x) {  // C_k: column sums from v_fusion_dense_G's tile partials
     float c = 0.f;
-    for (int i = 0; i < n; ++i) c += Gb[(size_t)i * n + k];
+    for (int t = 0; t < t1; ++t) c += rcb[((size_t)t * 2 + 1) * n + k];
     acc[GNCDE_FC_VR_A] += c * rb[k];
     acc[GNCDE_FC_VR_DA] += c * rb[n + k];
     acc[GNCDE_FC_VC_A] += c * rb[2 * n + k];
     acc[GNCDE_FC_VC_DA] += c * rb[3 * n + k];
   }
-  for (int i = w; i < n; i += 4) {  // R_i: row sums (one wave per row); D_i: diagonal
+  (void)w;
+  (void)lane;
+  for (int i = tid; i < n; i += blockDim.x) {  // R_i: row sums from the tile partials; D_i: diagonal
     float r = 0.f;
-    for (int k = lane; k < n; k += 64) r += Gb[(size_t)i * n + k];
-    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
-    if (lane == 0) {
+    for (int t = 0; t < t1; ++t) r += rcb[(size_t)t * 2 * n + i];
+    {
       const float D = Gb[(size_t)i * n + i];
       acc[GNCDE_FC_WR_A] += r * rb[i];
       acc[GNCDE_FC_WR_DA] += r * rb[n + i];
@@ -341,6 +374,7 @@ struct VjpWs {
   float *g0, *g1, *gm, *xh, *zn, *gzn;
   float* ZL;                     // last layer output (CDE data-spline cotangent only)
   float *cpart, *kpart, *dpart, *fpart;  // column-sum, split-K and dense-fusion partials
+  float* rcpart;                 // per-tile row / column partial sums of G: [B, tiles1, 2, n]
   float *gsum, *gfc;             // batch-summed parameter gradient [P]; per-sample fusion gradient [B, L, 24]
   float *y, *lam, *gyacc, *tmp;
   float* U[7];                   // stage inputs
@@ -393,6 +427,7 @@ void carve(const GncdeProblem& p, char* ws, VjpWs& w, size_t* bytes) {
   w.cpart = tk(cdiv(R, kChunk) * D);
   w.kpart = tk(cdiv(R, split_rows(R)) * D * D);
   w.dpart = tk(B * tiles * 4);
+  w.rcpart = tk(B * cdiv(n, 32) * 2 * n);
   w.fpart = tk(vf_forms_scratch(p));
   w.gsum = tk(P);
   w.gfc = tk(B * p.L * GNCDE_FC);
@@ -518,9 +553,10 @@ void vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* 
     gg.ldc = n;
     gg.sC = (long)nn;
     gemm(gg, B, true, st);
-    hipLaunchKernelGGL(v_fusion_dense_G, dim3(tiles1, tiles1, B), dim3(256), 0, st, n, w.A, w.dA, w.G, w.dpart);
+    hipLaunchKernelGGL(v_fusion_dense_G, dim3(tiles1, tiles1, B), dim3(256), 0, st, n, w.A, w.dA, w.G, w.dpart,
+                       w.rcpart);
     hipLaunchKernelGGL(v_fusion_finish, dim3(B), dim3(256), 0, st, n, L, l, (int)(tiles1 * tiles1), w.red, w.G,
-                       w.dpart, w.gfc);
+                       w.dpart, w.rcpart, w.gfc);
     // gm = (I+Abar)^T gpre
     GemmArgs gmq{};
     gmq.M = n;
