@@ -357,7 +357,8 @@ __global__ void v_step_row(int B, size_t E, int G, int k, const float* __restric
 }
 
 // ---- workspace ----------------------------------------------------------------------------------------
-constexpr int kMinSplitRows = 1024;  // split-K chunk of the gW GEMM (rows of B*n), at most 64 chunks
+constexpr int kMinSplitRows = 128;  // split-K chunk of the gW GEMM (rows of B*n), at most 64 chunks: one block
+                                     // per chunk, so 1024-row chunks left 4 blocks each walking 32 K chunks (54 us)
 
 inline int split_rows(size_t rows) {
   size_t ck = (rows + 63) / 64;
