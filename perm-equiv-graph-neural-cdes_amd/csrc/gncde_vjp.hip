@@ -245,8 +245,6 @@ __global__ void __launch_bounds__(256) v_fusion_finish(int n, int L, int l, int 
     acc[GNCDE_FC_VC_A] += c * rb[2 * n + k];
     acc[GNCDE_FC_VC_DA] += c * rb[3 * n + k];
   }
-  (void)w;
-  (void)lane;
   for (int i = tid; i < n; i += blockDim.x) {  // R_i: row sums from the tile partials; D_i: diagonal
     float r = 0.f;
     for (int t = 0; t < t1; ++t) r += rcb[(size_t)t * 2 * n + i];
@@ -271,14 +269,19 @@ __global__ void __launch_bounds__(256) v_fusion_finish(int n, int L, int l, int 
   }
   if (tid < 4)
     for (int t = 0; t < tiles; ++t) acc[tid] += part[((size_t)b * tiles + t) * 4 + tid];  // E_A, E_DA, ET_A, ET_DA
-  __shared__ float sred[GNCDE_FC][256];
-  for (int q = 0; q < GNCDE_FC; ++q) sred[q][tid] = acc[q];
-  __syncthreads();
-  if (tid < GNCDE_FC) {
-    float tot = 0.f;
-    for (int j = 0; j < (int)blockDim.x; ++j) tot += sred[tid][j];
-    gfc[((size_t)b * L + l) * GNCDE_FC + tid] += tot;
+  // 24 block sums: a butterfly over each wave's 64 lanes, then the 4 wave partials in order (one LDS round trip
+  // instead of 24 threads each walking 256 LDS entries)
+  __shared__ float sred[GNCDE_FC][4];
+#pragma unroll
+  for (int q = 0; q < GNCDE_FC; ++q) {
+    float v = acc[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) sred[q][w] = v;
   }
+  __syncthreads();
+  if (tid < GNCDE_FC)
+    gfc[((size_t)b * L + l) * GNCDE_FC + tid] += (sred[tid][0] + sred[tid][1]) + (sred[tid][2] + sred[tid][3]);
 }
 
 // out = sum over b of x[b, :]  (fixed order: deterministic)
