@@ -10,7 +10,13 @@ steps x 4 vector-field evaluations = 409,600 sample-evals) with inputs already r
 
 Multi-GPU: samples are independent, so each rank integrates its own 1024-sample shard
 with no collective in the data path ("scaling": "weak"); the timed region is bracketed by barrier +
-synchronize and the max over ranks is reported.  Rank 0 prints ONE JSON line.
+synchronize and the max over ranks is reported.  Rank 0 prints ONE JSON line.  `--gpus N` with N > 1 and no
+torch.distributed environment starts the N ranks itself (a torch.distributed.run child, before any GPU call) and
+exits with its status; a WORLD_SIZE that disagrees with --gpus is an error.
+
+The line also carries "train": BASELINE config 4's data-parallel training step (community graph n = 128, 1024
+samples per GPU, h = 16, L = 2, RK4 x 100: forward, discrete adjoint, ONE gradient all-reduce over RCCL, ClipAdamW),
+timed the same way (barrier + synchronize, max over ranks), so the 1 -> N curve includes the collective.
 """
 from __future__ import annotations
 
@@ -128,6 +134,86 @@ def cpu_baseline(prob, spec, y0, layers, target_s):
                       f"{dt:.1f} s, oracle/gncde_oracle.c fp32, literal reference fusion, OpenMP)"}
 
 
+def world_from_env(gpus: int):
+    """(world, rank, local_rank) from the torch.distributed environment; the world size must equal --gpus."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}")
+    return world, rank, local
+
+
+def launch_ranks(gpus: int, argv) -> int:
+    """Run this script as `gpus` ranks (one process per GPU) under torch.distributed.run; returns its status.
+    Called before anything touches the GPU (the parent only waits)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def reduce_over_ranks(dist, device, elapsed: float, units: float):
+    """(max elapsed over ranks, sum of units over ranks): the job's time and its whole work."""
+    el = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    tot = torch.tensor([units], dtype=torch.float64, device=device)
+    if dist is not None:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    return float(el.item()), float(tot.item())
+
+
+def train_line(dist, rank, world, steps, warmup, rk4_steps):
+    """BASELINE config 4's training step per rank (tools/bench_train.py's workload), whole-job samples/s."""
+    import gncde
+    from gncde import layout, synthetic, train
+    from gncde.models import GraphNeuralCDE, vector_fields as V
+    B, n, h, L, T = 1024, 128, 16, 2, 80
+    prob, _, _ = synthetic.heat_batch(B, num_nodes=n, hidden=h, num_layers=L, T=T, seed=4321 + rank,
+                                      graph="community")
+    vf = V.PermEquivGraphVectorField(h, h, h, L, 16, n, key=0)
+    model = GraphNeuralCDE({"hidden_dim": h}, vf, "cubic", 1, solver={"method": "rk4", "steps": rk4_steps}).to("cuda")
+    opt = train.ClipAdamW(model, learning_rate=1e-3, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(99 + rank)
+    x0 = torch.randn(B, n, 1, generator=g).cuda()
+    labels = torch.randn(B, n, generator=g).cuda()
+    grid, ns = layout.stack_grids([layout.rk4_grid(0.0, 5.0, rk4_steps)] * B)
+    spec = gncde.SolverSpec(method=gncde._lib.RK4, save_mode=gncde._lib.SAVE_T1, grid=grid, nsteps=ns)
+
+    def loss_terms():
+        pred = model.predict_packed(prob, x0, spec).squeeze(-1)
+        return ((pred - labels) ** 2).sum(), pred.numel()
+
+    for _ in range(warmup):
+        train.make_step(opt, loss_terms)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss, _, _ = train.make_step(opt, loss_terms)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed, samples = reduce_over_ranks(dist, "cuda", time.perf_counter() - t0, B * steps)
+    out = {"metric": "GNCDE training step (forward + discrete adjoint + gradient all-reduce + ClipAdamW)",
+           "value": round(samples / elapsed, 1), "unit": "samples/s", "n_gpus": world, "steps": steps,
+           "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 3), "scaling": "weak",
+           "loss": float(loss),
+           "config": {"workload": f"gene_community_n{n}_b{B}_L{L}_h{h}_T{T}_rk4x{rk4_steps}_train",
+                      "global_batch": B * world, "per_gpu_batch": B, "parallelism": f"dp{world}",
+                      "collective": "one fp64 all-reduce bucket per step (RCCL)" if world > 1 else "none"}}
+    del prob, model, opt
+    torch.cuda.empty_cache()
+    return out if rank == 0 else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,11 +223,24 @@ def main():
     ap.add_argument("--rk4-steps", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--train-steps", type=int, default=5, help="config-4 training steps timed (0: no train line)")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="CPU check of the rank plumbing: gloo ranks reduce (rank + 1, rank + 10), no GPU work")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local = world_from_env(args.gpus)
+    if args.dist_selftest:
+        import torch.distributed as tdist
+        if world > 1:
+            tdist.init_process_group("gloo")
+        mx, tot = reduce_over_ranks(tdist if world > 1 else None, "cpu", rank + 1.0, rank + 10.0)
+        if rank == 0:
+            print(json.dumps({"world": world, "max_elapsed": mx, "sum_units": tot}), flush=True)
+        if world > 1:
+            tdist.destroy_process_group()
+        return
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -185,14 +284,12 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one fused launch per step, same stream
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    tot = torch.tensor([evals_per_launch * args.steps], dtype=torch.float64, device="cuda")
-    if dist:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    elapsed = float(el.item())
-    total_evals = float(tot.item())
+    elapsed, total_evals = reduce_over_ranks(dist, "cuda", elapsed, evals_per_launch * args.steps)
     value = total_evals / elapsed
+    tr = None
+    if args.train_steps > 0:
+        del ys
+        tr = train_line(dist, rank, world, args.train_steps, 1, args.rk4_steps)
 
     if rank == 0:
         n = prob.n
@@ -224,6 +321,7 @@ def main():
             "roofline": roof,
             "roofline_other": alt,
             "cpu_baseline": cpu,
+            "train": tr,
         }
         print(json.dumps(out), flush=True)
     if dist:

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GNCDE_ABI_VERSION 4
+#define GNCDE_ABI_VERSION 5
 #define GNCDE_MAX_LAYERS 8
 #define GNCDE_FC 24
 
@@ -101,6 +101,11 @@ enum { GNCDE_RK4 = 0, GNCDE_TSIT5 = 1 };
 enum { GNCDE_COMPUTE_FP32 = 0, GNCDE_COMPUTE_BF16 = 1, GNCDE_COMPUTE_BF16_STORAGE = 2 };
 enum { GNCDE_CTRL_GRID = 0, GNCDE_CTRL_PID = 1 };
 enum { GNCDE_SAVE_T1 = 0, GNCDE_SAVE_STEPS = 1, GNCDE_SAVE_TS = 2 };
+/* GncdeSolver.flags.  GNCDE_FLAG_GENERIC: take the generic multi-kernel path in gncde_integrate AND the generic
+ * reverse sweep in gncde_integrate_vjp*, even where the fused kernels fit.  The two paths compute the same discrete
+ * solve (and its adjoint) with different fp32 summation orders; the flag exists so that callers and tests can check
+ * one against the other on identical inputs (e.g. the same recorded PID step grid). */
+enum { GNCDE_FLAG_GENERIC = 1 };
 /* stats[b*4 + k]: k=0 accepted steps, 1 rejected steps, 2 vector-field evaluations, 3 status
  * (0 ok, 1 max_steps exceeded, 2 non-finite error estimate, 3 step record (step_ts) too short) */
 enum { GNCDE_STAT_STEPS = 0, GNCDE_STAT_REJECTS = 1, GNCDE_STAT_EVALS = 2, GNCDE_STAT_STATUS = 3 };
@@ -148,8 +153,14 @@ typedef struct GncdeSolver {
    * gncde_integrate WRITES it; gncde_integrate_vjp* READ it (the same forward's record), so the reverse sweep
    * evaluates no stage twice: with 288 GB of HBM per GPU the forward stores what the reverse would recompute.
    * Both forward paths (fused, generic) write it and both reverse sweeps (fused, generic, the _data variant)
-   * read it; size it with gncde_stage_record_floats(). */
+   * read it; size it with gncde_stage_record_floats().  stage_rec_len is its row length in floats: when stage_rec
+   * is set it must equal gncde_stage_record_floats() for this problem and solver (both the forward and the reverse
+   * mode check it and return GNCDE_ERR_ARG otherwise), so a record sized for another grid, method or arithmetic is
+   * refused instead of read out of bounds.  The caller must pass the reverse mode the record the same forward wrote
+   * (the library cannot tell an unwritten buffer from a written one). */
   float* stage_rec;
+  int64_t stage_rec_len;
+  int32_t flags;                     /* GNCDE_FLAG_* (0 = default dispatch) */
 } GncdeSolver;
 
 /* Library / error helpers */

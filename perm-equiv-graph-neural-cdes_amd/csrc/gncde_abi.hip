@@ -27,14 +27,25 @@ int validate_problem(const GncdeProblem* p) {
   return GNCDE_OK;
 }
 
+// Floats per sample of the stage record an fp32 GRID solve writes and its reverse sweep reads (gncde.h).
+size_t record_floats(const GncdeProblem& p, const GncdeSolver& s) {
+  if (s.controller != GNCDE_CTRL_GRID || p.compute != GNCDE_COMPUTE_FP32 || s.grid_len < 2) return 0;
+  const size_t S = s.method == GNCDE_RK4 ? 4 : 6;
+  return (size_t)(s.grid_len - 1) * (S - 1) * (size_t)p.n * (size_t)p.dims[0];
+}
+
 int validate_solver(const GncdeProblem* p, const GncdeSolver* s) {
   if (!s) return GNCDE_ERR_ARG;
+  if (s->flags & ~GNCDE_FLAG_GENERIC) return GNCDE_ERR_ARG;
   if (s->method != GNCDE_RK4 && s->method != GNCDE_TSIT5) return GNCDE_ERR_ARG;
   if (s->save_mode < GNCDE_SAVE_T1 || s->save_mode > GNCDE_SAVE_TS) return GNCDE_ERR_ARG;
   if (p->cde_hidden == 0 && p->dims[0] != p->dims[p->L]) return GNCDE_ERR_SHAPE;  // ODE state width
   if (s->controller == GNCDE_CTRL_GRID) {
     if (!s->grid || !s->nsteps || s->grid_len < 1) return GNCDE_ERR_ARG;
     if (s->save_mode == GNCDE_SAVE_TS) return GNCDE_ERR_UNSUPPORTED;
+    // a record must be exactly the one this solve writes / its sweep reads (none exists for the bf16 modes)
+    if (s->stage_rec && (s->stage_rec_len <= 0 || (size_t)s->stage_rec_len != record_floats(*p, *s)))
+      return GNCDE_ERR_ARG;
   } else if (s->controller == GNCDE_CTRL_PID) {
     if (!s->t0 || !s->t1 || s->max_steps < 1) return GNCDE_ERR_ARG;
     if (!(s->rtol >= 0.f) || !(s->atol > 0.f)) return GNCDE_ERR_ARG;
@@ -70,6 +81,14 @@ GncdeProblem fp32_view(const GncdeProblem& p, size_t& head) {
   return q;
 }
 
+// GNCDE_FLAG_GENERIC forces the generic forward and the generic reverse sweep (gncde.h)
+bool use_fused(const GncdeProblem& p, const GncdeSolver& s, char* name, size_t len) {
+  return !(s.flags & GNCDE_FLAG_GENERIC) && fused_supported(p, s, name, len);
+}
+bool use_stage_vjp(const GncdeProblem& p, const GncdeSolver& s) {
+  return !(s.flags & GNCDE_FLAG_GENERIC) && stage_vjp_supported(p, s);
+}
+
 }  // namespace
 
 }  // namespace gncde
@@ -93,17 +112,17 @@ const char* gncde_strerror(int code) {
 }
 
 size_t gncde_stage_record_floats(const GncdeProblem* prob, const GncdeSolver* solver) {
-  if (validate_problem(prob) != GNCDE_OK || validate_solver(prob, solver) != GNCDE_OK) return 0;
-  if (solver->controller != GNCDE_CTRL_GRID || prob->compute != GNCDE_COMPUTE_FP32) return 0;
-  if (solver->grid_len < 2) return 0;
-  const size_t S = solver->method == GNCDE_RK4 ? 4 : 6;
-  return (size_t)(solver->grid_len - 1) * (S - 1) * (size_t)prob->n * (size_t)prob->dims[0];
+  if (validate_problem(prob) != GNCDE_OK || !solver) return 0;
+  GncdeSolver s = *solver;  // the record itself is not part of the question
+  s.stage_rec = nullptr;
+  if (validate_solver(prob, &s) != GNCDE_OK) return 0;
+  return record_floats(*prob, s);
 }
 
 size_t gncde_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* solver) {
   if (validate_problem(prob) != GNCDE_OK) return 0;
   if (!solver) return generic_vf_workspace(*prob);
-  if (fused_supported(*prob, *solver, nullptr, 0)) return 0;
+  if (use_fused(*prob, *solver, nullptr, 0)) return 0;
   return generic_integrate_workspace(*prob, *solver);
 }
 
@@ -113,7 +132,7 @@ int gncde_integrate_path(const GncdeProblem* prob, const GncdeSolver* solver, ch
   rc = validate_solver(prob, solver);
   if (rc) return rc;
   if (!buf || buf_len == 0) return GNCDE_ERR_ARG;
-  if (!fused_supported(*prob, *solver, buf, buf_len))
+  if (!use_fused(*prob, *solver, buf, buf_len))
     snprintf(buf, buf_len, prob->compute != GNCDE_COMPUTE_FP32 ? "generic_bf16" : "generic");
   return GNCDE_OK;
 }
@@ -138,7 +157,7 @@ int gncde_integrate(const GncdeProblem* prob, const GncdeSolver* solver, const f
   if (prob->B == 0) return GNCDE_OK;
   if (!y0 || !ys) return GNCDE_ERR_ARG;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (fused_supported(*prob, *solver, nullptr, 0)) return fused_integrate(*prob, *solver, y0, ys, stats, st);
+  if (use_fused(*prob, *solver, nullptr, 0)) return fused_integrate(*prob, *solver, y0, ys, stats, st);
   if (workspace_bytes < generic_integrate_workspace(*prob, *solver) || !workspace) return GNCDE_ERR_WORKSPACE;
   return generic_integrate(*prob, *solver, y0, ys, stats, static_cast<char*>(workspace), st);
 }
@@ -147,7 +166,7 @@ size_t gncde_vjp_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* so
   if (validate_problem(prob) != GNCDE_OK || validate_solver(prob, solver) != GNCDE_OK) return 0;
   size_t head = 0;
   const GncdeProblem p = fp32_view(*prob, head);
-  if (stage_vjp_supported(p, *solver)) return head + stage_vjp_workspace(p);
+  if (use_stage_vjp(p, *solver)) return head + stage_vjp_workspace(p);
   return head + generic_vjp_workspace(p, *solver);
 }
 
@@ -174,7 +193,7 @@ static int integrate_vjp(const GncdeProblem* prob, const GncdeSolver* solver, co
   size_t head = 0;
   GncdeProblem p = fp32_view(*prob, head);  // bf16 modes: the fp32 adjoint (see fp32_view)
   char* ws = static_cast<char*>(workspace);
-  const bool stage = !gdata && stage_vjp_supported(p, *solver);
+  const bool stage = !gdata && use_stage_vjp(p, *solver);
   const size_t need = head + (stage ? stage_vjp_workspace(p) : generic_vjp_workspace(p, *solver));
   if (workspace_bytes < need || !workspace) return GNCDE_ERR_WORKSPACE;
   if (head) {

@@ -30,10 +30,6 @@ namespace {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));  // v_pk_fma_f32 / v_pk_add_f32 operands
 
-#ifndef GNCDE_X_SKIP  // diagnostic builds only: 1/2/3 skip the operand build / the reductions / the Horner pass
-#define GNCDE_X_SKIP 0
-#endif
-
 constexpr int kTMax = 256;  // knots per sample held in LDS
 
 // Tsit5 row a[s][0..5] for stage s = 1..6 (row 6 = b_sol) and c[s], as compile-time immediates
@@ -199,9 +195,6 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     }
     int idx = cnt - 1;
     idx = idx < 0 ? 0 : (idx > T - 2 ? T - 2 : idx);
-#if GNCDE_X_NOCOEF  // diagnostic build only: every form reads interval 0 (cache-resident coefficients)
-    idx = 0;
-#endif
     const float f = t - sTs[idx];
     const float f3 = 3.0f * f;
     const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
@@ -214,8 +207,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       tc1 = tc[n + ii];
       tc2 = tc[2 * n + ii];
     }
-    if (GNCDE_X_SKIP == 3) {
-    } else if (n == NP) {
+    if (n == NP) {
       const float4* c4 = reinterpret_cast<const float4*>(cb);
       constexpr int NQ = NP * NP / 4;
       // fully unrolled: every coefficient load of the interval is in flight before the first use (one HBM
@@ -258,7 +250,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       }
     }
     __syncthreads();
-    if (GNCDE_X_SKIP != 2) {  // r, rd (row sums), c, cd (column sums), diagonals: 4 NP threads, one line each
+    {  // r, rd (row sums), c, cd (column sums), diagonals: 4 NP threads, one line each
       const int q = ftid / NP, j = ftid % NP;
       const float* M = (q & 1) ? sdA : sA;
       float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;  // 4 chains: latency, not adds, bound this
@@ -329,7 +321,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       for (int q = 0; q < 4; ++q)
         ec[l][q] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, fc[q])));
     }
-    if (GNCDE_X_SKIP != 1) {
+    {
       // Chunks of 4 slices: all 16 image reads and the L float4 reads of v_l are issued before the first
       // use, so a chunk waits on LDS once; the pins at the end of a chunk keep the next chunk's loads
       // from being hoisted (register pressure), not the loads of this one.
@@ -444,11 +436,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
   bool have = false;
   float tcache = 0.f;
   auto vf = [&](float t, const float (&Yin)[FB][4], float (&Kout)[FB][4]) __attribute__((always_inline)) {
-#if GNCDE_X_NOFORM  // diagnostic build only: one form per solve (times the evaluations alone)
-    if (!have) {
-#else
     if (!have || t != tcache) {
-#endif
       form(t);
       tcache = t;
       have = true;

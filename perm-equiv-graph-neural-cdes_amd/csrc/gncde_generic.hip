@@ -836,15 +836,6 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
 }
 
 size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s) {
-  return generic_integrate_workspace_one(p, s);
-}
-
-int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats, char* ws,
-                      hipStream_t st) {
-  return generic_integrate_one(p, s, y0, ys, stats, ws, st);
-}
-
-size_t generic_integrate_workspace_one(const GncdeProblem& p, const GncdeSolver& s) {
   if (s.controller == GNCDE_CTRL_PID) return generic_pid_workspace(p);
   const size_t B = p.B, E = (size_t)p.n * state_dim(p);
   size_t sz = generic_vf_workspace(p);
@@ -853,8 +844,8 @@ size_t generic_integrate_workspace_one(const GncdeProblem& p, const GncdeSolver&
   return sz;
 }
 
-int generic_integrate_one(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
-                          int32_t* stats, char* ws, hipStream_t st) {
+int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
+                      char* ws, hipStream_t st) {
   if (s.controller == GNCDE_CTRL_PID) return generic_integrate_pid(p, s, y0, ys, stats, ws, st);
   if (s.controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
   const int B = p.B;

@@ -182,28 +182,6 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
 size_t generic_pid_workspace(const GncdeProblem& p);
 int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
                           char* ws, hipStream_t st);
-// ... as resumable pieces (set up, one evaluation + controller stage, completion poll, stats)
-constexpr int kPidPoll = 16;  // controller iterations between completion polls
-inline long pid_max_iterations(const GncdeSolver& s) { return 3L + 6L * (long)s.max_steps; }
-struct PidRun {
-  alignas(16) char args[256];  // the controller kernels' argument block (PidArgs, gncde_pid.hip)
-  GncdeProblem p;
-  char* ws;
-  hipStream_t st;
-  float *K, *tst;
-  int* active;
-  int h_active;  // written by the polling copy; read after the stream is synchronised
-};
-int pid_begin(PidRun& r, const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, char* ws,
-              hipStream_t st);
-int pid_iterate(PidRun& r);
-void pid_poll_enqueue(PidRun& r);
-void pid_end(PidRun& r, int32_t* stats);
-
-size_t generic_integrate_workspace_one(const GncdeProblem& p, const GncdeSolver& s);
-int generic_integrate_one(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
-                          char* ws, hipStream_t st);
-
 // reverse mode (discrete adjoint, GRID controller): gncde_vjp.hip
 size_t generic_vjp_workspace(const GncdeProblem& p, const GncdeSolver& s);
 // gstage (optional): [B, G-1, S, E] cotangents added to the stage values (gncde_integrate_vjp_ex)

@@ -35,13 +35,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x8u __attribute__((ext_vector_type(8), aligned(2)));  // 8 bf16 of an (I + Abar) plane row
 
 constexpr int kRows = 32;  // node rows per workgroup: two 16-row MFMA tiles
-#ifndef GNCDE_X_LSKIP  // diagnostic builds only: 1/2/3 skip the product MFMAs / the read-out MFMAs / the Z loads
-#define GNCDE_X_LSKIP 0
-#endif
-#ifndef GNCDE_X_SPLIT
-#define GNCDE_X_SPLIT 2
-#endif
-constexpr int kSplit = GNCDE_X_SPLIT;  // CDE read-out: workgroups per row block (channel groups)
+constexpr int kSplit = 2;  // CDE read-out: workgroups per row block (channel groups)
 
 struct LayerArgs {
   int n;
@@ -165,7 +159,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = e0 + 256 * u;
-        v[u] = (e < valid && GNCDE_X_LSKIP != 3) ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
+        v[u] = e < valid ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -289,8 +283,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
             }
         }
       };
-      if (GNCDE_X_LSKIP == 1) {
-      } else if (two)
+      if (two)
         mm(std::true_type{});
       else
         mm(std::false_type{});
@@ -382,8 +375,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         }
       }
     };
-    if (GNCDE_X_LSKIP == 2) {
-    } else if (two)
+    if (two)
       kloop(std::true_type{});
     else
       kloop(std::false_type{});

@@ -363,6 +363,19 @@ __global__ void k_pid_stats(int B, const PidState* __restrict__ st, int32_t* __r
   stats[b * 4 + GNCDE_STAT_STATUS] = st[b].status;
 }
 
+constexpr int kPidPoll = 16;  // controller iterations between completion polls
+inline long pid_max_iterations(const GncdeSolver& s) { return 3L + 6L * (long)s.max_steps; }
+
+struct PidRun {
+  PidArgs a;  // the controller kernels' argument block
+  GncdeProblem p;
+  char* ws;
+  hipStream_t st;
+  float *K, *tst;
+  int* active;
+  int h_active;  // written by the polling copy; read after the stream is synchronised
+};
+
 }  // namespace
 
 size_t generic_pid_workspace(const GncdeProblem& p) {
@@ -373,9 +386,10 @@ size_t generic_pid_workspace(const GncdeProblem& p) {
   return sz;
 }
 
-// The PID solve as resumable pieces: pid_begin sets up and launches the init, pid_iterate enqueues one batched
-// evaluation + one controller stage, pid_poll_enqueue copies how many samples are still running to the host,
-// pid_end writes the stats.
+namespace {
+
+// The PID solve in pieces: pid_begin sets up and launches the init, pid_iterate enqueues one batched evaluation + one
+// controller stage, pid_poll_enqueue copies how many samples are still running to the host, pid_end writes the stats.
 int pid_begin(PidRun& r, const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, char* ws,
               hipStream_t st) {
   if (s.method != GNCDE_TSIT5) return GNCDE_ERR_UNSUPPORTED;
@@ -388,8 +402,7 @@ int pid_begin(PidRun& r, const GncdeProblem& p, const GncdeSolver& s, const floa
     cur += align_up(bytes, 256);
     return ptr;
   };
-  PidArgs& a = *reinterpret_cast<PidArgs*>(r.args);
-  static_assert(sizeof(PidArgs) <= sizeof(r.args), "PidRun::args too small");
+  PidArgs& a = r.a;
   a = PidArgs{};
   a.B = B;
   a.E = (int)E;
@@ -424,7 +437,7 @@ int pid_begin(PidRun& r, const GncdeProblem& p, const GncdeSolver& s, const floa
 }
 
 int pid_iterate(PidRun& r) {
-  const PidArgs& a = *reinterpret_cast<const PidArgs*>(r.args);
+  const PidArgs& a = r.a;
   const int rc = generic_vf_eval(r.p, r.tst, a.yt, r.K, r.ws, r.st, true);
   if (rc) return rc;
   hipLaunchKernelGGL(k_pid_advance, dim3(a.B), dim3(kAdvThreads), 0, r.st, a);
@@ -432,16 +445,18 @@ int pid_iterate(PidRun& r) {
 }
 
 void pid_poll_enqueue(PidRun& r) {
-  const PidArgs& a = *reinterpret_cast<const PidArgs*>(r.args);
+  const PidArgs& a = r.a;
   (void)hipMemsetAsync(r.active, 0, sizeof(int), r.st);
   hipLaunchKernelGGL(k_pid_tst, dim3((a.B + 255) / 256), dim3(256), 0, r.st, a.B, a.state, r.tst, r.active);
   (void)hipMemcpyAsync(&r.h_active, r.active, sizeof(int), hipMemcpyDeviceToHost, r.st);
 }
 
 void pid_end(PidRun& r, int32_t* stats) {
-  const PidArgs& a = *reinterpret_cast<const PidArgs*>(r.args);
+  const PidArgs& a = r.a;
   if (stats) hipLaunchKernelGGL(k_pid_stats, dim3((a.B + 255) / 256), dim3(256), 0, r.st, a.B, a.state, stats);
 }
+
+}  // namespace
 
 int generic_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
                           char* ws, hipStream_t st) {

@@ -104,32 +104,36 @@ __global__ void v_norm_rows(size_t rows, int d, const float* __restrict__ Z, con
 // mode 0: X; mode 1: X * Y (elementwise).  Chunks of 128 rows, each thread's 32 rows loaded 8 at a time (all in
 // flight): with 1024-row chunks and a serial row loop a chunk was 256 dependent L2 round trips (55 us at config 5).
 constexpr int kChunk = 128;
+// Chunks beyond gridDim.y (max 65535) are walked by a block-stride loop, so any row count launches.
 __global__ void __launch_bounds__(256) v_colsum_part(size_t rows, int d, const float* __restrict__ X,
                                                      const float* __restrict__ Y, float* __restrict__ part) {
   const int j = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;  // 4 row groups
-  const size_t r0 = (size_t)blockIdx.y * kChunk;
+  const size_t chunks = (rows + kChunk - 1) / kChunk;
   __shared__ float red[4][64];
-  float s = 0.f;
-  if (j < d) {
-    for (int q0 = 0; q0 < kChunk / 4; q0 += 8) {
-      float x[8], y[8];
+  for (size_t c = blockIdx.y; c < chunks; c += gridDim.y) {
+    const size_t r0 = c * kChunk;
+    float s = 0.f;
+    if (j < d) {
+      for (int q0 = 0; q0 < kChunk / 4; q0 += 8) {
+        float x[8], y[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const size_t r = r0 + g + 4 * (size_t)(q0 + u);
-        const bool ok = r < rows;
-        x[u] = ok ? X[r * d + j] : 0.f;
-        y[u] = (ok && Y) ? Y[r * d + j] : 1.f;
+        for (int u = 0; u < 8; ++u) {
+          const size_t r = r0 + g + 4 * (size_t)(q0 + u);
+          const bool ok = r < rows;
+          x[u] = ok ? X[r * d + j] : 0.f;
+          y[u] = (ok && Y) ? Y[r * d + j] : 1.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += Y ? x[u] * y[u] : x[u];
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += Y ? x[u] * y[u] : x[u];
     }
+    red[g][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (g == 0 && j < d)
+      part[c * d + j] = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    __syncthreads();
   }
-  red[g][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (g == 0 && j < d)
-    part[(size_t)blockIdx.y * d + j] = (red[0][threadIdx.x] + red[1][threadIdx.x]) +
-                                       (red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 __global__ void v_colsum_final(int chunks, int d, const float* __restrict__ part, float* __restrict__ out) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -453,7 +457,8 @@ void carve(const GncdeProblem& p, char* ws, VjpWs& w, size_t* bytes) {
 // out[j] += column sums of X (or X .* Y) over `rows` rows (fixed order)
 void colsum(size_t rows, int d, const float* X, const float* Y, float* part, float* out, hipStream_t st) {
   const unsigned chunks = cdiv(rows, kChunk);
-  hipLaunchKernelGGL(v_colsum_part, dim3(cdiv(d, 64), chunks), dim3(256), 0, st, rows, d, X, Y, part);
+  hipLaunchKernelGGL(v_colsum_part, dim3(cdiv(d, 64), chunks < 65535u ? chunks : 65535u), dim3(256), 0, st, rows, d,
+                     X, Y, part);
   hipLaunchKernelGGL(v_colsum_final, dim3(cdiv(d, 256)), dim3(256), 0, st, (int)chunks, d, part, out);
 }
 

@@ -12,11 +12,12 @@ from ctypes import POINTER, c_char_p, c_float, c_int32, c_size_t, c_void_p
 
 MAX_LAYERS = 8
 FC = 24
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 RK4, TSIT5 = 0, 1
 CTRL_GRID, CTRL_PID = 0, 1
 SAVE_T1, SAVE_STEPS, SAVE_TS = 0, 1, 2
+FLAG_GENERIC = 1  # GncdeSolver.flags: force the generic forward and reverse sweep
 COMPUTE_FP32, COMPUTE_BF16, COMPUTE_BF16_STORAGE = 0, 1, 2  # GncdeProblem.compute (gncde.h)
 STAT_STEPS, STAT_REJECTS, STAT_EVALS, STAT_STATUS = 0, 1, 2, 3
 STATUS_OK, STATUS_MAX_STEPS, STATUS_NONFINITE, STATUS_STEP_RECORD = 0, 1, 2, 3
@@ -87,6 +88,8 @@ class GncdeSolver(ctypes.Structure):
         ("step_ts", c_void_p),
         ("step_ts_len", c_int32),
         ("stage_rec", c_void_p),
+        ("stage_rec_len", ctypes.c_int64),
+        ("flags", c_int32),
     ]
 
 

@@ -34,7 +34,7 @@ def with_stage_record(prob: engine.Problem, spec: engine.SolverSpec, want: bool 
     floats = engine.stage_record_floats(prob, spec)
     if floats == 0 or prob.B == 0:
         return spec
-    free, _ = torch.cuda.mem_get_info()
+    free, _ = torch.cuda.mem_get_info(prob.params.device)
     if prob.B * floats * 4 > STAGE_RECORD_SHARE * free:
         return spec
     return dataclasses.replace(spec, stage_rec=torch.empty(prob.B, floats, dtype=torch.float32,
@@ -43,12 +43,12 @@ def with_stage_record(prob: engine.Problem, spec: engine.SolverSpec, want: bool 
 
 class _FixedGridSolve(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y0, params, fusion, data_coef, prob, spec):
+    def forward(ctx, y0, params, fusion, data_coef, prob, spec, record):
         p = dataclasses.replace(prob, params=params.detach().to(torch.float32).contiguous(),
                                 fusion=fusion.detach().to(torch.float32).contiguous())
         if data_coef is not None:
             p = dataclasses.replace(p, data_coef=data_coef.detach().to(torch.float32).contiguous())
-        steps = with_stage_record(p, dataclasses.replace(spec, save_mode=_lib.SAVE_STEPS, stage_rec=None))
+        steps = with_stage_record(p, dataclasses.replace(spec, save_mode=_lib.SAVE_STEPS, stage_rec=None), record)
         ys = engine.integrate(p, steps, y0.detach())
         ctx.prob, ctx.spec = p, dataclasses.replace(spec, stage_rec=steps.stage_rec)
         ctx.dtypes = (y0.dtype, params.dtype, fusion.dtype)
@@ -66,7 +66,7 @@ class _FixedGridSolve(torch.autograd.Function):
         else:
             gy0, gp, gf = engine.integrate_vjp(ctx.prob, ctx.spec, ys, g)
         d0, dp, df = ctx.dtypes
-        return gy0.to(d0), gp.to(dp), gf.to(df), gdata, None, None
+        return gy0.to(d0), gp.to(dp), gf.to(df), gdata, None, None, None
 
 
 def tsit5_dense_weights(theta: torch.Tensor) -> torch.Tensor:
@@ -150,7 +150,7 @@ class _PidSolve(torch.autograd.Function):
         dense = spec.save_mode == _lib.SAVE_TS
         grid, nst = pid_replay_grid(rec, ns, pad=1 if dense else 0)
         steps = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_STEPS, grid=grid,
-                                  nsteps=nst)
+                                  nsteps=nst, flags=spec.flags)
         want_data = ctx.needs_input_grad[3]
         steps = with_stage_record(ctx.prob, steps)
         ys = engine.integrate(ctx.prob, steps, y0)  # the checkpoints (and stage inputs): the accepted steps replayed
@@ -174,13 +174,15 @@ def solve(prob: engine.Problem, spec: engine.SolverSpec, y0: torch.Tensor, param
     in-forward spline of the embedded data)."""
     params = prob.params if params is None else params
     fusion = prob.fusion if fusion is None else fusion
+    # the forward's stage record only pays when a backward will read it
+    record = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (y0, params, fusion, data_coef))
     if spec.controller == _lib.CTRL_PID:
         if spec.method != _lib.TSIT5 or spec.save_mode not in (_lib.SAVE_T1, _lib.SAVE_TS):
             raise _lib.GncdeError("differentiable adaptive solve: Tsit5 with SAVE_T1 or SAVE_TS")
         return _PidSolve.apply(y0, params, fusion, data_coef, prob, spec)
     if spec.save_mode not in (_lib.SAVE_T1, _lib.SAVE_STEPS):
         raise _lib.GncdeError("differentiable fixed-grid solve: save_mode must be SAVE_T1 or SAVE_STEPS")
-    return _FixedGridSolve.apply(y0, params, fusion, data_coef, prob, spec)
+    return _FixedGridSolve.apply(y0, params, fusion, data_coef, prob, spec, record)
 
 
 class _Hermite(torch.autograd.Function):

@@ -10,9 +10,10 @@ ConstantStepSize controller, per sample, one solve per event segment of the time
 the previous segment's LAST saved state (gen_all_data's hand-over: the state jumps unchanged across the gap between
 the last time of one segment and the first of the next).  It runs batched in float64 torch on the device (data
 generation, not the hot path).  The graph operators and spline coefficients go through the engine's kernels
-(``gncde_graph_operator``, ``gncde_hermite_coefficients``) straight into the engine layout.  networkx is not
-installed: the community graph is a 4-block stochastic block model with the reference's block sizes
-(n/3, n/3, n/4, rest) and probabilities (0.25 inside, 0.01 across), ode_dataset.py:189-202.
+(``gncde_graph_operator``, ``gncde_hermite_coefficients``) straight into the engine layout.  Community graphs are
+the reference's own (ode_dataset.py:189-202): ``networkx.random_partition_graph([n/3, n/3, n/4, rest], 0.25, 0.01,
+seed=seed + i)`` for sample i, reordered by ``networkx_reorder_nodes(G, layout)`` (data_tools.py:32-72; the dyn
+YAMLs set ``layout: community``, greedy-modularity order).
 """
 from __future__ import annotations
 
@@ -45,6 +46,7 @@ class DynDataCfg:
     padding_mode: str = "same"
     interpolation: str = "cubic"
     amp_range: tuple = (1.0, 1.0)
+    layout: str | None = None  # node reordering of generated graphs: "community" | "degree" | None (data_tools.py:32)
     dt0: float = 0.01  # dataset_configs.py:74 (ConstantStepSize step of the ground-truth solve)
 
     @classmethod
@@ -65,13 +67,35 @@ def grid_8_neighbor_graph(N: int) -> np.ndarray:
     return A
 
 
-def community_graph(n: int, rng: np.random.Generator) -> np.ndarray:
-    sizes = [n // 3, n // 3, n // 4]
-    sizes.append(n - sum(sizes))
-    block = np.repeat(np.arange(4), sizes)
-    p = np.where(block[:, None] == block[None, :], 0.25, 0.01)
-    up = np.triu(rng.random((n, n)) < p, 1).astype(float)
-    return up + up.T
+def reorder_nodes(G, kind=None):
+    """networkx_reorder_nodes (data_tools.py:55-72) with generate_node_mapping (:32-52): a label -> position map by
+    descending degree ("degree") or greedy-modularity community ("community"); None keeps G.  The reference applies
+    that map to the COO row / column POSITIONS of nx.to_scipy_sparse_array(G) (positions in G's node order, which
+    for random_partition_graph is not sorted), i.e. a position is looked up as if it were a label; that quirk is
+    kept, since it decides which adjacency the model sees."""
+    import networkx as nx
+    import scipy.sparse as sp
+    if kind == "degree":
+        order = [v for v, _ in sorted(G.degree, key=lambda x: x[1], reverse=True)]
+    elif kind == "community":
+        order = [v for c in nx.community.greedy_modularity_communities(G) for v in c]
+    else:
+        return G
+    pos = {v: i for i, v in enumerate(order)}
+    C = nx.to_scipy_sparse_array(G, format="coo")
+    remap = np.vectorize(lambda x: pos[int(x)], otypes=[np.int64])
+    return nx.from_scipy_sparse_array(sp.coo_matrix((C.data, (remap(C.row), remap(C.col))), shape=C.shape))
+
+
+def community_graph(n: int, seed: int, layout_kind=None) -> np.ndarray:
+    """ODEDataset._gen_community_graph for one sample (ode_dataset.py:189-202): four blocks of n/3, n/3, n/4 and
+    the rest nodes, edge probability 0.25 inside a block and 0.01 across, networkx's generator with this seed
+    (the reference passes seed + i for sample i), then the layout reordering.  Dense [n, n] float adjacency."""
+    import networkx as nx
+    n1, n2, n3 = int(n / 3), int(n / 3), int(n / 4)
+    G = nx.random_partition_graph([n1, n2, n3, n - n1 - n2 - n3], 0.25, 0.01, seed=seed)
+    G = reorder_nodes(G, layout_kind)
+    return np.array(nx.to_numpy_array(G), dtype=float)
 
 
 def events_happen_time(rng, t: np.ndarray, event_times: int, split_ratio, all_dynamic: bool):
@@ -231,7 +255,7 @@ class DynDataset:
             self.N = int(math.ceil(math.sqrt(cfg.num_nodes)))
             base = np.tile(grid_8_neighbor_graph(self.N)[None], (B, 1, 1))
         elif cfg.graph_type == "community":
-            base = np.stack([community_graph(cfg.num_nodes, rng) for _ in range(B)])
+            base = np.stack([community_graph(cfg.num_nodes, cfg.seed + i, cfg.layout) for i in range(B)])
             self.N = None
         else:
             raise NotImplementedError(f"graph_type {cfg.graph_type}: grid and community are generated here")
@@ -368,7 +392,7 @@ def synthetic_snapshots(name: str, rng: np.random.Generator, num_snapshots: int 
     """Snapshot sequence (list of dicts adj [n,n], x, y, src) shaped like the reference's datasets."""
     if name.startswith("england"):
         n, S, F = 129, num_snapshots or 61, 8
-        base = community_graph(n, rng)
+        base = community_graph(n, int(rng.integers(1 << 30)))
         signal = np.abs(rng.standard_normal(n)) * 10.0
         hist = [signal.copy() for _ in range(F)]
         snaps = []

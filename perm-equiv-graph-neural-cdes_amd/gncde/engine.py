@@ -173,6 +173,7 @@ class SolverSpec:
     step_ts: torch.Tensor | None = None  # PID: OUTPUT [B, cap] accepted step times (t0 first), filled by integrate
     # GRID: stage record [B, stage_record_floats(prob, solver)] written by integrate, read by integrate_vjp
     stage_rec: torch.Tensor | None = None
+    flags: int = 0  # GNCDE_FLAG_* (FLAG_GENERIC: the generic forward and reverse sweep even where fused kernels fit)
 
     def c_struct(self) -> _lib.GncdeSolver:
         s = _lib.GncdeSolver()
@@ -197,13 +198,15 @@ class SolverSpec:
                     and self.stage_rec.is_contiguous() and self.stage_rec.dim() == 2):
                 raise _lib.GncdeError("SolverSpec.stage_rec must be a contiguous fp32 CUDA tensor [B, floats]")
             s.stage_rec = _ptr(self.stage_rec).value
+            s.stage_rec_len = int(self.stage_rec.shape[1])
+        s.flags = int(self.flags)
         return s
 
     def shard(self, start, stop):
         cut = lambda x: None if x is None else x[start:stop]  # noqa: E731
         return SolverSpec(self.method, self.controller, self.save_mode, cut(self.grid), cut(self.nsteps),
                           self.rtol, self.atol, self.max_steps, cut(self.t0), cut(self.t1), cut(self.dt0),
-                          cut(self.save_ts), cut(self.step_ts), cut(self.stage_rec))
+                          cut(self.save_ts), cut(self.step_ts), cut(self.stage_rec), self.flags)
 
 
 def stage_record_floats(prob: Problem, solver: SolverSpec) -> int:

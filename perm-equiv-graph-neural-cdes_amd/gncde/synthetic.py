@@ -34,16 +34,12 @@ def grid_adjacency(side: int, device="cuda") -> torch.Tensor:
     return A
 
 
-def community_adjacency(n: int, communities: int = 4, p_in: float = 0.3, p_out: float = 0.02, seed: int = 1234,
-                        device="cuda") -> torch.Tensor:
-    """Undirected stochastic-block graph on exactly n nodes (the gene-dynamics ``graph_type: community``
-    shape of SURVEY §8d C4; networkx is not used)."""
-    g = torch.Generator().manual_seed(seed)
-    block = torch.arange(n) * communities // n
-    same = block[:, None] == block[None, :]
-    p = torch.where(same, torch.tensor(p_in), torch.tensor(p_out))
-    up = torch.triu((torch.rand(n, n, generator=g) < p).float(), diagonal=1)
-    return (up + up.T).to(device)
+def community_adjacency(n: int, seed: int = 1234, device="cuda") -> torch.Tensor:
+    """The reference's community graph on exactly n nodes (the gene-dynamics ``graph_type: community`` of
+    SURVEY §8d C4): networkx.random_partition_graph([n/3, n/3, n/4, rest], 0.25, 0.01, seed) in the community
+    layout (ode_dataset.py:189-202, data.community_graph)."""
+    from .data import community_graph
+    return torch.tensor(community_graph(n, seed, "community"), dtype=torch.float32, device=device)
 
 
 def normalized_laplacian(A: torch.Tensor) -> torch.Tensor:

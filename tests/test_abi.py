@@ -44,9 +44,10 @@ def test_struct_layout_matches_c(tmp_path):
 #include <stddef.h>
 #include "{HEADER}"
 int main(void) {{
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(GncdeProblem), offsetof(GncdeProblem, ts),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(GncdeProblem), offsetof(GncdeProblem, ts),
          offsetof(GncdeProblem, params), sizeof(GncdeSolver), offsetof(GncdeSolver, save_ts),
-         offsetof(GncdeSolver, step_ts), offsetof(GncdeSolver, step_ts_len), offsetof(GncdeSolver, stage_rec));
+         offsetof(GncdeSolver, step_ts), offsetof(GncdeSolver, step_ts_len), offsetof(GncdeSolver, stage_rec),
+         offsetof(GncdeSolver, stage_rec_len), offsetof(GncdeSolver, flags));
   return 0;
 }}''')
     exe = tmp_path / "layout"
@@ -54,7 +55,8 @@ int main(void) {{
     vals = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
     P, S = _lib.GncdeProblem, _lib.GncdeSolver
     assert vals == [ctypes.sizeof(P), P.ts.offset, P.params.offset, ctypes.sizeof(S), S.save_ts.offset,
-                    S.step_ts.offset, S.step_ts_len.offset, S.stage_rec.offset]
+                    S.step_ts.offset, S.step_ts_len.offset, S.stage_rec.offset, S.stage_rec_len.offset,
+                    S.flags.offset]
 
 
 def _fake_problem(B=4, n=64, T=10, dims=(16, 16, 16, 16)):
@@ -86,6 +88,12 @@ def test_path_selection_and_workspace():
     assert lib.gncde_integrate_path(ctypes.byref(p2), ctypes.byref(s), buf, 64) == 0
     assert buf.value == b"generic"
     assert lib.gncde_workspace_bytes(ctypes.byref(p2), ctypes.byref(s)) > 0
+    s.flags = _lib.FLAG_GENERIC  # forced generic path: same problem, a workspace, both sweeps sized generic
+    assert lib.gncde_integrate_path(ctypes.byref(p), ctypes.byref(s), buf, 64) == 0
+    assert buf.value == b"generic"
+    assert lib.gncde_workspace_bytes(ctypes.byref(p), ctypes.byref(s)) > 0
+    s.flags = 4  # unknown flag bits are refused
+    assert lib.gncde_integrate_path(ctypes.byref(p), ctypes.byref(s), buf, 64) == 1
 
 
 @pytest.mark.parametrize("mutate,code", [
@@ -121,3 +129,19 @@ def test_stage_record_floats():
     bad = _fake_problem()
     bad.T = 1
     assert f(bad, _fake_solver()) == 0
+
+
+def test_stage_record_length_is_checked():
+    """A stage record whose length is not gncde_stage_record_floats() is refused (GNCDE_ERR_ARG) by the forward
+    (and, through the same validation, the reverse mode) instead of being written / read out of bounds."""
+    lib = _lib.load()
+    p, s = _fake_problem(), _fake_solver()
+    buf = ctypes.create_string_buffer(64)
+    s.stage_rec = 0x2000
+    for length, code in ((100 * 3 * 64 * 16, 0), (100 * 3 * 64 * 16 - 1, 1), (0, 1)):
+        s.stage_rec_len = length
+        assert lib.gncde_integrate_path(ctypes.byref(p), ctypes.byref(s), buf, 64) == code, length
+    bf = _fake_problem()
+    bf.compute = _lib.COMPUTE_BF16  # no record exists for the bf16 modes
+    s.stage_rec_len = 100 * 3 * 64 * 16
+    assert lib.gncde_integrate_path(ctypes.byref(bf), ctypes.byref(s), buf, 64) == 1

@@ -1,5 +1,7 @@
 """CPU: the dataset restatement's host logic — config parsing, event indices, split,
 padding by events — against the reference rules (ode_dataset.py, data_tools.py, dataset_configs.py)."""
+import os
+
 import numpy as np
 
 from gncde import data
@@ -83,3 +85,22 @@ def test_dynamic_ground_truth_hands_over_between_event_segments():
         assert np.array_equal(y[:, e], y[:, e - 1])
     inside = [j for j in range(1, y.shape[1]) if j not in set(ev)]
     assert any(not np.array_equal(y[:, j], y[:, j - 1]) for j in inside)
+
+
+def test_community_graph_matches_reference_generator():
+    """data.community_graph restates ODEDataset._gen_community_graph (ode_dataset.py:189-202) + the layout
+    reordering (data_tools.py:32-72): pinned against tests/golden/community_graphs.npz, which
+    tests/golden/make_community.py wrote from networkx directly (the reference's own call sequence)."""
+    import networkx as nx
+    from gncde import data
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "community_graphs.npz"))
+    assert str(z["networkx_version"]) == nx.__version__
+    for key in z.files:
+        if not key.startswith("A_"):
+            continue
+        _, n, seed, lay = key.split("_")
+        n, seed = int(n[1:]), int(seed[1:])
+        want = np.unpackbits(z[key])[:n * n].reshape(n, n).astype(float)
+        got = data.community_graph(n, seed, None if lay == "None" else lay)
+        assert np.array_equal(got, want), key
+        assert np.array_equal(got, got.T) and not np.any(np.diag(got))
