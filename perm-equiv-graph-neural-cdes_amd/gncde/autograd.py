@@ -138,6 +138,8 @@ class _PidSolve(torch.autograd.Function):
         ys, st = engine.integrate(p, dataclasses.replace(spec, step_ts=rec), y0.detach(), stats=True)
         if torch.any(st[:, _lib.STAT_STATUS] != 0):
             raise _lib.GncdeError("adaptive solve failed (max_steps reached or non-finite error estimate)")
+        if spec.stats_out is not None:
+            spec.stats_out.copy_(st)
         ctx.prob, ctx.spec = p, spec
         ctx.dtypes = (y0.dtype, params.dtype, fusion.dtype)
         ctx.save_for_backward(y0.detach().to(torch.float32).contiguous(), rec, st[:, _lib.STAT_STEPS].contiguous())

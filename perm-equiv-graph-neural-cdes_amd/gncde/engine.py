@@ -88,6 +88,14 @@ class Problem:
                        data_coef=None if self.data_coef is None else self.data_coef[start:stop],
                        cde_hidden=self.cde_hidden, cde_embed=self.cde_embed, compute=self.compute)
 
+    def take(self, idx) -> "Problem":
+        """The samples ``idx`` (any order) as their own Problem (a data-parallel rank's balanced shard)."""
+        ix = torch.as_tensor(idx, dtype=torch.long, device=self.ts.device)
+        return Problem(ts=self.ts[ix].contiguous(), coef=self.coef[ix].contiguous(), tcoef=self.tcoef[ix].contiguous(),
+                       fusion=self.fusion, params=self.params, dims=list(self.dims),
+                       data_coef=None if self.data_coef is None else self.data_coef[ix].contiguous(),
+                       cde_hidden=self.cde_hidden, cde_embed=self.cde_embed, compute=self.compute)
+
     def with_compute(self, compute: str) -> "Problem":
         """The same problem in another arithmetic ("fp32" | "bf16" | "bf16_storage": coefficients cast here)."""
         mode = COMPUTE_MODES[compute]
@@ -174,6 +182,9 @@ class SolverSpec:
     # GRID: stage record [B, stage_record_floats(prob, solver)] written by integrate, read by integrate_vjp
     stage_rec: torch.Tensor | None = None
     flags: int = 0  # GNCDE_FLAG_* (FLAG_GENERIC: the generic forward and reverse sweep even where fused kernels fit)
+    # host side only (not in GncdeSolver): autograd.solve copies the forward's stats [B, 4] here when given (the
+    # trainers balance data-parallel shards by the adaptive solves' accepted step counts)
+    stats_out: torch.Tensor | None = None
 
     def c_struct(self) -> _lib.GncdeSolver:
         s = _lib.GncdeSolver()

@@ -249,9 +249,14 @@ class PGTGraphNeuralCDE(nn.Module):
 class TGBGraphNeuralCDE(nn.Module):
     """``tgb_graph_neural_cde.py:13-171``: data spline built inside forward from Linear(n -> de) embeddings
     of the adjacency rows, Linear(n -> h) encoder, CDEWrapper(vf), Tsit5 + ConstantStepSize(dt0 = 0.01),
-    Linear(h -> n) decoder per node."""
+    Linear(h -> n) decoder per node.
 
-    def __init__(self, cfg, vector_field, interpolation="cubic", model_key=None, dt0=0.01, **kwargs):
+    ``solver="pid"`` (build extension, BASELINE config 5's "adaptive Tsit5 solver") replaces ConstantStepSize with
+    the dyn model's controller, PIDController(rtol 1e-3, atol 1e-6) with dt0 = None (graph_neural_cde.py:53-54,
+    94-104), differentiated on each window's accepted steps; ``last_steps`` then holds every window's accepted
+    step count of the latest forward (the data-parallel trainer balances ranks by it)."""
+
+    def __init__(self, cfg, vector_field, interpolation="cubic", model_key=None, dt0=0.01, solver=None, **kwargs):
         super().__init__()
         self.cfg = _cfg(cfg, hidden_dim=32, method="Tsit5", return_sequence=False, use_mlps=False)
         if getattr(self.cfg, "use_mlps", False):
@@ -266,6 +271,10 @@ class TGBGraphNeuralCDE(nn.Module):
         self.data_encoder = _linear(n, de, g)
         self.wrapped_vector_field = vector_fields.CDEWrapperVectorField(vector_field, self.cfg.hidden_dim)
         self.dt0 = dt0
+        if solver not in (None, "constant", "pid"):
+            raise ValueError(f"solver {solver!r}: None / 'constant' (ConstantStepSize) or 'pid'")
+        self.adaptive = solver == "pid"
+        self.last_steps = None
 
     def batched(self, ts, coeffs_adj, x_data, x0, start_time=None, evolving_out=False):
         if evolving_out:
@@ -280,15 +289,27 @@ class TGBGraphNeuralCDE(nn.Module):
         data_coef = autograd.hermite_coefficients(ts_d, X) if grad else engine.hermite_coefficients(ts_d, X)
         y0 = _affine(self.encoder, torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device))
         prob = self.wrapped_vector_field.problem(control_adj, None, data_coef=data_coef.detach())
-        grids = [layout.constant_step_grid(t[0], t[-1], self.dt0) for t in ts_d.cpu().numpy()]
-        grid, ns = layout.stack_grids(grids, device=ts_d.device)
-        spec = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_T1, grid=grid,
-                                 nsteps=ns)
+        if self.adaptive:
+            spec = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_PID, save_mode=_lib.SAVE_T1, rtol=1e-3,
+                                     atol=1e-6, t0=ts_d[:, 0].contiguous(), t1=ts_d[:, -1].contiguous(),
+                                     stats_out=torch.zeros(ts_d.shape[0], 4, dtype=torch.int32, device=ts_d.device))
+        else:
+            grids = [layout.constant_step_grid(t[0], t[-1], self.dt0) for t in ts_d.cpu().numpy()]
+            grid, ns = layout.stack_grids(grids, device=ts_d.device)
+            spec = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_T1, grid=grid,
+                                     nsteps=ns)
         if grad:  # differentiable: discrete adjoint incl. the data spline -> data_encoder
             params, fusion = self.vector_field.diff_tensors(prob.n, ts_d.device)
             ys = autograd.solve(prob, spec, y0, params, fusion, data_coef=data_coef)
+        elif self.adaptive:
+            ys, st = engine.integrate(prob, spec, y0, stats=True)
+            if torch.any(st[:, _lib.STAT_STATUS] != 0):
+                raise RuntimeError("diffrax-equivalent failure: max_steps reached or non-finite state")
+            spec.stats_out.copy_(st)
         else:
             ys = engine.integrate(prob, spec, y0)
+        if self.adaptive:
+            self.last_steps = spec.stats_out[:, _lib.STAT_STEPS]
         return _affine(self.decoder, ys)
 
     def loss_terms(self, ts, coeffs_adj, x_data, x0, labels, source_mask):

@@ -5,6 +5,10 @@ systems); ``WindowTrainer`` drives pgt_graph_neural_cde / tgb_graph_neural_cde o
 
     python -m gncde.run --config <reference>/configs/dynamical_systems/perm_equiv_gncde_config.yaml \\
                         [--epochs N] [--steps-per-interval M] [--out metrics.jsonl]
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m gncde.run --config ...
+
+Under torch.distributed.run every rank owns one GPU and a share of the samples (dyn: balanced by the adaptive
+solves' step counts; pgt/tgb: the windows of each optimiser step), with one gradient all-reduce per step.
 
 Flow (trainer.py:88-285): build the dataset (gncde.data, f2), the vector field by registry name
 (vector_field_configs.py:52) and GraphNeuralCDE (model_configs.py:46-59); full-batch training steps
@@ -59,6 +63,8 @@ class Trainer:
         self.model_cfg = m
 
     def _log(self, rec: dict):
+        if train.dist_world()[0] != 0:  # rank 0 speaks for the job
+            return
         line = json.dumps(rec)
         print(line, flush=True)
         if self.out:
@@ -80,6 +86,7 @@ class Trainer:
 
     def run(self) -> dict:
         ds, model = self.build()
+        rank, world = train.dist_world()
         opt_cfg = self.cfg.get("optimiser", {})
         sched = opt_cfg.get("schedule", {"name": "constant_schedule", "value": 1e-3})
         if sched.get("name", "constant_schedule") != "constant_schedule":
@@ -90,14 +97,49 @@ class Trainer:
         # training control over the training knots (the reference's train_graph_path_coeffs), validation over all
         ts_tr, coef_tr, tcoef_tr = ds.graph_path(ds.id_train)
         ts_all, coef_all, tcoef_all = ds.graph_path(list(range(ds.t.shape[1])))
-        y_tr = ds.true_y[:, torch.as_tensor(ds.id_train, device=ds.true_y.device)]
-        prob_tr = model.vector_field.problem_from_layout(ts_tr, coef_tr, tcoef_tr)
-        spec_tr = model._spec(ts_tr, evolving_out=True)
-        x0 = ds.x0
+        y_tr_all = ds.true_y[:, torch.as_tensor(ds.id_train, device=ds.true_y.device)]
+        prob_tr_all = model.vector_field.problem_from_layout(ts_tr, coef_tr, tcoef_tr)
+        prob_all_full = model.vector_field.problem_from_layout(ts_all, coef_all, tcoef_all)
+        B = prob_tr_all.B
+        adaptive = model.solver is None  # the reference's Tsit5 + PID solve: per-sample step counts differ
+
+        # Data parallelism: each rank owns a set of samples; the step all-reduces the gradient of the
+        # summed loss once (train.make_step), so the update equals the reference's full-batch step
+        # (trainer.py:288-327, loss_configs.py:44-47).  Adaptive solves rebalance the sets by the previous epoch's
+        # accepted step counts (balanced_partition) when the ranks' work differs by more than 10 %.
+        def shard(own):
+            st = dict(own=list(own))
+            st["prob"] = prob_tr_all.take(own) if world > 1 else prob_tr_all
+            st["x0"] = ds.x0[torch.as_tensor(own, device=ds.x0.device)] if world > 1 else ds.x0
+            st["y"] = y_tr_all[torch.as_tensor(own, device=y_tr_all.device)] if world > 1 else y_tr_all
+            st["spec"] = model._spec(st["prob"].ts, evolving_out=True)
+            if adaptive:
+                st["spec"].stats_out = torch.zeros(len(own), 4, dtype=torch.int32, device=ds.x0.device)
+            return st
+
+        parts = [list(range(*train.shard_range(B, r, world))) for r in range(world)]  # every rank's samples
+        sh = shard(parts[rank])
 
         def loss_terms():
-            pred = model.predict_packed(prob_tr, x0, spec_tr).squeeze(-1)
-            return ((pred - y_tr) ** 2).sum(), pred.numel()
+            pred = model.predict_packed(sh["prob"], sh["x0"], sh["spec"]).squeeze(-1)
+            return ((pred - sh["y"]) ** 2).sum(), pred.numel()
+
+        def validate():
+            """interpolation / extrapolation MSE over all samples (each rank its own, summed over ranks)."""
+            own = sh["own"]
+            with torch.no_grad():
+                pa = prob_all_full.take(own) if world > 1 else prob_all_full
+                pred = model.forward_packed(pa, sh["x0"], pa.ts).squeeze(-1)  # PID, SaveAt(ts)
+            yt = ds.true_y[torch.as_tensor(own, device=ds.true_y.device)] if world > 1 else ds.true_y
+            sums = []
+            for ids in (ds.id_test_inter or ds.id_test_extra, ds.id_test_extra):
+                if ids:
+                    sel = torch.as_tensor(ids, device=pred.device)
+                    sums += [float(((pred[:, sel] - yt[:, sel]) ** 2).sum()), pred[:, sel].numel()]
+                else:
+                    sums += [float("nan"), 0.0]
+            v_s, v_c, e_s, e_c = train.all_reduce_sum(sums, pred.device)
+            return (v_s / v_c if v_c else float("nan")), (e_s / e_c if e_c else float("nan"))
 
         best, best_epoch, corr_test, bad = float("inf"), -1, float("nan"), 0
         ckpt_dir = self.cfg.get("checkpoint_dir", ".checkpoints/")
@@ -107,21 +149,25 @@ class Trainer:
             loss, mg, mu = train.make_step(opt, loss_terms)
             torch.cuda.synchronize()
             step_time = time.time() - t0
+            if adaptive and world > 1:
+                steps = sh["spec"].stats_out[:, _lib.STAT_STEPS].tolist()
+                costs = train.global_costs(sh["own"], steps, B, ds.x0.device)
+                loads = [sum(costs[i] for i in p) for p in parts]
+                if max(loads) > 1.1 * max(min(loads), 1.0):
+                    parts = train.balanced_partition(costs, world)
+                    sh = shard(parts[rank])
             if epoch % self.log_freq == 0:
                 self._log({"epoch": epoch + 1, "train_loss": float(loss), "train_step_time": step_time,
                            "max_grad": float(mg), "max_update": float(mu)})
             if (epoch + 1) % self.eval_freq == 0 or epoch + 1 == self.epochs:
-                with torch.no_grad():
-                    prob_all = model.vector_field.problem_from_layout(ts_all, coef_all, tcoef_all)
-                    pred = model.forward_packed(prob_all, x0, ts_all).squeeze(-1)  # PID, SaveAt(ts)
-                val = _mse(pred, ds.true_y, ds.id_test_inter or ds.id_test_extra)
-                extra = _mse(pred, ds.true_y, ds.id_test_extra)
+                val, extra = validate()
                 self._log({"epoch": epoch + 1, "validation_loss": val, "test_loss_extra": extra})
                 if val < best:
                     best, best_epoch, corr_test, bad = val, epoch + 1, extra, 0
-                    os.makedirs(ckpt_dir, exist_ok=True)
-                    from safetensors.torch import save_file
-                    save_file({k: v.detach().cpu().contiguous() for k, v in model.state_dict().items()}, ckpt)
+                    if rank == 0:
+                        os.makedirs(ckpt_dir, exist_ok=True)
+                        from safetensors.torch import save_file
+                        save_file({k: v.detach().cpu().contiguous() for k, v in model.state_dict().items()}, ckpt)
                 else:
                     bad += self.eval_freq
                     if epoch + 1 >= self.min_epochs and bad >= self.patience:
@@ -130,7 +176,6 @@ class Trainer:
                "checkpoint": ckpt}
         self._log(res)
         return res
-
 
 class WindowTrainer:
     """Mirror of trainer_pgt.Trainer (trainer_pgt.py:140-316) and trainer_tgb.Trainer (trainer_tgb.py:150-307)
@@ -172,7 +217,10 @@ class WindowTrainer:
         vf = cls(input_dim=h, hidden_dim=int(vfc.get("hidden_dim", h)), output_dim=h * de * 2,
                  num_layers=int(vfc.get("num_layers", 2)), data_embed_dim=de, num_nodes=ds.n, key=self.seed)
         if self.tgb:
-            model = TGBGraphNeuralCDE(m, vf, m.get("interpolation", "cubic"), self.seed)
+            # build-only model key `solver: pid` (BASELINE config 5's adaptive Tsit5); absent: the reference's
+            # ConstantStepSize(0.01)
+            model = TGBGraphNeuralCDE({k: v for k, v in m.items() if k != "solver"}, vf, m.get("interpolation", "cubic"),
+                                      self.seed, solver=m.get("solver"))
         else:
             model = PGTGraphNeuralCDE(m, vf, m.get("interpolation", "cubic"), self.seed)
         return ds, model.to("cuda")
@@ -181,12 +229,14 @@ class WindowTrainer:
         return [starts[i:i + size] for i in range(0, len(starts), size)]
 
     def _evaluate(self, model, ds, starts):
-        """(mean loss, mean NDCG@10 or nan) over windows, one window at a time like the reference loader."""
+        """(mean loss, mean NDCG@10 or nan) over windows, one window at a time like the reference loader; with
+        data parallelism each rank evaluates every world-th window and the sums are all-reduced."""
         if len(starts) == 0:
             return float("nan"), float("nan")
+        rank, world = train.dist_world()
         loss, ndcg = 0.0, 0.0
         with torch.no_grad():
-            for s in starts:
+            for s in list(starts)[rank::world]:
                 b = ds.batch([s])
                 if self.tgb:
                     ce, cnt = model.loss_terms(*b)
@@ -197,6 +247,7 @@ class WindowTrainer:
                 else:
                     sse, cnt = model.loss_terms(*b)
                     loss += float(sse) / cnt
+        loss, ndcg = train.all_reduce_sum([loss, ndcg], "cuda")
         return loss / len(starts), (ndcg / len(starts) if self.tgb else float("nan"))
 
     def run(self) -> dict:
@@ -209,7 +260,23 @@ class WindowTrainer:
         opt = train.ClipAdamW(model, learning_rate=float(sched.get("value", 1e-3)),
                               weight_decay=float(opt_cfg.get("weight_decay", 0.0)),
                               gradient_clipping=bool(opt_cfg.get("gradient_clipping", True)))
-        batches = [ds.batch(c) for c in self._chunks(list(ds.train), self.window_batch)]
+        # Data parallelism: each optimiser step takes `window_batch` windows (at least one per rank),
+        # split over the ranks (balanced_partition by the windows' costs: the adaptive TGB solve's accepted step
+        # counts from the previous epoch, else equal), with one gradient all-reduce per step (train.make_step
+        # normalises by the global element count).
+        rank, world = train.dist_world()
+        wb = max(self.window_batch, world)
+        chunks = self._chunks(list(ds.train), wb)
+        cost = {w: 1.0 for w in ds.train}
+
+        def rank_batches():
+            out = []
+            for c in chunks:
+                part = train.balanced_partition([cost[w] for w in c], world)[rank]
+                out.append(([c[i] for i in part], ds.batch([c[i] for i in part]) if part else None))
+            return out
+
+        batches = rank_batches()
         best_val = -float("inf") if self.tgb else float("inf")
         best_epoch, test_loss, test_ndcg, bad = -1, float("nan"), float("nan"), 0
         ckpt_dir = self.cfg.get("checkpoint_dir", ".checkpoints/")
@@ -217,11 +284,25 @@ class WindowTrainer:
         for epoch in range(self.epochs):
             t0 = time.time()
             tot, mg, mu = 0.0, 0.0, 0.0
-            for b in batches:
-                loss, g, u = train.make_step(opt, model.loss_terms, *b)
+            steps_seen = {}
+            for wins, b in batches:
+                if b is None:  # more ranks than windows in this step: contribute a zero gradient
+                    loss, g, u = train.make_step(opt, lambda: (sum(p.sum() * 0.0 for p in model.parameters()), 0))
+                else:
+                    loss, g, u = train.make_step(opt, model.loss_terms, *b)
+                    if getattr(model, "last_steps", None) is not None:
+                        steps_seen.update(zip(wins, model.last_steps.tolist()))
                 tot += float(loss)
                 mg, mu = max(mg, float(g)), max(mu, float(u))
             torch.cuda.synchronize()
+            if world > 1 and getattr(model, "adaptive", False):
+                pos = {w: i for i, w in enumerate(ds.train)}
+                costs = train.global_costs([pos[w] for w in steps_seen], list(steps_seen.values()), len(ds.train),
+                                           "cuda")
+                new = {w: max(c, 1.0) for w, c in zip(ds.train, costs)}
+                if new != cost:
+                    cost = new
+                    batches = rank_batches()
             rec = {"epoch": epoch + 1, "train_loss": tot / max(len(batches), 1), "train_step_time": time.time() - t0,
                    "max_grad": mg, "max_update": mu}
             if epoch == 0 or (epoch + 1) % self.log_freq == 0:
@@ -251,6 +332,22 @@ class WindowTrainer:
         return res
 
 
+def init_distributed():
+    """One process per GPU under torch.distributed.run (WORLD_SIZE > 1): bind LOCAL_RANK's GPU and join the
+    process group (RCCL; GNCDE_DIST_BACKEND=gloo for CPU-transport tests).  The trainers then shard their samples /
+    windows and all-reduce one gradient bucket per step."""
+    import torch.distributed as dist
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or dist.is_initialized():
+        return
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    backend = os.environ.get("GNCDE_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--config", required=True)
@@ -261,6 +358,7 @@ def main(argv=None):
     ap.add_argument("--window-batch", type=int, default=1, help="pgt/tgb models: windows per optimiser step")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
+    init_distributed()
     with open(args.config) as fh:
         cfg = yaml.safe_load(fh)
     name = cfg.get("model", {}).get("name", "graph_neural_cde")

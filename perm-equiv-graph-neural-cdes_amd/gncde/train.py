@@ -30,6 +30,47 @@ def shard_range(total: int, rank: int, world: int) -> tuple[int, int]:
     return start, start + base + (1 if rank < extra else 0)
 
 
+def dist_world() -> tuple[int, int]:
+    """(rank, world) of the initialised process group, (0, 1) without one."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def balanced_partition(costs, world: int) -> list[list[int]]:
+    """Samples -> ranks so that the ranks' summed costs are balanced (adaptive solves have per-sample
+    step counts).  Longest-processing-time greedy: samples by decreasing cost (ties by index) each go to the rank
+    with the least cost so far (ties by rank).  Deterministic, so every rank computes the same partition; each
+    rank's list is returned in increasing sample order."""
+    costs = [float(c) for c in costs]
+    load = [0.0] * world
+    parts: list[list[int]] = [[] for _ in range(world)]
+    for i in sorted(range(len(costs)), key=lambda k: (-costs[k], k)):
+        r = min(range(world), key=lambda q: (load[q], q))
+        parts[r].append(i)
+        load[r] += costs[i]
+    return [sorted(p) for p in parts]
+
+
+def all_reduce_sum(values, device) -> list[float]:
+    """Sum a few host scalars over the ranks (one fp64 collective); identity without a process group."""
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.tolist()
+
+
+def global_costs(own, local_costs, total: int, device) -> list[float]:
+    """Every rank's per-sample costs for its own samples -> the full cost vector on every rank."""
+    c = torch.zeros(total, dtype=torch.float64, device=device)
+    if len(own):
+        c[torch.as_tensor(list(own), device=device)] = torch.as_tensor(local_costs, dtype=torch.float64,
+                                                                       device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return c.tolist()
+
+
 def reduce_gradients(flat_grad: torch.Tensor, sse: torch.Tensor, count: int):
     """All-reduce (SUM) the flat gradient of this rank's summed loss and (sse, count) across ranks, then
     normalise to the gradient of the global mean.  Returns (mean-loss gradient, global mean loss).

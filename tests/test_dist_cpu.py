@@ -5,6 +5,7 @@ tests/test_gpu_grad.py; here a torch surrogate loss stands in for it so the coll
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -72,3 +73,60 @@ def test_reduce_gradients_single_process_is_mean():
     g = torch.tensor([2.0, 4.0])
     gm, loss = reduce_gradients(g, torch.tensor(6.0), 3)
     assert torch.equal(gm, torch.tensor([2.0 / 3, 4.0 / 3])) and float(loss) == 2.0
+
+
+def test_balanced_partition_is_deterministic_and_balanced():
+    """train.balanced_partition (ranks balanced by the adaptive solves' step counts): every sample on
+    exactly one rank, same answer on every call, equal costs -> round robin, skewed costs -> loads within the
+    largest single cost of each other (LPT bound)."""
+    from gncde import train
+    rng = np.random.default_rng(3)
+    for world in (1, 2, 3, 4, 8):
+        for B in (0, 1, 7, 64, 1000):
+            costs = rng.integers(5, 400, size=B).tolist()
+            parts = train.balanced_partition(costs, world)
+            assert parts == train.balanced_partition(costs, world)
+            assert sorted(i for p in parts for i in p) == list(range(B))
+            loads = [sum(costs[i] for i in p) for p in parts]
+            if B:
+                assert max(loads) - min(loads) <= max(costs)
+    assert train.balanced_partition([1.0] * 6, 3) == [[0, 3], [1, 4], [2, 5]]
+
+
+def _dp_partition_rank(rank, world, port, out):
+    import torch.distributed as dist
+    from gncde import train
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B = 11
+        own = list(range(*train.shard_range(B, rank, world)))
+        steps = [10.0 * (i + 1) for i in own]  # this rank's samples' step counts
+        costs = train.global_costs(own, steps, B, "cpu")
+        parts = train.balanced_partition(costs, world)
+        s = train.all_reduce_sum([len(parts[rank]), sum(costs[i] for i in parts[rank])], "cpu")
+        out[rank, :B] = torch.tensor(costs)
+        out[rank, B] = s[0]
+        out[rank, B + 1] = s[1]
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_cost_gather_and_rebalance_over_gloo():
+    """Every rank rebuilds the full step-count vector from its own samples (global_costs) and computes the same
+    balanced partition; all_reduce_sum of the per-rank sample counts / loads gives the totals."""
+    import torch.multiprocessing as mp
+    world, B = 3, 11
+    out = torch.zeros(world, B + 2, dtype=torch.float64).share_memory_()
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_partition_rank, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    want = torch.tensor([10.0 * (i + 1) for i in range(B)], dtype=torch.float64)
+    for r in range(world):
+        assert torch.equal(out[r, :B], want)
+        assert out[r, B] == B and out[r, B + 1] == float(want.sum())

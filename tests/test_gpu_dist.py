@@ -90,3 +90,79 @@ def test_two_rank_step_equals_full_batch():
     assert torch.equal(out[0], out[1])  # replicas stay identical without a parameter broadcast
     assert torch.allclose(out[0, :-1], ref, rtol=0, atol=2e-6)  # only the reduction order differs
     assert abs(float(out[0, -1]) - float(loss)) <= 1e-5 * abs(float(loss))
+
+
+def _trainer_rank(rank, world, port, kind, cfg, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "perm-equiv-graph-neural-cdes_amd")]
+    import torch.distributed as dist
+    from gncde import run
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        res, flat = _run_trainer(kind, cfg)
+        out[rank, :-1] = flat
+        out[rank, -1] = float(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_trainer(kind, cfg):
+    """(the run's headline metric, final parameters) of run.Trainer / run.WindowTrainer on cfg."""
+    from gncde import run, train
+    captured = {}
+    real = train.ClipAdamW.__init__
+
+    def keep(self, *a, **k):  # capture the optimiser so the final flat buffer can be read
+        real(self, *a, **k)
+        captured["opt"] = self
+    train.ClipAdamW.__init__ = keep
+    try:
+        if kind == "dyn":
+            res = run.Trainer(cfg, epochs=3, steps_per_interval=None).run()["best_validation_loss"]
+        else:
+            res = run.WindowTrainer(cfg, epochs=2, window_batch=2).run()["best_validation_loss"]
+    finally:
+        train.ClipAdamW.__init__ = real
+    return res, captured["opt"].flat.detach().cpu()
+
+
+@pytest.mark.parametrize("kind", ["dyn", "pgt"])
+def test_two_rank_trainers_equal_single_process(tmp_path, kind):
+    """gncde.run's trainers in data-parallel mode (SURVEY §8e): the dyn Trainer shards its samples (the reference's
+    adaptive Tsit5 + PID solve, ranks rebalanced by step counts after each epoch) and the PGT WindowTrainer splits
+    each step's windows; two gloo ranks sharing the GPU end with the single process's parameters (up to the
+    all-reduce's summation order) and its validation metric."""
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    import yaml
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    name = "heat_grid_small.yaml" if kind == "dyn" else "pgt_england_small.yaml"
+    with open(os.path.join(root, "configs", name)) as fh:
+        cfg = yaml.safe_load(fh)
+    if kind == "dyn":
+        cfg["dataset"].update(num_nodes=16, time_tick=16, batch_size=5)
+        cfg["eval_freq"] = 3
+    else:
+        cfg["dataset"]["num_snapshots"] = 26
+        cfg["eval_freq"] = 2
+    cfg["checkpoint_dir"] = str(tmp_path)
+    ref_metric, ref = _run_trainer(kind, cfg)
+    world = 2
+    out = torch.zeros(world, ref.numel() + 1, dtype=torch.float64).share_memory_()
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_rank, args=(r, world, port, kind, cfg, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    assert torch.equal(out[0], out[1])  # replicas identical
+    d = float((out[0, :-1] - ref.double()).abs().max())
+    print(f"{kind}: two-rank vs single-process parameters max |diff| {d:.2e}; metric {float(out[0, -1]):.6g} vs "
+          f"{ref_metric:.6g}")
+    assert d <= 1e-4
+    assert abs(float(out[0, -1]) - ref_metric) <= 1e-3 * abs(ref_metric)

@@ -35,11 +35,13 @@ def test_dyn_single_run_small(tmp_path, spi):
     assert losses[-1] < losses[0]
 
 
-@pytest.mark.parametrize("config,metric", [("pgt_england_small.yaml", "best_validation_loss"),
-                                           ("tgb_trade_small.yaml", "best_validation_ndcg@10")])
-def test_window_single_run_small(tmp_path, config, metric):
+@pytest.mark.parametrize("config,metric,solver", [("pgt_england_small.yaml", "best_validation_loss", None),
+                                                  ("tgb_trade_small.yaml", "best_validation_ndcg@10", None),
+                                                  ("tgb_trade_small.yaml", "best_validation_ndcg@10", "pid")])
+def test_window_single_run_small(tmp_path, config, metric, solver):
     """trainer_pgt / trainer_tgb flow: windows -> one optimiser step per window -> validation (MSE / NDCG@10)
-    -> checkpoint -> test metrics of the best model."""
+    -> checkpoint -> test metrics of the best model.  solver "pid": the TGB model on BASELINE config 5's adaptive
+    Tsit5 + PIDController (build-only `model.solver: pid`), trained through the reverse mode on the accepted steps."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a HIP device")
     from gncde import data, run
@@ -49,6 +51,8 @@ def test_window_single_run_small(tmp_path, config, metric):
     cfg["dataset"]["num_snapshots"] = 26 if "pgt" in config else 16
     cfg["checkpoint_dir"] = str(tmp_path)
     cfg["eval_freq"] = 2
+    if solver:
+        cfg["model"]["solver"] = solver
     ds = data.WindowDataset(data.WindowDataCfg.from_dict(cfg["dataset"]))
     assert len(ds.train) >= 1 and len(ds.val) >= 1 and len(ds.test) >= 1
     out = tmp_path / "metrics.jsonl"

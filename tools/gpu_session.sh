@@ -23,7 +23,9 @@ run() {
 }
 for step in "$@"; do
   case $step in
-    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -q -s -x -p no:cacheprovider ;;
+    tests) run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -s -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    sel) run pytest_sel 900 python -u -m pytest ${SEL:-tests/test_gpu_grad.py} -v -s -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    benchtrain) run bench_train 600 python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     bench8) run bench_quick 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
