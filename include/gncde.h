@@ -107,7 +107,8 @@ enum { GNCDE_SAVE_T1 = 0, GNCDE_SAVE_STEPS = 1, GNCDE_SAVE_TS = 2 };
  * one against the other on identical inputs (e.g. the same recorded PID step grid). */
 enum { GNCDE_FLAG_GENERIC = 1 };
 /* stats[b*4 + k]: k=0 accepted steps, 1 rejected steps, 2 vector-field evaluations, 3 status
- * (0 ok, 1 max_steps exceeded, 2 non-finite error estimate, 3 step record (step_ts) too short) */
+ * (0 ok, 1 max_steps exceeded, 2 non-finite error estimate, 3 step record (step_ts) too short, 4 internal: a
+ * one-launch evaluation's workgroups did not all become resident, so its barrier gave up and the results are invalid) */
 enum { GNCDE_STAT_STEPS = 0, GNCDE_STAT_REJECTS = 1, GNCDE_STAT_EVALS = 2, GNCDE_STAT_STATUS = 3 };
 
 typedef struct GncdeProblem {

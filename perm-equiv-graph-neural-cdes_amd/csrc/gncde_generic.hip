@@ -574,7 +574,7 @@ __global__ void k_save_step(int B, size_t E, int G, int k, const float* __restri
   ys[((size_t)b * G + k) * E + e] = y[(size_t)b * E + e];
 }
 
-__global__ void k_grid_stats(int B, int method, const int32_t* __restrict__ nsteps,
+__global__ void k_grid_stats(int B, int method, const int32_t* __restrict__ nsteps, const int* __restrict__ fault,
                              int32_t* __restrict__ stats) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
@@ -582,7 +582,7 @@ __global__ void k_grid_stats(int B, int method, const int32_t* __restrict__ nste
   stats[b * 4 + GNCDE_STAT_STEPS] = ns;
   stats[b * 4 + GNCDE_STAT_REJECTS] = 0;
   stats[b * 4 + GNCDE_STAT_EVALS] = method == GNCDE_RK4 ? 4 * ns : 1 + 6 * ns;
-  stats[b * 4 + GNCDE_STAT_STATUS] = 0;
+  stats[b * 4 + GNCDE_STAT_STATUS] = *fault ? 4 : 0;
 }
 
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
@@ -597,6 +597,7 @@ inline const float* abar_layer(const GncdeProblem& p, const float* abar, int l) 
 
 struct VfWs {
   float *csum, *tg, *Z0, *Z1, *m, *abar, *wf, *wp, *bf, *inv, *q, *dx;
+  unsigned* sync;  // one-launch evaluation: per-group arrival counters [B] + the fault word, zeroed per solve
 };
 
 size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
@@ -617,13 +618,15 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.Z0 = take(B * n * D);
   w.Z1 = take(B * n * D);
   w.m = take(B * n * D);
-  w.abar = take((size_t)p.L * B * nn);  // (I + Abar_l) for every layer
+  // (I + Abar_l) for every layer (not needed by the one-launch evaluation)
+  w.abar = take(rows_supported(p) ? 1 : (size_t)p.L * B * nn);
   w.wf = take(wsum);  // W' = W diag(rms_w) per layer, back to back
   w.wp = take(wsum);  // W' in k_layer's operand order (layers with layer_mode >= 0)
   w.bf = take(bsum);  // bias' = bias + W rms_b per layer
   w.inv = take(B * n);
   w.q = take((size_t)p.L * B * n);                          // q_l = (I + Abar_l) 1
   w.dx = take(B * n * (size_t)(p.cde_hidden > 0 ? 2 * p.cde_embed : 1));  // data-spline derivative at t
+  w.sync = reinterpret_cast<unsigned*>(take(B + 4));
   return off;
 }
 
@@ -684,9 +687,16 @@ void vf_forms_direct(const GncdeProblem& p, const float* t, const float* csum, f
                        p.tcoef, t, p.fusion, abar, ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B);
 }
 
+const int* generic_vf_fault(const GncdeProblem& p, char* ws) {
+  VfWs w;
+  carve_vf(p, ws, w);
+  return reinterpret_cast<const int*>(w.sync + p.B);
+}
+
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
   VfWs w;
   carve_vf(p, ws, w);
+  (void)hipMemsetAsync(w.sync, 0, ((size_t)p.B + 4) * sizeof(unsigned), st);
   const dim3 gs(4, p.T - 1, p.B);
   if (p.compute == GNCDE_COMPUTE_BF16_STORAGE)
     hipLaunchKernelGGL(k_coef_sums<uint16_t>, gs, dim3(256), 0, st, p.n, p.T,
@@ -707,12 +717,22 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
 }
 
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st, bool prepared) {
+                    hipStream_t st, bool prepared, unsigned* bars) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
   VfWs w;
   carve_vf(p, ws, w);
+  unsigned local = 0;
   if (!prepared) generic_vf_prepare(p, ws, st);
+  if (rows_supported(p)) {  // one launch: spline, fusion, every layer and the read-out (gncde_rows.hip)
+    if (!bars) {
+      if (prepared) return GNCDE_ERR_ARG;
+      bars = &local;
+    }
+    // (the workspace holds no (I + Abar_l) planes for these problems: there is no multi-kernel fallback here)
+    return rows_vf_eval(p, t, y, dy, w.csum, w.wp, w.bf, w.Z0, w.Z1, w.sync, reinterpret_cast<int*>(w.sync + B), *bars,
+                        st);
+  }
   vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st);
   const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
   const float* Zin = y;
@@ -874,7 +894,8 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
 
   // Every evaluation's stage time tst is written by the launch before it (k_grid_step for c = 0, k_combo for the
   // others); the step's y <- y_{k+1} and Tsit5's FSAL k1 <- k7 are pointer swaps, not copies.
-  auto eval = [&](const float* yin, float* out) { return generic_vf_eval(p, tst, yin, out, ws, st, true); };
+  unsigned bars = 0;
+  auto eval = [&](const float* yin, float* out) { return generic_vf_eval(p, tst, yin, out, ws, st, true, &bars); };
   // stage record (GncdeSolver.stage_rec): the stage input U_i of step k goes to slot (k, i-1) as it is formed
   const int S = s.method == GNCDE_RK4 ? 4 : 6;
   float* rec = G >= 2 ? s.stage_rec : nullptr;
@@ -954,7 +975,9 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   }
   if (s.save_mode == GNCDE_SAVE_T1)
     (void)hipMemcpyAsync(ys, y, B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
-  if (stats) hipLaunchKernelGGL(k_grid_stats, dim3(gb), dim3(256), 0, st, B, s.method, s.nsteps, stats);
+  if (stats)
+    hipLaunchKernelGGL(k_grid_stats, dim3(gb), dim3(256), 0, st, B, s.method, s.nsteps, generic_vf_fault(p, ws),
+                       stats);
   if (hipGetLastError() != hipSuccess) return GNCDE_ERR_HIP;
   return rc;
 }

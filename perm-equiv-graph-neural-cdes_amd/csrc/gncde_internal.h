@@ -173,8 +173,18 @@ size_t vf_forms_scratch(const GncdeProblem& p);
 void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, float* part,
               float* abar, hipStream_t st, float* qrow = nullptr, float* dx = nullptr);
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st);
+// bars: the solve's count of per-group barriers done by one-launch evaluations so far (gncde_rows.hip); nullptr
+// only together with prepared = false (a standalone evaluation)
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st, bool prepared = false);
+                    hipStream_t st, bool prepared = false, unsigned* bars = nullptr);
+// the workspace's fault word (a one-launch evaluation's barrier gave up): solver status 4 when set
+const int* generic_vf_fault(const GncdeProblem& p, char* ws);
+
+// one-launch evaluation for one hidden width and n <= 256 (configs 3 / 5): gncde_rows.hip
+bool rows_supported(const GncdeProblem& p);
+int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum,
+                 const float* wperm, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
+                 unsigned& bars_done, hipStream_t st);
 int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
                       int32_t* stats, char* ws, hipStream_t st);
 

@@ -354,13 +354,14 @@ __global__ void k_pid_tst(int B, const PidState* __restrict__ st, float* __restr
   if (!st[b].done) atomicAdd(active, 1);
 }
 
-__global__ void k_pid_stats(int B, const PidState* __restrict__ st, int32_t* __restrict__ stats) {
+__global__ void k_pid_stats(int B, const PidState* __restrict__ st, const int* __restrict__ fault,
+                            int32_t* __restrict__ stats) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   stats[b * 4 + GNCDE_STAT_STEPS] = st[b].steps;
   stats[b * 4 + GNCDE_STAT_REJECTS] = st[b].rejects;
   stats[b * 4 + GNCDE_STAT_EVALS] = st[b].evals;
-  stats[b * 4 + GNCDE_STAT_STATUS] = st[b].status;
+  stats[b * 4 + GNCDE_STAT_STATUS] = *fault ? 4 : st[b].status;
 }
 
 constexpr int kPidPoll = 16;  // controller iterations between completion polls
@@ -374,6 +375,7 @@ struct PidRun {
   float *K, *tst;
   int* active;
   int h_active;  // written by the polling copy; read after the stream is synchronised
+  unsigned bars;  // barriers done by one-launch evaluations (generic_vf_eval)
 };
 
 }  // namespace
@@ -431,6 +433,7 @@ int pid_begin(PidRun& r, const GncdeProblem& p, const GncdeSolver& s, const floa
   r.ws = ws;
   r.st = st;
   r.h_active = 1;
+  r.bars = 0;
   hipLaunchKernelGGL(k_pid_init, dim3(B), dim3(256), 0, st, a, y0);
   generic_vf_prepare(p, ws, st);
   return GNCDE_OK;
@@ -438,7 +441,7 @@ int pid_begin(PidRun& r, const GncdeProblem& p, const GncdeSolver& s, const floa
 
 int pid_iterate(PidRun& r) {
   const PidArgs& a = r.a;
-  const int rc = generic_vf_eval(r.p, r.tst, a.yt, r.K, r.ws, r.st, true);
+  const int rc = generic_vf_eval(r.p, r.tst, a.yt, r.K, r.ws, r.st, true, &r.bars);
   if (rc) return rc;
   hipLaunchKernelGGL(k_pid_advance, dim3(a.B), dim3(kAdvThreads), 0, r.st, a);
   return GNCDE_OK;
@@ -453,7 +456,9 @@ void pid_poll_enqueue(PidRun& r) {
 
 void pid_end(PidRun& r, int32_t* stats) {
   const PidArgs& a = r.a;
-  if (stats) hipLaunchKernelGGL(k_pid_stats, dim3((a.B + 255) / 256), dim3(256), 0, r.st, a.B, a.state, stats);
+  if (stats)
+    hipLaunchKernelGGL(k_pid_stats, dim3((a.B + 255) / 256), dim3(256), 0, r.st, a.B, a.state,
+                       generic_vf_fault(r.p, r.ws), stats);
 }
 
 }  // namespace

@@ -1,0 +1,616 @@
+// One launch per vector-field evaluation for the generic path's large graphs (BASELINE configs 3 and 5: CDE wrapper,
+// n up to 256, one hidden width H in {16, 32, 64}) — the spline, the fusion and every ConvLayer of
+// PermEquivGraphVectorField.__call__ (perm_equiv_graph_vector_field.py:85-129; layers.py:36-48,102-160 via the
+// factored fusion table) and the CDE contraction (cde_wrapper_vector_field.py:19-26), with no (I + Abar_l) in HBM.
+//
+// A workgroup owns 16 node rows R of one sample (one MFMA row tile); a sample's ceil(n / 16) workgroups form a group
+// that meets at a barrier after every hidden layer (the next layer's product needs every row of Z):
+//
+//   form     the interval's coefficient rows R and the column strip [:, R] -> A(t), dA/dt(t) of those rows and
+//            columns (Horner), kept in registers in the product's A-operand layout; the row / column / diagonal /
+//            total reductions as cubics of k_coef_sums' per-plane sums (gncde_generic.hip) -> every layer's rank-1 and
+//            diagonal families u_l, w_l, v_l and q_l = (I + Abar_l) 1 in LDS.  The coefficients are read once per
+//            evaluation (each element twice: as a row element and as a column element, the second from L2).
+//   layer l  Z_l (all n rows: the stage input, or the group's previous layer output) -> LDS, RMSNorm factors;
+//            P = (I + Abar_l)[R, :] diag(inv) Z_l on v_mfma_f32_16x16x4f32 with the operand built in registers from
+//            the A / dA / A^T / dA^T elements (K split over the four waves, partials summed in LDS in a fixed order);
+//            Z_{l+1}[R] = relu(P W'^T + q_l b'^T) (W' = W diag(rms_w), b' = b + W rms_b folded once per solve), stored
+//            write-through (sc1) and published by one agent-scope arrival per workgroup; the group's workgroups poll
+//            the arrival count (sc1 loads) and read Z_{l+1} with sc1 loads (MI355X_MICROARCH.md, hand-off row 1).
+//   output   ODE: dy[R] = tg * (P W'^T + q b'^T).  CDE (de = 8): dy[R, m] = tg sum_{c,j} P[., c] dX[., j] W'[16m+j, c]
+//            + tg q sum_j b'[16m + j] dX[., j] (the read-out never materialises the n x 16h matrix).
+//
+// Residency: every group's workgroups must be co-resident (they wait on each other), so the grid is sized from the
+// occupancy query: G groups (at most what fits) loop over the samples g, g + G, ...; every spin is bounded and sets a
+// fault word (reported as solver status 4) instead of hanging.  Groups are laid out so a group's workgroups share
+// blockIdx % 8 (one XCD under the observed round-robin placement: its coefficient strips and Z re-reads stay in one
+// L2) — a speed choice, never needed for correctness.
+#include <mutex>
+
+#include "gncde_internal.h"
+
+namespace gncde {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned rows (n = 129, 255)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kRB = 16;      // node rows per workgroup
+constexpr int kMaxN = 256;   // four 16-column K chunks per wave
+constexpr int kNJ = kMaxN / 64;
+constexpr int kStrip = 17;   // LDS row stride of the transposed column strip
+
+struct RowsArgs {
+  int B, n, T, L, G, rounds, nb, big;  // big: floats of the LDS region shared by the strip, Z_l and the partials
+  const float* ts;
+  const float* coef;       // [B, T-1, 4, n, n]
+  const float* csum;       // k_coef_sums: [B, T-1, 12 n + 4]
+  const float* tcoef;      // [B, T-1, 3, n]
+  const float* data_coef;  // [B, T-1, 4, n, 8, 2] (CDE)
+  const float* fusion;     // [L, GNCDE_FC]
+  const float* wperm;      // W' per layer in the MFMA lane order (permute_linear), back to back
+  const float* bf;         // b' per layer, back to back
+  const float* t;          // [B] evaluation times
+  const float* y;          // [B, n, H] stage inputs
+  float* dy;               // [B, n, H] vector field
+  float* zbuf[2];          // [G, n, H] each: the groups' hidden layer outputs, alternating per step
+  unsigned* bar;           // [G] arrivals per group, monotonic within a solve
+  unsigned bar0;           // barriers every group completed before this launch
+  int* fault;              // set when a barrier wait gives up
+};
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float cubic(const float (&c)[4], float f) { return fmaf(f, fmaf(f, fmaf(f, c[0], c[1]), c[2]), c[3]); }
+__device__ __forceinline__ float dcubic(const float (&c)[4], float f) {
+  return fmaf(f, fmaf(3.0f * f, c[0], 2.0f * c[1]), c[2]);
+}
+
+__host__ __device__ constexpr int rows_zs(int H) { return H + 4; }
+__host__ __device__ inline int rows_np(int n) { return (n + 15) & ~15; }
+// floats of the shared region: the strip [2][NP][17] and the rows block [2][16][NP+4] during the form, then Z_l
+// [NP][H+4] and the partials [4][16][H+4]
+__host__ __device__ inline int rows_big(int n, int H) {
+  const int np = rows_np(n), z = (np > 64 ? np : 64) * rows_zs(H), s = 2 * np * kStrip + 32 * (np + 4);
+  return ((z > s ? z : s) + 3) & ~3;
+}
+inline size_t rows_smem(int n, int H, int L) {
+  const int np = rows_np(n);
+  // big | inv [NP] | v_l [L][NP] | w, u, q [3][L][16] | tg [16] | dX [16][17] | out tile [16][H+4] | red [4][64] x4
+  return sizeof(float) * ((size_t)rows_big(n, H) + np + (size_t)L * np + 48 * L + 16 + 16 * kStrip + 16 * rows_zs(H) +
+                          4 * 64 * 4 + 4);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// MODE 1: ODE output layer.  MODE 2: CDE read-out (de = 8, cde_hidden = H).
+template <int H, int MODE>
+__global__ void __launch_bounds__(256, 3) k_rows(RowsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int ZS = rows_zs(H);
+  constexpr int CT = H / 16;  // column tiles of a width-H operand / output
+  const int n = a.n, L = a.L, nb = a.nb, T = a.T;
+  const int NP = rows_np(n), nch = NP >> 4;
+  float* big = sm;
+  float* sInv = big + a.big;
+  float* sV = sInv + NP;
+  float* sRow = sV + (size_t)L * NP;  // w_l [L][16], u_l [L][16], q_l [L][16]
+  float* sTg = sRow + 48 * L;
+  float* sDx = sTg + 16;
+  float* sOut = sDx + 16 * kStrip;
+  floatx4* red = reinterpret_cast<floatx4*>(sOut + 16 * ZS);
+
+  const int x = blockIdx.x;
+  int g, rb;
+  if (a.G % 8 == 0) {  // a group's workgroups share blockIdx % 8 (bijective for G % 8 == 0)
+    g = (x & 7) + 8 * (x / (8 * nb));
+    rb = (x >> 3) % nb;
+  } else {
+    g = x / nb;
+    rb = x % nb;
+  }
+  const int r0 = rb * kRB;
+  const size_t nn = (size_t)n * n;
+  const size_t zgroup = (size_t)n * H;
+  unsigned epoch = a.bar0;
+
+  auto arrive = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores have reached memory
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(a.bar + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto wait_all = [&]() {
+    ++epoch;
+    if (threadIdx.x == 0) {
+      const unsigned target = epoch * (unsigned)nb;
+      unsigned spins = 0;
+      while (__hip_atomic_load(a.bar + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++spins & 1023u) == 0 &&
+            (spins > (1u << 22) || __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          __hip_atomic_store(a.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  };
+
+  for (int it = 0; it < a.rounds; ++it) {
+    // the lane's indices through an opaque move each round: otherwise every per-lane address and bounds mask of the
+    // form and the layers is hoisted out of the round loop and held in registers for the whole kernel
+    int tid;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
+    const int w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
+    const int ri = r0 + lo;  // this lane's operand row
+    const int bs = g + it * a.G;
+    const bool live = bs < a.B;
+    const int b = live ? bs : a.B - 1;  // an idle round computes on a valid sample, keeps its barriers, stores no dy
+    const float tb = a.t[b];
+    const float* tsb = a.ts + (size_t)b * T;
+    const int idx = interval_index(tsb, T, tb);
+    const float f = tb - tsb[idx];
+    const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
+
+    // ---- form ---------------------------------------------------------------------------------------------------
+    // Both coefficient reads are unconditional coalesced dwordx4 buffer loads from this (sample, interval)'s four
+    // planes (the descriptor's range check zero-fills anything past plane a); values outside the matrix are
+    // selected to 0 before they reach LDS, so no load sits in a divergent branch.
+    const auto crs = rsrc(cb, (unsigned)(4 * nn * sizeof(float)));
+    const int RS = NP + 4;                 // LDS row stride of the rows block
+    float* sAr = big + 2 * NP * kStrip;    // rows block A(t)[R, :] [16][RS], then dA/dt [16][RS]
+    {  // the column strip [:, R]: thread = (node row kk, four strip columns), Horner, transposed into LDS
+      const int c4 = 4 * (tid & 3);
+      floatx4 sc[4][4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int kk = (tid >> 2) + 64 * p;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          sc[p][q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     crs, (int)((q * nn + (size_t)kk * n + r0 + c4) * 4), 0, 0));
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int kk = (tid >> 2) + 64 * p;
+        if (kk < NP)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool in = kk < n && r0 + c4 + e < n;
+            const float cc[4] = {sc[p][0][e], sc[p][1][e], sc[p][2][e], sc[p][3][e]};
+            big[kk * kStrip + c4 + e] = in ? cubic(cc, f) : 0.f;
+            big[(NP + kk) * kStrip + c4 + e] = in ? dcubic(cc, f) : 0.f;
+          }
+      }
+    }
+    asm volatile("" ::: "memory");  // the rows' loads after the strip's: half the registers in flight
+    {  // the rows block: thread = (row tid / 16, columns 4 (tid % 16) + 64 u), 256 coalesced bytes per row and u
+      const int rr = tid >> 4, cq = 4 * (tid & 15);
+      floatx4 rc[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          rc[u][q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     crs, (int)((q * nn + (size_t)(r0 + rr) * n + cq + 64 * u) * 4), 0, 0));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c0 = cq + 64 * u;
+        if (c0 < NP)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool in = r0 + rr < n && c0 + e < n;
+            const float cc[4] = {rc[u][0][e], rc[u][1][e], rc[u][2][e], rc[u][3][e]};
+            sAr[rr * RS + c0 + e] = in ? cubic(cc, f) : 0.f;
+            sAr[(16 + rr) * RS + c0 + e] = in ? dcubic(cc, f) : 0.f;
+          }
+      }
+    }
+    // node vectors at t from the per-plane sums (thread = node), the layers' families; tg and dX of the rows
+    {
+      const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
+      float pv[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      if (tid < n)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int kd = 0; kd < 3; ++kd) pv[kd][q] = cs[(q * 3 + kd) * n + tid];
+      float pt[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pt[q] = cs[12 * n + q];
+      float tcv[3] = {0.f, 0.f, 0.f};
+      if (tid < 16 && r0 + tid < n) {
+        const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n + r0 + tid;
+        tcv[0] = tc[0];
+        tcv[1] = tc[n];
+        tcv[2] = tc[2 * n];
+      }
+      float dcv[3] = {0.f, 0.f, 0.f};
+      if (MODE == 2 && r0 + (tid >> 4) < n) {
+        const size_t blk = (size_t)n * 16;
+        const float* dc = a.data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)(r0 + (tid >> 4)) * 16 + (tid & 15);
+        dcv[0] = dc[0];
+        dcv[1] = dc[blk];
+        dcv[2] = dc[2 * blk];
+      }
+      const float r = cubic(pv[0], f), rd = dcubic(pv[0], f), c = cubic(pv[1], f), cd = dcubic(pv[1], f);
+      const float dg = cubic(pv[2], f), dgd = dcubic(pv[2], f);
+      const float s = cubic(pt, f), sd = dcubic(pt, f);
+      const bool row = tid >= r0 && tid < r0 + kRB && tid < n;
+      for (int l = 0; l < L; ++l) {
+        const float* fc = a.fusion + l * GNCDE_FC;
+        if (tid < NP)
+          sV[l * NP + tid] = tid < n ? fc[GNCDE_FC_VR_A] * r + fc[GNCDE_FC_VR_DA] * rd + fc[GNCDE_FC_VC_A] * c +
+                                           fc[GNCDE_FC_VC_DA] * cd
+                                     : 0.f;
+        if (row) {
+          const int t = tid - r0;
+          const float wv = fc[GNCDE_FC_WR_A] * r + fc[GNCDE_FC_WR_DA] * rd + fc[GNCDE_FC_WC_A] * c +
+                           fc[GNCDE_FC_WC_DA] * cd + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
+          const float uv = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dg + fc[GNCDE_FC_UD_DA] * dgd + fc[GNCDE_FC_UR_A] * r +
+                           fc[GNCDE_FC_UR_DA] * rd + fc[GNCDE_FC_UC_A] * c + fc[GNCDE_FC_UC_DA] * cd +
+                           fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
+          // q_l[i] = sum_k (I + Abar_l)[i][k]: dense terms -> row / column sums, w family n copies, v family
+          // sum_k v_k (sum r = sum c = s), the diagonal once
+          float qv = fc[GNCDE_FC_E_A] * r + fc[GNCDE_FC_E_DA] * rd + fc[GNCDE_FC_ET_A] * c + fc[GNCDE_FC_ET_DA] * cd;
+          qv += (float)n * wv;
+          qv += (fc[GNCDE_FC_VR_A] + fc[GNCDE_FC_VC_A]) * s + (fc[GNCDE_FC_VR_DA] + fc[GNCDE_FC_VC_DA]) * sd;
+          qv += uv;
+          sRow[l * 16 + t] = wv;
+          sRow[(L + l) * 16 + t] = uv;
+          sRow[(2 * L + l) * 16 + t] = qv;
+        }
+      }
+      if (tid < 16) sTg[tid] = r0 + tid < n ? fmaf(f, fmaf(3.0f * f, tcv[0], 2.0f * tcv[1]), tcv[2]) : 0.f;
+      if (MODE == 2) sDx[(tid >> 4) * kStrip + (tid & 15)] = fmaf(f, fmaf(3.0f * f, dcv[0], 2.0f * dcv[1]), dcv[2]);
+    }
+    __syncthreads();
+    // the product's A-operand elements of this lane: (I + Abar)[ri][k] needs A, dA at (ri, k) and at (k, ri), for
+    // k = 16 kc + 4 hi + s, kc = w + 4 j (chunks past the matrix read zeros)
+    float Ar[kNJ][4], dAr[kNJ][4], At[kNJ][4], dAt[kNJ][4];
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j) {
+      const int kc = w + 4 * j, k0 = 16 * kc + 4 * hi;
+      const bool in = kc < nch;
+      const floatx4 ar = in ? *reinterpret_cast<const floatx4*>(sAr + lo * RS + k0) : floatx4{0.f, 0.f, 0.f, 0.f};
+      const floatx4 dr = in ? *reinterpret_cast<const floatx4*>(sAr + (16 + lo) * RS + k0) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        Ar[j][s] = ar[s];
+        dAr[j][s] = dr[s];
+        At[j][s] = in ? big[(k0 + s) * kStrip + lo] : 0.f;
+        dAt[j][s] = in ? big[(NP + k0 + s) * kStrip + lo] : 0.f;
+      }
+    }
+    __syncthreads();  // the strip's region becomes Z_l
+
+    // ---- layers ----------------------------------------------------------------------------------------------
+    // Z_l -> LDS (the stage input with plain loads: written before this launch; a hidden output of the group with
+    // sc1 loads after the barrier) and the RMSNorm factors of its rows
+    auto load_z = [&](int l) __attribute__((always_inline)) {
+      float* Zs = big;
+      constexpr int G4 = H / 4, U = 8;
+      const int tot = NP * G4, valid = n * G4;
+      if (l == 0) {
+        const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.y + (size_t)b * zgroup);
+        for (int e0 = tid; e0 < tot; e0 += 256 * U) {
+          floatx4 v[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int e = e0 + 256 * u;
+            v[u] = e < valid ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int e = e0 + 256 * u;
+            if (e < tot) *reinterpret_cast<floatx4*>(Zs + (e / G4) * ZS + 4 * (e % G4)) = v[u];
+          }
+        }
+      } else {
+        wait_all();
+        // hidden outputs alternate buffers by their step index within the launch, so a buffer is rewritten only
+        // after a barrier that every reader of its previous contents has passed (also across rounds, for L = 2)
+        const float* zin = a.zbuf[(it * (L - 1) + l - 1) & 1] + (size_t)g * zgroup;
+        const auto rs = rsrc(zin, (unsigned)(zgroup * sizeof(float)));
+        for (int e0 = tid; e0 < tot; e0 += 256 * U) {
+          floatx4 v[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int e = e0 + 256 * u;
+            v[u] = e < valid ? __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, e * 16, 0, 16))
+                             : floatx4{0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int e = e0 + 256 * u;
+            if (e < tot) *reinterpret_cast<floatx4*>(Zs + (e / G4) * ZS + 4 * (e % G4)) = v[u];
+          }
+        }
+      }
+      __syncthreads();
+      for (int r = tid; r < NP; r += 256) {
+        float ss = 0.f;
+#pragma unroll
+        for (int q = 0; q < G4; ++q) {
+          const floatx4 z = *reinterpret_cast<const floatx4*>(Zs + r * ZS + 4 * q);
+          ss = fmaf(z.x, z.x, fmaf(z.y, z.y, fmaf(z.z, z.z, fmaf(z.w, z.w, ss))));
+        }
+        sInv[r] = r < n ? rms_inv(ss, 1.0f / (float)H) : 0.f;
+      }
+      __syncthreads();
+    };
+    // P = (I + Abar_l)[R, :] diag(inv) Z_l, the operand built in registers per 16-column chunk; the four K parts
+    // land in LDS (aliasing Z_l)
+    auto product = [&](int l) __attribute__((always_inline)) {
+      const float* Zs = big;
+      const float* fc = a.fusion + l * GNCDE_FC;
+      const float eA = fc[GNCDE_FC_E_A], edA = fc[GNCDE_FC_E_DA], eTA = fc[GNCDE_FC_ET_A], eTdA = fc[GNCDE_FC_ET_DA];
+      const float wl = sRow[l * 16 + lo], ul = sRow[(L + l) * 16 + lo];
+      floatx4 acc[CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < kNJ; ++j) {
+        const int kc = w + 4 * j;
+        if (kc >= nch) break;
+        const int k0 = 16 * kc + 4 * hi;
+        const floatx4 vk = *reinterpret_cast<const floatx4*>(sV + l * NP + k0);
+        const floatx4 iv = *reinterpret_cast<const floatx4*>(sInv + k0);
+        float bz[4][CT];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) bz[s][ct] = Zs[(k0 + s) * ZS + 16 * ct + lo];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          float v = fmaf(eA, Ar[j][s], fmaf(edA, dAr[j][s], fmaf(eTA, At[j][s], fmaf(eTdA, dAt[j][s], wl + vk[s]))));
+          if (k0 + s == ri) v += ul;
+          const float op = v * iv[s];
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma4(op, bz[s][ct], acc[ct]);
+        }
+      }
+      __syncthreads();  // every Z_l read done: the partials alias it
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) big[(w * 16 + 4 * hi + r) * ZS + 16 * ct + lo] = acc[ct][r];
+      __syncthreads();
+    };
+    // P row lo, columns 16 cc + 4 hi .. + 3: the four K parts in a fixed order
+    auto prow = [&](int cc) -> floatx4 {
+      const float* p = big + lo * ZS + 16 * cc + 4 * hi;
+      floatx4 v = *reinterpret_cast<const floatx4*>(p);
+#pragma unroll
+      for (int kp = 1; kp < 4; ++kp) v += *reinterpret_cast<const floatx4*>(p + kp * 16 * ZS);
+      return v;
+    };
+    // P W'^T + q b'^T for output tile `tile` (rows R, columns 16 tile + lo): acc[r] = row 4 hi + r
+    auto linear = [&](int l, int tile) __attribute__((always_inline)) -> floatx4 {
+      const floatx4* W4 = reinterpret_cast<const floatx4*>(a.wperm + (size_t)l * H * H);
+      floatx4 accL = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int cc = 0; cc < CT; ++cc) {
+        const floatx4 pv = prow(cc), wv = W4[(tile * CT + cc) * 64 + lane];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) accL = mfma4(pv[s], wv[s], accL);
+      }
+      const float bc = a.bf[l * H + 16 * tile + lo];
+      const float* qrow = sRow + (2 * L + l) * 16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) accL[r] = fmaf(qrow[4 * hi + r], bc, accL[r]);
+      return accL;
+    };
+
+    for (int l = 0; l + 1 < L; ++l) {  // hidden layers: Z_{l+1}[R] = relu(P W'^T + q b'^T), published to the group
+      load_z(l);
+      product(l);
+      for (int tile = w; tile < CT; tile += 4) {
+        const floatx4 v = linear(l, tile);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sOut[(4 * hi + r) * ZS + 16 * tile + lo] = fmaxf(v[r], 0.f);
+      }
+      __syncthreads();
+      float* zout = a.zbuf[(it * (L - 1) + l) & 1] + (size_t)g * zgroup;
+      const auto rs = rsrc(zout, (unsigned)(zgroup * sizeof(float)));
+      constexpr int G4 = H / 4;
+      if (tid < 16 * G4) {  // write-through 16-byte stores of this workgroup's rows, then one arrival
+        const int R = tid / G4, q = tid % G4;
+        if (r0 + R < n)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4, *reinterpret_cast<const floatx4*>(sOut + R * ZS + 4 * q)), rs,
+              ((r0 + R) * H + 4 * q) * 4, 0, 16);
+      }
+      arrive();  // its barrier also orders the partials' reuse by the next layer
+    }
+    {  // the output layer
+      const int l = L - 1;
+      load_z(l);
+      product(l);
+      if constexpr (MODE == 1) {  // ODE: dy[R] = tg (P W'^T + q b'^T)
+        for (int tile = w; tile < CT; tile += 4) {
+          const floatx4 v = linear(l, tile);
+          if (live)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int R = 4 * hi + r;
+              if (r0 + R < n) a.dy[((size_t)b * n + r0 + R) * H + 16 * tile + lo] = v[r] * sTg[R];
+            }
+        }
+      } else {
+        // CDE read-out: dy[R, m] = tg (sum_{c, j} P[., c] dX[., j] W'[16 m + j, c] + q sum_j b'[16 m + j] dX[., j])
+        constexpr int KP = 4 / CT, JP = 16 / KP;  // waves per channel tile (splitting j), j per wave
+        const int ct = w % CT, kp = w / CT, j0 = kp * JP;
+        const floatx4* W4 = reinterpret_cast<const floatx4*>(a.wperm + (size_t)l * H * H);
+        const float* bl = a.bf + (size_t)l * H;
+        const float* qrow = sRow + (2 * L + l) * 16;
+        float dxr[JP];
+#pragma unroll
+        for (int j = 0; j < JP; ++j) dxr[j] = sDx[lo * kStrip + j0 + j];
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int cc = 0; cc < CT; ++cc) {
+          floatx4 wv[JP];  // the chunk's W' operands: one L2 round trip, then the MFMA chain
+#pragma unroll
+          for (int j = 0; j < JP; ++j) wv[j] = W4[((ct * 16 + j0 + j) * CT + cc) * 64 + lane];
+          const floatx4 pv = prow(cc);
+#pragma unroll
+          for (int j = 0; j < JP; ++j) {
+            const floatx4 av = pv * dxr[j];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) acc = mfma4(av[s], wv[j][s], acc);
+          }
+        }
+        const int m = 16 * ct + lo;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int R = 4 * hi + r;
+          float sb = 0.f;
+#pragma unroll
+          for (int j = 0; j < JP; ++j) sb = fmaf(bl[16 * m + j0 + j], sDx[R * kStrip + j0 + j], sb);
+          acc[r] = fmaf(qrow[R], sb, acc[r]);
+        }
+        if constexpr (KP > 1) {
+          red[w * 64 + lane] = acc;
+          __syncthreads();
+          if (kp == 0)
+#pragma unroll
+            for (int p = 1; p < KP; ++p) acc += red[(w + p * CT) * 64 + lane];
+        }
+        if (kp == 0 && live)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int R = 4 * hi + r;
+            if (r0 + R < n) a.dy[((size_t)b * n + r0 + R) * H + m] = sTg[R] * acc[r];
+          }
+      }
+      __syncthreads();  // P (aliasing Z_l) and the LDS vectors are rewritten by the next round's form
+    }
+  }
+}
+
+struct Inst {
+  const void* fn;
+  void (*launch)(const RowsArgs&, int, size_t, hipStream_t);
+};
+
+template <int H, int MODE>
+void launch_rows(const RowsArgs& a, int grid, size_t smem, hipStream_t st) {
+  hipLaunchKernelGGL((k_rows<H, MODE>), dim3(grid), dim3(256), smem, st, a);
+}
+
+template <int H, int MODE>
+Inst inst() {
+  return Inst{reinterpret_cast<const void*>(&k_rows<H, MODE>), &launch_rows<H, MODE>};
+}
+
+bool find_inst(int H, int mode, Inst& out) {
+  if (mode == 1) {
+    if (H == 16) out = inst<16, 1>();
+    else if (H == 32) out = inst<32, 1>();
+    else if (H == 64) out = inst<64, 1>();
+    else return false;
+  } else {
+    if (H == 16) out = inst<16, 2>();
+    else if (H == 32) out = inst<32, 2>();
+    else if (H == 64) out = inst<64, 2>();
+    else return false;
+  }
+  return true;
+}
+
+// workgroups of one instance resident per CU at this LDS size (occupancy query, cached per device) x CUs
+int resident_blocks(const Inst& k, size_t smem) {
+  struct Entry {
+    int dev;
+    const void* fn;
+    size_t smem;
+    int blocks;
+  };
+  static std::mutex mu;
+  static Entry cache[64];
+  static int used = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lock(mu);
+  for (int i = 0; i < used; ++i)
+    if (cache[i].dev == dev && cache[i].fn == k.fn && cache[i].smem == smem) return cache[i].blocks;
+  int cus = 0, per = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (smem > 64 * 1024 &&
+      hipFuncSetAttribute(k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
+    return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k.fn, 256, smem) != hipSuccess) return 0;
+  const int blocks = per * cus;
+  if (used < 64) cache[used++] = Entry{dev, k.fn, smem, blocks};
+  return blocks;
+}
+
+}  // namespace
+
+// The one-launch evaluation's envelope: every hidden width H in {16, 32, 64}, n <= 256, fp32, and an ODE output of
+// width H or the de = 8 CDE read-out with cde_hidden = H.
+bool rows_supported(const GncdeProblem& p) {
+  if (p.compute != GNCDE_COMPUTE_FP32 || p.n > kMaxN || p.n < 1) return false;
+  const int H = p.dims[0];
+  if (H != 16 && H != 32 && H != 64) return false;
+  for (int l = 0; l < p.L; ++l)
+    if (p.dims[l] != H) return false;
+  if (p.cde_hidden > 0) return p.cde_embed == 8 && p.cde_hidden == H && p.dims[p.L] == 16 * H;
+  return p.dims[p.L] == H;
+}
+
+size_t rows_sync_ints(const GncdeProblem& p) { return align_up((size_t)p.B + 4, 4); }
+
+// Launch one evaluation (RowsState: the group layout, fixed per problem, and the barriers done so far).
+int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum,
+                 const float* wperm, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
+                 unsigned& bars_done, hipStream_t st) {
+  Inst k;
+  const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
+  if (!find_inst(H, mode, k)) return GNCDE_ERR_UNSUPPORTED;
+  const size_t smem = rows_smem(p.n, H, p.L);
+  const int nb = (p.n + kRB - 1) / kRB;
+  const int cap = resident_blocks(k, smem);
+  int G = cap / nb;
+  if (G < 1) return GNCDE_ERR_UNSUPPORTED;
+  if (G >= p.B) {
+    G = p.B;
+  } else if (G >= 8) {
+    G -= G % 8;
+  }
+  RowsArgs a{};
+  a.B = p.B;
+  a.n = p.n;
+  a.T = p.T;
+  a.L = p.L;
+  a.G = G;
+  a.rounds = (p.B + G - 1) / G;
+  a.nb = nb;
+  a.big = rows_big(p.n, H);
+  a.ts = p.ts;
+  a.coef = p.coef;
+  a.csum = csum;
+  a.tcoef = p.tcoef;
+  a.data_coef = p.data_coef;
+  a.fusion = p.fusion;
+  a.wperm = wperm;
+  a.bf = bf;
+  a.t = t;
+  a.y = y;
+  a.dy = dy;
+  a.zbuf[0] = z0;
+  a.zbuf[1] = z1;
+  a.bar = bar;
+  a.bar0 = bars_done;
+  a.fault = fault;
+  k.launch(a, G * nb, smem, st);
+  bars_done += (unsigned)(a.rounds * (p.L - 1));
+  return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+}
+
+}  // namespace gncde

@@ -683,6 +683,7 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
   char* vf_ws = ws + bytes;
   const Tableau tab = s.method == GNCDE_RK4 ? rk4_tab() : tsit5_tab();
   generic_vf_prepare(p, vf_ws, st);
+  unsigned bars = 0;  // barriers of one-launch stage evaluations (generic_vf_eval)
   {
     size_t wo = 0, bo = 0;
     for (int l = 0; l < p.L; ++l) {
@@ -728,7 +729,7 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
       hipLaunchKernelGGL(v_lincomb, ge, dim3(256), 0, st, B, E, w.y, lc, w.hcur, w.U[i], 0);
       hipLaunchKernelGGL(v_stage_time, dim3(gb), dim3(256), 0, st, B, tab.c[i], w.tcur, w.hcur, w.tst);
       if (i + 1 < tab.stages) {  // the last stage's value is not needed for the reverse sweep
-        const int rc = generic_vf_eval(p, w.tst, w.U[i], w.K[i], vf_ws, st, true);
+        const int rc = generic_vf_eval(p, w.tst, w.U[i], w.K[i], vf_ws, st, true, &bars);
         if (rc) return rc;
       }
     }
