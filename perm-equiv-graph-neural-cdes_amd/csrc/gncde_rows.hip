@@ -163,7 +163,52 @@ __global__ void __launch_bounds__(256, 3) k_rows(RowsArgs a) {
     const auto crs = rsrc(cb, (unsigned)(4 * nn * sizeof(float)));
     const int RS = NP + 4;                 // LDS row stride of the rows block
     float* sAr = big + 2 * NP * kStrip;    // rows block A(t)[R, :] [16][RS], then dA/dt [16][RS]
-    {  // the column strip [:, R]: thread = (node row kk, four strip columns), Horner, transposed into LDS
+    // 1. issue the rows block (thread = (row tid / 16, columns 4 (tid % 16) + 64 u): 256 coalesced bytes per row
+    //    and u) and every small load of the form (node-vector plane sums, time channel, data spline) at once; the
+    //    rows come from HBM, and the column strip below reads the same lines again from L2 (a group shares one XCD)
+    const int rr = tid >> 4, cq = 4 * (tid & 15);
+    floatx4 rc[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        rc[u][q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   crs, (int)((q * nn + (size_t)(r0 + rr) * n + cq + 64 * u) * 4), 0, 0));
+    const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
+    const int nd = tid < n ? tid : n - 1;  // clamped indices + selects: no load inside a divergent branch
+    float pv[3][4], pt[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int kd = 0; kd < 3; ++kd) pv[kd][q] = cs[(q * 3 + kd) * n + nd];
+      pt[q] = cs[12 * n + q];
+    }
+    const int tr = r0 + (tid & 15) < n ? r0 + (tid & 15) : n - 1;
+    const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n + tr;
+    const float tcv[3] = {tc[0], tc[n], tc[2 * n]};
+    float dcv[3] = {0.f, 0.f, 0.f};
+    if constexpr (MODE == 2) {
+      const size_t blk = (size_t)n * 16;
+      const int dr = r0 + rr < n ? r0 + rr : n - 1;
+      const float* dc = a.data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)dr * 16 + (tid & 15);
+      dcv[0] = dc[0];
+      dcv[1] = dc[blk];
+      dcv[2] = dc[2 * blk];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c0 = cq + 64 * u;
+      if (c0 < NP)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool in = r0 + rr < n && c0 + e < n;
+          const float cc[4] = {rc[u][0][e], rc[u][1][e], rc[u][2][e], rc[u][3][e]};
+          sAr[rr * RS + c0 + e] = in ? cubic(cc, f) : 0.f;
+          sAr[(16 + rr) * RS + c0 + e] = in ? dcubic(cc, f) : 0.f;
+        }
+    }
+    asm volatile("" ::: "memory");  // the strip's loads after the rows' (registers, and L2 reuse)
+    {  // 2. the column strip [:, R]: thread = (node row kk, four strip columns), Horner, transposed into LDS
       const int c4 = 4 * (tid & 3);
       floatx4 sc[4][4];
 #pragma unroll
@@ -187,66 +232,19 @@ __global__ void __launch_bounds__(256, 3) k_rows(RowsArgs a) {
           }
       }
     }
-    asm volatile("" ::: "memory");  // the rows' loads after the strip's: half the registers in flight
-    {  // the rows block: thread = (row tid / 16, columns 4 (tid % 16) + 64 u), 256 coalesced bytes per row and u
-      const int rr = tid >> 4, cq = 4 * (tid & 15);
-      floatx4 rc[4][4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          rc[u][q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     crs, (int)((q * nn + (size_t)(r0 + rr) * n + cq + 64 * u) * 4), 0, 0));
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int c0 = cq + 64 * u;
-        if (c0 < NP)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bool in = r0 + rr < n && c0 + e < n;
-            const float cc[4] = {rc[u][0][e], rc[u][1][e], rc[u][2][e], rc[u][3][e]};
-            sAr[rr * RS + c0 + e] = in ? cubic(cc, f) : 0.f;
-            sAr[(16 + rr) * RS + c0 + e] = in ? dcubic(cc, f) : 0.f;
-          }
-      }
-    }
-    // node vectors at t from the per-plane sums (thread = node), the layers' families; tg and dX of the rows
+    // 3. node vectors at t from the per-plane sums (thread = node), the layers' families; tg and dX of the rows
     {
-      const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
-      float pv[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      if (tid < n)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int kd = 0; kd < 3; ++kd) pv[kd][q] = cs[(q * 3 + kd) * n + tid];
-      float pt[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) pt[q] = cs[12 * n + q];
-      float tcv[3] = {0.f, 0.f, 0.f};
-      if (tid < 16 && r0 + tid < n) {
-        const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n + r0 + tid;
-        tcv[0] = tc[0];
-        tcv[1] = tc[n];
-        tcv[2] = tc[2 * n];
-      }
-      float dcv[3] = {0.f, 0.f, 0.f};
-      if (MODE == 2 && r0 + (tid >> 4) < n) {
-        const size_t blk = (size_t)n * 16;
-        const float* dc = a.data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)(r0 + (tid >> 4)) * 16 + (tid & 15);
-        dcv[0] = dc[0];
-        dcv[1] = dc[blk];
-        dcv[2] = dc[2 * blk];
-      }
-      const float r = cubic(pv[0], f), rd = dcubic(pv[0], f), c = cubic(pv[1], f), cd = dcubic(pv[1], f);
+      const bool nin = tid < n;
+      const float r = nin ? cubic(pv[0], f) : 0.f, rd = nin ? dcubic(pv[0], f) : 0.f;
+      const float c = nin ? cubic(pv[1], f) : 0.f, cd = nin ? dcubic(pv[1], f) : 0.f;
       const float dg = cubic(pv[2], f), dgd = dcubic(pv[2], f);
       const float s = cubic(pt, f), sd = dcubic(pt, f);
-      const bool row = tid >= r0 && tid < r0 + kRB && tid < n;
+      const bool row = tid >= r0 && tid < r0 + kRB && nin;
       for (int l = 0; l < L; ++l) {
         const float* fc = a.fusion + l * GNCDE_FC;
         if (tid < NP)
-          sV[l * NP + tid] = tid < n ? fc[GNCDE_FC_VR_A] * r + fc[GNCDE_FC_VR_DA] * rd + fc[GNCDE_FC_VC_A] * c +
-                                           fc[GNCDE_FC_VC_DA] * cd
-                                     : 0.f;
+          sV[l * NP + tid] = fc[GNCDE_FC_VR_A] * r + fc[GNCDE_FC_VR_DA] * rd + fc[GNCDE_FC_VC_A] * c +
+                             fc[GNCDE_FC_VC_DA] * cd;
         if (row) {
           const int t = tid - r0;
           const float wv = fc[GNCDE_FC_WR_A] * r + fc[GNCDE_FC_WR_DA] * rd + fc[GNCDE_FC_WC_A] * c +
@@ -266,7 +264,8 @@ __global__ void __launch_bounds__(256, 3) k_rows(RowsArgs a) {
         }
       }
       if (tid < 16) sTg[tid] = r0 + tid < n ? fmaf(f, fmaf(3.0f * f, tcv[0], 2.0f * tcv[1]), tcv[2]) : 0.f;
-      if (MODE == 2) sDx[(tid >> 4) * kStrip + (tid & 15)] = fmaf(f, fmaf(3.0f * f, dcv[0], 2.0f * dcv[1]), dcv[2]);
+      if (MODE == 2)
+        sDx[rr * kStrip + (tid & 15)] = r0 + rr < n ? fmaf(f, fmaf(3.0f * f, dcv[0], 2.0f * dcv[1]), dcv[2]) : 0.f;
     }
     __syncthreads();
     // the product's A-operand elements of this lane: (I + Abar)[ri][k] needs A, dA at (ri, k) and at (k, ri), for
@@ -451,20 +450,30 @@ __global__ void __launch_bounds__(256, 3) k_rows(RowsArgs a) {
         float dxr[JP];
 #pragma unroll
         for (int j = 0; j < JP; ++j) dxr[j] = sDx[lo * kStrip + j0 + j];
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        // steps of (c chunk, JH j's): the next step's W' operands are in flight while this step's MFMAs run, and
+        // even / odd j accumulate into two independent chains (the MFMA result latency is not exposed per step)
+        constexpr int JH = JP < 8 ? JP : 8, NH = JP / JH, NSTEP = CT * NH;
+        floatx4 wv[2][JH];
+        auto wload = [&](int step, floatx4 (&dst)[JH]) __attribute__((always_inline)) {
+          const int cc = step / NH, jh = step % NH;
 #pragma unroll
-        for (int cc = 0; cc < CT; ++cc) {
-          floatx4 wv[JP];  // the chunk's W' operands: one L2 round trip, then the MFMA chain
+          for (int j = 0; j < JH; ++j) dst[j] = W4[((ct * 16 + j0 + jh * JH + j) * CT + cc) * 64 + lane];
+        };
+        wload(0, wv[0]);
+        floatx4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-          for (int j = 0; j < JP; ++j) wv[j] = W4[((ct * 16 + j0 + j) * CT + cc) * 64 + lane];
+        for (int step = 0; step < NSTEP; ++step) {
+          if (step + 1 < NSTEP) wload(step + 1, wv[(step + 1) & 1]);
+          const int cc = step / NH, jh = step % NH;
           const floatx4 pv = prow(cc);
 #pragma unroll
-          for (int j = 0; j < JP; ++j) {
-            const floatx4 av = pv * dxr[j];
+          for (int j = 0; j < JH; ++j) {
+            const floatx4 av = pv * dxr[jh * JH + j];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) acc = mfma4(av[s], wv[j][s], acc);
+            for (int s = 0; s < 4; ++s) acc2[j & 1] = mfma4(av[s], wv[step & 1][j][s], acc2[j & 1]);
           }
         }
+        floatx4 acc = acc2[0] + acc2[1];
         const int m = 16 * ct + lo;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -553,14 +562,17 @@ int resident_blocks(const Inst& k, size_t smem) {
 }  // namespace
 
 // The one-launch evaluation's envelope: every hidden width H in {16, 32, 64}, n <= 256, fp32, and an ODE output of
-// width H or the de = 8 CDE read-out with cde_hidden = H.
+// width H or the de = 8 CDE read-out with cde_hidden = H <= 32.  At H = 64 the CDE read-out weight is 256 KB (n x 16h
+// x h): every 16-row workgroup streams all of it and its fp32 MFMA chain dominates the launch (config 3 measured
+// 81 us per evaluation against 70 us for the multi-kernel path, whose read-out launch splits 32-row blocks over
+// channel halves), so that shape keeps the multi-kernel path.
 bool rows_supported(const GncdeProblem& p) {
   if (p.compute != GNCDE_COMPUTE_FP32 || p.n > kMaxN || p.n < 1) return false;
   const int H = p.dims[0];
   if (H != 16 && H != 32 && H != 64) return false;
   for (int l = 0; l < p.L; ++l)
     if (p.dims[l] != H) return false;
-  if (p.cde_hidden > 0) return p.cde_embed == 8 && p.cde_hidden == H && p.dims[p.L] == 16 * H;
+  if (p.cde_hidden > 0) return p.cde_embed == 8 && p.cde_hidden == H && H <= 32 && p.dims[p.L] == 16 * H;
   return p.dims[p.L] == H;
 }
 
