@@ -87,9 +87,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
 
-// MODE 1: ODE output layer.  MODE 2: CDE read-out (de = 8, cde_hidden = H).
+// MODE 1: ODE output layer.  MODE 2: CDE read-out (de = 8, cde_hidden = H).  Three workgroups per CU (168 VGPRs)
+// for the ODE output, two for the CDE read-out (its weight slice is prefetched into registers).
 template <int H, int MODE>
-__global__ void __launch_bounds__(256, 3) k_rows(RowsArgs a) {
+__global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int ZS = rows_zs(H);
   constexpr int CT = H / 16;  // column tiles of a width-H operand / output
@@ -164,8 +165,9 @@ __global__ void __launch_bounds__(256, 3) k_rows(RowsArgs a) {
     const int RS = NP + 4;                 // LDS row stride of the rows block
     float* sAr = big + 2 * NP * kStrip;    // rows block A(t)[R, :] [16][RS], then dA/dt [16][RS]
     // 1. issue the rows block (thread = (row tid / 16, columns 4 (tid % 16) + 64 u): 256 coalesced bytes per row
-    //    and u) and every small load of the form (node-vector plane sums, time channel, data spline) at once; the
-    //    rows come from HBM, and the column strip below reads the same lines again from L2 (a group shares one XCD)
+    //    and u), the column strip and every small load of the form (node-vector plane sums, time channel, data
+    //    spline) at once: one memory round trip (L2 is cold at every launch, so the strip's second read of the
+    //    same lines is not cheaper later)
     const int rr = tid >> 4, cq = 4 * (tid & 15);
     floatx4 rc[4][4];
 #pragma unroll
@@ -174,6 +176,17 @@ __global__ void __launch_bounds__(256, 3) k_rows(RowsArgs a) {
       for (int q = 0; q < 4; ++q)
         rc[u][q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
                                                    crs, (int)((q * nn + (size_t)(r0 + rr) * n + cq + 64 * u) * 4), 0, 0));
+    // ... and the column strip [:, R] (thread = (node row kk, four strip columns)): both blocks in flight at once
+    const int c4 = 4 * (tid & 3);
+    floatx4 sc[4][4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int kk = (tid >> 2) + 64 * p;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        sc[p][q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   crs, (int)((q * nn + (size_t)kk * n + r0 + c4) * 4), 0, 0));
+    }
     const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
     const int nd = tid < n ? tid : n - 1;  // clamped indices + selects: no load inside a divergent branch
     float pv[3][4], pt[4];
@@ -207,18 +220,7 @@ __global__ void __launch_bounds__(256, 3) k_rows(RowsArgs a) {
           sAr[(16 + rr) * RS + c0 + e] = in ? dcubic(cc, f) : 0.f;
         }
     }
-    asm volatile("" ::: "memory");  // the strip's loads after the rows' (registers, and L2 reuse)
-    {  // 2. the column strip [:, R]: thread = (node row kk, four strip columns), Horner, transposed into LDS
-      const int c4 = 4 * (tid & 3);
-      floatx4 sc[4][4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int kk = (tid >> 2) + 64 * p;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          sc[p][q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     crs, (int)((q * nn + (size_t)kk * n + r0 + c4) * 4), 0, 0));
-      }
+    {  // 2. the column strip: Horner, transposed into LDS
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int kk = (tid >> 2) + 64 * p;
@@ -428,6 +430,17 @@ __global__ void __launch_bounds__(256, 3) k_rows(RowsArgs a) {
     }
     {  // the output layer
       const int l = L - 1;
+      // CDE: this wave's whole read-out weight slice (16 KB at h = 32) is requested before the barrier wait, the
+      // Z load and the product, so the L2 / MALL latency of W' (cold in every launch) hides behind them
+      constexpr int KP = MODE == 2 ? 4 / CT : 1, JP = 16 / KP;
+      const int ct = w % CT, kp = w / CT, j0 = kp * JP;
+      const floatx4* W4 = reinterpret_cast<const floatx4*>(a.wperm + (size_t)l * H * H);
+      floatx4 wv[MODE == 2 ? CT : 1][MODE == 2 ? JP : 1];
+      if constexpr (MODE == 2)
+#pragma unroll
+        for (int cc = 0; cc < CT; ++cc)
+#pragma unroll
+          for (int j = 0; j < JP; ++j) wv[cc][j] = W4[((ct * 16 + j0 + j) * CT + cc) * 64 + lane];
       load_z(l);
       product(l);
       if constexpr (MODE == 1) {  // ODE: dy[R] = tg (P W'^T + q b'^T)
@@ -442,35 +455,21 @@ __global__ void __launch_bounds__(256, 3) k_rows(RowsArgs a) {
         }
       } else {
         // CDE read-out: dy[R, m] = tg (sum_{c, j} P[., c] dX[., j] W'[16 m + j, c] + q sum_j b'[16 m + j] dX[., j])
-        constexpr int KP = 4 / CT, JP = 16 / KP;  // waves per channel tile (splitting j), j per wave
-        const int ct = w % CT, kp = w / CT, j0 = kp * JP;
-        const floatx4* W4 = reinterpret_cast<const floatx4*>(a.wperm + (size_t)l * H * H);
         const float* bl = a.bf + (size_t)l * H;
         const float* qrow = sRow + (2 * L + l) * 16;
         float dxr[JP];
 #pragma unroll
         for (int j = 0; j < JP; ++j) dxr[j] = sDx[lo * kStrip + j0 + j];
-        // steps of (c chunk, JH j's): the next step's W' operands are in flight while this step's MFMAs run, and
-        // even / odd j accumulate into two independent chains (the MFMA result latency is not exposed per step)
-        constexpr int JH = JP < 8 ? JP : 8, NH = JP / JH, NSTEP = CT * NH;
-        floatx4 wv[2][JH];
-        auto wload = [&](int step, floatx4 (&dst)[JH]) __attribute__((always_inline)) {
-          const int cc = step / NH, jh = step % NH;
-#pragma unroll
-          for (int j = 0; j < JH; ++j) dst[j] = W4[((ct * 16 + j0 + jh * JH + j) * CT + cc) * 64 + lane];
-        };
-        wload(0, wv[0]);
+        // even / odd j accumulate into two independent chains (the MFMA result latency is not exposed per j)
         floatx4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-        for (int step = 0; step < NSTEP; ++step) {
-          if (step + 1 < NSTEP) wload(step + 1, wv[(step + 1) & 1]);
-          const int cc = step / NH, jh = step % NH;
+        for (int cc = 0; cc < CT; ++cc) {
           const floatx4 pv = prow(cc);
 #pragma unroll
-          for (int j = 0; j < JH; ++j) {
-            const floatx4 av = pv * dxr[jh * JH + j];
+          for (int j = 0; j < JP; ++j) {
+            const floatx4 av = pv * dxr[j];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) acc2[j & 1] = mfma4(av[s], wv[step & 1][j][s], acc2[j & 1]);
+            for (int s = 0; s < 4; ++s) acc2[j & 1] = mfma4(av[s], wv[cc][j][s], acc2[j & 1]);
           }
         }
         floatx4 acc = acc2[0] + acc2[1];
@@ -523,10 +522,9 @@ bool find_inst(int H, int mode, Inst& out) {
     else if (H == 32) out = inst<32, 1>();
     else if (H == 64) out = inst<64, 1>();
     else return false;
-  } else {
+  } else {  // (the H = 64 read-out keeps the multi-kernel path: rows_supported)
     if (H == 16) out = inst<16, 2>();
     else if (H == 32) out = inst<32, 2>();
-    else if (H == 64) out = inst<64, 2>();
     else return false;
   }
   return true;
