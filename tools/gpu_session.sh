@@ -31,13 +31,13 @@ for step in "$@"; do
     bench8) run bench_quick 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     prof) (cd /tmp && run_dir="$ROOTDIR/gpurun_out/prof" && rm -rf "$run_dir" && \
            timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$run_dir" -o run -- \
-             python3 "$ROOTDIR/bench.py" --steps 20 --warmup 2 --no-cpu-baseline > "$ROOTDIR/gpurun_out/prof.log" 2>&1; \
+             python3 "$ROOTDIR/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --train-steps 0 > "$ROOTDIR/gpurun_out/prof.log" 2>&1; \
            rc=$?; echo "prof rc=$rc"; tail -n 5 "$ROOTDIR/gpurun_out/prof.log"; \
            case $rc in 124|134|137|139) exit $rc;; esac) || exit $? ;;
     pmc) for ctr in FETCH_SIZE WRITE_SIZE; do
            (cd /tmp && run_dir="$ROOTDIR/gpurun_out/pmc_$ctr" && rm -rf "$run_dir" && \
             timeout -k 10 900 rocprofv3 --pmc $ctr --output-format csv -d "$run_dir" -o run -- \
-              python3 "$ROOTDIR/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$ROOTDIR/gpurun_out/pmc_$ctr.log" 2>&1; \
+              python3 "$ROOTDIR/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --train-steps 0 > "$ROOTDIR/gpurun_out/pmc_$ctr.log" 2>&1; \
             rc=$?; echo "pmc $ctr rc=$rc"; tail -n 3 "$ROOTDIR/gpurun_out/pmc_$ctr.log"; \
             case $rc in 124|134|137|139) exit $rc;; esac) || exit $?
          done ;;
@@ -64,7 +64,7 @@ for step in "$@"; do
            i=$((i+1))
            (cd /tmp && run_dir="$ROOTDIR/gpurun_out/pmcsq_$i" && rm -rf "$run_dir" && \
             timeout -k 10 900 rocprofv3 --pmc $ctrs --output-format csv -d "$run_dir" -o run -- \
-              python3 "$ROOTDIR/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$ROOTDIR/gpurun_out/pmcsq_$i.log" 2>&1; \
+              python3 "$ROOTDIR/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --train-steps 0 > "$ROOTDIR/gpurun_out/pmcsq_$i.log" 2>&1; \
             rc=$?; echo "pmcsq $i rc=$rc"; tail -n 3 "$ROOTDIR/gpurun_out/pmcsq_$i.log"; \
             case $rc in 124|134|137|139) exit $rc;; esac) || exit $?
          done ;;
