@@ -94,11 +94,17 @@ enum { GNCDE_RK4 = 0, GNCDE_TSIT5 = 1 };
  *   BF16_STORAGE: as BF16, and `coef` holds bfloat16 values (same shape, uint16 storage): the operator spline's
  *                 input is quantised to bf16, halving the dominant HBM stream.  Results equal the fp32 reference
  *                 evaluated on the bf16-rounded coefficients.
- * Splines, reductions, the Linears, solver and epilogues stay fp32.  The bf16 modes always take the generic path.
+ *   BF16_MFMA:    `coef` in bfloat16 as for BF16_STORAGE, and EVERY matrix product — (I + Abar_l) diag(inv) Z, the
+ *                 Linears, the CDE read-out — on v_mfma_f32_16x16x32_bf16 with single-plane bf16 operands rounded
+ *                 from the fp32 values and fp32 accumulation (~2^-8 relative per operand: a genuinely bf16 solve, the
+ *                 throughput mode of config 5).  Only the one-launch evaluation runs it (gncde_rows.hip: n <= 256,
+ *                 one hidden width H in {16, 32, 64}, ODE output or the de = 8 read-out); other shapes return
+ *                 GNCDE_ERR_UNSUPPORTED.
+ * Splines, reductions, RMSNorm, solver and epilogues stay fp32.  The bf16 modes always take the generic path.
  * Their reverse mode (gncde_integrate_vjp*) is the fp32 discrete adjoint over the coefficients the forward read
  * (BF16_STORAGE: the bf16 planes widened exactly into the workspace head, which gncde_vjp_workspace_bytes
  * includes): the gradient of the bf16 solve to its own ~2^-16 product rounding. */
-enum { GNCDE_COMPUTE_FP32 = 0, GNCDE_COMPUTE_BF16 = 1, GNCDE_COMPUTE_BF16_STORAGE = 2 };
+enum { GNCDE_COMPUTE_FP32 = 0, GNCDE_COMPUTE_BF16 = 1, GNCDE_COMPUTE_BF16_STORAGE = 2, GNCDE_COMPUTE_BF16_MFMA = 3 };
 enum { GNCDE_CTRL_GRID = 0, GNCDE_CTRL_PID = 1 };
 enum { GNCDE_SAVE_T1 = 0, GNCDE_SAVE_STEPS = 1, GNCDE_SAVE_TS = 2 };
 /* GncdeSolver.flags.  GNCDE_FLAG_GENERIC: take the generic multi-kernel path in gncde_integrate AND the generic

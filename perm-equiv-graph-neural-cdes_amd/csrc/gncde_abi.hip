@@ -16,7 +16,7 @@ int validate_problem(const GncdeProblem* p) {
   for (int l = 0; l <= p->L; ++l)
     if (p->dims[l] <= 0) return GNCDE_ERR_SHAPE;
   if (!p->ts || !p->coef || !p->tcoef || !p->fusion || !p->params) return GNCDE_ERR_ARG;
-  if (p->compute < GNCDE_COMPUTE_FP32 || p->compute > GNCDE_COMPUTE_BF16_STORAGE) return GNCDE_ERR_ARG;
+  if (p->compute < GNCDE_COMPUTE_FP32 || p->compute > GNCDE_COMPUTE_BF16_MFMA) return GNCDE_ERR_ARG;
   if (p->cde_hidden > 0) {
     if (p->cde_embed <= 0 || !p->data_coef) return GNCDE_ERR_ARG;
     if (p->dims[p->L] != p->cde_hidden * p->cde_embed * 2) return GNCDE_ERR_SHAPE;
@@ -24,6 +24,8 @@ int validate_problem(const GncdeProblem* p) {
   } else if (p->cde_hidden < 0) {
     return GNCDE_ERR_SHAPE;
   }
+  // the single-plane bf16 mode exists only in the one-launch evaluation
+  if (p->compute == GNCDE_COMPUTE_BF16_MFMA && !rows_supported(*p)) return GNCDE_ERR_UNSUPPORTED;
   return GNCDE_OK;
 }
 
@@ -63,7 +65,9 @@ int validate_solver(const GncdeProblem* p, const GncdeSolver* s) {
 // bf16 pairs with fp32 accumulation (~2^-16 relative per product), and, for BF16_STORAGE, in reading the operator
 // coefficients as bfloat16.  Their reverse mode is the fp32 discrete adjoint over the coefficients that forward
 // read: the fp32 planes themselves (BF16), or the bf16 planes widened exactly into the head of the workspace
-// (BF16_STORAGE).  It is the gradient of the bf16 solve to the forward's own product rounding.
+// (BF16_STORAGE).  It is the gradient of the bf16 solve to the forward's own product rounding.  BF16_MFMA (single-plane
+// products, ~2^-8 per operand) gets the same fp32 adjoint over its widened coefficients, evaluated along the
+// trajectory the bf16 forward saved: the gradient of the fp32 solve on the bf16 input, not of the bf16 rounding.
 namespace {
 
 __global__ void k_widen_bf16(size_t N, const uint16_t* __restrict__ in, float* __restrict__ out) {
@@ -77,7 +81,7 @@ size_t coef_floats(const GncdeProblem& p) { return (size_t)p.B * (p.T - 1) * 4 *
 GncdeProblem fp32_view(const GncdeProblem& p, size_t& head) {
   GncdeProblem q = p;
   q.compute = GNCDE_COMPUTE_FP32;
-  head = p.compute == GNCDE_COMPUTE_BF16_STORAGE ? align_up(coef_floats(p) * sizeof(float), 256) : 0;
+  head = coef_is_bf16(p) ? align_up(coef_floats(p) * sizeof(float), 256) : 0;
   return q;
 }
 
@@ -133,7 +137,8 @@ int gncde_integrate_path(const GncdeProblem* prob, const GncdeSolver* solver, ch
   if (rc) return rc;
   if (!buf || buf_len == 0) return GNCDE_ERR_ARG;
   if (!use_fused(*prob, *solver, buf, buf_len))
-    snprintf(buf, buf_len, prob->compute != GNCDE_COMPUTE_FP32 ? "generic_bf16" : "generic");
+    snprintf(buf, buf_len,
+             prob->compute == GNCDE_COMPUTE_BF16_MFMA ? "rows_bf16" : prob->compute != GNCDE_COMPUTE_FP32 ? "generic_bf16" : "generic");
   return GNCDE_OK;
 }
 

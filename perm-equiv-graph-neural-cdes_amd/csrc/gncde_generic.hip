@@ -23,7 +23,7 @@ constexpr int kRedStride = 8;  // red[b][q][n]: r, rd, c, cd, diagA, diagdA, {s}
 // go to part[b][slab][2][n]; k_abar_all sums them over slabs (fixed order) and forms the totals.
 constexpr int kSlab = 16;
 
-// Coefficient storage: fp32, or bf16 (GNCDE_COMPUTE_BF16_STORAGE) widened on load.
+// Coefficient storage: fp32, or bf16 (GNCDE_COMPUTE_BF16_STORAGE / _BF16_MFMA) widened on load.
 __device__ __forceinline__ float coef_at(const float* c, size_t e) { return c[e]; }
 __device__ __forceinline__ float coef_at(const uint16_t* c, size_t e) {
   return __builtin_bit_cast(float, (uint32_t)c[e] << 16);
@@ -587,6 +587,11 @@ __global__ void k_grid_stats(int B, int method, const int32_t* __restrict__ nste
 
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
+__global__ void k_round_bf16(size_t N, const float* __restrict__ in, uint16_t* __restrict__ out) {
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += (size_t)gridDim.x * blockDim.x)
+    out[e] = __builtin_bit_cast(uint16_t, (__bf16)in[e]);
+}
+
 // (I + Abar_l) of layer l: [B, n, n] fp32, or the hi plane of its bf16 (hi, lo) pair (bf16 modes: planes
 // [L, B, n, n] of uint16 each, the lo plane L*B*n*n elements after the hi plane — the fp32 buffer's bytes)
 inline const float* abar_layer(const GncdeProblem& p, const float* abar, int l) {
@@ -597,6 +602,7 @@ inline const float* abar_layer(const GncdeProblem& p, const float* abar, int l) 
 
 struct VfWs {
   float *csum, *tg, *Z0, *Z1, *m, *abar, *wf, *wp, *bf, *inv, *q, *dx;
+  uint16_t* wbf;   // GNCDE_COMPUTE_BF16_MFMA: W' per layer rounded to bfloat16, natural layout
   unsigned* sync;  // one-launch evaluation: per-group arrival counters [B] + the fault word, zeroed per solve
 };
 
@@ -627,6 +633,7 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.q = take((size_t)p.L * B * n);                          // q_l = (I + Abar_l) 1
   w.dx = take(B * n * (size_t)(p.cde_hidden > 0 ? 2 * p.cde_embed : 1));  // data-spline derivative at t
   w.sync = reinterpret_cast<unsigned*>(take(B + 4));
+  w.wbf = reinterpret_cast<uint16_t*>(take(p.compute == GNCDE_COMPUTE_BF16_MFMA ? (wsum + 1) / 2 : 1));
   return off;
 }
 
@@ -648,7 +655,7 @@ void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float*
   const unsigned slabs = cdiv(n, kSlab);
   const bool bf16 = p.compute != GNCDE_COMPUTE_FP32;
   float* dxo = p.cde_hidden > 0 ? dx : nullptr;
-  if (p.compute == GNCDE_COMPUTE_BF16_STORAGE)
+  if (coef_is_bf16(p))
     hipLaunchKernelGGL(k_spline_slab<uint16_t>, dim3(slabs, B), dim3(256), 0, st, n, p.T, p.ts,
                        reinterpret_cast<const uint16_t*>(p.coef), p.tcoef, t, A, dA, tg, red, part, p.data_coef,
                        2 * p.cde_embed, dxo);
@@ -674,7 +681,7 @@ void vf_forms_direct(const GncdeProblem& p, const float* t, const float* csum, f
   float* dxo = p.cde_hidden > 0 ? dx : nullptr;
   const size_t ls = (size_t)B * n * n;
   const bool bf16 = p.compute != GNCDE_COMPUTE_FP32;
-  if (p.compute == GNCDE_COMPUTE_BF16_STORAGE)
+  if (coef_is_bf16(p))
     hipLaunchKernelGGL((k_abar_direct<uint16_t, uint16_t>), grid, dim3(256), 0, st, n, p.T, p.L, p.ts,
                        reinterpret_cast<const uint16_t*>(p.coef), csum, p.tcoef, t, p.fusion,
                        reinterpret_cast<uint16_t*>(abar), ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B);
@@ -698,22 +705,30 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
   carve_vf(p, ws, w);
   (void)hipMemsetAsync(w.sync, 0, ((size_t)p.B + 4) * sizeof(unsigned), st);
   const dim3 gs(4, p.T - 1, p.B);
-  if (p.compute == GNCDE_COMPUTE_BF16_STORAGE)
+  if (coef_is_bf16(p))
     hipLaunchKernelGGL(k_coef_sums<uint16_t>, gs, dim3(256), 0, st, p.n, p.T,
                        reinterpret_cast<const uint16_t*>(p.coef), w.csum);
   else
     hipLaunchKernelGGL(k_coef_sums<float>, gs, dim3(256), 0, st, p.n, p.T, p.coef, w.csum);
+  const bool rows = rows_supported(p);
   size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
     const LayerOffsets o = layer_offsets(p, l);
     fold_linear(din, dout, p.params + o.rms_w, p.params + o.rms_b, p.params + o.W, p.params + o.b, w.wf + wo,
                 w.bf + bo, st);
+    // W' in the MFMA operand order for every layer the evaluation runs through an operand-ordered kernel: all of
+    // them on the one-launch path (whatever k_layer's own LDS envelope says), else k_layer's layers
+    const bool cde_out = p.cde_hidden > 0 && l == p.L - 1;
     const int mode = layer_mode(p, l);
-    if (mode >= 0) permute_linear(dout, din, mode == 2, w.wf + wo, w.wp + wo, st);
+    if (rows) permute_linear(dout, din, cde_out, w.wf + wo, w.wp + wo, st);
+    else if (mode >= 0) permute_linear(dout, din, mode == 2, w.wf + wo, w.wp + wo, st);
     wo += (size_t)din * dout;
     bo += dout;
   }
+  if (p.compute == GNCDE_COMPUTE_BF16_MFMA)
+    hipLaunchKernelGGL(k_round_bf16, dim3(cdiv(wo, 256) < 4096 ? cdiv(wo, 256) : 4096), dim3(256), 0, st, wo, w.wf,
+                       w.wbf);
 }
 
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
@@ -730,7 +745,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
       bars = &local;
     }
     // (the workspace holds no (I + Abar_l) planes for these problems: there is no multi-kernel fallback here)
-    return rows_vf_eval(p, t, y, dy, w.csum, w.wp, w.bf, w.Z0, w.Z1, w.sync, reinterpret_cast<int*>(w.sync + B), *bars,
+    return rows_vf_eval(p, t, y, dy, w.csum, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync, reinterpret_cast<int*>(w.sync + B), *bars,
                         st);
   }
   vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st);

@@ -182,8 +182,12 @@ const int* generic_vf_fault(const GncdeProblem& p, char* ws);
 
 // one-launch evaluation for one hidden width and n <= 256 (configs 3 / 5): gncde_rows.hip
 bool rows_supported(const GncdeProblem& p);
+// coefficients stored as bfloat16 (GNCDE_COMPUTE_BF16_STORAGE, GNCDE_COMPUTE_BF16_MFMA)
+inline bool coef_is_bf16(const GncdeProblem& p) {
+  return p.compute == GNCDE_COMPUTE_BF16_STORAGE || p.compute == GNCDE_COMPUTE_BF16_MFMA;
+}
 int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum,
-                 const float* wperm, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
+                 const float* wperm, const uint16_t* wbf, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
                  unsigned& bars_done, hipStream_t st);
 int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
                       int32_t* stats, char* ws, hipStream_t st);

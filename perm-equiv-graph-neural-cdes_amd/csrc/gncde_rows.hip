@@ -35,21 +35,23 @@ namespace {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned rows (n = 129, 255)
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kRB = 16;      // node rows per workgroup
-constexpr int kMaxN = 256;   // four 16-column K chunks per wave
-constexpr int kNJ = kMaxN / 64;
+constexpr int kMaxN = 256;   // per wave: four 16-column K chunks (fp32) or two 32-column chunks (bf16)
 constexpr int kStrip = 17;   // LDS row stride of the transposed column strip
 
 struct RowsArgs {
   int B, n, T, L, G, rounds, nb, big;  // big: floats of the LDS region shared by the strip, Z_l and the partials
+  int np;                  // n rounded up to the K chunk (16 fp32, 32 bf16)
   const float* ts;
-  const float* coef;       // [B, T-1, 4, n, n]
+  const void* coef;        // [B, T-1, 4, n, n] fp32, or bfloat16 (GNCDE_COMPUTE_BF16_MFMA)
   const float* csum;       // k_coef_sums: [B, T-1, 12 n + 4]
   const float* tcoef;      // [B, T-1, 3, n]
   const float* data_coef;  // [B, T-1, 4, n, 8, 2] (CDE)
   const float* fusion;     // [L, GNCDE_FC]
   const float* wperm;      // W' per layer in the MFMA lane order (permute_linear), back to back
+  const uint16_t* wbf;     // bf16 mode: W' per layer as bfloat16 in its natural [d_out, d_in] layout
   const float* bf;         // b' per layer, back to back
   const float* t;          // [B] evaluation times
   const float* y;          // [B, n, H] stage inputs
@@ -63,23 +65,50 @@ struct RowsArgs {
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ floatx4 mfma_bf(bf16x8 a, bf16x8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float bf2f(unsigned u, int half) {  // element `half` (0 low, 1 high) of a bf16 pair
+  return __builtin_bit_cast(float, half ? (u & 0xffff0000u) : (u << 16));
+}
 __device__ __forceinline__ float cubic(const float (&c)[4], float f) { return fmaf(f, fmaf(f, fmaf(f, c[0], c[1]), c[2]), c[3]); }
 __device__ __forceinline__ float dcubic(const float (&c)[4], float f) {
   return fmaf(f, fmaf(3.0f * f, c[0], 2.0f * c[1]), c[2]);
 }
 
+// 8 bf16 at element `e` of a buffer: the 16-byte load at the dword boundary at or below e and the next dword,
+// funnel-shifted by one element when e is odd (odd n puts rows at 2-byte boundaries; every load stays dword-aligned)
+__device__ __forceinline__ u32x4 load8_bf16(__amdgpu_buffer_rsrc_t r, int e) {
+  const int e0 = e & ~1;
+  const unsigned sh = (unsigned)(e & 1) * 16u;
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, e0 * 2, 0, 0);
+  const unsigned x = __builtin_amdgcn_raw_buffer_load_b32(r, e0 * 2 + 16, 0, 0);
+  return u32x4{__builtin_amdgcn_alignbit(v[1], v[0], sh), __builtin_amdgcn_alignbit(v[2], v[1], sh),
+               __builtin_amdgcn_alignbit(v[3], v[2], sh), __builtin_amdgcn_alignbit(x, v[3], sh)};
+}
+
+// element e of a 16-byte coefficient load as fp32 (fp32: element e; bf16: half e % 2 of dword e / 2)
+template <bool BF>
+__device__ __forceinline__ float coef_el(u32x4 v, int e) {
+  if constexpr (BF) return bf2f(v[e >> 1], e & 1);
+  else {
+    const unsigned x = v[e];  // (a vector element, not the vector: bit_cast of `v[e]` itself reads element 0)
+    return __builtin_bit_cast(float, x);
+  }
+}
+
 __host__ __device__ constexpr int rows_zs(int H) { return H + 4; }
-__host__ __device__ inline int rows_np(int n) { return (n + 15) & ~15; }
+__host__ __device__ inline int rows_np(int n, bool bf) { return bf ? (n + 31) & ~31 : (n + 15) & ~15; }
 // floats of the shared region: the strip [2][NP][17] and the rows block [2][16][NP+4] during the form, then Z_l
 // [NP][H+4] and the partials [4][16][H+4]
-__host__ __device__ inline int rows_big(int n, int H) {
-  const int np = rows_np(n), z = (np > 64 ? np : 64) * rows_zs(H), s = 2 * np * kStrip + 32 * (np + 4);
+__host__ __device__ inline int rows_big(int n, int H, bool bf) {
+  const int np = rows_np(n, bf), z = (np > 64 ? np : 64) * rows_zs(H), s = 2 * np * kStrip + 32 * (np + 4);
   return ((z > s ? z : s) + 3) & ~3;
 }
-inline size_t rows_smem(int n, int H, int L) {
-  const int np = rows_np(n);
+inline size_t rows_smem(int n, int H, int L, bool bf) {
+  const int np = rows_np(n, bf);
   // big | inv [NP] | v_l [L][NP] | w, u, q [3][L][16] | tg [16] | dX [16][17] | out tile [16][H+4] | red [4][64] x4
-  return sizeof(float) * ((size_t)rows_big(n, H) + np + (size_t)L * np + 48 * L + 16 + 16 * kStrip + 16 * rows_zs(H) +
+  return sizeof(float) * ((size_t)rows_big(n, H, bf) + np + (size_t)L * np + 48 * L + 16 + 16 * kStrip + 16 * rows_zs(H) +
                           4 * 64 * 4 + 4);
 }
 
@@ -89,13 +118,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
 
 // MODE 1: ODE output layer.  MODE 2: CDE read-out (de = 8, cde_hidden = H).  Three workgroups per CU (168 VGPRs)
 // for the ODE output, two for the CDE read-out (its weight slice is prefetched into registers).
-template <int H, int MODE>
+// BF (GNCDE_COMPUTE_BF16_MFMA): bfloat16 coefficients, and every product — (I + Abar_l) diag(inv) Z, the Linears, the
+// read-out — on v_mfma_f32_16x16x32_bf16 with single-plane bf16 operands rounded from the fp32 values (fp32
+// accumulation); the spline, the reductions, RMSNorm and all sums outside the MFMAs stay fp32.
+template <int H, int MODE, bool BF>
 __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int ZS = rows_zs(H);
-  constexpr int CT = H / 16;  // column tiles of a width-H operand / output
+  constexpr int CT = H / 16;           // column tiles of a width-H operand / output
+  constexpr int KW = BF ? 32 : 16;     // K chunk of one MFMA step
+  constexpr int EL = KW / 4;           // consecutive k per lane per chunk
+  constexpr int NJ = kMaxN / (4 * KW);  // chunks per wave
+  constexpr int KC = (H + 31) / 32;    // bf16: 32-deep K chunks of a width-H contraction
   const int n = a.n, L = a.L, nb = a.nb, T = a.T;
-  const int NP = rows_np(n), nch = NP >> 4;
+  const int NP = a.np, nch = NP / KW;
   float* big = sm;
   float* sInv = big + a.big;
   float* sV = sInv + NP;
@@ -155,37 +191,46 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
     const float* tsb = a.ts + (size_t)b * T;
     const int idx = interval_index(tsb, T, tb);
     const float f = tb - tsb[idx];
-    const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
+    using CT_ = typename std::conditional<BF, uint16_t, float>::type;
+    const CT_* cb = reinterpret_cast<const CT_*>(a.coef) + ((size_t)b * (T - 1) + idx) * 4 * nn;
 
     // ---- form ---------------------------------------------------------------------------------------------------
     // Both coefficient reads are unconditional coalesced dwordx4 buffer loads from this (sample, interval)'s four
     // planes (the descriptor's range check zero-fills anything past plane a); values outside the matrix are
     // selected to 0 before they reach LDS, so no load sits in a divergent branch.
-    const auto crs = rsrc(cb, (unsigned)(4 * nn * sizeof(float)));
+    const auto crs = rsrc(cb, (unsigned)(4 * nn * sizeof(CT_)));
     const int RS = NP + 4;                 // LDS row stride of the rows block
     float* sAr = big + 2 * NP * kStrip;    // rows block A(t)[R, :] [16][RS], then dA/dt [16][RS]
     // 1. issue the rows block (thread = (row tid / 16, columns 4 (tid % 16) + 64 u): 256 coalesced bytes per row
     //    and u), the column strip and every small load of the form (node-vector plane sums, time channel, data
     //    spline) at once: one memory round trip (L2 is cold at every launch, so the strip's second read of the
     //    same lines is not cheaper later)
-    const int rr = tid >> 4, cq = 4 * (tid & 15);
-    floatx4 rc[4][4];
+    const int rr = tid >> 4;
+    // fp32: 4 columns per 16-byte load (rows: 4 (tid % 16) + 64 u, u < 4; strip: node kk = tid / 4 + 64 p, p < 4,
+    // columns 4 (tid % 4)); bf16: 8 per load (rows: 8 (tid % 16) + 128 u, u < 2; strip: kk = tid / 2 + 128 p,
+    // p < 2, columns 8 (tid % 2))
+    constexpr int CE = BF ? 8 : 4, NU = BF ? 2 : 4;
+    const int cq = CE * (tid & 15), c4 = CE * (tid & (BF ? 1 : 3));
+    u32x4 rc[NU][4], sc[NU][4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        rc[u][q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   crs, (int)((q * nn + (size_t)(r0 + rr) * n + cq + 64 * u) * 4), 0, 0));
-    // ... and the column strip [:, R] (thread = (node row kk, four strip columns)): both blocks in flight at once
-    const int c4 = 4 * (tid & 3);
-    floatx4 sc[4][4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int kk = (tid >> 2) + 64 * p;
+    for (int u = 0; u < NU; ++u)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        sc[p][q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   crs, (int)((q * nn + (size_t)kk * n + r0 + c4) * 4), 0, 0));
+      {
+        const int e = (int)(q * nn + (size_t)(r0 + rr) * n + cq + 16 * CE * u);
+        if constexpr (BF) rc[u][q] = load8_bf16(crs, e);
+        else rc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, e * 4, 0, 0);
+      }
+#pragma unroll
+    for (int p = 0; p < NU; ++p) {
+      const int kk = (tid >> (BF ? 1 : 2)) + (BF ? 128 : 64) * p;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+      {
+        const int e = (int)(q * nn + (size_t)kk * n + r0 + c4);
+        if constexpr (BF) sc[p][q] = load8_bf16(crs, e);
+        else sc[p][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, e * 4, 0, 0);
+      }
     }
     const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
     const int nd = tid < n ? tid : n - 1;  // clamped indices + selects: no load inside a divergent branch
@@ -209,26 +254,27 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
       dcv[2] = dc[2 * blk];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int c0 = cq + 64 * u;
+    for (int u = 0; u < NU; ++u) {
+      const int c0 = cq + 16 * CE * u;
       if (c0 < NP)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < CE; ++e) {
           const bool in = r0 + rr < n && c0 + e < n;
-          const float cc[4] = {rc[u][0][e], rc[u][1][e], rc[u][2][e], rc[u][3][e]};
+          const float cc[4] = {coef_el<BF>(rc[u][0], e), coef_el<BF>(rc[u][1], e), coef_el<BF>(rc[u][2], e), coef_el<BF>(rc[u][3], e)};
           sAr[rr * RS + c0 + e] = in ? cubic(cc, f) : 0.f;
           sAr[(16 + rr) * RS + c0 + e] = in ? dcubic(cc, f) : 0.f;
         }
     }
     {  // 2. the column strip: Horner, transposed into LDS
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int kk = (tid >> 2) + 64 * p;
+      for (int p = 0; p < NU; ++p) {
+        const int kk = (tid >> (BF ? 1 : 2)) + (BF ? 128 : 64) * p;
         if (kk < NP)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
+          for (int e = 0; e < CE; ++e) {
             const bool in = kk < n && r0 + c4 + e < n;
-            const float cc[4] = {sc[p][0][e], sc[p][1][e], sc[p][2][e], sc[p][3][e]};
+            const float cc[4] = {coef_el<BF>(sc[p][0], e), coef_el<BF>(sc[p][1], e), coef_el<BF>(sc[p][2], e),
+                                 coef_el<BF>(sc[p][3], e)};
             big[kk * kStrip + c4 + e] = in ? cubic(cc, f) : 0.f;
             big[(NP + kk) * kStrip + c4 + e] = in ? dcubic(cc, f) : 0.f;
           }
@@ -271,20 +317,27 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
     }
     __syncthreads();
     // the product's A-operand elements of this lane: (I + Abar)[ri][k] needs A, dA at (ri, k) and at (k, ri), for
-    // k = 16 kc + 4 hi + s, kc = w + 4 j (chunks past the matrix read zeros)
-    float Ar[kNJ][4], dAr[kNJ][4], At[kNJ][4], dAt[kNJ][4];
+    // k = KW kc + EL hi + e, kc = w + 4 j (chunks past the matrix read zeros)
+    float Ar[NJ][EL], dAr[NJ][EL], At[NJ][EL], dAt[NJ][EL];
 #pragma unroll
-    for (int j = 0; j < kNJ; ++j) {
-      const int kc = w + 4 * j, k0 = 16 * kc + 4 * hi;
+    for (int j = 0; j < NJ; ++j) {
+      const int kc = w + 4 * j, k0 = KW * kc + EL * hi;
       const bool in = kc < nch;
-      const floatx4 ar = in ? *reinterpret_cast<const floatx4*>(sAr + lo * RS + k0) : floatx4{0.f, 0.f, 0.f, 0.f};
-      const floatx4 dr = in ? *reinterpret_cast<const floatx4*>(sAr + (16 + lo) * RS + k0) : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        Ar[j][s] = ar[s];
-        dAr[j][s] = dr[s];
-        At[j][s] = in ? big[(k0 + s) * kStrip + lo] : 0.f;
-        dAt[j][s] = in ? big[(NP + k0 + s) * kStrip + lo] : 0.f;
+      for (int e4 = 0; e4 < EL; e4 += 4) {
+        const floatx4 ar = in ? *reinterpret_cast<const floatx4*>(sAr + lo * RS + k0 + e4) : floatx4{0.f, 0.f, 0.f, 0.f};
+        const floatx4 dr =
+            in ? *reinterpret_cast<const floatx4*>(sAr + (16 + lo) * RS + k0 + e4) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          Ar[j][e4 + e] = ar[e];
+          dAr[j][e4 + e] = dr[e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EL; ++e) {
+        At[j][e] = in ? big[(k0 + e) * kStrip + lo] : 0.f;
+        dAt[j][e] = in ? big[(NP + k0 + e) * kStrip + lo] : 0.f;
       }
     }
     __syncthreads();  // the strip's region becomes Z_l
@@ -355,24 +408,49 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < kNJ; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const int kc = w + 4 * j;
         if (kc >= nch) break;
-        const int k0 = 16 * kc + 4 * hi;
-        const floatx4 vk = *reinterpret_cast<const floatx4*>(sV + l * NP + k0);
-        const floatx4 iv = *reinterpret_cast<const floatx4*>(sInv + k0);
-        float bz[4][CT];
+        const int k0 = KW * kc + EL * hi;
+        float vk[EL], iv[EL];
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int e4 = 0; e4 < EL; e4 += 4) {
+          const floatx4 v4 = *reinterpret_cast<const floatx4*>(sV + l * NP + k0 + e4);
+          const floatx4 i4 = *reinterpret_cast<const floatx4*>(sInv + k0 + e4);
 #pragma unroll
-          for (int ct = 0; ct < CT; ++ct) bz[s][ct] = Zs[(k0 + s) * ZS + 16 * ct + lo];
+          for (int e = 0; e < 4; ++e) {
+            vk[e4 + e] = v4[e];
+            iv[e4 + e] = i4[e];
+          }
+        }
+        float op[EL];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          float v = fmaf(eA, Ar[j][s], fmaf(edA, dAr[j][s], fmaf(eTA, At[j][s], fmaf(eTdA, dAt[j][s], wl + vk[s]))));
-          if (k0 + s == ri) v += ul;
-          const float op = v * iv[s];
+        for (int e = 0; e < EL; ++e) {
+          float v = fmaf(eA, Ar[j][e], fmaf(edA, dAr[j][e], fmaf(eTA, At[j][e], fmaf(eTdA, dAt[j][e], wl + vk[e]))));
+          if (k0 + e == ri) v += ul;
+          op[e] = v * iv[e];
+        }
+        if constexpr (BF) {
+          bf16x8 av;
 #pragma unroll
-          for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma4(op, bz[s][ct], acc[ct]);
+          for (int e = 0; e < 8; ++e) av[e] = (__bf16)op[e];
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) {
+            bf16x8 bv;  // Z_l column 16 ct + lo, rows k0 .. k0 + 7
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bv[e] = (__bf16)Zs[(k0 + e) * ZS + 16 * ct + lo];
+            acc[ct] = mfma_bf(av, bv, acc[ct]);
+          }
+        } else {
+          float bz[EL][CT];
+#pragma unroll
+          for (int e = 0; e < EL; ++e)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) bz[e][ct] = Zs[(k0 + e) * ZS + 16 * ct + lo];
+#pragma unroll
+          for (int e = 0; e < EL; ++e)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma4(op[e], bz[e][ct], acc[ct]);
         }
       }
       __syncthreads();  // every Z_l read done: the partials alias it
@@ -383,22 +461,55 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
       __syncthreads();
     };
     // P row lo, columns 16 cc + 4 hi .. + 3: the four K parts in a fixed order
-    auto prow = [&](int cc) -> floatx4 {
-      const float* p = big + lo * ZS + 16 * cc + 4 * hi;
+    auto psum4 = [&](int c) -> floatx4 {
+      const float* p = big + lo * ZS + c;
       floatx4 v = *reinterpret_cast<const floatx4*>(p);
 #pragma unroll
       for (int kp = 1; kp < 4; ++kp) v += *reinterpret_cast<const floatx4*>(p + kp * 16 * ZS);
       return v;
     };
+    auto prow = [&](int cc) -> floatx4 { return psum4(16 * cc + 4 * hi); };
+    // bf16: P[lo][32 cc + 8 hi .. + 7] (zero past H) as the A operand of a 16x16x32 step
+    auto prow8 = [&](int cc, float (&x)[8]) {
+      const int c0 = 32 * cc + 8 * hi;
+      const bool in = c0 < H;
+      const floatx4 p0 = psum4(in ? c0 : 0), p1 = psum4(in ? c0 + 4 : 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[e] = in ? p0[e] : 0.f;
+        x[4 + e] = in ? p1[e] : 0.f;
+      }
+    };
+    auto prow_bf = [&](int cc) -> bf16x8 {
+      float x[8];
+      prow8(cc, x);
+      bf16x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (__bf16)x[e];
+      return v;
+    };
+    // a bf16 W' operand: row r of the natural [rows, H] layout, columns 32 cc + 8 hi .. + 7 (zero past H)
+    auto wrow_bf = [&](const uint16_t* Wl, int r, int cc) -> bf16x8 {
+      const int c0 = 32 * cc + 8 * hi;
+      u32x4 u = {0u, 0u, 0u, 0u};
+      if (c0 < H) u = *reinterpret_cast<const u32x4*>(Wl + (size_t)r * H + c0);
+      return __builtin_bit_cast(bf16x8, u);
+    };
     // P W'^T + q b'^T for output tile `tile` (rows R, columns 16 tile + lo): acc[r] = row 4 hi + r
     auto linear = [&](int l, int tile) __attribute__((always_inline)) -> floatx4 {
-      const floatx4* W4 = reinterpret_cast<const floatx4*>(a.wperm + (size_t)l * H * H);
       floatx4 accL = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (BF) {
+        const uint16_t* Wl = a.wbf + (size_t)l * H * H;
 #pragma unroll
-      for (int cc = 0; cc < CT; ++cc) {
-        const floatx4 pv = prow(cc), wv = W4[(tile * CT + cc) * 64 + lane];
+        for (int cc = 0; cc < KC; ++cc) accL = mfma_bf(prow_bf(cc), wrow_bf(Wl, 16 * tile + lo, cc), accL);
+      } else {
+        const floatx4* W4 = reinterpret_cast<const floatx4*>(a.wperm + (size_t)l * H * H);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) accL = mfma4(pv[s], wv[s], accL);
+        for (int cc = 0; cc < CT; ++cc) {
+          const floatx4 pv = prow(cc), wv = W4[(tile * CT + cc) * 64 + lane];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) accL = mfma4(pv[s], wv[s], accL);
+        }
       }
       const float bc = a.bf[l * H + 16 * tile + lo];
       const float* qrow = sRow + (2 * L + l) * 16;
@@ -435,12 +546,22 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
       constexpr int KP = MODE == 2 ? 4 / CT : 1, JP = 16 / KP;
       const int ct = w % CT, kp = w / CT, j0 = kp * JP;
       const floatx4* W4 = reinterpret_cast<const floatx4*>(a.wperm + (size_t)l * H * H);
-      floatx4 wv[MODE == 2 ? CT : 1][MODE == 2 ? JP : 1];
-      if constexpr (MODE == 2)
+      constexpr bool F32R = MODE == 2 && !BF, BFR = MODE == 2 && BF;
+      floatx4 wv[F32R ? CT : 1][F32R ? JP : 1];
+      // bf16: W'[16 m + j, 32 cc + 8 hi ..], m = 16 ct + lo; at H = 64 the first K chunk (64 VGPRs) is prefetched,
+      // the second is requested after the product
+      constexpr int KPF = H == 64 ? 1 : KC;
+      bf16x8 wb[BFR ? KC : 1][BFR ? JP : 1];
+      if constexpr (F32R)
 #pragma unroll
         for (int cc = 0; cc < CT; ++cc)
 #pragma unroll
           for (int j = 0; j < JP; ++j) wv[cc][j] = W4[((ct * 16 + j0 + j) * CT + cc) * 64 + lane];
+      if constexpr (BFR)
+#pragma unroll
+        for (int cc = 0; cc < KPF; ++cc)
+#pragma unroll
+          for (int j = 0; j < JP; ++j) wb[cc][j] = wrow_bf(a.wbf + (size_t)l * H * H, 16 * (16 * ct + lo) + j0 + j, cc);
       load_z(l);
       product(l);
       if constexpr (MODE == 1) {  // ODE: dy[R] = tg (P W'^T + q b'^T)
@@ -462,14 +583,33 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
         for (int j = 0; j < JP; ++j) dxr[j] = sDx[lo * kStrip + j0 + j];
         // even / odd j accumulate into two independent chains (the MFMA result latency is not exposed per j)
         floatx4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+        if constexpr (BF) {
 #pragma unroll
-        for (int cc = 0; cc < CT; ++cc) {
-          const floatx4 pv = prow(cc);
+          for (int cc = KPF; cc < KC; ++cc)
 #pragma unroll
-          for (int j = 0; j < JP; ++j) {
-            const floatx4 av = pv * dxr[j];
+            for (int j = 0; j < JP; ++j) wb[cc][j] = wrow_bf(a.wbf + (size_t)l * H * H, 16 * (16 * ct + lo) + j0 + j, cc);
 #pragma unroll
-            for (int s = 0; s < 4; ++s) acc2[j & 1] = mfma4(av[s], wv[cc][j][s], acc2[j & 1]);
+          for (int cc = 0; cc < KC; ++cc) {
+            float pf[8];
+            prow8(cc, pf);
+#pragma unroll
+            for (int j = 0; j < JP; ++j) {
+              bf16x8 av;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) av[e] = (__bf16)(pf[e] * dxr[j]);
+              acc2[j & 1] = mfma_bf(av, wb[cc][j], acc2[j & 1]);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int cc = 0; cc < CT; ++cc) {
+            const floatx4 pv = prow(cc);
+#pragma unroll
+            for (int j = 0; j < JP; ++j) {
+              const floatx4 av = pv * dxr[j];
+#pragma unroll
+              for (int s = 0; s < 4; ++s) acc2[j & 1] = mfma4(av[s], wv[cc][j][s], acc2[j & 1]);
+            }
           }
         }
         floatx4 acc = acc2[0] + acc2[1];
@@ -506,29 +646,36 @@ struct Inst {
   void (*launch)(const RowsArgs&, int, size_t, hipStream_t);
 };
 
-template <int H, int MODE>
+template <int H, int MODE, bool BF>
 void launch_rows(const RowsArgs& a, int grid, size_t smem, hipStream_t st) {
-  hipLaunchKernelGGL((k_rows<H, MODE>), dim3(grid), dim3(256), smem, st, a);
+  hipLaunchKernelGGL((k_rows<H, MODE, BF>), dim3(grid), dim3(256), smem, st, a);
 }
 
-template <int H, int MODE>
+template <int H, int MODE, bool BF>
 Inst inst() {
-  return Inst{reinterpret_cast<const void*>(&k_rows<H, MODE>), &launch_rows<H, MODE>};
+  return Inst{reinterpret_cast<const void*>(&k_rows<H, MODE, BF>), &launch_rows<H, MODE, BF>};
 }
 
-bool find_inst(int H, int mode, Inst& out) {
+template <bool BF>
+bool find_inst_t(int H, int mode, Inst& out) {
   if (mode == 1) {
-    if (H == 16) out = inst<16, 1>();
-    else if (H == 32) out = inst<32, 1>();
-    else if (H == 64) out = inst<64, 1>();
+    if (H == 16) out = inst<16, 1, BF>();
+    else if (H == 32) out = inst<32, 1, BF>();
+    else if (H == 64) out = inst<64, 1, BF>();
     else return false;
-  } else {  // (the H = 64 read-out keeps the multi-kernel path: rows_supported)
-    if (H == 16) out = inst<16, 2>();
-    else if (H == 32) out = inst<32, 2>();
-    else return false;
+  } else {
+    if (H == 16) out = inst<16, 2, BF>();
+    else if (H == 32) out = inst<32, 2, BF>();
+    else if constexpr (BF) {  // (fp32: the H = 64 read-out keeps the multi-kernel path)
+      if (H == 64) out = inst<64, 2, BF>();
+      else return false;
+    } else {
+      return false;
+    }
   }
   return true;
 }
+bool find_inst(int H, int mode, bool bf, Inst& out) { return bf ? find_inst_t<true>(H, mode, out) : find_inst_t<false>(H, mode, out); }
 
 // workgroups of one instance resident per CU at this LDS size (occupancy query, cached per device) x CUs
 int resident_blocks(const Inst& k, size_t smem) {
@@ -564,13 +711,17 @@ int resident_blocks(const Inst& k, size_t smem) {
 // x h): every 16-row workgroup streams all of it and its fp32 MFMA chain dominates the launch (config 3 measured
 // 81 us per evaluation against 70 us for the multi-kernel path, whose read-out launch splits 32-row blocks over
 // channel halves), so that shape keeps the multi-kernel path.
+// GNCDE_COMPUTE_BF16_MFMA runs only here (every shape of the envelope, the H = 64 read-out included: its bf16 MFMA
+// chain is an eighth of the fp32 one).
 bool rows_supported(const GncdeProblem& p) {
-  if (p.compute != GNCDE_COMPUTE_FP32 || p.n > kMaxN || p.n < 1) return false;
+  const bool bf = p.compute == GNCDE_COMPUTE_BF16_MFMA;
+  if ((p.compute != GNCDE_COMPUTE_FP32 && !bf) || p.n > kMaxN || p.n < 1) return false;
   const int H = p.dims[0];
   if (H != 16 && H != 32 && H != 64) return false;
   for (int l = 0; l < p.L; ++l)
     if (p.dims[l] != H) return false;
-  if (p.cde_hidden > 0) return p.cde_embed == 8 && p.cde_hidden == H && H <= 32 && p.dims[p.L] == 16 * H;
+  if (p.cde_hidden > 0)
+    return p.cde_embed == 8 && p.cde_hidden == H && (H <= 32 || bf) && p.dims[p.L] == 16 * H;
   return p.dims[p.L] == H;
 }
 
@@ -578,12 +729,13 @@ size_t rows_sync_ints(const GncdeProblem& p) { return align_up((size_t)p.B + 4, 
 
 // Launch one evaluation (RowsState: the group layout, fixed per problem, and the barriers done so far).
 int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum,
-                 const float* wperm, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
+                 const float* wperm, const uint16_t* wbf, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
                  unsigned& bars_done, hipStream_t st) {
   Inst k;
   const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
-  if (!find_inst(H, mode, k)) return GNCDE_ERR_UNSUPPORTED;
-  const size_t smem = rows_smem(p.n, H, p.L);
+  const bool bfm = p.compute == GNCDE_COMPUTE_BF16_MFMA;
+  if (!find_inst(H, mode, bfm, k)) return GNCDE_ERR_UNSUPPORTED;
+  const size_t smem = rows_smem(p.n, H, p.L, bfm);
   const int nb = (p.n + kRB - 1) / kRB;
   const int cap = resident_blocks(k, smem);
   int G = cap / nb;
@@ -601,7 +753,8 @@ int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* d
   a.G = G;
   a.rounds = (p.B + G - 1) / G;
   a.nb = nb;
-  a.big = rows_big(p.n, H);
+  a.big = rows_big(p.n, H, bfm);
+  a.np = rows_np(p.n, bfm);
   a.ts = p.ts;
   a.coef = p.coef;
   a.csum = csum;
@@ -609,6 +762,7 @@ int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* d
   a.data_coef = p.data_coef;
   a.fusion = p.fusion;
   a.wperm = wperm;
+  a.wbf = wbf;
   a.bf = bf;
   a.t = t;
   a.y = y;

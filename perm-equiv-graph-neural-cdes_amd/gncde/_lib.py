@@ -18,7 +18,8 @@ RK4, TSIT5 = 0, 1
 CTRL_GRID, CTRL_PID = 0, 1
 SAVE_T1, SAVE_STEPS, SAVE_TS = 0, 1, 2
 FLAG_GENERIC = 1  # GncdeSolver.flags: force the generic forward and reverse sweep
-COMPUTE_FP32, COMPUTE_BF16, COMPUTE_BF16_STORAGE = 0, 1, 2  # GncdeProblem.compute (gncde.h)
+COMPUTE_FP32, COMPUTE_BF16, COMPUTE_BF16_STORAGE, COMPUTE_BF16_MFMA = 0, 1, 2, 3  # GncdeProblem.compute (gncde.h)
+BF16_COEF_MODES = (COMPUTE_BF16_STORAGE, COMPUTE_BF16_MFMA)  # modes whose coefficients are stored as bfloat16
 STAT_STEPS, STAT_REJECTS, STAT_EVALS, STAT_STATUS = 0, 1, 2, 3
 STATUS_OK, STATUS_MAX_STEPS, STATUS_NONFINITE, STATUS_STEP_RECORD = 0, 1, 2, 3
 OP_NORM_LAP, OP_NORM_ADJ, OP_KIPF, OP_NORMALIZED_PLUS = 0, 1, 2, 3

@@ -65,7 +65,7 @@ class Problem:
     def c_struct(self) -> _lib.GncdeProblem:
         for name in ("ts", "coef", "tcoef", "fusion", "params"):
             t = getattr(self, name)
-            want = torch.bfloat16 if (name == "coef" and self.compute == _lib.COMPUTE_BF16_STORAGE) else torch.float32
+            want = torch.bfloat16 if (name == "coef" and self.compute in _lib.BF16_COEF_MODES) else torch.float32
             if not (t.is_cuda and t.dtype == want and t.is_contiguous()):
                 raise _lib.GncdeError(f"Problem.{name} must be a contiguous {want} CUDA tensor")
         if len(self.dims) - 1 > _lib.MAX_LAYERS:
@@ -97,15 +97,17 @@ class Problem:
                        cde_hidden=self.cde_hidden, cde_embed=self.cde_embed, compute=self.compute)
 
     def with_compute(self, compute: str) -> "Problem":
-        """The same problem in another arithmetic ("fp32" | "bf16" | "bf16_storage": coefficients cast here)."""
+        """The same problem in another arithmetic ("fp32" | "bf16" | "bf16_storage" | "bf16_mfma": coefficients cast
+        here)."""
         mode = COMPUTE_MODES[compute]
-        dt = torch.bfloat16 if mode == _lib.COMPUTE_BF16_STORAGE else torch.float32
+        dt = torch.bfloat16 if mode in _lib.BF16_COEF_MODES else torch.float32
         return Problem(ts=self.ts, coef=self.coef.to(dt).contiguous(), tcoef=self.tcoef, fusion=self.fusion,
                        params=self.params, dims=list(self.dims), data_coef=self.data_coef,
                        cde_hidden=self.cde_hidden, cde_embed=self.cde_embed, compute=mode)
 
 
-COMPUTE_MODES = {"fp32": _lib.COMPUTE_FP32, "bf16": _lib.COMPUTE_BF16, "bf16_storage": _lib.COMPUTE_BF16_STORAGE}
+COMPUTE_MODES = {"fp32": _lib.COMPUTE_FP32, "bf16": _lib.COMPUTE_BF16, "bf16_storage": _lib.COMPUTE_BF16_STORAGE,
+                 "bf16_mfma": _lib.COMPUTE_BF16_MFMA}
 
 
 def make_problem(ts, coeffs, kind, layers, data_coeffs=None, cde_hidden=0, cde_embed=0, device="cuda",
@@ -113,10 +115,12 @@ def make_problem(ts, coeffs, kind, layers, data_coeffs=None, cde_hidden=0, cde_e
     """Build a Problem from reference-layout inputs (ts [B,T], coeffs (d,c,b,a) [B,T-1,n,n,2], layer dicts).
 
     compute="bf16" runs the n x n products on bf16 MFMA (split pairs, fp32-class results); "bf16_storage" also
-    stores the operator coefficients in bfloat16 (BASELINE config 5; reverse mode = the fp32 adjoint over the coefficients read, see gncde.h GNCDE_COMPUTE_*)."""
+    stores the operator coefficients in bfloat16; "bf16_mfma" stores them in bfloat16 and runs every product on
+    single-plane bf16 MFMA operands (BASELINE config 5's throughput mode; one-launch evaluation shapes only).  Reverse
+    mode = the fp32 adjoint over the coefficients read, see gncde.h GNCDE_COMPUTE_*."""
     coef, tcoef = layout.pack_control(coeffs, device=device)
     mode = COMPUTE_MODES[compute]
-    if mode == _lib.COMPUTE_BF16_STORAGE:
+    if mode in _lib.BF16_COEF_MODES:
         coef = coef.to(torch.bfloat16).contiguous()
     ts = torch.as_tensor(ts, dtype=torch.float32)
     if ts.dim() == 1:

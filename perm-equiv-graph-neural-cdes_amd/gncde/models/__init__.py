@@ -254,9 +254,13 @@ class TGBGraphNeuralCDE(nn.Module):
     ``solver="pid"`` (build extension, BASELINE config 5's "adaptive Tsit5 solver") replaces ConstantStepSize with
     the dyn model's controller, PIDController(rtol 1e-3, atol 1e-6) with dt0 = None (graph_neural_cde.py:53-54,
     94-104), differentiated on each window's accepted steps; ``last_steps`` then holds every window's accepted
-    step count of the latest forward (the data-parallel trainer balances ranks by it)."""
+    step count of the latest forward (the data-parallel trainer balances ranks by it).
 
-    def __init__(self, cfg, vector_field, interpolation="cubic", model_key=None, dt0=0.01, solver=None, **kwargs):
+    ``compute`` (build extension): the solve's arithmetic, engine.COMPUTE_MODES — "bf16_mfma" is config 5's
+    single-plane bf16 MFMA mode (bf16 coefficients, every product on bf16 operands; include/gncde.h)."""
+
+    def __init__(self, cfg, vector_field, interpolation="cubic", model_key=None, dt0=0.01, solver=None,
+                 compute="fp32", **kwargs):
         super().__init__()
         self.cfg = _cfg(cfg, hidden_dim=32, method="Tsit5", return_sequence=False, use_mlps=False)
         if getattr(self.cfg, "use_mlps", False):
@@ -274,6 +278,9 @@ class TGBGraphNeuralCDE(nn.Module):
         if solver not in (None, "constant", "pid"):
             raise ValueError(f"solver {solver!r}: None / 'constant' (ConstantStepSize) or 'pid'")
         self.adaptive = solver == "pid"
+        if compute not in engine.COMPUTE_MODES:
+            raise ValueError(f"compute {compute!r}: one of {sorted(engine.COMPUTE_MODES)}")
+        self.compute = compute
         self.last_steps = None
 
     def batched(self, ts, coeffs_adj, x_data, x0, start_time=None, evolving_out=False):
@@ -289,6 +296,8 @@ class TGBGraphNeuralCDE(nn.Module):
         data_coef = autograd.hermite_coefficients(ts_d, X) if grad else engine.hermite_coefficients(ts_d, X)
         y0 = _affine(self.encoder, torch.as_tensor(x0, dtype=torch.float32, device=ts_d.device))
         prob = self.wrapped_vector_field.problem(control_adj, None, data_coef=data_coef.detach())
+        if self.compute != "fp32":
+            prob = prob.with_compute(self.compute)
         if self.adaptive:
             spec = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_PID, save_mode=_lib.SAVE_T1, rtol=1e-3,
                                      atol=1e-6, t0=ts_d[:, 0].contiguous(), t1=ts_d[:, -1].contiguous(),

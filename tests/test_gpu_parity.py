@@ -438,10 +438,16 @@ def test_generic_cde_full_size_properties(gncde, B, n, T, h, L, t1, dt):
 
 
 @pytest.mark.parametrize("n,dims,kind,cde", [(300, [32, 32, 32], "undirected", None),   # product K in two rounds
-                                             (272, [16, 16, 256], "directed", (16, 8))])  # + CDE read-out
+                                             (272, [16, 16, 256], "directed", (16, 8)),   # + CDE read-out
+                                             # the one-launch evaluation (gncde_rows.hip) at n in (128, 256]:
+                                             (255, [32, 32, 32, 32, 512], "undirected", (32, 8)),  # config 5 shape
+                                             (200, [64, 64, 64], "directed", None),
+                                             (256, [16, 16, 16, 256], "plain", (16, 8))])
 def test_generic_vf_large_n_vs_oracle(gncde, n, dims, kind, cde):
-    """n > 256: the fused layer kernel's product runs more than one round of K chunks per wave; one evaluation
-    against the fp64 oracle computed here (no fixture: the coefficients alone would be megabytes)."""
+    """n > 128: the fused layer kernel's product runs more than one round of K chunks per wave (n > 256), and the
+    one-launch evaluation's waves walk up to four 16-column K chunks each (n <= 256, sixteen 16-row workgroups per
+    sample meeting at their barriers); one evaluation against the fp64 oracle computed here (no fixture: the
+    coefficients alone would be megabytes)."""
     from tests.golden import make_golden as MG2
     rng = np.random.default_rng(n)
     B, T = 2, 4

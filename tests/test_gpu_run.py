@@ -35,13 +35,20 @@ def test_dyn_single_run_small(tmp_path, spi):
     assert losses[-1] < losses[0]
 
 
-@pytest.mark.parametrize("config,metric,solver", [("pgt_england_small.yaml", "best_validation_loss", None),
-                                                  ("tgb_trade_small.yaml", "best_validation_ndcg@10", None),
-                                                  ("tgb_trade_small.yaml", "best_validation_ndcg@10", "pid")])
-def test_window_single_run_small(tmp_path, config, metric, solver):
+# config 5's bf16 MFMA mode needs the one-launch evaluation's shapes: h = 16 = the hidden width, de = 8
+BF16M_TGB = {"solver": "pid", "compute": "bf16_mfma", "hidden_dim": 16,
+             "vector_field": {"name": "PermEquivGraphVectorField", "hidden_dim": 16, "num_layers": 2, "data_embed_dim": 8}}
+
+
+@pytest.mark.parametrize("config,metric,model", [("pgt_england_small.yaml", "best_validation_loss", None),
+                                                 ("tgb_trade_small.yaml", "best_validation_ndcg@10", None),
+                                                 ("tgb_trade_small.yaml", "best_validation_ndcg@10", {"solver": "pid"}),
+                                                 ("tgb_trade_small.yaml", "best_validation_ndcg@10", BF16M_TGB)])
+def test_window_single_run_small(tmp_path, config, metric, model):
     """trainer_pgt / trainer_tgb flow: windows -> one optimiser step per window -> validation (MSE / NDCG@10)
     -> checkpoint -> test metrics of the best model.  solver "pid": the TGB model on BASELINE config 5's adaptive
-    Tsit5 + PIDController (build-only `model.solver: pid`), trained through the reverse mode on the accepted steps."""
+    Tsit5 + PIDController (build-only `model.solver: pid`), trained through the reverse mode on the accepted steps;
+    with `model.compute: bf16_mfma`, its forward solves in the single-plane bf16 mode."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a HIP device")
     from gncde import data, run
@@ -51,8 +58,8 @@ def test_window_single_run_small(tmp_path, config, metric, solver):
     cfg["dataset"]["num_snapshots"] = 26 if "pgt" in config else 16
     cfg["checkpoint_dir"] = str(tmp_path)
     cfg["eval_freq"] = 2
-    if solver:
-        cfg["model"]["solver"] = solver
+    if model:
+        cfg["model"].update(model)
     ds = data.WindowDataset(data.WindowDataCfg.from_dict(cfg["dataset"]))
     assert len(ds.train) >= 1 and len(ds.val) >= 1 and len(ds.test) >= 1
     out = tmp_path / "metrics.jsonl"

@@ -67,7 +67,8 @@ def main():
             prob, y0 = synthetic.cde_batch(64, 129, 4, 64, 8, 3, 3.0)
             grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, 3.0, 0.1)] * prob.B)
             spec = gncde.SolverSpec(method=L.TSIT5, save_mode=L.SAVE_T1, grid=grid, nsteps=ns)
-            run("3_england_n129_h64_de8_L3_tsit5c", prob, spec, y0, args.reps)
+            ys = run("3_england_n129_h64_de8_L3_tsit5c", prob, spec, y0, args.reps)
+            run("3_england_n129_h64_de8_L3_tsit5c_bf16_mfma", prob.with_compute("bf16_mfma"), spec, y0, args.reps, ref=ys)
         elif c == "4":  # gene community n=128, h=16, L=2, RK4 100 steps, B=1024 (forward)
             prob, y0, _ = synthetic.heat_batch(1024, num_nodes=128, hidden=16, num_layers=2, T=80, graph="community")
             grid, ns = layout.stack_grids([layout.rk4_grid(0.0, 5.0, 100)] * prob.B)
@@ -82,6 +83,13 @@ def main():
             ys = run("5_trade_n255_h32_de8_L4_tsit5pid", prob, spec, y0, args.reps)
             # BASELINE config 5's bf16 MFMA path: bf16 coefficients and (I + Abar), bf16 n x n products
             run("5_trade_n255_h32_de8_L4_tsit5pid_bf16", prob.with_compute("bf16"), spec, y0, args.reps, ref=ys)
+            # the single-plane mode: bf16 coefficients, every product on bf16 operands (one launch per evaluation)
+            run("5_trade_n255_h32_de8_L4_tsit5pid_bf16_mfma", prob.with_compute("bf16_mfma"), spec, y0, args.reps, ref=ys)
+            # the same per-evaluation comparison on one fixed grid (100 Tsit5 steps; adaptive step counts differ)
+            grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, 1.0, 0.01)] * B)
+            fspec = gncde.SolverSpec(method=L.TSIT5, save_mode=L.SAVE_T1, grid=grid, nsteps=ns)
+            yf = run("5_trade_fixed100", prob, fspec, y0, args.reps)
+            run("5_trade_fixed100_bf16_mfma", prob.with_compute("bf16_mfma"), fspec, y0, args.reps, ref=yf)
 
 
 if __name__ == "__main__":
