@@ -694,6 +694,12 @@ void vf_forms_direct(const GncdeProblem& p, const float* t, const float* csum, f
                        p.tcoef, t, p.fusion, abar, ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B);
 }
 
+const float* generic_vf_csum(const GncdeProblem& p, char* ws) {
+  VfWs w;
+  carve_vf(p, ws, w);
+  return w.csum;
+}
+
 const int* generic_vf_fault(const GncdeProblem& p, char* ws) {
   VfWs w;
   carve_vf(p, ws, w);
@@ -732,7 +738,7 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
 }
 
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st, bool prepared, unsigned* bars) {
+                    hipStream_t st, bool prepared, unsigned* bars, float* keep) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
   VfWs w;
@@ -746,7 +752,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     }
     // (the workspace holds no (I + Abar_l) planes for these problems: there is no multi-kernel fallback here)
     return rows_vf_eval(p, t, y, dy, w.csum, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync, reinterpret_cast<int*>(w.sync + B), *bars,
-                        st);
+                        st, keep);
   }
   vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st);
   const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
@@ -755,7 +761,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
-    float* Zout = bufs[l & 1];
+    float* Zout = keep && l + 1 < p.L ? keep + (size_t)l * B * n * p.dims[l + 1] : bufs[l & 1];
     const bool last = l == p.L - 1;
     // A widening layer (d_out > d_in: the CDE wrapper's h -> h*de*2 read-out layer) is evaluated in the
     // reassociated order (I + Abar)(diag(inv) Z W'^T + 1 b'^T) = ((I + Abar) diag(inv) Z) W'^T + q b'^T with

@@ -175,8 +175,9 @@ void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float*
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st);
 // bars: the solve's count of per-group barriers done by one-launch evaluations so far (gncde_rows.hip); nullptr
 // only together with prepared = false (a standalone evaluation)
+// keep (optional, [L-1, B, n, d]): every hidden layer's output Z_{l+1} kept for the reverse mode (uniform width d)
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st, bool prepared = false, unsigned* bars = nullptr);
+                    hipStream_t st, bool prepared = false, unsigned* bars = nullptr, float* keep = nullptr);
 // the workspace's fault word (a one-launch evaluation's barrier gave up): solver status 4 when set
 const int* generic_vf_fault(const GncdeProblem& p, char* ws);
 
@@ -188,9 +189,20 @@ inline bool coef_is_bf16(const GncdeProblem& p) {
 }
 int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum,
                  const float* wperm, const uint16_t* wbf, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
-                 unsigned& bars_done, hipStream_t st);
+                 unsigned& bars_done, hipStream_t st, float* keep = nullptr);
 int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
                       int32_t* stats, char* ws, hipStream_t st);
+// k_coef_sums' per-plane reductions in a prepared evaluation workspace
+const float* generic_vf_csum(const GncdeProblem& p, char* ws);
+
+// reverse mode of one evaluation, one launch per ConvLayer (n <= 256, one width H): gncde_rows_vjp.hip
+bool rows_vjp_supported(const GncdeProblem& p);
+size_t rows_vjp_workspace(const GncdeProblem& p);
+void rows_vjp_begin(const GncdeProblem& p, char* ws, hipStream_t st);
+int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* gF, float* gu, float* gdata,
+                const float* csum, const float* wf, const float* bfold, char* ws, char* vf_ws, unsigned* bars,
+                hipStream_t st);
+void rows_vjp_finish(const GncdeProblem& p, char* ws, float* gparams, float* gfusion, hipStream_t st);
 
 // generic Tsit5 + PIDController (any shape, CDE wrapper): gncde_pid.hip
 size_t generic_pid_workspace(const GncdeProblem& p);

@@ -57,6 +57,8 @@ struct RowsArgs {
   const float* y;          // [B, n, H] stage inputs
   float* dy;               // [B, n, H] vector field
   float* zbuf[2];          // [G, n, H] each: the groups' hidden layer outputs, alternating per step
+  float* keep;             // optional [L-1, B, n, H]: every sample's hidden layer outputs kept (reverse mode), used
+                           // instead of zbuf
   unsigned* bar;           // [G] arrivals per group, monotonic within a solve
   unsigned bar0;           // barriers every group completed before this launch
   int* fault;              // set when a barrier wait gives up
@@ -368,7 +370,8 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
         wait_all();
         // hidden outputs alternate buffers by their step index within the launch, so a buffer is rewritten only
         // after a barrier that every reader of its previous contents has passed (also across rounds, for L = 2)
-        const float* zin = a.zbuf[(it * (L - 1) + l - 1) & 1] + (size_t)g * zgroup;
+        const float* zin = a.keep && live ? a.keep + ((size_t)(l - 1) * a.B + b) * zgroup
+                                  : a.zbuf[(it * (L - 1) + l - 1) & 1] + (size_t)g * zgroup;
         const auto rs = rsrc(zin, (unsigned)(zgroup * sizeof(float)));
         for (int e0 = tid; e0 < tot; e0 += 256 * U) {
           floatx4 v[U];
@@ -527,7 +530,9 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
         for (int r = 0; r < 4; ++r) sOut[(4 * hi + r) * ZS + 16 * tile + lo] = fmaxf(v[r], 0.f);
       }
       __syncthreads();
-      float* zout = a.zbuf[(it * (L - 1) + l) & 1] + (size_t)g * zgroup;
+      // (an idle round keeps to its group's own buffers: the sample it recomputes is another group's)
+      float* zout = a.keep && live ? a.keep + ((size_t)l * a.B + b) * zgroup
+                                   : a.zbuf[(it * (L - 1) + l) & 1] + (size_t)g * zgroup;
       const auto rs = rsrc(zout, (unsigned)(zgroup * sizeof(float)));
       constexpr int G4 = H / 4;
       if (tid < 16 * G4) {  // write-through 16-byte stores of this workgroup's rows, then one arrival
@@ -730,7 +735,7 @@ size_t rows_sync_ints(const GncdeProblem& p) { return align_up((size_t)p.B + 4, 
 // Launch one evaluation (RowsState: the group layout, fixed per problem, and the barriers done so far).
 int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum,
                  const float* wperm, const uint16_t* wbf, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
-                 unsigned& bars_done, hipStream_t st) {
+                 unsigned& bars_done, hipStream_t st, float* keep) {
   Inst k;
   const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
   const bool bfm = p.compute == GNCDE_COMPUTE_BF16_MFMA;
@@ -769,6 +774,7 @@ int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* d
   a.dy = dy;
   a.zbuf[0] = z0;
   a.zbuf[1] = z1;
+  a.keep = keep;
   a.bar = bar;
   a.bar0 = bars_done;
   a.fault = fault;

@@ -1,0 +1,919 @@
+// Reverse mode of one vector-field evaluation, one launch per ConvLayer (configs 3 and 5 training: n <= 256, one
+// hidden width H in {16, 32, 64}, ODE output or the de = 8 CDE read-out).  It replaces the generic sweep's ~14
+// launches per layer (gncde_vjp.hip vf_vjp) with one, and needs no (I + Abar) or G in HBM.
+//
+// Every layer is taken in the reassociated order the forward evaluates (gncde_rows.hip, gncde_layer.hip):
+//   zhat = diag(inv) Z_l,  P = (I + Abar_l) zhat,  q = (I + Abar_l) 1,  out_l = P W'^T + q b'^T
+// (W' = W diag(rms_w), b' = b + W rms_b; out_l is Z_{l+1} before the ReLU, or the read-out).  For a cotangent
+// g_out of out_l, with g_P = g_out W' and g_q = g_out b':
+//   g_W' += g_out^T P,  g_b' += g_out^T q
+//   G = g_P zhat^T + g_q 1^T                     the cotangent of (I + Abar_l) -> fusion-table gradient
+//   g_zhat = (I + Abar_l)^T g_P,  g_Z = RMSNorm^T(g_zhat),  g_out_{l-1} = g_Z * [Z_l > 0]
+// The fusion-table gradient needs, besides the four dense contractions sum_ik G_ik X_ik (X = A, dA, A^T, dA^T),
+// only the row sums R_i = g_P_i . sum_k zhat_k + n g_q_i, the diagonal D_i = g_P_i . zhat_i + g_q_i and
+// sum_k C_k f_k = sum_i (g_P_i . sum_k zhat_k f_k + g_q_i sum_k f_k) against the form's node features — all O(n H).
+//
+// Launches per stage (after the forward kept Z_1 .. Z_{L-1}, generic_vf_eval keep mode):
+//   k_bwd_head      per 16-row block: g_out, g_P, g_q of the output layer from the stage cotangent gF
+//                   (ODE g_out = tg gF; CDE g_P_i = tg_i sum_{m,j} gF_im dX_ij W'[16m+j, :] without the n x 16h
+//                   g_out, and the factors tg gF, dX for the read-out weight gradient)
+//   k_bwd_layer<H>  per 16-row block, l = L-1 .. 0: the interval's rows block and column strip -> A, dA, A^T, dA^T in
+//                   the product's operand layout (the forward form), zhat and g_P of every node in LDS, then one K
+//                   loop over the block's node chunks that runs three MFMA products per chunk: P = (I+Abar) zhat,
+//                   g_zhat = (I+Abar)^T g_P (the same registers, the transposed coefficients) and the G^T tile
+//                   zhat g_P^T, which meets A, dA, A^T, dA^T in registers for the dense contractions; then g_W'
+//                   partials, RMSNorm^T, the ReLU mask and the next layer's g_out, g_P, g_q (or the stage input's
+//                   cotangent at l = 0)
+//   k_bwd_readout   (CDE) the read-out weight and bias gradient, split over 32-row chunks of all samples
+//   k_bwd_data      (CDE data-spline cotangent, TGB) g_dX_ij = tg_i sum_m gF_im (P_i . W'[16m+j,:] + q_i b'[16m+j])
+// Parameter and fusion partials accumulate in per-(sample, row block) / per-chunk slots that only their owner
+// workgroup updates (fixed order, no atomics); k_bwd_finish reduces them once per reverse sweep and maps g_W', g_b'
+// to the reference's W, b, rms_w, rms_b.
+#include "gncde_internal.h"
+
+namespace gncde {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kRB = 16;
+constexpr int kMaxN = 256;
+constexpr int kStrip = 17;
+constexpr int kRoChunk = 32;  // rows per read-out gradient chunk
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float cubic(const float (&c)[4], float f) { return fmaf(f, fmaf(f, fmaf(f, c[0], c[1]), c[2]), c[3]); }
+__device__ __forceinline__ float dcubic(const float (&c)[4], float f) {
+  return fmaf(f, fmaf(3.0f * f, c[0], 2.0f * c[1]), c[2]);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float u2f(unsigned x) { return __builtin_bit_cast(float, x); }
+
+__host__ __device__ constexpr int bwd_zs(int H) { return H + 4; }
+__host__ __device__ inline int bwd_np(int n) { return (n + 15) & ~15; }
+// rows of the two big regions: every node (NP), at least 80 (the 64 partial rows of the products + 16 result rows)
+__host__ __device__ inline int bwd_rows(int n) { return bwd_np(n) > 80 ? bwd_np(n) : 80; }
+// floats of region 1 (the form's strip + rows block, then zhat of every node, then the P partials and P[R])
+__host__ __device__ inline int bwd_big(int n, int H) {
+  const int np = bwd_np(n), z = bwd_rows(n) * bwd_zs(H), s = 2 * np * kStrip + 32 * (np + 4);
+  return ((z > s ? z : s) + 3) & ~3;
+}
+inline size_t bwd_smem(int n, int H) {
+  const int np = bwd_np(n);
+  // big | gP region [rows][H+4] | inv, gq, r, rd, c, cd, dg, dgd, v, w [10][NP] | u, q [2][16] | scratch [1280]
+  // | fusion sums [24][4]
+  return sizeof(float) * ((size_t)bwd_big(n, H) + (size_t)bwd_rows(n) * bwd_zs(H) + 10 * (size_t)np + 32 + 1280 +
+                          GNCDE_FC * 4);
+}
+
+struct BwdArgs {
+  int B, n, T, L, l, nb;
+  const float* ts;
+  const float* coef;       // [B, T-1, 4, n, n]
+  const float* csum;       // k_coef_sums [B, T-1, 12 n + 4]
+  const float* fusion;     // [L, GNCDE_FC]
+  const float* t;          // [B] stage times
+  const float* zin;        // Z_l [B, n, H] (the stage input at l = 0, else the forward's kept hidden output)
+  const float* gP;         // this layer's g_P [B, n, H]
+  const float* gq;         // g_q [B, n]
+  const float* gout;       // g_out [B, n, H] (layers with d_out = H; unused for the CDE read-out layer)
+  const float* wprev;      // W'_{l-1} natural [H, H] (l > 0)
+  const float* bprev;      // b'_{l-1} [H]
+  float* gP_next;          // layer l-1's g_P, g_q, g_out (l > 0)
+  float* gq_next;
+  float* gout_next;
+  float* gz;               // l = 0: the stage input's cotangent [B, n, H]
+  float* pq;               // CDE read-out layer: P | q per node [B, n, H + 1]
+  float* gfc;              // [B * nb, L, GNCDE_FC] accumulated
+  float* gw;               // [B * nb, gw_stride] accumulated; this layer's H x H g_W' then H g_b' at gw_off
+  int gw_stride, gw_off;
+  int cde_out;             // layer l is the CDE read-out layer
+};
+
+// One ConvLayer's reverse mode for a 16-row block R of one sample (see the file comment).
+template <int H>
+__global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int ZS = bwd_zs(H);
+  constexpr int CT = H / 16;
+  constexpr int KH = H / 4;  // MFMA K steps over a width-H contraction
+  const int n = a.n, T = a.T, l = a.l;
+  const int NP = bwd_np(n), nch = NP >> 4, RWS = bwd_rows(n);
+  float* big = sm;
+  float* sG = big + bwd_big(n, H);     // g_P of every node [RWS][ZS]; later the g_zhat partials and g_zhat[R]
+  float* sInv = sG + (size_t)RWS * ZS;
+  float* sGq = sInv + NP;
+  float* sF = sGq + NP;                // r, rd, c, cd, dg, dgd [6][NP]
+  float* sV = sF + 6 * NP;             // v_l [NP]
+  float* sW = sV + NP;                 // w_l [NP]
+  float* sRow = sW + NP;               // u_l [16], q_l [16] of the block's rows
+  float* sScr = sRow + 32;             // [1280] reduction scratch
+  float* sFus = sScr + 1280;           // [GNCDE_FC][4]
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
+  const int b = blockIdx.x / a.nb, rb = blockIdx.x % a.nb;
+  const int r0 = rb * kRB, ri = r0 + lo;
+  const size_t nn = (size_t)n * n, zgroup = (size_t)n * H;
+  const float tb = a.t[b];
+  const float* tsb = a.ts + (size_t)b * T;
+  const int idx = interval_index(tsb, T, tb);
+  const float f = tb - tsb[idx];
+  const float* fc = a.fusion + l * GNCDE_FC;
+
+  // ---- form: the interval's rows block and column strip (as the forward) --------------------------------------
+  const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
+  const auto crs = rsrc(cb, (unsigned)(4 * nn * sizeof(float)));
+  const int RS = NP + 4;
+  float* sAr = big + 2 * NP * kStrip;
+  const int rr = tid >> 4, cq = 4 * (tid & 15), c4 = 4 * (tid & 3);
+  u32x4 rc[4][4], sc[4][4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      rc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)((q * nn + (size_t)(r0 + rr) * n + cq + 64 * u) * 4), 0, 0);
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      sc[p][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)((q * nn + (size_t)((tid >> 2) + 64 * p) * n + r0 + c4) * 4),
+                                                       0, 0);
+  const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
+  const int nd = tid < n ? tid : n - 1;
+  float pv[3][4], pt[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int kd = 0; kd < 3; ++kd) pv[kd][q] = cs[(q * 3 + kd) * n + nd];
+    pt[q] = cs[12 * n + q];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c0 = cq + 64 * u;
+    if (c0 < NP)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool in = r0 + rr < n && c0 + e < n;
+        const unsigned x0 = rc[u][0][e], x1 = rc[u][1][e], x2 = rc[u][2][e], x3 = rc[u][3][e];
+        const float cc[4] = {u2f(x0), u2f(x1), u2f(x2), u2f(x3)};
+        sAr[rr * RS + c0 + e] = in ? cubic(cc, f) : 0.f;
+        sAr[(16 + rr) * RS + c0 + e] = in ? dcubic(cc, f) : 0.f;
+      }
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int kk = (tid >> 2) + 64 * p;
+    if (kk < NP)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool in = kk < n && r0 + c4 + e < n;
+        const unsigned x0 = sc[p][0][e], x1 = sc[p][1][e], x2 = sc[p][2][e], x3 = sc[p][3][e];
+        const float cc[4] = {u2f(x0), u2f(x1), u2f(x2), u2f(x3)};
+        big[kk * kStrip + c4 + e] = in ? cubic(cc, f) : 0.f;
+        big[(NP + kk) * kStrip + c4 + e] = in ? dcubic(cc, f) : 0.f;
+      }
+  }
+  // node features and this layer's families at every node (thread = node)
+  const float s_t = cubic(pt, f), sd_t = dcubic(pt, f);
+  {
+    const bool nin = tid < n;
+    const float r = nin ? cubic(pv[0], f) : 0.f, rd = nin ? dcubic(pv[0], f) : 0.f;
+    const float c = nin ? cubic(pv[1], f) : 0.f, cd = nin ? dcubic(pv[1], f) : 0.f;
+    const float dg = nin ? cubic(pv[2], f) : 0.f, dgd = nin ? dcubic(pv[2], f) : 0.f;
+    if (tid < NP) {
+      sF[tid] = r;
+      sF[NP + tid] = rd;
+      sF[2 * NP + tid] = c;
+      sF[3 * NP + tid] = cd;
+      sF[4 * NP + tid] = dg;
+      sF[5 * NP + tid] = dgd;
+      sV[tid] = fc[GNCDE_FC_VR_A] * r + fc[GNCDE_FC_VR_DA] * rd + fc[GNCDE_FC_VC_A] * c + fc[GNCDE_FC_VC_DA] * cd;
+      const float wv = fc[GNCDE_FC_WR_A] * r + fc[GNCDE_FC_WR_DA] * rd + fc[GNCDE_FC_WC_A] * c + fc[GNCDE_FC_WC_DA] * cd +
+                       fc[GNCDE_FC_WS_A] * s_t + fc[GNCDE_FC_WS_DA] * sd_t;
+      sW[tid] = nin ? wv : 0.f;
+    }
+    if (tid >= r0 && tid < r0 + kRB && nin) {
+      const float wv = fc[GNCDE_FC_WR_A] * r + fc[GNCDE_FC_WR_DA] * rd + fc[GNCDE_FC_WC_A] * c + fc[GNCDE_FC_WC_DA] * cd +
+                       fc[GNCDE_FC_WS_A] * s_t + fc[GNCDE_FC_WS_DA] * sd_t;
+      const float uv = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dg + fc[GNCDE_FC_UD_DA] * dgd + fc[GNCDE_FC_UR_A] * r +
+                       fc[GNCDE_FC_UR_DA] * rd + fc[GNCDE_FC_UC_A] * c + fc[GNCDE_FC_UC_DA] * cd + fc[GNCDE_FC_US_A] * s_t +
+                       fc[GNCDE_FC_US_DA] * sd_t;
+      float qv = fc[GNCDE_FC_E_A] * r + fc[GNCDE_FC_E_DA] * rd + fc[GNCDE_FC_ET_A] * c + fc[GNCDE_FC_ET_DA] * cd;
+      qv += (float)n * wv;
+      qv += (fc[GNCDE_FC_VR_A] + fc[GNCDE_FC_VC_A]) * s_t + (fc[GNCDE_FC_VR_DA] + fc[GNCDE_FC_VC_DA]) * sd_t;
+      qv += uv;
+      sRow[tid - r0] = uv;
+      sRow[16 + tid - r0] = qv;
+    } else if (tid >= r0 && tid < r0 + kRB) {
+      sRow[tid - r0] = 0.f;
+      sRow[16 + tid - r0] = 0.f;
+    }
+  }
+  __syncthreads();
+  // the operand elements: (ri, k) and (k, ri) of A and dA, k = 16 kc + 4 hi + s, kc = w + 4 j
+  float Ar[4][4], dAr[4][4], At[4][4], dAt[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int kc = w + 4 * j, k0 = 16 * kc + 4 * hi;
+    const bool in = kc < nch;
+    const floatx4 ar = in ? *reinterpret_cast<const floatx4*>(sAr + lo * RS + k0) : floatx4{0.f, 0.f, 0.f, 0.f};
+    const floatx4 dr = in ? *reinterpret_cast<const floatx4*>(sAr + (16 + lo) * RS + k0) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      Ar[j][s] = ar[s];
+      dAr[j][s] = dr[s];
+      At[j][s] = in ? big[(k0 + s) * kStrip + lo] : 0.f;
+      dAt[j][s] = in ? big[(NP + k0 + s) * kStrip + lo] : 0.f;
+    }
+  }
+  __syncthreads();  // the strip's region becomes zhat
+
+  // ---- Z_l and g_P of every node ----------------------------------------------------------------------------
+  {
+    constexpr int G4 = H / 4;
+    const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.zin + (size_t)b * zgroup);
+    const floatx4* P4 = reinterpret_cast<const floatx4*>(a.gP + (size_t)b * zgroup);
+    const int tot = NP * G4, valid = n * G4;
+    for (int e0 = tid; e0 < tot; e0 += 256 * 4) {
+      floatx4 vz[4], vp[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + 256 * u;
+        vz[u] = e < valid ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
+        vp[u] = e < valid ? P4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + 256 * u;
+        if (e < tot) {
+          *reinterpret_cast<floatx4*>(big + (e / G4) * ZS + 4 * (e % G4)) = vz[u];
+          *reinterpret_cast<floatx4*>(sG + (e / G4) * ZS + 4 * (e % G4)) = vp[u];
+        }
+      }
+    }
+    for (int k = tid; k < NP; k += 256) sGq[k] = k < n ? a.gq[(size_t)b * n + k] : 0.f;
+  }
+  __syncthreads();
+  for (int k = tid; k < NP; k += 256) {
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < H / 4; ++q) {
+      const floatx4 z = *reinterpret_cast<const floatx4*>(big + k * ZS + 4 * q);
+      ss = fmaf(z.x, z.x, fmaf(z.y, z.y, fmaf(z.z, z.z, fmaf(z.w, z.w, ss))));
+    }
+    sInv[k] = k < n ? rms_inv(ss, 1.0f / (float)H) : 0.f;
+  }
+  __syncthreads();
+  // zsum = sum_k zhat_k and zf_x = sum_k zhat_k x_k (x = r, rd, c, cd): column c = tid % H, rows k = g mod NG
+  {
+    constexpr int NG = 256 / H;
+    const int c = tid % H, g = tid / H;
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = g; k < n; k += NG) {
+      const float z = big[k * ZS + c] * sInv[k];
+      acc[0] += z;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) acc[1 + x] = fmaf(z, sF[x * NP + k], acc[1 + x]);
+    }
+#pragma unroll
+    for (int x = 0; x < 5; ++x) sScr[(g * 5 + x) * H + c] = acc[x];
+  }
+  __syncthreads();
+  float* sZv = sScr + 1280 - 5 * H;  // zsum, zf_r, zf_rd, zf_c, zf_cd [5][H] (after the group partials)
+  for (int e = tid; e < 5 * H; e += 256) {
+    // (NG * 5 H = 1280 floats: the total for (x, c) lands in the last group's slot for (x, c), which only this
+    // thread reads, after reading it)
+    constexpr int NG = 256 / H;
+    const int x = e / H, c = e % H;
+    float v = 0.f;
+    for (int g = 0; g < NG; ++g) v += sScr[(g * 5 + x) * H + c];
+    sZv[x * H + c] = v;
+  }
+  __syncthreads();
+
+  // ---- the K loop: P = (I+Abar) zhat, g_zhat = (I+Abar)^T g_P, G^T tiles meeting A, dA, A^T, dA^T ----------
+  const float eA = fc[GNCDE_FC_E_A], edA = fc[GNCDE_FC_E_DA], eTA = fc[GNCDE_FC_ET_A], eTdA = fc[GNCDE_FC_ET_DA];
+  const float wi = sW[ri < NP ? ri : 0], vi = sV[ri < NP ? ri : 0], ui = sRow[lo], gqi = sGq[ri < NP ? ri : 0];
+  float gpr[KH];  // this lane's B operand of the G^T tiles: g_P[ri][4 s + hi]
+#pragma unroll
+  for (int s = 0; s < KH; ++s) gpr[s] = sG[ri * ZS + 4 * s + hi];
+  floatx4 accP[CT], accT[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    accP[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+    accT[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  float dsum[4] = {0.f, 0.f, 0.f, 0.f};  // sum G.*A, G.*dA, G.*A^T, G.*dA^T over this lane's elements
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int kc = w + 4 * j;
+    if (kc >= nch) break;
+    const int k0 = 16 * kc + 4 * hi;
+    const floatx4 vk = *reinterpret_cast<const floatx4*>(sV + k0);
+    const floatx4 wk = *reinterpret_cast<const floatx4*>(sW + k0);
+    const floatx4 iv = *reinterpret_cast<const floatx4*>(sInv + k0);
+    // G^T tile rows k = 16 kc + (0..15), columns R: A operand zhat[16 kc + lo][4 s + hi], B operand g_P[ri][4 s + hi]
+    floatx4 gt = {0.f, 0.f, 0.f, 0.f};
+    {
+      const int kr = 16 * kc + lo;
+      const float ik = sInv[kr];
+#pragma unroll
+      for (int s = 0; s < KH; ++s) gt = mfma4(big[kr * ZS + 4 * s + hi] * ik, gpr[s], gt);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float g = gt[s] + gqi;  // G[ri][k0 + s] (zero operands past n: padded k add nothing below)
+      dsum[0] = fmaf(g, Ar[j][s], dsum[0]);
+      dsum[1] = fmaf(g, dAr[j][s], dsum[1]);
+      dsum[2] = fmaf(g, At[j][s], dsum[2]);
+      dsum[3] = fmaf(g, dAt[j][s], dsum[3]);
+    }
+    float bz[4][CT], bg[4][CT];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        bz[s][ct] = big[(k0 + s) * ZS + 16 * ct + lo];
+        bg[s][ct] = sG[(k0 + s) * ZS + 16 * ct + lo];
+      }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float v = fmaf(eA, Ar[j][s], fmaf(edA, dAr[j][s], fmaf(eTA, At[j][s], fmaf(eTdA, dAt[j][s], wi + vk[s]))));
+      float vt = fmaf(eA, At[j][s], fmaf(edA, dAt[j][s], fmaf(eTA, Ar[j][s], fmaf(eTdA, dAr[j][s], wk[s] + vi))));
+      if (k0 + s == ri) {
+        v += ui;
+        vt += ui;
+      }
+      const float op = v * iv[s];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        accP[ct] = mfma4(op, bz[s][ct], accP[ct]);
+        accT[ct] = mfma4(vt, bg[s][ct], accT[ct]);
+      }
+    }
+  }
+  // row terms of the fusion gradient (threads 0..15: row r0 + tid), from every node's zhat / g_P still in LDS
+  float facc[GNCDE_FC];
+#pragma unroll
+  for (int q = 0; q < GNCDE_FC; ++q) facc[q] = 0.f;
+  if (tid < kRB && r0 + tid < n) {
+    const int i = r0 + tid;
+    float gz = 0.f, gd = 0.f, gfr = 0.f, gfrd = 0.f, gfc_ = 0.f, gfcd = 0.f;
+    for (int c = 0; c < H; ++c) {
+      const float g = sG[i * ZS + c];
+      gz = fmaf(g, sZv[c], gz);
+      gd = fmaf(g, big[i * ZS + c], gd);
+      gfr = fmaf(g, sZv[H + c], gfr);
+      gfrd = fmaf(g, sZv[2 * H + c], gfrd);
+      gfc_ = fmaf(g, sZv[3 * H + c], gfc_);
+      gfcd = fmaf(g, sZv[4 * H + c], gfcd);
+    }
+    const float gqv = sGq[i];
+    const float R = fmaf((float)n, gqv, gz);
+    const float D = fmaf(gd, sInv[i], gqv);
+    const float r = sF[i], rd = sF[NP + i], c = sF[2 * NP + i], cd = sF[3 * NP + i];
+    const float dg = sF[4 * NP + i], dgd = sF[5 * NP + i];
+    facc[GNCDE_FC_WR_A] = R * r;
+    facc[GNCDE_FC_WR_DA] = R * rd;
+    facc[GNCDE_FC_WC_A] = R * c;
+    facc[GNCDE_FC_WC_DA] = R * cd;
+    facc[GNCDE_FC_WS_A] = R * s_t;
+    facc[GNCDE_FC_WS_DA] = R * sd_t;
+    facc[GNCDE_FC_UD_A] = D * dg;
+    facc[GNCDE_FC_UD_DA] = D * dgd;
+    facc[GNCDE_FC_UR_A] = D * r;
+    facc[GNCDE_FC_UR_DA] = D * rd;
+    facc[GNCDE_FC_UC_A] = D * c;
+    facc[GNCDE_FC_UC_DA] = D * cd;
+    facc[GNCDE_FC_US_A] = D * s_t;
+    facc[GNCDE_FC_US_DA] = D * sd_t;
+    facc[GNCDE_FC_IDC] = D;
+    facc[GNCDE_FC_VR_A] = fmaf(gqv, s_t, gfr);
+    facc[GNCDE_FC_VR_DA] = fmaf(gqv, sd_t, gfrd);
+    facc[GNCDE_FC_VC_A] = fmaf(gqv, s_t, gfc_);
+    facc[GNCDE_FC_VC_DA] = fmaf(gqv, sd_t, gfcd);
+  }
+  facc[GNCDE_FC_E_A] += dsum[0];
+  facc[GNCDE_FC_E_DA] += dsum[1];
+  facc[GNCDE_FC_ET_A] += dsum[2];
+  facc[GNCDE_FC_ET_DA] += dsum[3];
+  // this layer's own g_zhat / zhat rows are needed after the partials overwrite the node regions: the rows' Z and
+  // inv stay available through HBM (zin) and sInv
+  __syncthreads();  // every read of zhat / g_P of all nodes done: the partial rows alias them
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      big[(w * 16 + 4 * hi + r) * ZS + 16 * ct + lo] = accP[ct][r];
+      sG[(w * 16 + 4 * hi + r) * ZS + 16 * ct + lo] = accT[ct][r];
+    }
+  // fusion sums: a butterfly per wave, then the four wave partials in order
+#pragma unroll
+  for (int q = 0; q < GNCDE_FC; ++q) {
+    float v = facc[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) sFus[q * 4 + w] = v;
+  }
+  __syncthreads();
+  if (tid < GNCDE_FC) {
+    float* dst = a.gfc + ((size_t)blockIdx.x * a.L + l) * GNCDE_FC + tid;
+    *dst += (sFus[tid * 4] + sFus[tid * 4 + 1]) + (sFus[tid * 4 + 2] + sFus[tid * 4 + 3]);
+  }
+  // P[R], g_zhat[R]: the four K parts in a fixed order, into rows 64..79 of the two regions
+  for (int e = tid; e < 16 * H; e += 256) {
+    const int i = e / H, c = e % H;
+    float p = big[i * ZS + c], g = sG[i * ZS + c];
+#pragma unroll
+    for (int kp = 1; kp < 4; ++kp) {
+      p += big[(kp * 16 + i) * ZS + c];
+      g += sG[(kp * 16 + i) * ZS + c];
+    }
+    big[(64 + i) * ZS + c] = p;
+    sG[(64 + i) * ZS + c] = g;
+  }
+  __syncthreads();
+  const float* sP = big + 64 * ZS;   // P[R] [16][ZS]
+  const float* sGz = sG + 64 * ZS;   // g_zhat[R]
+  // ---- parameter partials: g_W' += g_out[R]^T P[R], g_b' += g_out[R]^T q[R] (d_out = H), or P | q out (CDE) ----
+  if (a.cde_out) {
+    for (int e = tid; e < 16 * (H + 1); e += 256) {
+      const int i = e / (H + 1), c = e % (H + 1);
+      if (r0 + i < n) a.pq[((size_t)b * n + r0 + i) * (H + 1) + c] = c < H ? sP[i * ZS + c] : sRow[16 + i];
+    }
+  } else {
+    float* go = sG;  // g_out[R] staged in rows 0..15 of the g_P region (the partials are consumed)
+    for (int e = tid; e < 16 * H; e += 256) {
+      const int i = e / H, c = e % H;
+      go[i * ZS + c] = r0 + i < n ? a.gout[((size_t)b * n + r0 + i) * H + c] : 0.f;
+    }
+    __syncthreads();
+    float* gw = a.gw + (size_t)blockIdx.x * a.gw_stride + a.gw_off;
+    for (int e = tid; e < H * H + H; e += 256) {
+      float acc = 0.f;
+      if (e < H * H) {
+        const int jo = e / H, c = e % H;
+#pragma unroll
+        for (int i = 0; i < kRB; ++i) acc = fmaf(go[i * ZS + jo], sP[i * ZS + c], acc);
+      } else {
+        const int jo = e - H * H;
+#pragma unroll
+        for (int i = 0; i < kRB; ++i) acc = fmaf(go[i * ZS + jo], sRow[16 + i], acc);
+      }
+      gw[e] += acc;
+    }
+    __syncthreads();  // go is reused below
+  }
+  // ---- RMSNorm^T of the block's rows and the next cotangents ------------------------------------------------
+  // thread = (row tid / 16, columns (tid % 16) + 16 u): a row's 16 threads are 16 consecutive lanes
+  {
+    const int i = tid >> 4, cl = tid & 15;
+    constexpr int U = H / 16;
+    const bool iin = r0 + i < n;
+    const float inv = iin ? sInv[r0 + i] : 0.f;
+    float z[U], gzh[U];
+    float dot = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      z[u] = iin ? a.zin[((size_t)b * n + r0 + i) * H + cl + 16 * u] : 0.f;
+      gzh[u] = sGz[i * ZS + cl + 16 * u];
+      dot = fmaf(gzh[u], z[u] * inv, dot);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+    const float cdot = dot / (float)H;
+    float gZ[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) gZ[u] = inv * (gzh[u] - z[u] * inv * cdot);
+    if (l == 0) {
+      if (iin)
+#pragma unroll
+        for (int u = 0; u < U; ++u) a.gz[((size_t)b * n + r0 + i) * H + cl + 16 * u] = gZ[u];
+    } else {
+      float* go = sG;  // g_out_{l-1}[R] = g_Z * [Z_l > 0]
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float g = z[u] > 0.f ? gZ[u] : 0.f;
+        go[i * ZS + cl + 16 * u] = g;
+        if (iin) a.gout_next[((size_t)b * n + r0 + i) * H + cl + 16 * u] = g;
+      }
+    }
+  }
+  if (l == 0) return;
+  __syncthreads();
+  {
+    const float* go = sG;
+    for (int e = tid; e < 16 * H; e += 256) {  // g_P_{l-1}[i][c] = sum_j g_out[i][j] W'_{l-1}[j][c]
+      const int i = e / H, c = e % H;
+      float acc = 0.f;
+#pragma unroll 8
+      for (int jo = 0; jo < H; ++jo) acc = fmaf(go[i * ZS + jo], a.wprev[jo * H + c], acc);
+      if (r0 + i < n) a.gP_next[((size_t)b * n + r0 + i) * H + c] = acc;
+    }
+    if (tid < kRB && r0 + tid < n) {
+      float acc = 0.f;
+      for (int jo = 0; jo < H; ++jo) acc = fmaf(go[tid * ZS + jo], a.bprev[jo], acc);
+      a.gq_next[(size_t)b * n + r0 + tid] = acc;
+    }
+  }
+}
+
+struct HeadArgs {
+  int B, n, T, H, cde;
+  const float* ts;
+  const float* tcoef;      // [B, T-1, 3, n]
+  const float* data_coef;  // [B, T-1, 4, n, 8, 2]
+  const float* t;
+  const float* gF;         // [B, n, H] the stage value's cotangent
+  const float* wl;         // W'_{L-1} natural [d_L, H]
+  const float* bl;         // b'_{L-1} [d_L]
+  float* gout;             // ODE: [B, n, H]
+  float* gP;               // [B, n, H]
+  float* gq;               // [B, n]
+  float* tgF;              // CDE: tg gF [B, n, H]
+  float* dxo;              // CDE: dX [B, n, 16]
+};
+
+// Output layer's cotangents for a 16-row block (thread = (row tid / 16, column tid % 16 + 16 u)).
+__global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
+  const int nb = (a.n + kRB - 1) / kRB;
+  const int b = blockIdx.x / nb, r0 = (blockIdx.x % nb) * kRB;
+  const int n = a.n, H = a.H, T = a.T, tid = threadIdx.x;
+  const int i = tid >> 4, cl = tid & 15;
+  __shared__ float sgo[kRB][65];   // ODE g_out rows / CDE tg gF rows
+  __shared__ float sdx[kRB][17];
+  __shared__ float sK[kRB][64];    // CDE: sum_j dX_ij b'[16m + j] per (row, m)
+  const float tb = a.t[b];
+  const float* tsb = a.ts + (size_t)b * T;
+  const int idx = interval_index(tsb, T, tb);
+  const float f = tb - tsb[idx];
+  const bool iin = r0 + i < n;
+  const int row = iin ? r0 + i : n - 1;
+  const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n + row;
+  const float tg = iin ? fmaf(f, fmaf(3.0f * f, tc[0], 2.0f * tc[n]), tc[2 * n]) : 0.f;
+  for (int c = cl; c < H; c += 16) {
+    const float g = iin ? tg * a.gF[((size_t)b * n + row) * H + c] : 0.f;
+    sgo[i][c] = g;
+    if (iin) (a.cde ? a.tgF : a.gout)[((size_t)b * n + row) * H + c] = g;
+  }
+  if (a.cde) {
+    const size_t blk = (size_t)n * 16;
+    const float* dc = a.data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)row * 16 + cl;
+    const float dx = iin ? fmaf(f, fmaf(3.0f * f, dc[0], 2.0f * dc[blk]), dc[2 * blk]) : 0.f;
+    sdx[i][cl] = dx;
+    if (iin) a.dxo[((size_t)b * n + row) * 16 + cl] = dx;
+  }
+  __syncthreads();
+  if (!a.cde) {
+    for (int c = cl; c < H; c += 16) {  // g_P[i][c] = sum_j g_out[i][j] W'[j][c]
+      float acc = 0.f;
+      for (int jo = 0; jo < H; ++jo) acc = fmaf(sgo[i][jo], a.wl[jo * H + c], acc);
+      if (iin) a.gP[((size_t)b * n + row) * H + c] = acc;
+    }
+    if (cl == 0) {
+      float acc = 0.f;
+      for (int jo = 0; jo < H; ++jo) acc = fmaf(sgo[i][jo], a.bl[jo], acc);
+      if (iin) a.gq[(size_t)b * n + row] = acc;
+    }
+    return;
+  }
+  // CDE: g_P[i][c] = sum_m tgF_im sum_j dX_ij W'[16 m + j][c];  g_q_i = sum_m tgF_im sum_j dX_ij b'[16 m + j]
+  for (int m = cl; m < H; m += 16) {
+    float acc = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) acc = fmaf(sdx[i][jj], a.bl[16 * m + jj], acc);
+    sK[i][m] = acc;
+  }
+  __syncthreads();
+  for (int c = cl; c < H; c += 16) {
+    float acc = 0.f;
+    for (int m = 0; m < H; ++m) {
+      const float* wr = a.wl + (size_t)(16 * m) * H + c;
+      float s = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) s = fmaf(sdx[i][jj], wr[(size_t)jj * H], s);
+      acc = fmaf(sgo[i][m], s, acc);
+    }
+    if (iin) a.gP[((size_t)b * n + row) * H + c] = acc;
+  }
+  if (cl == 0) {
+    float acc = 0.f;
+    for (int m = 0; m < H; ++m) acc = fmaf(sgo[i][m], sK[i][m], acc);
+    if (iin) a.gq[(size_t)b * n + row] = acc;
+  }
+}
+
+// CDE read-out weight / bias gradient over a 32-row chunk of all samples' nodes:
+//   part[(16 m + j) * (H + 1) + c] += sum_rows tgF[r][m] dX[r][j] (P | q)[r][c]
+__global__ void __launch_bounds__(256) k_bwd_readout(int rows, int H, const float* __restrict__ tgF,
+                                                     const float* __restrict__ dx, const float* __restrict__ pq,
+                                                     float* __restrict__ part) {
+  __shared__ float st[kRoChunk][65], sx[kRoChunk][17], sp[kRoChunk][66];
+  const int r0 = blockIdx.x * kRoChunk;
+  const int cnt = rows - r0 < kRoChunk ? rows - r0 : kRoChunk;
+  for (int e = threadIdx.x; e < kRoChunk * H; e += 256) {
+    const int r = e / H, c = e % H;
+    st[r][c] = r < cnt ? tgF[(size_t)(r0 + r) * H + c] : 0.f;
+  }
+  for (int e = threadIdx.x; e < kRoChunk * 16; e += 256) {
+    const int r = e / 16, c = e % 16;
+    sx[r][c] = r < cnt ? dx[(size_t)(r0 + r) * 16 + c] : 0.f;
+  }
+  for (int e = threadIdx.x; e < kRoChunk * (H + 1); e += 256) {
+    const int r = e / (H + 1), c = e % (H + 1);
+    sp[r][c] = r < cnt ? pq[(size_t)(r0 + r) * (H + 1) + c] : 0.f;
+  }
+  __syncthreads();
+  float* dst = part + (size_t)blockIdx.x * 16 * H * (H + 1);
+  for (int e = threadIdx.x; e < 16 * H * (H + 1); e += 256) {
+    const int mj = e / (H + 1), c = e % (H + 1), m = mj >> 4, jj = mj & 15;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < kRoChunk; ++r) acc = fmaf(st[r][m] * sx[r][jj], sp[r][c], acc);
+    dst[e] += acc;
+  }
+}
+
+// CDE data-spline cotangent (TGB): g_dX[i][j] = sum_m tgF_im (P_i . W'[16m+j, :] + q_i b'[16m+j]), scattered onto
+// the stage interval's (d, c, b) with weights (3 f^2, 2 f, 1) (as v_data_grad).  One thread per (sample, node, j).
+__global__ void k_bwd_data(int B, int n, int H, int T, const float* __restrict__ ts, const float* __restrict__ t,
+                           const float* __restrict__ tgF, const float* __restrict__ pq, const float* __restrict__ wl,
+                           const float* __restrict__ bl, float* __restrict__ gcoef) {
+  const int b = blockIdx.y;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * 16) return;
+  const int i = e >> 4, jj = e & 15;
+  const float* g = tgF + ((size_t)b * n + i) * H;
+  const float* p = pq + ((size_t)b * n + i) * (H + 1);
+  float s = 0.f;
+  for (int m = 0; m < H; ++m) {
+    const float* wr = wl + (size_t)(16 * m + jj) * H;
+    float fv = p[H] * bl[16 * m + jj];
+    for (int c = 0; c < H; ++c) fv = fmaf(p[c], wr[c], fv);
+    s = fmaf(g[m], fv, s);
+  }
+  const float tb = t[b];
+  const float* tsb = ts + (size_t)b * T;
+  const int idx = interval_index(tsb, T, tb);
+  const float f = tb - tsb[idx];
+  const size_t blk = (size_t)n * 16;
+  float* cb = gcoef + ((size_t)b * (T - 1) + idx) * 4 * blk + e;
+  cb[0] = fmaf(3.0f * f * f, s, cb[0]);
+  cb[blk] = fmaf(2.0f * f, s, cb[blk]);
+  cb[2 * blk] += s;
+}
+
+// Reduce the partial slots (fixed order) into gW'[l] [d_out, H] and gb'[l] [d_out] per layer, and the fusion gradient.
+__global__ void k_bwd_reduce(int slots, int L, int H, int gw_stride, int cde, int ro_chunks,
+                             const float* __restrict__ gfc, const float* __restrict__ gw, const float* __restrict__ gwo,
+                             float* __restrict__ gfusion, float* __restrict__ gwp, float* __restrict__ gbp) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nfc = L * GNCDE_FC;
+  const int nh = (cde ? L - 1 : L) * (H * H + H);
+  if (e < nfc) {
+    float s = 0.f;
+    for (int k = 0; k < slots; ++k) s += gfc[(size_t)k * nfc + e];
+    gfusion[e] = s;
+    return;
+  }
+  int q = e - nfc;
+  if (q < nh) {
+    float s = 0.f;
+    for (int k = 0; k < slots; ++k) s += gw[(size_t)k * gw_stride + q];
+    const int l = q / (H * H + H), r = q % (H * H + H);
+    if (r < H * H) gwp[(size_t)l * H * H + r] = s;  // layers < L-1 (and the ODE output) are H x H
+    else gbp[(size_t)l * H + r - H * H] = s;
+    return;
+  }
+  q -= nh;
+  if (cde && q < 16 * H * (H + 1)) {
+    float s = 0.f;
+    for (int k = 0; k < ro_chunks; ++k) s += gwo[(size_t)k * 16 * H * (H + 1) + q];
+    const int mj = q / (H + 1), c = q % (H + 1);
+    const size_t wo = (size_t)(L - 1) * H * H, bo = (size_t)(L - 1) * H;
+    if (c < H) gwp[wo + (size_t)mj * H + c] = s;
+    else gbp[bo + mj] = s;
+  }
+}
+
+// g_W'[l], g_b'[l] -> the packed parameter gradient: g_W = g_W' diag(rms_w) + g_b' rms_b^T, g_b = g_b',
+// g_rms_w[c] = sum_j g_W'[j][c] W[j][c], g_rms_b[c] = sum_j g_b'[j] W[j][c].  One block per layer.
+__global__ void k_bwd_params(int L, int H, int dlast, const float* __restrict__ params, const float* __restrict__ gwp,
+                             const float* __restrict__ gbp, float* __restrict__ gparams) {
+  const int l = blockIdx.x;
+  const int din = H, dout = l == L - 1 ? dlast : H;
+  size_t off = 0;
+  for (int j = 0; j < l; ++j) off += 2 * (size_t)H + (size_t)H * H + H;
+  const float* rw = params + off;
+  const float* rb = rw + din;
+  const float* W = rb + din;
+  const float* gW_ = gwp + (size_t)l * H * H;
+  const float* gb_ = gbp + (size_t)l * H;
+  float* g = gparams + off;
+  for (int e = threadIdx.x; e < dout * din; e += blockDim.x) {
+    const int jo = e / din, c = e % din;
+    g[2 * din + e] = fmaf(gW_[e], rw[c], gb_[jo] * rb[c]);
+  }
+  for (int jo = threadIdx.x; jo < dout; jo += blockDim.x) g[2 * din + dout * din + jo] = gb_[jo];
+  for (int c = threadIdx.x; c < din; c += blockDim.x) {
+    float sw = 0.f, sb = 0.f;
+    for (int jo = 0; jo < dout; ++jo) {
+      sw = fmaf(gW_[(size_t)jo * din + c], W[(size_t)jo * din + c], sw);
+      sb = fmaf(gb_[jo], W[(size_t)jo * din + c], sb);
+    }
+    g[c] = sw;
+    g[din + c] = sb;
+  }
+}
+
+template <int H>
+void launch_layer(const BwdArgs& a, int grid, size_t smem, hipStream_t st) {
+  hipLaunchKernelGGL((k_bwd_layer<H>), dim3(grid), dim3(256), smem, st, a);
+}
+
+bool set_smem(int H, size_t smem) {
+  static bool done[3] = {false, false, false};
+  const int k = H == 16 ? 0 : (H == 32 ? 1 : 2);
+  if (done[k] || smem <= 64 * 1024) return true;
+  const void* fn = H == 16 ? reinterpret_cast<const void*>(&k_bwd_layer<16>)
+                           : (H == 32 ? reinterpret_cast<const void*>(&k_bwd_layer<32>)
+                                      : reinterpret_cast<const void*>(&k_bwd_layer<64>));
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) return false;
+  done[k] = true;
+  return true;
+}
+
+}  // namespace
+
+// Envelope: fp32 (the reverse mode of every compute mode runs on the fp32 view), n <= 256, one hidden width
+// H in {16, 32, 64} for every layer input, and an ODE output of width H or the de = 8 read-out with h = H.
+bool rows_vjp_supported(const GncdeProblem& p) {
+  if (p.compute != GNCDE_COMPUTE_FP32 || p.n < 1 || p.n > kMaxN) return false;
+  const int H = p.dims[0];
+  if (H != 16 && H != 32 && H != 64) return false;
+  for (int l = 0; l < p.L; ++l)
+    if (p.dims[l] != H) return false;
+  if (p.cde_hidden > 0) return p.cde_embed == 8 && p.cde_hidden == H && p.dims[p.L] == 16 * H;
+  if (p.dims[p.L] != H) return false;
+  // the forward keep needs every layer on the one-launch path or on k_layer (gncde_generic.hip generic_vf_eval)
+  if (rows_supported(p)) return true;
+  for (int l = 0; l < p.L; ++l)
+    if (layer_mode(p, l) < 0) return false;
+  return true;
+}
+
+namespace {
+struct RowsVjpWs {
+  float *keep, *gP[2], *gq[2], *gout[2], *tgF, *dx, *pq, *gfc, *gw, *gwo, *gwp, *gbp, *dy;
+  int nb, slots, gw_stride, ro_chunks;
+};
+size_t carve_rows_vjp(const GncdeProblem& p, char* ws, RowsVjpWs& w) {
+  const size_t B = p.B, n = p.n, H = p.dims[0];
+  const bool cde = p.cde_hidden > 0;
+  w.nb = (int)((n + kRB - 1) / kRB);
+  w.slots = (int)B * w.nb;
+  w.gw_stride = (int)((cde ? p.L - 1 : p.L) * (H * H + H));
+  w.ro_chunks = cde ? (int)((B * n + kRoChunk - 1) / kRoChunk) : 0;
+  size_t off = 0;
+  auto take = [&](size_t floats) {
+    float* ptr = ws ? reinterpret_cast<float*>(ws + off) : nullptr;
+    off += align_up((floats ? floats : 1) * sizeof(float), 256);
+    return ptr;
+  };
+  const size_t E = B * n * H;
+  w.keep = take((size_t)(p.L - 1) * E);
+  for (int k = 0; k < 2; ++k) {
+    w.gP[k] = take(E);
+    w.gq[k] = take(B * n);
+    w.gout[k] = take(E);
+  }
+  w.tgF = take(cde ? E : 0);
+  w.dx = take(cde ? B * n * 16 : 0);
+  w.pq = take(cde ? B * n * (H + 1) : 0);
+  w.gfc = take((size_t)w.slots * p.L * GNCDE_FC);
+  w.gw = take((size_t)w.slots * w.gw_stride);
+  w.gwo = take((size_t)w.ro_chunks * 16 * H * (H + 1));
+  w.gwp = take((size_t)(p.L - 1) * H * H + (size_t)p.dims[p.L] * H);
+  w.gbp = take((size_t)(p.L - 1) * H + p.dims[p.L]);
+  w.dy = take(B * n * (size_t)out_dim(p));
+  return off;
+}
+}  // namespace
+
+size_t rows_vjp_workspace(const GncdeProblem& p) {
+  RowsVjpWs w;
+  return carve_rows_vjp(p, nullptr, w);
+}
+
+void rows_vjp_begin(const GncdeProblem& p, char* ws, hipStream_t st) {
+  RowsVjpWs w;
+  carve_rows_vjp(p, ws, w);
+  const size_t H = p.dims[0];
+  (void)hipMemsetAsync(w.gfc, 0, (size_t)w.slots * p.L * GNCDE_FC * sizeof(float), st);
+  (void)hipMemsetAsync(w.gw, 0, (size_t)w.slots * w.gw_stride * sizeof(float), st);
+  if (w.ro_chunks) (void)hipMemsetAsync(w.gwo, 0, (size_t)w.ro_chunks * 16 * H * (H + 1) * sizeof(float), st);
+}
+
+// The VJP of one evaluation at (t, u) for the cotangent gF: the stage input's cotangent into gu (overwritten), the
+// parameter / fusion partials accumulated in the workspace, gdata (optional) accumulated.  wf / bfold: W', b' of
+// every layer back to back (generic_vf_prepare's fold).
+int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* gF, float* gu, float* gdata,
+                const float* csum, const float* wf, const float* bfold, char* ws, char* vf_ws, unsigned* bars,
+                hipStream_t st) {
+  RowsVjpWs w;
+  carve_rows_vjp(p, ws, w);
+  const int B = p.B, n = p.n, H = p.dims[0], L = p.L;
+  const bool cde = p.cde_hidden > 0;
+  // forward with the hidden outputs kept
+  int rc = generic_vf_eval(p, t, u, w.dy, vf_ws, st, true, bars, w.keep);
+  if (rc) return rc;
+  const size_t E = (size_t)B * n * H;
+  size_t wo_last = 0, bo_last = 0;
+  for (int l = 0; l + 1 < L; ++l) {
+    wo_last += (size_t)H * H;
+    bo_last += H;
+  }
+  {
+    HeadArgs h{};
+    h.B = B;
+    h.n = n;
+    h.T = p.T;
+    h.H = H;
+    h.cde = cde ? 1 : 0;
+    h.ts = p.ts;
+    h.tcoef = p.tcoef;
+    h.data_coef = p.data_coef;
+    h.t = t;
+    h.gF = gF;
+    h.wl = wf + wo_last;
+    h.bl = bfold + bo_last;
+    h.gout = w.gout[0];
+    h.gP = w.gP[0];
+    h.gq = w.gq[0];
+    h.tgF = w.tgF;
+    h.dxo = w.dx;
+    hipLaunchKernelGGL(k_bwd_head, dim3(B * w.nb), dim3(256), 0, st, h);
+  }
+  const size_t smem = bwd_smem(n, H);
+  if (!set_smem(H, smem)) return GNCDE_ERR_HIP;
+  int cur = 0;
+  for (int l = L - 1; l >= 0; --l) {
+    BwdArgs a{};
+    a.B = B;
+    a.n = n;
+    a.T = p.T;
+    a.L = L;
+    a.l = l;
+    a.nb = w.nb;
+    a.ts = p.ts;
+    a.coef = p.coef;
+    a.csum = csum;
+    a.fusion = p.fusion;
+    a.t = t;
+    a.zin = l == 0 ? u : w.keep + (size_t)(l - 1) * E;
+    a.gP = w.gP[cur];
+    a.gq = w.gq[cur];
+    a.gout = w.gout[cur];
+    a.wprev = l > 0 ? wf + (size_t)(l - 1) * H * H : nullptr;
+    a.bprev = l > 0 ? bfold + (size_t)(l - 1) * H : nullptr;
+    a.gP_next = w.gP[cur ^ 1];
+    a.gq_next = w.gq[cur ^ 1];
+    a.gout_next = w.gout[cur ^ 1];
+    a.gz = gu;
+    a.pq = w.pq;
+    a.gfc = w.gfc;
+    a.gw = w.gw;
+    a.gw_stride = w.gw_stride;
+    a.gw_off = l * (H * H + H);
+    a.cde_out = (cde && l == L - 1) ? 1 : 0;
+    if (H == 16) launch_layer<16>(a, B * w.nb, smem, st);
+    else if (H == 32) launch_layer<32>(a, B * w.nb, smem, st);
+    else launch_layer<64>(a, B * w.nb, smem, st);
+    cur ^= 1;
+  }
+  if (cde) {
+    hipLaunchKernelGGL(k_bwd_readout, dim3(w.ro_chunks), dim3(256), 0, st, B * n, H, w.tgF, w.dx, w.pq, w.gwo);
+    if (gdata)
+      hipLaunchKernelGGL(k_bwd_data, dim3((n * 16 + 255) / 256, B), dim3(256), 0, st, B, n, H, p.T, p.ts, t, w.tgF,
+                         w.pq, wf + wo_last, bfold + bo_last, gdata);
+  }
+  return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+}
+
+void rows_vjp_finish(const GncdeProblem& p, char* ws, float* gparams, float* gfusion, hipStream_t st) {
+  RowsVjpWs w;
+  carve_rows_vjp(p, ws, w);
+  const int H = p.dims[0], L = p.L;
+  const bool cde = p.cde_hidden > 0;
+  const int tot = L * GNCDE_FC + (cde ? L - 1 : L) * (H * H + H) + (cde ? 16 * H * (H + 1) : 0);
+  hipLaunchKernelGGL(k_bwd_reduce, dim3((tot + 255) / 256), dim3(256), 0, st, w.slots, L, H, w.gw_stride, cde ? 1 : 0,
+                     w.ro_chunks, w.gfc, w.gw, w.gwo, gfusion, w.gwp, w.gbp);
+  hipLaunchKernelGGL(k_bwd_params, dim3(L), dim3(256), 0, st, L, H, p.dims[L], p.params, w.gwp, w.gbp, gparams);
+}
+
+}  // namespace gncde

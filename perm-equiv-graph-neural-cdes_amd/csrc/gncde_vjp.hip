@@ -514,7 +514,7 @@ size_t generic_vjp_workspace(const GncdeProblem& p, const GncdeSolver& s) {
   VjpWs w;
   size_t bytes = 0;
   carve(p, nullptr, w, &bytes);
-  return bytes + generic_vf_workspace(p);
+  return bytes + (rows_vjp_supported(p) ? rows_vjp_workspace(p) : 0) + generic_vf_workspace(p);
 }
 
 namespace {
@@ -680,7 +680,10 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
   VjpWs w;
   size_t bytes = 0;
   carve(p, ws, w, &bytes);
-  char* vf_ws = ws + bytes;
+  // one launch per ConvLayer for the reverse mode of an evaluation where it fits (gncde_rows_vjp.hip)
+  const bool rows = rows_vjp_supported(p);
+  char* rows_ws = ws + bytes;
+  char* vf_ws = rows_ws + (rows ? rows_vjp_workspace(p) : 0);
   const Tableau tab = s.method == GNCDE_RK4 ? rk4_tab() : tsit5_tab();
   generic_vf_prepare(p, vf_ws, st);
   unsigned bars = 0;  // barriers of one-launch stage evaluations (generic_vf_eval)
@@ -697,6 +700,7 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
   }
   const unsigned gb = cdiv(B, 256);
   const dim3 ge(cdiv(E, 256), B);
+  if (rows) rows_vjp_begin(p, rows_ws, st);
   (void)hipMemsetAsync(w.gsum, 0, P * sizeof(float), st);
   (void)hipMemsetAsync(w.gfc, 0, (size_t)B * p.L * GNCDE_FC * sizeof(float), st);
   if (gdata)
@@ -742,7 +746,13 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
       hipLaunchKernelGGL(v_stage_time, dim3(gb), dim3(256), 0, st, B, tab.c[i], w.tcur, w.hcur, w.tst);
       // tmp = cotangent of U_i
       (void)hipMemsetAsync(w.tmp, 0, (size_t)B * E * sizeof(float), st);
-      vf_vjp(p, w.tst, w.U[i], w.gK[i], w.tmp, gdata, w, st);
+      if (rows) {
+        const int rc = rows_vf_vjp(p, w.tst, w.U[i], w.gK[i], w.tmp, gdata, generic_vf_csum(p, vf_ws), w.wf, w.bf,
+                                   rows_ws, vf_ws, &bars, st);
+        if (rc) return rc;
+      } else {
+        vf_vjp(p, w.tst, w.U[i], w.gK[i], w.tmp, gdata, w, st);
+      }
       // gy += tmp ; gK_j += h a_ij tmp
       Lin one{};
       one.x[0] = w.tmp;
@@ -764,9 +774,13 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
       hipLaunchKernelGGL(v_step_row, ge, dim3(256), 0, st, B, E, G, k, gys, w.lam, 1);
   }
   (void)hipMemcpyAsync(gy0, w.lam, (size_t)B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
-  (void)hipMemcpyAsync(gparams, w.gsum, P * sizeof(float), hipMemcpyDeviceToDevice, st);
-  hipLaunchKernelGGL(v_batch_sum, dim3(cdiv((size_t)p.L * GNCDE_FC, 256)), dim3(256), 0, st, B,
-                     (size_t)p.L * GNCDE_FC, w.gfc, gfusion);
+  if (rows) {
+    rows_vjp_finish(p, rows_ws, gparams, gfusion, st);
+  } else {
+    (void)hipMemcpyAsync(gparams, w.gsum, P * sizeof(float), hipMemcpyDeviceToDevice, st);
+    hipLaunchKernelGGL(v_batch_sum, dim3(cdiv((size_t)p.L * GNCDE_FC, 256)), dim3(256), 0, st, B,
+                       (size_t)p.L * GNCDE_FC, w.gfc, gfusion);
+  }
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }
 

@@ -706,3 +706,89 @@ def test_config4_training_shape(G):
             sz = total[l][k].size
             assert rel_err(gp[off:off + sz].reshape(total[l][k].shape), total[l][k]) <= RTOL_GRAD, (l, k)
             off += sz
+
+
+# ---- the per-layer reverse kernels (gncde_rows_vjp.hip): n <= 256, one hidden width, ODE or de = 8 CDE ----------
+ROWS_VJP_CASES = [  # (kind, n, H, L, cde, method, B)
+    ("undirected", 40, 32, 2, False, "rk4", 2),
+    ("directed", 200, 16, 3, False, "rk4", 2),
+    ("undirected", 150, 64, 2, False, "tsit5", 2),
+    ("undirected", 40, 16, 2, True, "rk4", 2),
+    ("plain", 129, 64, 3, True, "rk4", 2),          # config-3 shape: the forward keeps its layers on k_layer
+    ("undirected", 255, 32, 4, True, "rk4", 2),     # config-5 shape
+]
+
+
+@pytest.mark.parametrize("kind,n,H,L,cde,method,B", ROWS_VJP_CASES)
+def test_rows_vjp_matches_oracle(G, kind, n, H, L, cde, method, B):
+    """The one-launch-per-layer reverse mode of an evaluation (gncde_rows_vjp.hip), inside the generic fixed-grid
+    sweep, against the fp64 oracle's discrete adjoint: the initial-state, parameter and fusion-table gradients (and,
+    for the CDE wrapper, the data spline's coefficient gradient, TGB's data-encoder path).  Samples are redrawn until
+    their gradient is stable under a 1e-6 change of y0 (ReLU kinks)."""
+    rng = np.random.default_rng(7000 + n + H)
+    T = 4
+    dims = [H] * L + [16 * H if cde else H]
+    ts, coeffs, P = MG.problem(rng, B, n, T, kind, dims, irregular=False)
+    for lay in P.layers:
+        for nm in OG.FUSION_NAMES[kind]:
+            lay[nm] = lay[nm] * 3.0
+    kw, dco = {}, None
+    if cde:
+        dco = []
+        for b in range(B):
+            x = rng.standard_normal((T, n, 8))
+            X = np.stack([np.broadcast_to(ts[b][:, None, None], x.shape), x], axis=-1)
+            dco.append(O.backward_hermite_coefficients(ts[b], X))
+        kw = dict(data_coeffs=tuple(np.stack([c[q] for c in dco]) for q in range(4)), cde_hidden=H, cde_embed=8)
+    prob = G.make_problem(ts, coeffs, P.kind, P.layers, **kw)
+    grids = [O.rk4_grid(ts[b, 0], ts[b, -1], 3) if method == "rk4" else O.constant_grid(ts[b, 0], ts[b, -1], 1.0)
+             for b in range(B)]
+    y0 = rng.standard_normal((B, n, H))
+    gfin = rng.standard_normal((B, n, H))
+    gy0_ref, total, gdata_ref = [], None, []
+    for b in range(B):
+        ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
+        if cde:
+            cx = O.CubicInterpolation(ts[b], dco[b])
+            f = lambda t, y, c=ctrl, x=cx: O.cde_wrapper(P, H, 8, t, y, c, x)  # noqa: E731
+            fv = lambda t, y, g, c=ctrl, x=cx: OG.cde_wrapper_vjp(P, H, 8, t, y, c, x, g, data_grad=True)  # noqa: E731
+        else:
+            f = lambda t, y, c=ctrl: O.vector_field(P, t, y, c)  # noqa: E731
+            fv = lambda t, y, g, c=ctrl: OG.vector_field_vjp(P, t, y, c, g)  # noqa: E731
+        for _ in range(6):
+            g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], method, g_final=gfin[b])
+            g1, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b] * (1 + 1e-6), method, g_final=gfin[b])
+            if np.max(np.abs(g1 - g0)) <= 1e-5 * np.max(np.abs(g0)):
+                break
+            y0[b] = rng.standard_normal((n, H))
+        gy0_ref.append(g0)
+        if cde:
+            gdata_ref.append(gr[-1]["data_coef"])
+            gr = gr[:-1]
+        total = OG._acc(total, gr)
+    grid, ns = G.layout.stack_grids(grids)
+    spec = G.SolverSpec(method=G._lib.RK4 if method == "rk4" else G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS,
+                        grid=grid, nsteps=ns)
+    ys = G.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda"))
+    spec.save_mode = G._lib.SAVE_T1
+    out = G.integrate_vjp(prob, spec, ys, torch.tensor(gfin, dtype=torch.float32, device="cuda"), data_grad=cde)
+    gy0, gp, gf = out[:3]
+    errs = {"gy0": rel_err(gy0.cpu().numpy(), np.stack(gy0_ref))}
+    gp = gp.cpu().numpy()
+    off = 0
+    for l in range(L):
+        for k in ("rms_w", "rms_b", "W", "b"):
+            sz = total[l][k].size
+            errs[f"{k}{l}"] = rel_err(gp[off:off + sz].reshape(total[l][k].shape), total[l][k])
+            off += sz
+    names, base, M = G.layout.fusion_map(kind, n)
+    if names:  # (the plain vector field has no fusion parameters)
+        gparams_ref = np.stack([np.concatenate([total[l][nm] for nm in names]) for l in range(L)])
+        errs["fusion"] = rel_err(gf.double().cpu().numpy() @ M.numpy().T, gparams_ref)
+    if cde:
+        gd = out[3].cpu().numpy()  # [B, T-1, 4, n, 8, 2]
+        errs["data"] = max(rel_err(gd[b].transpose(1, 0, 2, 3, 4), gdata_ref[b]) for b in range(B))
+    worst = max(errs, key=errs.get)
+    print(f"rows vjp {kind} n={n} H={H} L={L} cde={cde} {method}: worst {worst} {errs[worst]:.2e}")
+    for k, e in errs.items():
+        assert e <= RTOL_GRAD, (k, e)
