@@ -24,7 +24,7 @@
 //                   zhat g_P^T, which meets A, dA, A^T, dA^T in registers for the dense contractions; then g_W'
 //                   partials, RMSNorm^T, the ReLU mask and the next layer's g_out, g_P, g_q (or the stage input's
 //                   cotangent at l = 0)
-//   k_bwd_readout   (CDE) the read-out weight and bias gradient, split over 32-row chunks of all samples
+//   k_bwd_readout   (CDE) the read-out weight and bias gradient on MFMA, split over 128-row slices of all samples
 //   k_bwd_data      (CDE data-spline cotangent, TGB) g_dX_ij = tg_i sum_m gF_im (P_i . W'[16m+j,:] + q_i b'[16m+j])
 // Parameter and fusion partials accumulate in per-(sample, row block) / per-chunk slots that only their owner
 // workgroup updates (fixed order, no atomics); k_bwd_finish reduces them once per reverse sweep and maps g_W', g_b'
@@ -40,7 +40,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kRB = 16;
 constexpr int kMaxN = 256;
 constexpr int kStrip = 17;
-constexpr int kRoChunk = 32;  // rows per read-out gradient chunk
+constexpr int kRoRows = 128;  // rows per read-out gradient slice
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -454,18 +454,20 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
     }
     __syncthreads();
     float* gw = a.gw + (size_t)blockIdx.x * a.gw_stride + a.gw_off;
-    for (int e = tid; e < H * H + H; e += 256) {
+    // g_W'[j][c] += sum_{i in R} g_out[i][j] P[i][c]: CT x CT MFMA tiles over the waves, K = the 16 rows
+    for (int tile = w; tile < CT * CT; tile += 4) {
+      const int jt = tile / CT, ct = tile % CT;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = mfma4(go[(4 * s + hi) * ZS + 16 * jt + lo], sP[(4 * s + hi) * ZS + 16 * ct + lo], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gw[(16 * jt + 4 * hi + r) * H + 16 * ct + lo] += acc[r];
+    }
+    if (tid < H) {
       float acc = 0.f;
-      if (e < H * H) {
-        const int jo = e / H, c = e % H;
 #pragma unroll
-        for (int i = 0; i < kRB; ++i) acc = fmaf(go[i * ZS + jo], sP[i * ZS + c], acc);
-      } else {
-        const int jo = e - H * H;
-#pragma unroll
-        for (int i = 0; i < kRB; ++i) acc = fmaf(go[i * ZS + jo], sRow[16 + i], acc);
-      }
-      gw[e] += acc;
+      for (int i = 0; i < kRB; ++i) acc = fmaf(go[i * ZS + tid], sRow[16 + i], acc);
+      gw[H * H + tid] += acc;
     }
     __syncthreads();  // go is reused below
   }
@@ -508,12 +510,16 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
   __syncthreads();
   {
     const float* go = sG;
-    for (int e = tid; e < 16 * H; e += 256) {  // g_P_{l-1}[i][c] = sum_j g_out[i][j] W'_{l-1}[j][c]
-      const int i = e / H, c = e % H;
-      float acc = 0.f;
-#pragma unroll 8
-      for (int jo = 0; jo < H; ++jo) acc = fmaf(go[i * ZS + jo], a.wprev[jo * H + c], acc);
-      if (r0 + i < n) a.gP_next[((size_t)b * n + r0 + i) * H + c] = acc;
+    // g_P_{l-1}[i][c] = sum_j g_out[i][j] W'_{l-1}[j][c]: wave ct's 16 x 16 tile, K = H (W' rows from L2)
+    if (w < CT) {
+      const int ct = w;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KH; ++s)
+        acc = mfma4(go[lo * ZS + 4 * s + hi], a.wprev[(4 * s + hi) * H + 16 * ct + lo], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r0 + 4 * hi + r < n) a.gP_next[((size_t)b * n + r0 + 4 * hi + r) * H + 16 * ct + lo] = acc[r];
     }
     if (tid < kRB && r0 + tid < n) {
       float acc = 0.f;
@@ -539,15 +545,20 @@ struct HeadArgs {
   float* dxo;              // CDE: dX [B, n, 16]
 };
 
-// Output layer's cotangents for a 16-row block (thread = (row tid / 16, column tid % 16 + 16 u)).
+// Output layer's cotangents for a 16-row block (thread = (row tid / 16, column tid % 16 + 16 u) for the elementwise
+// parts; the products on MFMA).
+template <int H>
 __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
+  constexpr int CT = H / 16, KH = H / 4;
   const int nb = (a.n + kRB - 1) / kRB;
   const int b = blockIdx.x / nb, r0 = (blockIdx.x % nb) * kRB;
-  const int n = a.n, H = a.H, T = a.T, tid = threadIdx.x;
+  const int n = a.n, T = a.T, tid = threadIdx.x;
+  const int w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const int i = tid >> 4, cl = tid & 15;
-  __shared__ float sgo[kRB][65];   // ODE g_out rows / CDE tg gF rows
+  __shared__ float sgo[kRB][H + 1];  // ODE g_out rows / CDE tg gF rows
   __shared__ float sdx[kRB][17];
-  __shared__ float sK[kRB][64];    // CDE: sum_j dX_ij b'[16m + j] per (row, m)
+  __shared__ float sK[kRB][H];       // CDE: sum_j dX_ij b'[16m + j] per (row, m)
+  __shared__ float spart[4][kRB][H + 1];
   const float tb = a.t[b];
   const float* tsb = a.ts + (size_t)b * T;
   const int idx = interval_index(tsb, T, tb);
@@ -570,19 +581,45 @@ __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
   }
   __syncthreads();
   if (!a.cde) {
-    for (int c = cl; c < H; c += 16) {  // g_P[i][c] = sum_j g_out[i][j] W'[j][c]
-      float acc = 0.f;
-      for (int jo = 0; jo < H; ++jo) acc = fmaf(sgo[i][jo], a.wl[jo * H + c], acc);
-      if (iin) a.gP[((size_t)b * n + row) * H + c] = acc;
+    // g_P = g_out W': wave ct's 16 x 16 tile, K = H
+    if (w < CT) {
+      const int ct = w;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KH; ++s) acc = mfma4(sgo[lo][4 * s + hi], a.wl[(4 * s + hi) * H + 16 * ct + lo], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r0 + 4 * hi + r < n) a.gP[((size_t)b * n + r0 + 4 * hi + r) * H + 16 * ct + lo] = acc[r];
     }
-    if (cl == 0) {
+    if (tid < kRB) {
       float acc = 0.f;
-      for (int jo = 0; jo < H; ++jo) acc = fmaf(sgo[i][jo], a.bl[jo], acc);
-      if (iin) a.gq[(size_t)b * n + row] = acc;
+      for (int jo = 0; jo < H; ++jo) acc = fmaf(sgo[tid][jo], a.bl[jo], acc);
+      if (r0 + tid < n) a.gq[(size_t)b * n + r0 + tid] = acc;
     }
     return;
   }
-  // CDE: g_P[i][c] = sum_m tgF_im sum_j dX_ij W'[16 m + j][c];  g_q_i = sum_m tgF_im sum_j dX_ij b'[16 m + j]
+  // CDE: g_P[i][c] = sum_{j, m} (tgF_im dX_ij) W'[16 m + j][c] — wave w takes j = w, w + 4, ..., K = m per j
+  {
+    floatx4 acc[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq) {
+      const int jj = w + 4 * jq;
+      const float dx = sdx[lo][jj];
+#pragma unroll
+      for (int s = 0; s < KH; ++s) {
+        const float av = sgo[lo][4 * s + hi] * dx;
+        const float* wr = a.wl + (size_t)(16 * (4 * s + hi) + jj) * H + lo;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma4(av, wr[16 * ct], acc[ct]);
+      }
+    }
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) spart[w][4 * hi + r][16 * ct + lo] = acc[ct][r];
+  }
   for (int m = cl; m < H; m += 16) {
     float acc = 0.f;
 #pragma unroll
@@ -591,15 +628,8 @@ __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
   }
   __syncthreads();
   for (int c = cl; c < H; c += 16) {
-    float acc = 0.f;
-    for (int m = 0; m < H; ++m) {
-      const float* wr = a.wl + (size_t)(16 * m) * H + c;
-      float s = 0.f;
-#pragma unroll
-      for (int jj = 0; jj < 16; ++jj) s = fmaf(sdx[i][jj], wr[(size_t)jj * H], s);
-      acc = fmaf(sgo[i][m], s, acc);
-    }
-    if (iin) a.gP[((size_t)b * n + row) * H + c] = acc;
+    const float g = (spart[0][i][c] + spart[1][i][c]) + (spart[2][i][c] + spart[3][i][c]);
+    if (iin) a.gP[((size_t)b * n + row) * H + c] = g;
   }
   if (cl == 0) {
     float acc = 0.f;
@@ -608,35 +638,76 @@ __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
   }
 }
 
-// CDE read-out weight / bias gradient over a 32-row chunk of all samples' nodes:
-//   part[(16 m + j) * (H + 1) + c] += sum_rows tgF[r][m] dX[r][j] (P | q)[r][c]
-__global__ void __launch_bounds__(256) k_bwd_readout(int rows, int H, const float* __restrict__ tgF,
+// CDE read-out weight / bias gradient over a kRoRows-row slice of all samples' nodes, on MFMA:
+//   part[slot][(16 m + j) (H + 1) + c] += sum_rows (tgF[r][m] dX[r][j]) (P | q)[r][c]
+// one 16-row output tile per m (its rows are the 16 j), N tiles over c = 0..H (zero past H), K = the slice's rows;
+// wave w takes m = w, w + 4, ... in batches of 4.
+template <int H>
+__global__ void __launch_bounds__(256) k_bwd_readout(int rows, const float* __restrict__ tgF,
                                                      const float* __restrict__ dx, const float* __restrict__ pq,
                                                      float* __restrict__ part) {
-  __shared__ float st[kRoChunk][65], sx[kRoChunk][17], sp[kRoChunk][66];
-  const int r0 = blockIdx.x * kRoChunk;
-  const int cnt = rows - r0 < kRoChunk ? rows - r0 : kRoChunk;
-  for (int e = threadIdx.x; e < kRoChunk * H; e += 256) {
+  constexpr int NT = (H + 1 + 15) / 16, NC = NT * 16;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* st = sm;                      // [kRoRows][H + 1]
+  float* sx = st + kRoRows * (H + 1);  // [kRoRows][17]
+  float* sp = sx + kRoRows * 17;       // [kRoRows][NC + 1]
+  const int r0 = blockIdx.x * kRoRows;
+  const int cnt = rows - r0 < kRoRows ? rows - r0 : kRoRows;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
+  for (int e = tid; e < kRoRows * H; e += 256) {
     const int r = e / H, c = e % H;
-    st[r][c] = r < cnt ? tgF[(size_t)(r0 + r) * H + c] : 0.f;
+    st[r * (H + 1) + c] = r < cnt ? tgF[(size_t)(r0 + r) * H + c] : 0.f;
   }
-  for (int e = threadIdx.x; e < kRoChunk * 16; e += 256) {
+  for (int e = tid; e < kRoRows * 16; e += 256) {
     const int r = e / 16, c = e % 16;
-    sx[r][c] = r < cnt ? dx[(size_t)(r0 + r) * 16 + c] : 0.f;
+    sx[r * 17 + c] = r < cnt ? dx[(size_t)(r0 + r) * 16 + c] : 0.f;
   }
-  for (int e = threadIdx.x; e < kRoChunk * (H + 1); e += 256) {
-    const int r = e / (H + 1), c = e % (H + 1);
-    sp[r][c] = r < cnt ? pq[(size_t)(r0 + r) * (H + 1) + c] : 0.f;
+  for (int e = tid; e < kRoRows * NC; e += 256) {
+    const int r = e / NC, c = e % NC;
+    sp[r * (NC + 1) + c] = (r < cnt && c <= H) ? pq[(size_t)(r0 + r) * (H + 1) + c] : 0.f;
   }
   __syncthreads();
   float* dst = part + (size_t)blockIdx.x * 16 * H * (H + 1);
-  for (int e = threadIdx.x; e < 16 * H * (H + 1); e += 256) {
-    const int mj = e / (H + 1), c = e % (H + 1), m = mj >> 4, jj = mj & 15;
-    float acc = 0.f;
-#pragma unroll 8
-    for (int r = 0; r < kRoChunk; ++r) acc = fmaf(st[r][m] * sx[r][jj], sp[r][c], acc);
-    dst[e] += acc;
+  for (int m0 = w; m0 < H; m0 += 16) {  // batch: m = m0, m0 + 4, m0 + 8, m0 + 12
+    floatx4 acc[4][NT];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[q][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < kRoRows / 4; ++s) {
+      const int r = 4 * s + hi;
+      const float xv = sx[r * 17 + lo];
+      float bv[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) bv[nt] = sp[r * (NC + 1) + 16 * nt + lo];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = m0 + 4 * q;
+        if (m < H) {
+          const float av = st[r * (H + 1) + m] * xv;
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) acc[q][nt] = mfma4(av, bv[nt], acc[q][nt]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = m0 + 4 * q;
+      if (m < H)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int c = 16 * nt + lo;
+            if (c <= H) dst[(size_t)(16 * m + 4 * hi + rr) * (H + 1) + c] += acc[q][nt][rr];
+          }
+    }
   }
+}
+
+inline size_t readout_smem(int H) {
+  const int nc = ((H + 1 + 15) / 16) * 16;
+  return sizeof(float) * (size_t)kRoRows * ((H + 1) + 17 + nc + 1);
 }
 
 // CDE data-spline cotangent (TGB): g_dX[i][j] = sum_m tgF_im (P_i . W'[16m+j, :] + q_i b'[16m+j]), scattered onto
@@ -778,7 +849,7 @@ size_t carve_rows_vjp(const GncdeProblem& p, char* ws, RowsVjpWs& w) {
   w.nb = (int)((n + kRB - 1) / kRB);
   w.slots = (int)B * w.nb;
   w.gw_stride = (int)((cde ? p.L - 1 : p.L) * (H * H + H));
-  w.ro_chunks = cde ? (int)((B * n + kRoChunk - 1) / kRoChunk) : 0;
+  w.ro_chunks = cde ? (int)((B * n + kRoRows - 1) / kRoRows) : 0;
   size_t off = 0;
   auto take = [&](size_t floats) {
     float* ptr = ws ? reinterpret_cast<float*>(ws + off) : nullptr;
@@ -857,7 +928,9 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     h.gq = w.gq[0];
     h.tgF = w.tgF;
     h.dxo = w.dx;
-    hipLaunchKernelGGL(k_bwd_head, dim3(B * w.nb), dim3(256), 0, st, h);
+    if (H == 16) hipLaunchKernelGGL(k_bwd_head<16>, dim3(B * w.nb), dim3(256), 0, st, h);
+    else if (H == 32) hipLaunchKernelGGL(k_bwd_head<32>, dim3(B * w.nb), dim3(256), 0, st, h);
+    else hipLaunchKernelGGL(k_bwd_head<64>, dim3(B * w.nb), dim3(256), 0, st, h);
   }
   const size_t smem = bwd_smem(n, H);
   if (!set_smem(H, smem)) return GNCDE_ERR_HIP;
@@ -897,7 +970,17 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     cur ^= 1;
   }
   if (cde) {
-    hipLaunchKernelGGL(k_bwd_readout, dim3(w.ro_chunks), dim3(256), 0, st, B * n, H, w.tgF, w.dx, w.pq, w.gwo);
+    const size_t rsm = readout_smem(H);
+    if (H == 16) hipLaunchKernelGGL(k_bwd_readout<16>, dim3(w.ro_chunks), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
+    else if (H == 32) hipLaunchKernelGGL(k_bwd_readout<32>, dim3(w.ro_chunks), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
+    else {
+      static bool attr = false;  // 82 KB of LDS at H = 64
+      if (!attr && hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bwd_readout<64>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)rsm) != hipSuccess)
+        return GNCDE_ERR_HIP;
+      attr = true;
+      hipLaunchKernelGGL(k_bwd_readout<64>, dim3(w.ro_chunks), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
+    }
     if (gdata)
       hipLaunchKernelGGL(k_bwd_data, dim3((n * 16 + 255) / 256, B), dim3(256), 0, st, B, n, H, p.T, p.ts, t, w.tgF,
                          w.pq, wf + wo_last, bfold + bo_last, gdata);
@@ -917,3 +1000,66 @@ void rows_vjp_finish(const GncdeProblem& p, char* ws, float* gparams, float* gfu
 }
 
 }  // namespace gncde
+
+// Diagnostic (not part of include/gncde.h): one evaluation with the hidden outputs kept, for tests.
+extern "C" int gncde_diag_keep(const GncdeProblem* prob, const float* t, const float* y, float* dy, float* keep,
+                               void* ws, size_t ws_bytes, void* stream) {
+  using namespace gncde;
+  const int rc = validate_problem(prob);
+  if (rc) return rc;
+  if (ws_bytes < generic_vf_workspace(*prob)) return GNCDE_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  generic_vf_prepare(*prob, static_cast<char*>(ws), st);
+  unsigned bars = 0;
+  return generic_vf_eval(*prob, t, y, dy, static_cast<char*>(ws), st, true, &bars, keep);
+}
+
+// Diagnostic (not part of include/gncde.h): the reverse mode of ONE evaluation through the per-layer kernels.
+extern "C" int gncde_diag_vf_vjp(const GncdeProblem* prob, const float* t, const float* y, const float* gF, float* gy,
+                                 float* gparams, float* gfusion, void* ws, size_t ws_bytes, void* stream) {
+  using namespace gncde;
+  const int rc0 = validate_problem(prob);
+  if (rc0) return rc0;
+  const GncdeProblem& p = *prob;
+  if (!rows_vjp_supported(p)) return GNCDE_ERR_UNSUPPORTED;
+  const size_t L = p.L, H = p.dims[0];
+  size_t wfs = 0, bfs = 0;
+  for (size_t l = 0; l < L; ++l) {
+    wfs += (size_t)p.dims[l] * p.dims[l + 1];
+    bfs += p.dims[l + 1];
+  }
+  const size_t need = align_up((wfs + bfs) * sizeof(float), 256) + rows_vjp_workspace(p) + generic_vf_workspace(p);
+  if (ws_bytes < need || !ws) return GNCDE_ERR_WORKSPACE;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float* wf = static_cast<float*>(ws);
+  float* bf = wf + wfs;
+  char* rows_ws = static_cast<char*>(ws) + align_up((wfs + bfs) * sizeof(float), 256);
+  char* vf_ws = rows_ws + rows_vjp_workspace(p);
+  size_t wo = 0, bo = 0;
+  for (int l = 0; l < p.L; ++l) {
+    const LayerOffsets o = layer_offsets(p, l);
+    fold_linear(p.dims[l], p.dims[l + 1], p.params + o.rms_w, p.params + o.rms_b, p.params + o.W, p.params + o.b,
+                wf + wo, bf + bo, st);
+    wo += (size_t)p.dims[l] * p.dims[l + 1];
+    bo += p.dims[l + 1];
+  }
+  (void)H;
+  generic_vf_prepare(p, vf_ws, st);
+  rows_vjp_begin(p, rows_ws, st);
+  unsigned bars = 0;
+  const int rc = rows_vf_vjp(p, t, y, gF, gy, nullptr, generic_vf_csum(p, vf_ws), wf, bf, rows_ws, vf_ws, &bars, st);
+  if (rc) return rc;
+  rows_vjp_finish(p, rows_ws, gparams, gfusion, st);
+  return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+}
+
+extern "C" size_t gncde_diag_vf_vjp_bytes(const GncdeProblem* prob) {
+  using namespace gncde;
+  const GncdeProblem& p = *prob;
+  size_t wfs = 0, bfs = 0;
+  for (int l = 0; l < p.L; ++l) {
+    wfs += (size_t)p.dims[l] * p.dims[l + 1];
+    bfs += p.dims[l + 1];
+  }
+  return align_up((wfs + bfs) * sizeof(float), 256) + rows_vjp_workspace(p) + generic_vf_workspace(p);
+}

@@ -276,11 +276,11 @@ def test_stage_vjp_large_graphs_match_oracle(G, n, L, method, rec):
         ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
         f = lambda t, y, ctrl=ctrl: O.vector_field(P, t, y, ctrl)  # noqa: E731
         fv = lambda t, y, g, ctrl=ctrl: OG.vector_field_vjp(P, t, y, ctrl, g)  # noqa: E731
-        for _ in range(10):
+        for attempt in range(10):
             g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], method, g_final=gfin[b])
             g1, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b] * (1 + 1e-6), method, g_final=gfin[b])
-            if np.max(np.abs(g1 - g0)) <= 1e-5 * np.max(np.abs(g0)):
-                break
+            if np.max(np.abs(g1 - g0)) <= 1e-5 * np.max(np.abs(g0)) or attempt == 9:
+                break  # (the reference gradient always belongs to the y0 the GPU gets)
             y0[b] = rng.standard_normal((n, h))
         gy0_ref.append(g0)
         total = OG._acc(total, gr)
@@ -716,6 +716,11 @@ ROWS_VJP_CASES = [  # (kind, n, H, L, cde, method, B)
     ("undirected", 40, 16, 2, True, "rk4", 2),
     ("plain", 129, 64, 3, True, "rk4", 2),          # config-3 shape: the forward keeps its layers on k_layer
     ("undirected", 255, 32, 4, True, "rk4", 2),     # config-5 shape
+    ("undirected", 255, 32, 2, True, "rk4", 2),
+    ("undirected", 200, 32, 4, True, "rk4", 2),
+    ("undirected", 255, 32, 4, False, "rk4", 2),
+    ("undirected", 255, 16, 2, True, "rk4", 1),
+    ("undirected", 64, 32, 4, True, "rk4", 2),
 ]
 
 
@@ -729,9 +734,11 @@ def test_rows_vjp_matches_oracle(G, kind, n, H, L, cde, method, B):
     T = 4
     dims = [H] * L + [16 * H if cde else H]
     ts, coeffs, P = MG.problem(rng, B, n, T, kind, dims, irregular=False)
+    # fusion terms large enough to matter; at L = 4 the x3 stack is chaotic enough that fp32 forwards cross ReLU
+    # kinks the fp64 oracle does not (every sample redrawn 10 times and still 1e-3 apart), so it keeps x1
     for lay in P.layers:
         for nm in OG.FUSION_NAMES[kind]:
-            lay[nm] = lay[nm] * 3.0
+            lay[nm] = lay[nm] * (3.0 if L < 4 else 1.0)
     kw, dco = {}, None
     if cde:
         dco = []
@@ -755,11 +762,11 @@ def test_rows_vjp_matches_oracle(G, kind, n, H, L, cde, method, B):
         else:
             f = lambda t, y, c=ctrl: O.vector_field(P, t, y, c)  # noqa: E731
             fv = lambda t, y, g, c=ctrl: OG.vector_field_vjp(P, t, y, c, g)  # noqa: E731
-        for _ in range(6):
+        for attempt in range(10):
             g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], method, g_final=gfin[b])
             g1, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b] * (1 + 1e-6), method, g_final=gfin[b])
-            if np.max(np.abs(g1 - g0)) <= 1e-5 * np.max(np.abs(g0)):
-                break
+            if np.max(np.abs(g1 - g0)) <= 1e-5 * np.max(np.abs(g0)) or attempt == 9:
+                break  # (the reference gradient always belongs to the y0 the GPU gets)
             y0[b] = rng.standard_normal((n, H))
         gy0_ref.append(g0)
         if cde:
@@ -770,6 +777,14 @@ def test_rows_vjp_matches_oracle(G, kind, n, H, L, cde, method, B):
     spec = G.SolverSpec(method=G._lib.RK4 if method == "rk4" else G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS,
                         grid=grid, nsteps=ns)
     ys = G.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda"))
+    fwd = []
+    for b in range(B):  # the checkpoints the sweep starts from
+        ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
+        f = ((lambda t, y, c=ctrl, x=O.CubicInterpolation(ts[b], dco[b]): O.cde_wrapper(P, H, 8, t, y, c, x)) if cde
+             else (lambda t, y, c=ctrl: O.vector_field(P, t, y, c)))
+        traj, _ = O.solve_fixed_grid(f, grids[b], y0[b], method, save_every_step=True, time_dtype=np.float32)
+        fwd.append(rel_err(ys[b, :len(traj)].cpu().numpy(), traj))
+    print(f"   forward trajectories vs oracle: {max(fwd):.2e}")
     spec.save_mode = G._lib.SAVE_T1
     out = G.integrate_vjp(prob, spec, ys, torch.tensor(gfin, dtype=torch.float32, device="cuda"), data_grad=cde)
     gy0, gp, gf = out[:3]
@@ -790,5 +805,7 @@ def test_rows_vjp_matches_oracle(G, kind, n, H, L, cde, method, B):
         errs["data"] = max(rel_err(gd[b].transpose(1, 0, 2, 3, 4), gdata_ref[b]) for b in range(B))
     worst = max(errs, key=errs.get)
     print(f"rows vjp {kind} n={n} H={H} L={L} cde={cde} {method}: worst {worst} {errs[worst]:.2e}")
+    if errs[worst] > RTOL_GRAD:
+        print("   all:", {k: f"{e:.1e}" for k, e in errs.items()})
     for k, e in errs.items():
         assert e <= RTOL_GRAD, (k, e)
