@@ -97,6 +97,24 @@ __device__ __forceinline__ int swz(int i, int k) {
   return i * (NP + 1) + k;
 }
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// Sum over all 64 lanes, result in every lane: DPP within each 16-lane row (quad swaps, then the half-row and row
+// mirrors), then the gfx950 row swaps (xor_sum_rows4).  No LDS and no lane-index arithmetic.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum64(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  return xor_sum_rows4(v);
+}
+
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -198,27 +216,48 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     const float f = t - sTs[idx];
     const float f3 = 3.0f * f;
     const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
-    // time-channel coefficients: loaded first so their HBM round trip overlaps the interval's Horner pass
+    // time-channel coefficients: loaded first so their HBM round trip overlaps the interval's Horner pass.
+    // Buffer loads: the (sample, interval) base is wave-uniform (descriptor in SGPRs), so a load costs no
+    // 64-bit VALU address arithmetic; the plane / iteration offsets ride in soffset.
     float tc0, tc1, tc2;
     {
-      const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n;
-      const int ii = i < n ? i : 0;
-      tc0 = tc[ii];
-      tc1 = tc[n + ii];
-      tc2 = tc[2 * n + ii];
+      const auto trs = rsrc(a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n, 12u * (unsigned)n);
+      const int vo = (i < n ? i : 0) * 4;
+      tc0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(trs, vo, 0, 0));
+      tc1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(trs, vo, 4 * n, 0));
+      tc2 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(trs, vo, 8 * n, 0));
     }
     if (n == NP) {
-      const float4* c4 = reinterpret_cast<const float4*>(cb);
-      constexpr int NQ = NP * NP / 4;
-      // fully unrolled: every coefficient load of the interval is in flight before the first use (one HBM
-      // round trip per form instead of NP/16 dependent ones)
+      constexpr int NQ = NP * NP / 4;   // float4s per plane
+      constexpr int QR = NP / 4;        // float4s per image row
+      constexpr int RPI = NT / QR;      // image rows per iteration (16)
+      static_assert(NQ % NT == 0 && NT % QR == 0, "Horner tiling");
+      // thread -> (row, 4 columns) of the first iteration; later iterations move RPI rows down, so every LDS
+      // address is one per-lane base plus a compile-time offset
+      const unsigned uft = (unsigned)ftid;
+      const int rr = (int)(uft / QR), kq = (int)(uft % QR) * 4;
+      const int vo = (int)uft * 16;
+      const auto crs = rsrc(cb, 16u * NQ * 4);
+      float* pa0 = sA + swz<NP>(rr, kq);
+      float* pd0 = sdA + swz<NP>(rr, kq);
+      // every coefficient load of the interval is issued before the first use (one HBM round trip per form
+      // instead of NQ/NT dependent ones)
+      // (in groups of at most 4 iterations = 64 VGPRs of loads: NP = 128 takes two round trips)
+      constexpr int NIT = NQ / NT, GRP = NIT > 4 ? 4 : NIT;
 #pragma unroll
-      for (int it = 0; it < NQ / NT; ++it) {
-        const int e4 = ftid + it * NT;
-        const float4 d = c4[e4], c = c4[NQ + e4], bb = c4[2 * NQ + e4], aa = c4[3 * NQ + e4];
-        const int r = (e4 * 4) / NP, k = (e4 * 4) % NP;
-        float* pa = sA + swz<NP>(r, k);
-        float* pd = sdA + swz<NP>(r, k);
+      for (int g0 = 0; g0 < NIT; g0 += GRP) {
+      floatx4 cq[GRP][4];
+#pragma unroll
+      for (int u = 0; u < GRP; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          cq[u][q] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(crs, vo, (q * NQ + (g0 + u) * NT) * 16, 0));
+#pragma unroll
+      for (int u = 0; u < GRP; ++u) {
+        const int it = g0 + u;
+        const floatx4 d = cq[u][0], c = cq[u][1], bb = cq[u][2], aa = cq[u][3];
+        float* pa = pa0 + it * RPI * (NP + 1);
+        float* pd = pd0 + it * RPI * (NP + 1);
         // element pairs on packed FMAs (same per-element Horner order as a scalar chain)
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
@@ -234,6 +273,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
           pd[2 * h2] = vd.x;
           pd[2 * h2 + 1] = vd.y;
         }
+      }
       }
     } else {  // padded image: rows/cols >= n are zero, so they add nothing to sums or operands
       for (int e = ftid; e < NP * NP; e += NT) {
@@ -289,11 +329,8 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       s += sVec[j];
       sd += sVec[NP + j];
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      s += __shfl_xor(s, o);
-      sd += __shfl_xor(sd, o);
-    }
+    s = wave_sum64(s);
+    sd = wave_sum64(sd);
     __syncthreads();
     const float ri = sVec[i], rdi = sVec[NP + i], ci = sVec[2 * NP + i], cdi = sVec[3 * NP + i];
     const float dgi = sVec[4 * NP + i], dgdi = sVec[5 * NP + i];
@@ -325,8 +362,11 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       // Chunks of 4 slices: all 16 image reads and the L float4 reads of v_l are issued before the first
       // use, so a chunk waits on LDS once; the pins at the end of a chunk keep the next chunk's loads
       // from being hoisted (register pressure), not the loads of this one.
-      int r0 = swz<NP>(i, hi * KS), c0 = swz<NP>(hi * KS, i), v0 = 6 * NP + hi * KS;
-      asm volatile("" : "+v"(r0), "+v"(c0), "+v"(v0));
+      // v0 stays a visible multiple of 16 floats (hi comes from the opaque ftid), so the v_l reads are aligned
+      // ds_read_b128 with immediate offsets
+      int r0 = swz<NP>(i, hi * KS), c0 = swz<NP>(hi * KS, i);
+      const int v0 = 6 * NP + hi * KS;
+      asm volatile("" : "+v"(r0), "+v"(c0));
 #pragma unroll
       for (int s4 = 0; s4 < KS; s4 += 4) {
         float ar[4], dr[4], ac[4], dc[4];

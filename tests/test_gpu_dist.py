@@ -97,61 +97,94 @@ def _trainer_rank(rank, world, port, kind, cfg, out):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "perm-equiv-graph-neural-cdes_amd")]
     import torch.distributed as dist
-    from gncde import run
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        res, flat = _run_trainer(kind, cfg)
-        out[rank, :-1] = flat
+        res, flat, g1, parts = _run_trainer(kind, cfg)
+        P = flat.numel()
+        out[rank, :P] = flat
+        out[rank, P:2 * P] = g1
+        out[rank, -2] = float(len(parts))
         out[rank, -1] = float(res)
+        if parts:  # every rebalanced partition covers each sample exactly once
+            assert all(sorted(i for p in pr for i in p) == list(range(len(c))) for c, pr in parts)
     finally:
         dist.destroy_process_group()
 
 
 def _run_trainer(kind, cfg):
-    """(the run's headline metric, final parameters) of run.Trainer / run.WindowTrainer on cfg."""
+    """(the run's headline metric, final parameters, first step's all-reduced gradient, the (costs, partition) of
+    every rebalancing) of run.Trainer / run.WindowTrainer on cfg."""
     from gncde import run, train
-    captured = {}
+    captured = {"grads": [], "parts": []}
     real = train.ClipAdamW.__init__
+    real_reduce = train.reduce_gradients
+    real_bp = train.balanced_partition
 
     def keep(self, *a, **k):  # capture the optimiser so the final flat buffer can be read
         real(self, *a, **k)
         captured["opt"] = self
+
+    def reduce_keep(*a, **k):  # capture every step's all-reduced mean-loss gradient
+        g, loss = real_reduce(*a, **k)
+        captured["grads"].append(g.detach().double().cpu().clone())
+        return g, loss
+
+    def bp(costs, world):
+        parts = real_bp(costs, world)
+        captured["parts"].append((list(costs), parts))
+        return parts
     train.ClipAdamW.__init__ = keep
+    train.reduce_gradients = reduce_keep
+    train.balanced_partition = bp
     try:
-        if kind == "dyn":
-            res = run.Trainer(cfg, epochs=3, steps_per_interval=None).run()["best_validation_loss"]
+        if kind in ("dyn", "dyn_rk4"):
+            spi = None if kind == "dyn" else 2
+            res = run.Trainer(cfg, epochs=3, steps_per_interval=spi).run()["best_validation_loss"]
         else:
             res = run.WindowTrainer(cfg, epochs=2, window_batch=2).run()["best_validation_loss"]
     finally:
         train.ClipAdamW.__init__ = real
-    return res, captured["opt"].flat.detach().cpu()
+        train.reduce_gradients = real_reduce
+        train.balanced_partition = real_bp
+    return res, captured["opt"].flat.detach().cpu(), captured["grads"][0], captured["parts"]
 
 
-@pytest.mark.parametrize("kind", ["dyn", "pgt"])
+@pytest.mark.parametrize("kind", ["dyn", "dyn_rk4", "pgt"])
 def test_two_rank_trainers_equal_single_process(tmp_path, kind):
-    """gncde.run's trainers in data-parallel mode (SURVEY §8e): the dyn Trainer shards its samples (the reference's
-    adaptive Tsit5 + PID solve, ranks rebalanced by step counts after each epoch) and the PGT WindowTrainer splits
-    each step's windows; two gloo ranks sharing the GPU end with the single process's parameters (up to the
-    all-reduce's summation order) and its validation metric."""
+    """gncde.run's trainers in data-parallel mode: the dyn Trainer shards its samples and the PGT
+    WindowTrainer splits each step's windows over two gloo ranks sharing the GPU.
+
+    * Every run: the replicas stay identical and the first step's all-reduced gradient is the single process's
+      full-batch gradient up to summation order.
+    * Fixed grids (``dyn_rk4``: RK4, 2 steps per knot interval; ``pgt``: Tsit5 at dt0 0.1): the final parameters
+      are the single process's (and the PGT validation metric).
+    * ``dyn`` (the reference's adaptive Tsit5 + PIDController): the ranks are rebalanced by the first epoch's
+      accepted step counts (each rebalanced partition covers every sample once).  From step 2 on the parameters
+      differ from the single process's by the summation order (~1e-9), and the PID controller's accept/reject
+      decisions are discontinuous in them: a sample may take a different (equally valid, rtol-accurate) step
+      sequence, which moves its gradient by ~rtol.  So parameters are held to Adam's per-step bound (|update| <=
+      lr, 3 steps) and the metric to 5 %; tools/diag_partition.py checks that the gradient is additive over any
+      partition of the samples at fixed parameters (measured 5e-8 .. 9e-8)."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a HIP device")
     import yaml
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    name = "heat_grid_small.yaml" if kind == "dyn" else "pgt_england_small.yaml"
+    name = "pgt_england_small.yaml" if kind == "pgt" else "heat_grid_small.yaml"
     with open(os.path.join(root, "configs", name)) as fh:
         cfg = yaml.safe_load(fh)
-    if kind == "dyn":
-        cfg["dataset"].update(num_nodes=16, time_tick=16, batch_size=5)
-        cfg["eval_freq"] = 3
-    else:
+    if kind == "pgt":
         cfg["dataset"]["num_snapshots"] = 26
         cfg["eval_freq"] = 2
+    else:
+        cfg["dataset"].update(num_nodes=16, time_tick=16, batch_size=5)
+        cfg["eval_freq"] = 3
     cfg["checkpoint_dir"] = str(tmp_path)
-    ref_metric, ref = _run_trainer(kind, cfg)
+    ref_metric, ref, ref_g1, _ = _run_trainer(kind, cfg)
+    P = ref.numel()
     world = 2
-    out = torch.zeros(world, ref.numel() + 1, dtype=torch.float64).share_memory_()
+    out = torch.zeros(world, 2 * P + 2, dtype=torch.float64).share_memory_()
     ctx = mp.get_context("spawn")
     port = _free_port()
     procs = [ctx.Process(target=_trainer_rank, args=(r, world, port, kind, cfg, out)) for r in range(world)]
@@ -161,8 +194,21 @@ def test_two_rank_trainers_equal_single_process(tmp_path, kind):
         p.join(timeout=300)
         assert p.exitcode == 0
     assert torch.equal(out[0], out[1])  # replicas identical
-    d = float((out[0, :-1] - ref.double()).abs().max())
-    print(f"{kind}: two-rank vs single-process parameters max |diff| {d:.2e}; metric {float(out[0, -1]):.6g} vs "
-          f"{ref_metric:.6g}")
-    assert d <= 1e-4
-    assert abs(float(out[0, -1]) - ref_metric) <= 1e-3 * abs(ref_metric)
+    g1 = out[0, P:2 * P]
+    dg = float((g1 - ref_g1).abs().max() / ref_g1.abs().max())
+    d = float((out[0, :P] - ref.double()).abs().max())
+    metric = float(out[0, -1])
+    print(f"{kind}: first-step gradient rel diff {dg:.2e}; parameters max |diff| {d:.2e}; metric {metric:.6g} vs "
+          f"{ref_metric:.6g}; rebalancings {int(out[0, -2])}")
+    assert dg <= 1e-5
+    if kind == "dyn":
+        lr = float(cfg["optimiser"]["schedule"]["value"])
+        assert int(out[0, -2]) >= 1  # the step counts differ enough to rebalance on this data
+        assert d <= 2 * lr * 3
+    else:
+        assert d <= 1e-4
+    # the dyn Trainer validates with the reference's adaptive solve (forward_packed: Tsit5 + PID, SaveAt(ts)) for
+    # either training solver, so its metric inherits the controller's discontinuity (dyn_rk4: parameters equal to
+    # 6e-8, metric 0.27 % apart); the PGT metric is a fixed-grid solve
+    tol = 5e-2 if kind.startswith("dyn") else 1e-3
+    assert abs(metric - ref_metric) <= tol * abs(ref_metric)
