@@ -29,6 +29,7 @@ namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));  // v_pk_fma_f32 / v_pk_add_f32 operands
+typedef __attribute__((address_space(4))) const float CFloat;  // constant address space: uniform reads are s_load
 
 constexpr int kTMax = 256;  // knots per sample held in LDS
 
@@ -193,6 +194,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
   float* sVl = sVec + 6 * NP;  // v_l[k], L x NP
 
   // ---- (I + Abar_l) operands for stage time t --------------------------------------------------------
+  int widx = 0;  // interval index of the previous form (wave-uniform)
   auto form = [&](float t) __attribute__((always_inline)) {
     // The form phase (HBM loads, VALU, LDS) runs at raised wave priority: the co-resident waves of the other
     // samples on this SIMD are mostly in their MFMA-bound eval phase and fill the gaps (config 2: -6%).
@@ -205,14 +207,13 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     const int lane = ftid & 63, lo = lane & 15, hi = lane >> 4;
     const int i = 16 * (ftid >> 6) + lo;
     const float* fus = sFus;  // fusion table staged in LDS (uniform broadcast reads)
-    int cnt = 0;
-    for (int j0 = 0; j0 < T; j0 += 64) {
-      const int j = j0 + lane;
-      const bool p = (j < T) && (sTs[j < T ? j : 0] < t);
-      cnt += __popcll(__ballot(p));
-    }
-    int idx = cnt - 1;
-    idx = idx < 0 ? 0 : (idx > T - 2 ? T - 2 : idx);
+    // interval index clip(searchsorted(ts, t, 'left') - 1, 0, T-2), i.e. the largest j <= T-2 with ts[j] < t (or 0),
+    // walked from the previous form's index on wave-uniform LDS reads: a stage time moves by about one knot per
+    // form, and the walk also runs backwards for the PID controller's rejected attempts
+    int idx = widx;
+    while (idx < T - 2 && sTs[idx + 1] < t) ++idx;
+    while (idx > 0 && !(sTs[idx] < t)) --idx;
+    widx = idx;
     const float f = t - sTs[idx];
     const float f3 = 3.0f * f;
     const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
@@ -317,12 +318,27 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
       sVec[q * NP + j] = (acc0 + acc1) + (acc2 + acc3);
     }
     __syncthreads();
+    // The per-layer fusion coefficients are read through the constant address space: wave-uniform scalar loads
+    // into SGPRs, so the factored families below are one FMA per term with no VALU spent on the coefficients.
+    const CFloat* fz = (const CFloat*)(a.fusion);
     // v_l[k] = vR_A r_k + vR_dA rd_k + vC_A c_k + vC_dA cd_k  (zero for padded k: sums are zero)
-    for (int e = ftid; e < L * NP; e += NT) {
-      const int l = e / NP, k = e % NP;
-      const float* fc = fus + l * GNCDE_FC;
-      sVl[e] = fc[GNCDE_FC_VR_A] * sVec[k] + fc[GNCDE_FC_VR_DA] * sVec[NP + k] +
-               fc[GNCDE_FC_VC_A] * sVec[2 * NP + k] + fc[GNCDE_FC_VC_DA] * sVec[3 * NP + k];
+    if constexpr (NP >= 64) {  // one layer per wave (or wave pair): the layer index is wave-uniform
+      constexpr int WPL = NP / 64;
+      const int wv = __builtin_amdgcn_readfirstlane(ftid >> 6);
+      const int l = wv / WPL;
+      if (l < L) {
+        const int k = (wv % WPL) * 64 + lane;
+        const CFloat* fc = fz + l * GNCDE_FC;
+        sVl[l * NP + k] = fmaf(fc[GNCDE_FC_VR_A], sVec[k], fmaf(fc[GNCDE_FC_VR_DA], sVec[NP + k],
+                          fmaf(fc[GNCDE_FC_VC_A], sVec[2 * NP + k], fc[GNCDE_FC_VC_DA] * sVec[3 * NP + k])));
+      }
+    } else {
+      for (unsigned e = (unsigned)ftid; e < (unsigned)(L * NP); e += NT) {
+        const unsigned l = e / NP, k = e % NP;
+        const float* fc = fus + l * GNCDE_FC;
+        sVl[e] = fc[GNCDE_FC_VR_A] * sVec[k] + fc[GNCDE_FC_VR_DA] * sVec[NP + k] +
+                 fc[GNCDE_FC_VC_A] * sVec[2 * NP + k] + fc[GNCDE_FC_VC_DA] * sVec[3 * NP + k];
+      }
     }
     float s = 0.f, sd = 0.f;
     for (int j = lane; j < NP; j += 64) {
@@ -337,13 +353,14 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     float wl[L];
 #pragma unroll
     for (int l = 0; l < L; ++l) {
-      const float* fc = fus + l * GNCDE_FC;
-      const float w = fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci +
-                      fc[GNCDE_FC_WC_DA] * cdi + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
+      const CFloat* fc = fz + l * GNCDE_FC;
+      const float ws = fmaf(fc[GNCDE_FC_WS_A], s, fc[GNCDE_FC_WS_DA] * sd);
+      const float w = fmaf(fc[GNCDE_FC_WR_A], ri, fmaf(fc[GNCDE_FC_WR_DA], rdi,
+                      fmaf(fc[GNCDE_FC_WC_A], ci, fmaf(fc[GNCDE_FC_WC_DA], cdi, ws))));
       wl[l] = i < n ? w : 0.f;
-      ul[l] = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dgi + fc[GNCDE_FC_UD_DA] * dgdi +
-              fc[GNCDE_FC_UR_A] * ri + fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci +
-              fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
+      ul[l] = fmaf(fc[GNCDE_FC_UD_A], dgi, fmaf(fc[GNCDE_FC_UD_DA], dgdi, fmaf(fc[GNCDE_FC_UR_A], ri,
+              fmaf(fc[GNCDE_FC_UR_DA], rdi, fmaf(fc[GNCDE_FC_UC_A], ci, fmaf(fc[GNCDE_FC_UC_DA], cdi,
+              fmaf(fc[GNCDE_FC_US_A], s, fmaf(fc[GNCDE_FC_US_DA], sd, fc[GNCDE_FC_IDC]))))))));
     }
     // operand slice: row i of A/dA at columns k = hi*KS + sl, column i at rows k.  Each of the four image
     // elements is read ONCE and feeds every layer's operand (4 + L LDS reads per element instead of 5 L);
@@ -352,12 +369,9 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
     // values stay short-lived.
     float ec[L][4];
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
-      const float* fc = fus + l * GNCDE_FC;
+    for (int l = 0; l < L; ++l)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        ec[l][q] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, fc[q])));
-    }
+      for (int q = 0; q < 4; ++q) ec[l][q] = fz[l * GNCDE_FC + q];
     {
       // Chunks of 4 slices: all 16 image reads and the L float4 reads of v_l are issued before the first
       // use, so a chunk waits on LDS once; the pins at the end of a chunk keep the next chunk's loads
