@@ -37,6 +37,13 @@ typedef float floatx4u __attribute__((ext_vector_type(4), aligned(4)));  // dwor
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+#ifdef GNCDE_ROWS_STAMPS
+__device__ unsigned long long g_rows_stamps[4096 * 16];
+#define ROWS_STAMP(k) \
+  do { if (threadIdx.x == 0 && it == 0) g_rows_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define ROWS_STAMP(k) do {} while (0)
+#endif
 constexpr int kRB = 16;      // node rows per workgroup
 constexpr int kMaxN = 256;   // per wave: four 16-column K chunks (fp32) or two 32-column chunks (bf16)
 constexpr int kStrip = 17;   // LDS row stride of the transposed column strip
@@ -186,6 +193,7 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
     asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
     const int w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
     const int ri = r0 + lo;  // this lane's operand row
+    ROWS_STAMP(0);
     const int bs = g + it * a.G;
     const bool live = bs < a.B;
     const int b = live ? bs : a.B - 1;  // an idle round computes on a valid sample, keeps its barriers, stores no dy
@@ -318,6 +326,7 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
         sDx[rr * kStrip + (tid & 15)] = r0 + rr < n ? fmaf(f, fmaf(3.0f * f, dcv[0], 2.0f * dcv[1]), dcv[2]) : 0.f;
     }
     __syncthreads();
+    ROWS_STAMP(1);
     // the product's A-operand elements of this lane: (I + Abar)[ri][k] needs A, dA at (ri, k) and at (k, ri), for
     // k = KW kc + EL hi + e, kc = w + 4 j (chunks past the matrix read zeros)
     float Ar[NJ][EL], dAr[NJ][EL], At[NJ][EL], dAt[NJ][EL];
@@ -343,6 +352,7 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
       }
     }
     __syncthreads();  // the strip's region becomes Z_l
+    ROWS_STAMP(2);
 
     // ---- layers ----------------------------------------------------------------------------------------------
     // Z_l -> LDS (the stage input with plain loads: written before this launch; a hidden output of the group with
@@ -523,7 +533,9 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
 
     for (int l = 0; l + 1 < L; ++l) {  // hidden layers: Z_{l+1}[R] = relu(P W'^T + q b'^T), published to the group
       load_z(l);
+      ROWS_STAMP(3 + 3 * l);
       product(l);
+      ROWS_STAMP(4 + 3 * l);
       for (int tile = w; tile < CT; tile += 4) {
         const floatx4 v = linear(l, tile);
 #pragma unroll
@@ -543,6 +555,7 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
               ((r0 + R) * H + 4 * q) * 4, 0, 16);
       }
       arrive();  // its barrier also orders the partials' reuse by the next layer
+      ROWS_STAMP(5 + 3 * l);
     }
     {  // the output layer
       const int l = L - 1;
@@ -568,7 +581,9 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
 #pragma unroll
           for (int j = 0; j < JP; ++j) wb[cc][j] = wrow_bf(a.wbf + (size_t)l * H * H, 16 * (16 * ct + lo) + j0 + j, cc);
       load_z(l);
+      ROWS_STAMP(12);
       product(l);
+      ROWS_STAMP(13);
       if constexpr (MODE == 1) {  // ODE: dy[R] = tg (P W'^T + q b'^T)
         for (int tile = w; tile < CT; tile += 4) {
           const floatx4 v = linear(l, tile);
@@ -642,6 +657,7 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
           }
       }
       __syncthreads();  // P (aliasing Z_l) and the LDS vectors are rewritten by the next round's form
+      ROWS_STAMP(14);
     }
   }
 }
@@ -729,6 +745,12 @@ bool rows_supported(const GncdeProblem& p) {
     return p.cde_embed == 8 && p.cde_hidden == H && (H <= 32 || bf) && p.dims[p.L] == 16 * H;
   return p.dims[p.L] == H;
 }
+
+#ifdef GNCDE_ROWS_STAMPS
+extern "C" int gncde_debug_rows_stamps(unsigned long long* host, int count) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rows_stamps), sizeof(unsigned long long) * count) == hipSuccess ? 0 : -1;
+}
+#endif
 
 size_t rows_sync_ints(const GncdeProblem& p) { return align_up((size_t)p.B + 4, 4); }
 

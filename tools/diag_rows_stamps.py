@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Diagnostic (GPU, experiment build only): per-phase wall time of one k_rows evaluation at BASELINE config 5's
+shape, from s_memrealtime stamps (100 MHz) that a -DGNCDE_ROWS_STAMPS build of gncde_rows.hip writes for round 0
+of every workgroup.  Run with GNCDE_LIB pointing at that build."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "perm-equiv-graph-neural-cdes_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import gncde  # noqa: E402
+from gncde import _lib, synthetic  # noqa: E402
+
+NAMES = ["start", "form", "operands"] + [f"{p}{l}" for l in range(3) for p in ("z", "prod", "pub")] + \
+        ["z_out", "prod_out", "readout"]
+
+
+def main():
+    B = int(os.environ.get("DIAG_B", "16"))
+    compute = os.environ.get("DIAG_COMPUTE", "fp32")
+    prob, y0 = synthetic.cde_batch(B, 255, 3, 32, 8, 4, 1.0)
+    prob = prob.with_compute(compute)
+    t = torch.full((B,), 0.37, dtype=torch.float32, device="cuda")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    fn = lib.gncde_debug_rows_stamps
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    nwg = B * 16
+    for rep in range(3):
+        gncde.vf_eval(prob, t, y0)
+        torch.cuda.synchronize()
+    buf = np.zeros(nwg * 16, dtype=np.uint64)
+    assert fn(buf.ctypes.data, buf.size) == 0
+    st = buf.reshape(nwg, 16)[:, :15].astype(np.float64)
+    t0 = st[:, 0].min()
+    rel = (st - t0) * 0.01  # us
+    print(f"B={B} {compute}: launch span {rel[:, 14].max():.2f} us; first WG start {0:.2f}, last WG start "
+          f"{rel[:, 0].max():.2f} us")
+    for k in range(1, 15):
+        d = (st[:, k] - st[:, k - 1]) * 0.01
+        print(f"  {NAMES[k]:>9}: median {np.median(d):6.2f} us  max {d.max():6.2f}  (ends at median {np.median(rel[:, k]):6.2f})")
+
+
+if __name__ == "__main__":
+    main()
