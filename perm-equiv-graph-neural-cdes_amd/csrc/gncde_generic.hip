@@ -602,6 +602,7 @@ inline const float* abar_layer(const GncdeProblem& p, const float* abar, int l) 
 
 struct VfWs {
   float *csum, *tg, *Z0, *Z1, *m, *abar, *wf, *wp, *bf, *inv, *q, *dx;
+  void* coefT;     // one-launch evaluation: every (sample, interval, plane) transposed, once per solve
   uint16_t* wbf;   // GNCDE_COMPUTE_BF16_MFMA: W' per layer rounded to bfloat16, natural layout
   unsigned* sync;  // one-launch evaluation: per-group arrival counters [B] + the fault word, zeroed per solve
 };
@@ -634,6 +635,10 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.dx = take(B * n * (size_t)(p.cde_hidden > 0 ? 2 * p.cde_embed : 1));  // data-spline derivative at t
   w.sync = reinterpret_cast<unsigned*>(take(B + 4));
   w.wbf = reinterpret_cast<uint16_t*>(take(p.compute == GNCDE_COMPUTE_BF16_MFMA ? (wsum + 1) / 2 : 1));
+  // the one-launch evaluation reads a node block's column strip [:, R] as rows R of the transposed planes (whole
+  // cache lines, like its rows block) instead of 16-column segments of every row
+  const size_t planes = B * (size_t)(p.T - 1) * 4 * nn;
+  w.coefT = take(rows_supported(p) || rows_vjp_supported(p) ? (coef_is_bf16(p) ? (planes + 1) / 2 : planes) : 1);
   return off;
 }
 
@@ -700,10 +705,46 @@ const float* generic_vf_csum(const GncdeProblem& p, char* ws) {
   return w.csum;
 }
 
+const void* generic_vf_coefT(const GncdeProblem& p, char* ws) {
+  VfWs w;
+  carve_vf(p, ws, w);
+  return w.coefT;
+}
+
 const int* generic_vf_fault(const GncdeProblem& p, char* ws) {
   VfWs w;
   carve_vf(p, ws, w);
   return reinterpret_cast<const int*>(w.sync + p.B);
+}
+
+// plane z (= (sample, interval, coefficient)) of [*, n, n] -> its transpose, 32 x 32 tiles through LDS
+template <typename CT>
+__global__ void __launch_bounds__(256) k_transpose_planes(int n, size_t planes, const CT* __restrict__ in,
+                                                          CT* __restrict__ out) {
+  __shared__ CT tile[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  for (size_t z = blockIdx.z; z < planes; z += gridDim.z) {
+    const size_t base = z * n * n;
+    for (int r = threadIdx.y; r < 32; r += 8)
+      if (r0 + r < n && c0 + (int)threadIdx.x < n) tile[r][threadIdx.x] = in[base + (size_t)(r0 + r) * n + c0 + threadIdx.x];
+    __syncthreads();
+    for (int c = threadIdx.y; c < 32; c += 8)
+      if (c0 + c < n && r0 + (int)threadIdx.x < n) out[base + (size_t)(c0 + c) * n + r0 + threadIdx.x] = tile[threadIdx.x][c];
+    __syncthreads();
+  }
+}
+
+void generic_vf_transpose(const GncdeProblem& p, char* ws, hipStream_t st) {
+  VfWs w;
+  carve_vf(p, ws, w);
+  const size_t planes = (size_t)p.B * (p.T - 1) * 4;
+  const dim3 tg(cdiv(p.n, 32), cdiv(p.n, 32), planes < 65535 ? (unsigned)planes : 65535u);
+  if (coef_is_bf16(p))
+    hipLaunchKernelGGL(k_transpose_planes<uint16_t>, tg, dim3(32, 8), 0, st, p.n, planes,
+                       reinterpret_cast<const uint16_t*>(p.coef), reinterpret_cast<uint16_t*>(w.coefT));
+  else
+    hipLaunchKernelGGL(k_transpose_planes<float>, tg, dim3(32, 8), 0, st, p.n, planes, p.coef,
+                       reinterpret_cast<float*>(w.coefT));
 }
 
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
@@ -717,6 +758,7 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
   else
     hipLaunchKernelGGL(k_coef_sums<float>, gs, dim3(256), 0, st, p.n, p.T, p.coef, w.csum);
   const bool rows = rows_supported(p);
+  if (rows) generic_vf_transpose(p, ws, st);
   size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
@@ -751,7 +793,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
       bars = &local;
     }
     // (the workspace holds no (I + Abar_l) planes for these problems: there is no multi-kernel fallback here)
-    return rows_vf_eval(p, t, y, dy, w.csum, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync, reinterpret_cast<int*>(w.sync + B), *bars,
+    return rows_vf_eval(p, t, y, dy, w.csum, w.coefT, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync, reinterpret_cast<int*>(w.sync + B), *bars,
                         st, keep);
   }
   vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st);

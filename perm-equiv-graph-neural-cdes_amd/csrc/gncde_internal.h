@@ -187,13 +187,18 @@ bool rows_supported(const GncdeProblem& p);
 inline bool coef_is_bf16(const GncdeProblem& p) {
   return p.compute == GNCDE_COMPUTE_BF16_STORAGE || p.compute == GNCDE_COMPUTE_BF16_MFMA;
 }
-int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum,
+int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum, const void* coefT,
                  const float* wperm, const uint16_t* wbf, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
                  unsigned& bars_done, hipStream_t st, float* keep = nullptr);
 int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
                       int32_t* stats, char* ws, hipStream_t st);
 // k_coef_sums' per-plane reductions in a prepared evaluation workspace
 const float* generic_vf_csum(const GncdeProblem& p, char* ws);
+// the transposed coefficient planes of the one-launch evaluation and the per-layer reverse kernels:
+// generic_vf_prepare fills them when rows_supported(p); a reverse sweep on a shape only rows_vjp_supported covers
+// calls generic_vf_transpose itself
+const void* generic_vf_coefT(const GncdeProblem& p, char* ws);
+void generic_vf_transpose(const GncdeProblem& p, char* ws, hipStream_t st);
 
 // reverse mode of one evaluation, one launch per ConvLayer (n <= 256, one width H): gncde_rows_vjp.hip
 bool rows_vjp_supported(const GncdeProblem& p);

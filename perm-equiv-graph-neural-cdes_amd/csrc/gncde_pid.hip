@@ -19,6 +19,7 @@ constexpr int kAdvThreads = 1024;
 // The per-stage element loops run in passes of kAdvU elements per thread (E <= 8192 in one pass); a pass issues
 // all of its loads before the first use, so a loop costs about one memory round trip per pass, not per element.
 constexpr int kAdvU = 8;
+constexpr int kAdvMaxSlices = 16;  // workgroups per sample for an in-attempt stage
 
 struct PidState {
   int phase, st, steps, rejects, evals, status, done, si;
@@ -32,7 +33,9 @@ struct PidArgs {
   const float* t1;
   const float* dt0;
   const float* save_ts;  // [B, S] or nullptr
-  PidState* state;
+  PidState* state;      // [B] controller states read by k_pid_advance (and written by k_pid_init)
+  PidState* state_out;  // [B] the states it writes (the host swaps the two after every launch: the slices of one
+                        // sample never read a state another slice of the same launch has already advanced)
   float* y;     // [B, E]
   float* yt;    // [B, E] stage input (next evaluation)
   float* kk;    // [7, B, E]
@@ -108,18 +111,25 @@ __global__ void k_pid_init(PidArgs a, const float* __restrict__ y0) {
   }
 }
 
+// grid (slices, B): an in-attempt stage (5 launches in 6) is spread over the sample's slices; every other step of the
+// state machine (the attempt end with its error norm, the initial-step heuristic, finishing) runs on slice 0
 __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
   __shared__ float red[kAdvThreads / 64];
   __shared__ PidState sh;
-  const int b = blockIdx.x;
+  const int b = blockIdx.y, slice = blockIdx.x, NS = gridDim.x;
   const int tid = threadIdx.x;
   if (tid == 0) sh = a.state[b];
   __syncthreads();
   PidState s = sh;
-  if (s.done) return;
+  if (s.done) {
+    if (slice == 0 && tid == 0) a.state_out[b] = s;
+    return;
+  }
+  const bool mid = s.phase == 2 && s.st < 6;
+  if (!mid && slice != 0) return;
   const int E = a.E;
   const size_t base = (size_t)b * E;
-  const size_t BE = (size_t)gridDim.x * E;
+  const size_t BE = (size_t)a.B * E;
   const float rtol = a.rtol, atol = a.atol;
   const float t0 = a.t0[b], t1 = a.t1[b];
   const float inv_cnt = 1.0f / (float)E;
@@ -173,40 +183,51 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
     start = true;
   } else {
     float* kst = kk(s.st);
-    if (s.st < 6 && E <= P) {
-      // A stage inside an attempt, one pass (e.g. config 5's 255 x 32): K, y and only the stage buffers the next
-      // input reads (j < st + 1, the current one taken from K in registers) in one round trip, instead of K, then
-      // all six buffers (the CU's load path, not HBM, bounds a one-workgroup-per-sample kernel).
+    if (mid) {
+      // A stage inside an attempt (e.g. config 5's 255 x 32 over 8 slices): K, y and only the stage buffers the next
+      // input reads (j < st + 1, the current one taken from K in registers) in one round trip per pass.
+      constexpr int U2 = 2;
       const int ns1 = s.st + 1;
+      const int stride = NS * kAdvThreads;
       float ar[6], cst;
       stage_row(ns1, ar, cst);
-      float kq[U], yv[U], kv[6][U];
-      ldu(K, tid, kq);
-      ldu(y, tid, yv);
+      for (int e0 = slice * kAdvThreads + tid; e0 < E; e0 += stride * U2) {
+        float kq[U2], yv[U2], kv[6][U2];
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        if (j < ns1 && j != s.st) {  // uniform: a scalar branch around the loads
-          ldu(kk(j), tid, kv[j]);
-        } else {
-#pragma unroll
-          for (int u = 0; u < U; ++u) kv[j][u] = 0.f;
+        for (int u = 0; u < U2; ++u) {
+          const int e = e0 + u * stride;
+          kq[u] = e < E ? K[e] : 0.f;
+          yv[u] = e < E ? y[e] : 0.f;
         }
-      }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = tid + u * kAdvThreads;
-        float acc = 0.f;  // the memory path's summation order
+        for (int j = 0; j < 6; ++j) {
+          if (j < ns1 && j != s.st) {  // uniform: a scalar branch around the loads
 #pragma unroll
-        for (int j = 0; j < 6; ++j) acc = j < ns1 ? fmaf(ar[j], j == s.st ? kq[u] : kv[j][u], acc) : acc;
-        if (e < E) {
-          kst[e] = kq[u];
-          yt[e] = fmaf(s.h, acc, yv[u]);
+            for (int u = 0; u < U2; ++u) {
+              const int e = e0 + u * stride;
+              kv[j][u] = e < E ? kk(j)[e] : 0.f;
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < U2; ++u) kv[j][u] = 0.f;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U2; ++u) {
+          const int e = e0 + u * stride;
+          float acc = 0.f;  // the memory path's summation order
+#pragma unroll
+          for (int j = 0; j < 6; ++j) acc = j < ns1 ? fmaf(ar[j], j == s.st ? kq[u] : kv[j][u], acc) : acc;
+          if (e < E) {
+            kst[e] = kq[u];
+            yt[e] = fmaf(s.h, acc, yv[u]);
+          }
         }
       }
       s.tst = ns1 >= 5 ? __fadd_rn(s.t, s.h) : stage_time(s.t, cst, s.h);
       s.st = ns1;
-      if (tid == 0) {
-        a.state[b] = s;
+      if (slice == 0 && tid == 0) {
+        a.state_out[b] = s;
         a.tst[b] = s.tst;
       }
       return;
@@ -301,7 +322,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
         }
         if (a.S > 0) s.si = a.S;
         s.done = 1;
-        if (tid == 0) a.state[b] = s;
+        if (tid == 0) a.state_out[b] = s;
         return;
       }
       s.tn = s.t + s.dt;
@@ -316,7 +337,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
       s.tst = stage_time(s.t, TSIT5_C2, s.h);
       s.st = 1;
       if (tid == 0) {
-        a.state[b] = s;
+        a.state_out[b] = s;
         a.tst[b] = s.tst;
       }
       return;
@@ -419,7 +440,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
           for (int e = tid; e < E; e += blockDim.x) a.ys[((size_t)b * a.S + s.si) * E + e] = y[e];
       }
       s.done = 1;
-      if (tid == 0) a.state[b] = s;  // tst keeps its last value: finished samples' evaluations are ignored
+      if (tid == 0) a.state_out[b] = s;  // tst keeps its last value: finished samples' evaluations are ignored
       return;
     }
     s.tn = s.t + s.dt;
@@ -452,7 +473,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
     s.st = ns1;
   }
   if (tid == 0) {
-    a.state[b] = s;
+    a.state_out[b] = s;
     a.tst[b] = s.tst;
   }
 }
@@ -494,7 +515,7 @@ size_t generic_pid_workspace(const GncdeProblem& p) {
   const size_t B = p.B, E = (size_t)p.n * state_dim(p);
   size_t sz = generic_vf_workspace(p);
   sz += 10 * align_up(B * E * 4, 256);                 // y, yt, K, kk[7]
-  sz += align_up(B * sizeof(PidState), 256) + 2 * align_up(B * 4, 256) + 256;
+  sz += 2 * align_up(B * sizeof(PidState), 256) + 2 * align_up(B * 4, 256) + 256;
   return sz;
 }
 
@@ -533,6 +554,7 @@ int pid_begin(PidRun& r, const GncdeProblem& p, const GncdeSolver& s, const floa
   a.K = r.K;
   a.kk = reinterpret_cast<float*>(take(7 * B * E * 4));
   a.state = reinterpret_cast<PidState*>(take(B * sizeof(PidState)));
+  a.state_out = reinterpret_cast<PidState*>(take(B * sizeof(PidState)));
   r.tst = reinterpret_cast<float*>(take(B * 4));
   r.active = reinterpret_cast<int*>(take(B * 4));
   a.ys = ys;
@@ -550,10 +572,15 @@ int pid_begin(PidRun& r, const GncdeProblem& p, const GncdeSolver& s, const floa
 }
 
 int pid_iterate(PidRun& r) {
-  const PidArgs& a = r.a;
+  PidArgs& a = r.a;
   const int rc = generic_vf_eval(r.p, r.tst, a.yt, r.K, r.ws, r.st, true, &r.bars);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_pid_advance, dim3(a.B), dim3(kAdvThreads), 0, r.st, a);
+  const int slices = (a.E + kAdvThreads - 1) / kAdvThreads;
+  hipLaunchKernelGGL(k_pid_advance, dim3(slices < kAdvMaxSlices ? slices : kAdvMaxSlices, a.B), dim3(kAdvThreads), 0,
+                     r.st, a);
+  PidState* t = a.state;  // what this launch wrote is the next one's input
+  a.state = a.state_out;
+  a.state_out = t;
   return GNCDE_OK;
 }
 

@@ -53,6 +53,7 @@ struct RowsArgs {
   int np;                  // n rounded up to the K chunk (16 fp32, 32 bf16)
   const float* ts;
   const void* coef;        // [B, T-1, 4, n, n] fp32, or bfloat16 (GNCDE_COMPUTE_BF16_MFMA)
+  const void* coefT;       // the same planes transposed (generic_vf_prepare, once per solve)
   const float* csum;       // k_coef_sums: [B, T-1, 12 n + 4]
   const float* tcoef;      // [B, T-1, 3, n]
   const float* data_coef;  // [B, T-1, 4, n, 8, 2] (CDE)
@@ -216,11 +217,10 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
     //    spline) at once: one memory round trip (L2 is cold at every launch, so the strip's second read of the
     //    same lines is not cheaper later)
     const int rr = tid >> 4;
-    // fp32: 4 columns per 16-byte load (rows: 4 (tid % 16) + 64 u, u < 4; strip: node kk = tid / 4 + 64 p, p < 4,
-    // columns 4 (tid % 4)); bf16: 8 per load (rows: 8 (tid % 16) + 128 u, u < 2; strip: kk = tid / 2 + 128 p,
-    // p < 2, columns 8 (tid % 2))
+    // fp32: 4 columns per 16-byte load (row rr = tid / 16, columns 4 (tid % 16) + 64 u, u < 4); bf16: 8 per load
+    // (columns 8 (tid % 16) + 128 u, u < 2); the strip the same over the transposed planes
     constexpr int CE = BF ? 8 : 4, NU = BF ? 2 : 4;
-    const int cq = CE * (tid & 15), c4 = CE * (tid & (BF ? 1 : 3));
+    const int cq = CE * (tid & 15);
     u32x4 rc[NU][4], sc[NU][4];
 #pragma unroll
     for (int u = 0; u < NU; ++u)
@@ -231,17 +231,18 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
         if constexpr (BF) rc[u][q] = load8_bf16(crs, e);
         else rc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, e * 4, 0, 0);
       }
+    // the column strip [:, R] = rows R of the transposed planes: the same whole-line pattern as the rows block
+    const CT_* cbt = reinterpret_cast<const CT_*>(a.coefT) + ((size_t)b * (T - 1) + idx) * 4 * nn;
+    const auto crt = rsrc(cbt, (unsigned)(4 * nn * sizeof(CT_)));
 #pragma unroll
-    for (int p = 0; p < NU; ++p) {
-      const int kk = (tid >> (BF ? 1 : 2)) + (BF ? 128 : 64) * p;
+    for (int u = 0; u < NU; ++u)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
       {
-        const int e = (int)(q * nn + (size_t)kk * n + r0 + c4);
-        if constexpr (BF) sc[p][q] = load8_bf16(crs, e);
-        else sc[p][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, e * 4, 0, 0);
+        const int e = (int)(q * nn + (size_t)(r0 + rr) * n + cq + 16 * CE * u);
+        if constexpr (BF) sc[u][q] = load8_bf16(crt, e);
+        else sc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crt, e * 4, 0, 0);
       }
-    }
     const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
     const int nd = tid < n ? tid : n - 1;  // clamped indices + selects: no load inside a divergent branch
     float pv[3][4], pt[4];
@@ -275,18 +276,20 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
           sAr[(16 + rr) * RS + c0 + e] = in ? dcubic(cc, f) : 0.f;
         }
     }
-    {  // 2. the column strip: Horner, transposed into LDS
+    ROWS_STAMP(15);
+    {  // 2. the column strip: Horner of transposed row rr (= column r0 + rr), element kk = node; LDS [node][column]
 #pragma unroll
-      for (int p = 0; p < NU; ++p) {
-        const int kk = (tid >> (BF ? 1 : 2)) + (BF ? 128 : 64) * p;
-        if (kk < NP)
+      for (int u = 0; u < NU; ++u) {
+        const int c0 = cq + 16 * CE * u;
+        if (c0 < NP)
 #pragma unroll
           for (int e = 0; e < CE; ++e) {
-            const bool in = kk < n && r0 + c4 + e < n;
-            const float cc[4] = {coef_el<BF>(sc[p][0], e), coef_el<BF>(sc[p][1], e), coef_el<BF>(sc[p][2], e),
-                                 coef_el<BF>(sc[p][3], e)};
-            big[kk * kStrip + c4 + e] = in ? cubic(cc, f) : 0.f;
-            big[(NP + kk) * kStrip + c4 + e] = in ? dcubic(cc, f) : 0.f;
+            const int kk = c0 + e;
+            const bool in = r0 + rr < n && kk < n;
+            const float cc[4] = {coef_el<BF>(sc[u][0], e), coef_el<BF>(sc[u][1], e), coef_el<BF>(sc[u][2], e),
+                                 coef_el<BF>(sc[u][3], e)};
+            big[kk * kStrip + rr] = in ? cubic(cc, f) : 0.f;
+            big[(NP + kk) * kStrip + rr] = in ? dcubic(cc, f) : 0.f;
           }
       }
     }
@@ -755,7 +758,7 @@ extern "C" int gncde_debug_rows_stamps(unsigned long long* host, int count) {
 size_t rows_sync_ints(const GncdeProblem& p) { return align_up((size_t)p.B + 4, 4); }
 
 // Launch one evaluation (RowsState: the group layout, fixed per problem, and the barriers done so far).
-int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum,
+int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum, const void* coefT,
                  const float* wperm, const uint16_t* wbf, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
                  unsigned& bars_done, hipStream_t st, float* keep) {
   Inst k;
@@ -784,6 +787,7 @@ int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* d
   a.np = rows_np(p.n, bfm);
   a.ts = p.ts;
   a.coef = p.coef;
+  a.coefT = coefT;
   a.csum = csum;
   a.tcoef = p.tcoef;
   a.data_coef = p.data_coef;

@@ -75,6 +75,7 @@ struct BwdArgs {
   int B, n, T, L, l, nb;
   const float* ts;
   const float* coef;       // [B, T-1, 4, n, n]
+  const float* coefT;      // the same planes transposed (generic_vf_prepare): the column strip as whole-line rows
   const float* csum;       // k_coef_sums [B, T-1, 12 n + 4]
   const float* fusion;     // [L, GNCDE_FC]
   const float* t;          // [B] stage times
@@ -130,19 +131,17 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
   const auto crs = rsrc(cb, (unsigned)(4 * nn * sizeof(float)));
   const int RS = NP + 4;
   float* sAr = big + 2 * NP * kStrip;
-  const int rr = tid >> 4, cq = 4 * (tid & 15), c4 = 4 * (tid & 3);
+  const int rr = tid >> 4, cq = 4 * (tid & 15);
+  const auto crt = rsrc(a.coefT + ((size_t)b * (T - 1) + idx) * 4 * nn, (unsigned)(4 * nn * sizeof(float)));
   u32x4 rc[4][4], sc[4][4];
 #pragma unroll
   for (int u = 0; u < 4; ++u)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      rc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)((q * nn + (size_t)(r0 + rr) * n + cq + 64 * u) * 4), 0, 0);
-#pragma unroll
-  for (int p = 0; p < 4; ++p)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      sc[p][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)((q * nn + (size_t)((tid >> 2) + 64 * p) * n + r0 + c4) * 4),
-                                                       0, 0);
+    for (int q = 0; q < 4; ++q) {
+      const int e = (int)((q * nn + (size_t)(r0 + rr) * n + cq + 64 * u) * 4);
+      rc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, e, 0, 0);
+      sc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crt, e, 0, 0);  // transposed row rr = column r0 + rr
+    }
   const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
   const int nd = tid < n ? tid : n - 1;
   float pv[3][4], pt[4];
@@ -166,16 +165,17 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
       }
   }
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int kk = (tid >> 2) + 64 * p;
-    if (kk < NP)
+  for (int u = 0; u < 4; ++u) {
+    const int c0 = cq + 64 * u;
+    if (c0 < NP)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const bool in = kk < n && r0 + c4 + e < n;
-        const unsigned x0 = sc[p][0][e], x1 = sc[p][1][e], x2 = sc[p][2][e], x3 = sc[p][3][e];
+        const int kk = c0 + e;
+        const bool in = r0 + rr < n && kk < n;
+        const unsigned x0 = sc[u][0][e], x1 = sc[u][1][e], x2 = sc[u][2][e], x3 = sc[u][3][e];
         const float cc[4] = {u2f(x0), u2f(x1), u2f(x2), u2f(x3)};
-        big[kk * kStrip + c4 + e] = in ? cubic(cc, f) : 0.f;
-        big[(NP + kk) * kStrip + c4 + e] = in ? dcubic(cc, f) : 0.f;
+        big[kk * kStrip + rr] = in ? cubic(cc, f) : 0.f;
+        big[(NP + kk) * kStrip + rr] = in ? dcubic(cc, f) : 0.f;
       }
   }
   // node features and this layer's families at every node (thread = node)
@@ -945,6 +945,7 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     a.nb = w.nb;
     a.ts = p.ts;
     a.coef = p.coef;
+    a.coefT = static_cast<const float*>(generic_vf_coefT(p, vf_ws));
     a.csum = csum;
     a.fusion = p.fusion;
     a.t = t;
@@ -1045,6 +1046,7 @@ extern "C" int gncde_diag_vf_vjp(const GncdeProblem* prob, const float* t, const
   }
   (void)H;
   generic_vf_prepare(p, vf_ws, st);
+  if (!rows_supported(p) && rows_vjp_supported(p)) generic_vf_transpose(p, vf_ws, st);
   rows_vjp_begin(p, rows_ws, st);
   unsigned bars = 0;
   const int rc = rows_vf_vjp(p, t, y, gF, gy, nullptr, generic_vf_csum(p, vf_ws), wf, bf, rows_ws, vf_ws, &bars, st);

@@ -686,6 +686,7 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
   char* vf_ws = rows_ws + (rows ? rows_vjp_workspace(p) : 0);
   const Tableau tab = s.method == GNCDE_RK4 ? rk4_tab() : tsit5_tab();
   generic_vf_prepare(p, vf_ws, st);
+  if (!rows_supported(p) && rows_vjp_supported(p)) generic_vf_transpose(p, vf_ws, st);
   unsigned bars = 0;  // barriers of one-launch stage evaluations (generic_vf_eval)
   {
     size_t wo = 0, bo = 0;
