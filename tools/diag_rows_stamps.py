@@ -34,11 +34,24 @@ def main():
         torch.cuda.synchronize()
     buf = np.zeros(nwg * 16, dtype=np.uint64)
     assert fn(buf.ctypes.data, buf.size) == 0
-    st = buf.reshape(nwg, 16)[:, :15].astype(np.float64)
+    full = buf.reshape(nwg, 16).astype(np.float64)
+    st = full[:, :15]
+    print(f"  rows-block Horner done (coefficient loads landed) at median {np.median((full[:, 15] - full[:, 0]) * 0.01):.2f} us")
     t0 = st[:, 0].min()
     rel = (st - t0) * 0.01  # us
     print(f"B={B} {compute}: launch span {rel[:, 14].max():.2f} us; first WG start {0:.2f}, last WG start "
           f"{rel[:, 0].max():.2f} us")
+    # group barriers: a sample's 16 workgroups (blockIdx layout of rows_vf_eval: g = (x & 7) + 8 (x / 128) when
+    # the group count is a multiple of 8, else x / 16)
+    G = B
+    x = np.arange(nwg)
+    g = (x & 7) + 8 * (x // (8 * 16)) if G % 8 == 0 else x // 16
+    for name, pub, z in (("barrier 1", 5, 6), ("barrier 2", 8, 9), ("barrier 3", 11, 12)):
+        last = np.array([rel[g == q, pub].max() for q in range(G)])
+        first_z = np.array([rel[g == q, z].min() for q in range(G)])
+        skew = np.array([rel[g == q, pub].max() - rel[g == q, pub].min() for q in range(G)])
+        print(f"  {name}: last arrival -> first Z loaded median {np.median(first_z - last):.2f} us; arrival skew "
+              f"median {np.median(skew):.2f} us")
     for k in range(1, 15):
         d = (st[:, k] - st[:, k - 1]) * 0.01
         print(f"  {NAMES[k]:>9}: median {np.median(d):6.2f} us  max {d.max():6.2f}  (ends at median {np.median(rel[:, k]):6.2f})")
