@@ -46,6 +46,15 @@ def algorithmic_flops_per_eval(n, dims):
     return f
 
 
+def executed_flops_per_sample(n, dims, rk4_steps):
+    """The §8(d) flops as the fused kernel executes them: the spline (19 n^2) and every layer's fusion build
+    (22 n^2) once per DISTINCT stage time (2 S + 1 forms per RK4 solve), the layer products once per evaluation."""
+    forms, evals = 2 * rk4_steps + 1, 4 * rk4_steps
+    per_form = 19 * n * n + 22 * n * n * (len(dims) - 1)
+    per_eval = sum(2 * n * n * dims[l] + 2 * n * dims[l - 1] * dims[l] + 6 * n * dims[l] for l in range(1, len(dims)))
+    return forms * per_form + evals * per_eval
+
+
 def algorithmic_bytes_per_sample(n, d0, dL, T, rk4_steps):
     """HBM bytes one RK4 solve of one sample must move.  SURVEY §8(d) charges the active interval's fp32
     (d, c, b, a) operator-channel coefficients (16 n^2 B) and the time-channel means (12 n B) per vector-field
@@ -296,6 +305,10 @@ def main():
         bytes_launch = B * algorithmic_bytes_per_sample(n, hidden, hidden, T, args.rk4_steps)
         flops_launch = evals_per_launch * algorithmic_flops_per_eval(n, prob.dims)
         roof, alt = roofline(bytes_launch, flops_launch, kernel_ms, load_traffic(workload, path))
+        if roof["bound"] == "mfma":  # beside the §8(d) model: the flops the kernel actually executes per launch
+            ex = B * executed_flops_per_sample(n, prob.dims, args.rk4_steps)
+            roof["executed_per_launch"] = ex
+            roof["executed_frac"] = round(ex / (kernel_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFS, 4)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(prob, spec, y0, layers, args.cpu_seconds)

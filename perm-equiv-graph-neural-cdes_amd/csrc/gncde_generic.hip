@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* 
   const size_t nn = (size_t)n * n;
   const float tb = t[b];
   const float* tsb = ts + (size_t)b * T;
-  const int idx = interval_index(tsb, T, tb);
+  const int idx = interval_index_wave(tsb, T, tb);
   const float f = tb - tsb[idx];
   const float f3 = 3.0f * f;
   const CT* cb = coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
@@ -311,7 +311,7 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
   const float tb = t[b];
   const float* tsb = ts + (size_t)b * T;
   const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;  // 32 x 8
-  const int idx = interval_index(tsb, T, tb);
+  const int idx = interval_index_wave(tsb, T, tb);
   const float f = tb - tsb[idx], f3 = 3.0f * f;
   const CT* cb = coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
   const float* cs = csum + ((size_t)b * (T - 1) + idx) * csum_stride(n);

@@ -80,6 +80,21 @@ __device__ __forceinline__ int interval_index(const float* ts, int T, float t) {
   return i > T - 2 ? T - 2 : i;
 }
 
+// The same index from one round of loads: every lane of the wave reads a knot and the ballot counts the knots
+// below t (searchsorted 'left' on sorted knots), instead of log2(T) dependent loads.  Call with the whole wave
+// active (uniform control flow).
+__device__ __forceinline__ int interval_index_wave(const float* ts, int T, float t) {
+  const int lane = threadIdx.x & 63;
+  int cnt = 0;
+  for (int j0 = 0; j0 < T; j0 += 64) {
+    const int j = j0 + lane;
+    const float v = ts[j < T ? j : T - 1];
+    cnt += __popcll(__ballot(j < T && v < t));
+  }
+  const int i = cnt - 1 < 0 ? 0 : cnt - 1;
+  return i > T - 2 ? T - 2 : i;
+}
+
 // Offsets of layer l's parameters inside the packed params buffer (see gncde.h).
 struct LayerOffsets {
   size_t rms_w, rms_b, W, b;

@@ -118,6 +118,27 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
   __shared__ PidState sh;
   const int b = blockIdx.y, slice = blockIdx.x, NS = gridDim.x;
   const int tid = threadIdx.x;
+  const int E = a.E;
+  const size_t base = (size_t)b * E;
+  const size_t BE = (size_t)a.B * E;
+  // An in-attempt stage (5 launches in 6) reads K, y and the stage buffers it needs; when one pass covers the
+  // sample (e.g. config 5) they are all requested here, before the state's load returns (which of kk_0..kk_5 are
+  // used depends on the state), so the stage costs one memory round trip instead of two.
+  constexpr int U2 = 2;
+  const int stride = NS * kAdvThreads, e0 = slice * kAdvThreads + tid;
+  const bool one_pass = E <= stride * U2;
+  float pk[U2], py[U2], pkv[6][U2];
+  if (one_pass) {
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+      const int e = e0 + u * stride;
+      const int ec = e < E ? e : E - 1;
+      pk[u] = a.K[base + ec];
+      py[u] = a.y[base + ec];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) pkv[j][u] = a.kk[(size_t)j * BE + base + ec];
+    }
+  }
   if (tid == 0) sh = a.state[b];
   __syncthreads();
   PidState s = sh;
@@ -127,9 +148,6 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
   }
   const bool mid = s.phase == 2 && s.st < 6;
   if (!mid && slice != 0) return;
-  const int E = a.E;
-  const size_t base = (size_t)b * E;
-  const size_t BE = (size_t)a.B * E;
   const float rtol = a.rtol, atol = a.atol;
   const float t0 = a.t0[b], t1 = a.t1[b];
   const float inv_cnt = 1.0f / (float)E;
@@ -186,35 +204,45 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
     if (mid) {
       // A stage inside an attempt (e.g. config 5's 255 x 32 over 8 slices): K, y and only the stage buffers the next
       // input reads (j < st + 1, the current one taken from K in registers) in one round trip per pass.
-      constexpr int U2 = 2;
       const int ns1 = s.st + 1;
-      const int stride = NS * kAdvThreads;
       float ar[6], cst;
       stage_row(ns1, ar, cst);
-      for (int e0 = slice * kAdvThreads + tid; e0 < E; e0 += stride * U2) {
+      for (int ep = e0; ep < E; ep += stride * U2) {
         float kq[U2], yv[U2], kv[6][U2];
+        if (one_pass) {
 #pragma unroll
-        for (int u = 0; u < U2; ++u) {
-          const int e = e0 + u * stride;
-          kq[u] = e < E ? K[e] : 0.f;
-          yv[u] = e < E ? y[e] : 0.f;
-        }
+          for (int u = 0; u < U2; ++u) {
+            kq[u] = pk[u];
+            yv[u] = py[u];
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
-          if (j < ns1 && j != s.st) {  // uniform: a scalar branch around the loads
+            for (int j = 0; j < 6; ++j) kv[j][u] = pkv[j][u];
+          }
+        } else {
 #pragma unroll
-            for (int u = 0; u < U2; ++u) {
-              const int e = e0 + u * stride;
-              kv[j][u] = e < E ? kk(j)[e] : 0.f;
+          for (int u = 0; u < U2; ++u) {
+            const int e = ep + u * stride;
+            kq[u] = e < E ? K[e] : 0.f;
+            yv[u] = e < E ? y[e] : 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 6; ++j) {
+            if (j < ns1 && j != s.st) {  // uniform: a scalar branch around the loads
+#pragma unroll
+              for (int u = 0; u < U2; ++u) {
+                const int e = ep + u * stride;
+                kv[j][u] = e < E ? kk(j)[e] : 0.f;
+              }
             }
-          } else {
-#pragma unroll
-            for (int u = 0; u < U2; ++u) kv[j][u] = 0.f;
           }
         }
 #pragma unroll
+        for (int j = 0; j < 6; ++j)  // buffers past the stage (allocated, possibly stale) are never multiplied
+          if (!(j < ns1 && j != s.st))
+#pragma unroll
+            for (int u = 0; u < U2; ++u) kv[j][u] = 0.f;
+#pragma unroll
         for (int u = 0; u < U2; ++u) {
-          const int e = e0 + u * stride;
+          const int e = ep + u * stride;
           float acc = 0.f;  // the memory path's summation order
 #pragma unroll
           for (int j = 0; j < 6; ++j) acc = j < ns1 ? fmaf(ar[j], j == s.st ? kq[u] : kv[j][u], acc) : acc;

@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
     const int b = live ? bs : a.B - 1;  // an idle round computes on a valid sample, keeps its barriers, stores no dy
     const float tb = a.t[b];
     const float* tsb = a.ts + (size_t)b * T;
-    const int idx = interval_index(tsb, T, tb);
+    const int idx = interval_index_wave(tsb, T, tb);
     const float f = tb - tsb[idx];
     using CT_ = typename std::conditional<BF, uint16_t, float>::type;
     const CT_* cb = reinterpret_cast<const CT_*>(a.coef) + ((size_t)b * (T - 1) + idx) * 4 * nn;
@@ -737,6 +737,9 @@ int resident_blocks(const Inst& k, size_t smem) {
 // channel halves), so that shape keeps the multi-kernel path.
 // GNCDE_COMPUTE_BF16_MFMA runs only here (every shape of the envelope, the H = 64 read-out included: its bf16 MFMA
 // chain is an eighth of the fp32 one).
+// In fp32 it is also used only when every sample's group is resident at once (one round per launch): with more
+// samples than resident groups the rounds serialise their barrier chains, and the multi-kernel path is faster
+// (config 5 at B = 64: 42.7 ms per solve on this kernel's two rounds against 36.9 ms multi-kernel).
 bool rows_supported(const GncdeProblem& p) {
   const bool bf = p.compute == GNCDE_COMPUTE_BF16_MFMA;
   if ((p.compute != GNCDE_COMPUTE_FP32 && !bf) || p.n > kMaxN || p.n < 1) return false;
@@ -744,9 +747,16 @@ bool rows_supported(const GncdeProblem& p) {
   if (H != 16 && H != 32 && H != 64) return false;
   for (int l = 0; l < p.L; ++l)
     if (p.dims[l] != H) return false;
+  bool shape;
   if (p.cde_hidden > 0)
-    return p.cde_embed == 8 && p.cde_hidden == H && (H <= 32 || bf) && p.dims[p.L] == 16 * H;
-  return p.dims[p.L] == H;
+    shape = p.cde_embed == 8 && p.cde_hidden == H && (H <= 32 || bf) && p.dims[p.L] == 16 * H;
+  else
+    shape = p.dims[p.L] == H;
+  if (!shape || bf) return shape;
+  Inst k;
+  if (!find_inst(H, p.cde_hidden > 0 ? 2 : 1, false, k)) return false;
+  const int nb = (p.n + kRB - 1) / kRB;
+  return resident_blocks(k, rows_smem(p.n, H, p.L, false)) / nb >= p.B;
 }
 
 #ifdef GNCDE_ROWS_STAMPS

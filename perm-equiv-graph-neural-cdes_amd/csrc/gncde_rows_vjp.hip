@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
   const size_t nn = (size_t)n * n, zgroup = (size_t)n * H;
   const float tb = a.t[b];
   const float* tsb = a.ts + (size_t)b * T;
-  const int idx = interval_index(tsb, T, tb);
+  const int idx = interval_index_wave(tsb, T, tb);
   const float f = tb - tsb[idx];
   const float* fc = a.fusion + l * GNCDE_FC;
 
@@ -561,7 +561,7 @@ __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
   __shared__ float spart[4][kRB][H + 1];
   const float tb = a.t[b];
   const float* tsb = a.ts + (size_t)b * T;
-  const int idx = interval_index(tsb, T, tb);
+  const int idx = interval_index_wave(tsb, T, tb);
   const float f = tb - tsb[idx];
   const bool iin = r0 + i < n;
   const int row = iin ? r0 + i : n - 1;

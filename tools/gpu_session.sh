@@ -53,6 +53,7 @@ for step in "$@"; do
            rc=$?; echo "proftrain rc=$rc"; tail -n 5 "$ROOTDIR/gpurun_out/proftrain.log"; \
            case $rc in 124|134|137|139) exit $rc;; esac) || exit $? ;;
     configs) run configs 900 python tools/bench_configs.py ;;
+    gradcfg) run gradcfg 900 python tools/bench_grad_configs.py ;;
     profgrad) (cd /tmp && run_dir="$ROOTDIR/gpurun_out/profgrad" && rm -rf "$run_dir" && \
            timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$run_dir" -o run -- \
              python3 "$ROOTDIR/tools/bench_grad_configs.py" --configs "${CFGS:-5}" --reps 1 > "$ROOTDIR/gpurun_out/profgrad.log" 2>&1; \
