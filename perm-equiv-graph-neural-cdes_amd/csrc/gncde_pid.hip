@@ -121,24 +121,8 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
   const int E = a.E;
   const size_t base = (size_t)b * E;
   const size_t BE = (size_t)a.B * E;
-  // An in-attempt stage (5 launches in 6) reads K, y and the stage buffers it needs; when one pass covers the
-  // sample (e.g. config 5) they are all requested here, before the state's load returns (which of kk_0..kk_5 are
-  // used depends on the state), so the stage costs one memory round trip instead of two.
   constexpr int U2 = 2;
   const int stride = NS * kAdvThreads, e0 = slice * kAdvThreads + tid;
-  const bool one_pass = E <= stride * U2;
-  float pk[U2], py[U2], pkv[6][U2];
-  if (one_pass) {
-#pragma unroll
-    for (int u = 0; u < U2; ++u) {
-      const int e = e0 + u * stride;
-      const int ec = e < E ? e : E - 1;
-      pk[u] = a.K[base + ec];
-      py[u] = a.y[base + ec];
-#pragma unroll
-      for (int j = 0; j < 6; ++j) pkv[j][u] = a.kk[(size_t)j * BE + base + ec];
-    }
-  }
   if (tid == 0) sh = a.state[b];
   __syncthreads();
   PidState s = sh;
@@ -209,37 +193,25 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
       stage_row(ns1, ar, cst);
       for (int ep = e0; ep < E; ep += stride * U2) {
         float kq[U2], yv[U2], kv[6][U2];
-        if (one_pass) {
 #pragma unroll
-          for (int u = 0; u < U2; ++u) {
-            kq[u] = pk[u];
-            yv[u] = py[u];
-#pragma unroll
-            for (int j = 0; j < 6; ++j) kv[j][u] = pkv[j][u];
-          }
-        } else {
-#pragma unroll
-          for (int u = 0; u < U2; ++u) {
-            const int e = ep + u * stride;
-            kq[u] = e < E ? K[e] : 0.f;
-            yv[u] = e < E ? y[e] : 0.f;
-          }
-#pragma unroll
-          for (int j = 0; j < 6; ++j) {
-            if (j < ns1 && j != s.st) {  // uniform: a scalar branch around the loads
-#pragma unroll
-              for (int u = 0; u < U2; ++u) {
-                const int e = ep + u * stride;
-                kv[j][u] = e < E ? kk(j)[e] : 0.f;
-              }
-            }
-          }
+        for (int u = 0; u < U2; ++u) {
+          const int e = ep + u * stride;
+          kq[u] = e < E ? K[e] : 0.f;
+          yv[u] = e < E ? y[e] : 0.f;
         }
 #pragma unroll
-        for (int j = 0; j < 6; ++j)  // buffers past the stage (allocated, possibly stale) are never multiplied
-          if (!(j < ns1 && j != s.st))
+        for (int j = 0; j < 6; ++j) {
+          if (j < ns1 && j != s.st) {  // uniform: a scalar branch around the loads
+#pragma unroll
+            for (int u = 0; u < U2; ++u) {
+              const int e = ep + u * stride;
+              kv[j][u] = e < E ? kk(j)[e] : 0.f;
+            }
+          } else {
 #pragma unroll
             for (int u = 0; u < U2; ++u) kv[j][u] = 0.f;
+          }
+        }
 #pragma unroll
         for (int u = 0; u < U2; ++u) {
           const int e = ep + u * stride;

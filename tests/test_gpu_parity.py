@@ -546,3 +546,34 @@ def test_cde8_fixed_grid_trajectory_matches_oracle(gncde, golden_dir, name):
         worst = max(worst, max(errs))
         print(f"{name} sample {b}: worst step error {max(errs):.2e} at step {int(np.argmax(errs))} of {len(errs)}")
     assert worst <= RTOL_SOLVE
+
+
+def test_generic_dispatch_by_batch_agrees(gncde):
+    """The generic path takes the one-launch evaluation (gncde_rows.hip) only when one round of its co-resident
+    groups covers the batch, else the multi-kernel evaluation (gncde_rows.hip rows_supported).  At config 5's shape
+    (n = 255, h = 32, L = 4, de = 8) a batch of 64 takes the multi-kernel path and its first 16 samples alone take
+    the one-launch kernel.  One evaluation agrees to the VF tolerance (fp32 summation order only); a 20-step
+    Tsit5 solve to 10x its own response to a one-ulp change of y0 (this operator amplifies rounding, as in the
+    config-5 tests above)."""
+    G = gncde
+    from gncde import layout, synthetic
+    prob, y0 = synthetic.cde_batch(64, 255, 3, 32, 8, 4, 1.0, seed=7)
+    sub, y16 = prob.take(list(range(16))), y0[:16].contiguous()
+    t = (prob.ts[:, 0] + 0.37 * (prob.ts[:, 1] - prob.ts[:, 0])).contiguous()
+    dy = G.vf_eval(prob, t, y0)
+    dy16 = G.vf_eval(sub, t[:16].contiguous(), y16)
+    err_vf = rel_err(dy16.cpu().numpy(), dy[:16].cpu().numpy())
+
+    def spec_for(B):
+        grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, 1.0, 0.05)] * B)
+        return G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=grid, nsteps=ns)
+    ys = G.integrate(prob, spec_for(64), y0)
+    ys16 = G.integrate(sub, spec_for(16), y16)
+    err = rel_err(ys16.cpu().numpy(), ys[:16].cpu().numpy())
+    ulp = torch.where(torch.rand(y16.shape, generator=torch.Generator().manual_seed(4)) < 0.5, -1.0, 1.0).cuda()
+    sens = rel_err(G.integrate(sub, spec_for(16), y16 * (1.0 + ulp * 2.0 ** -24)).cpu().numpy(), ys16.cpu().numpy())
+    print(f"B=64 multi-kernel vs B=16 one-launch: one evaluation {err_vf:.2e}, solve {err:.2e} "
+          f"(1-ulp response {sens:.2e})")
+    assert torch.isfinite(ys).all()
+    assert err_vf <= RTOL_VF
+    assert err <= max(RTOL_SOLVE, 10.0 * sens)
