@@ -24,7 +24,8 @@
 //                   zhat g_P^T, which meets A, dA, A^T, dA^T in registers for the dense contractions; then g_W'
 //                   partials, RMSNorm^T, the ReLU mask and the next layer's g_out, g_P, g_q (or the stage input's
 //                   cotangent at l = 0)
-//   k_bwd_readout   (CDE) the read-out weight and bias gradient on MFMA, split over 128-row slices of all samples
+//   k_bwd_readout   (CDE) the read-out weight and bias gradient on MFMA, split over 64-row slices of all samples
+//                   and H / 16 output-row groups
 //   k_bwd_data      (CDE data-spline cotangent, TGB) g_dX_ij = tg_i sum_m gF_im (P_i . W'[16m+j,:] + q_i b'[16m+j])
 // Parameter and fusion partials accumulate in per-(sample, row block) / per-chunk slots that only their owner
 // workgroup updates (fixed order, no atomics); k_bwd_finish reduces them once per reverse sweep and maps g_W', g_b'
@@ -40,7 +41,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kRB = 16;
 constexpr int kMaxN = 256;
 constexpr int kStrip = 17;
-constexpr int kRoRows = 128;  // rows per read-out gradient slice
+constexpr int kRoRows = 64;   // rows per read-out gradient slice (with the m split below: 128 workgroups at config 5)
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -668,7 +669,8 @@ __global__ void __launch_bounds__(256) k_bwd_readout(int rows, const float* __re
   }
   __syncthreads();
   float* dst = part + (size_t)blockIdx.x * 16 * H * (H + 1);
-  for (int m0 = w; m0 < H; m0 += 16) {  // batch: m = m0, m0 + 4, m0 + 8, m0 + 12
+  // gridDim.y = H / 16 workgroups share the slice, each the output rows m of its own m0 (disjoint partial rows)
+  for (int m0 = w + 16 * (int)blockIdx.y; m0 < H; m0 += 16 * (int)gridDim.y) {  // batch: m = m0, m0 + 4, m0 + 8, m0 + 12
     floatx4 acc[4][NT];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -972,15 +974,15 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
   }
   if (cde) {
     const size_t rsm = readout_smem(H);
-    if (H == 16) hipLaunchKernelGGL(k_bwd_readout<16>, dim3(w.ro_chunks), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
-    else if (H == 32) hipLaunchKernelGGL(k_bwd_readout<32>, dim3(w.ro_chunks), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
+    if (H == 16) hipLaunchKernelGGL(k_bwd_readout<16>, dim3(w.ro_chunks, 1), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
+    else if (H == 32) hipLaunchKernelGGL(k_bwd_readout<32>, dim3(w.ro_chunks, 2), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
     else {
       static bool attr = false;  // 82 KB of LDS at H = 64
       if (!attr && hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bwd_readout<64>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)rsm) != hipSuccess)
         return GNCDE_ERR_HIP;
       attr = true;
-      hipLaunchKernelGGL(k_bwd_readout<64>, dim3(w.ro_chunks), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
+      hipLaunchKernelGGL(k_bwd_readout<64>, dim3(w.ro_chunks, 4), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
     }
     if (gdata)
       hipLaunchKernelGGL(k_bwd_data, dim3((n * 16 + 255) / 256, B), dim3(256), 0, st, B, n, H, p.T, p.ts, t, w.tgF,

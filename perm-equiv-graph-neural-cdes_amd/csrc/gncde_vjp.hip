@@ -341,16 +341,42 @@ __global__ void v_lincomb(int B, size_t E, const float* __restrict__ base, Lin l
   out[o] = fmaf(hb, s, b0);
 }
 
-// gK_i = h_b b_i lam (+ gstage[b, k, i], the extra cotangent of stage i of step k: [B, G1, S, E])
-__global__ void v_seed(int B, size_t E, int G1, int S, int k, int i, float bi, const float* __restrict__ lam,
-                       const float* __restrict__ hcur, const float* __restrict__ gst, float* __restrict__ out) {
+// every stage's seed of one step in one pass: gK_i = h_b b_i lam (+ gstage[b, k, i], the extra cotangent of stage i
+// of step k: [B, G1, S, E]), i < S
+struct Seeds {
+  float* out[8];
+  float b[8];
+};
+__global__ void v_seed_all(int B, size_t E, int G1, int S, int k, const float* __restrict__ lam,
+                           const float* __restrict__ hcur, const float* __restrict__ gst, Seeds sd) {
   const int b = blockIdx.y;
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= E) return;
   const size_t o = (size_t)b * E + e;
-  float v = hcur[b] * (bi * lam[o]);
-  if (gst) v += gst[(((size_t)b * G1 + k) * S + i) * E + e];
-  out[o] = v;
+  const float l = lam[o], h = hcur[b];
+  for (int i = 0; i < S; ++i) {
+    float v = h * (sd.b[i] * l);
+    if (gst) v += gst[(((size_t)b * G1 + k) * S + i) * E + e];
+    sd.out[i][o] = v;
+  }
+}
+
+// the reverse of stage i's input in one pass: gy += tmp and gK_j += h_b (a_ij tmp) for the stages j < i with
+// a_ij != 0 (the same roundings as one v_lincomb per target)
+struct Scatter {
+  float* gk[8];
+  float a[8];
+  int n;
+};
+__global__ void v_stage_scatter(int B, size_t E, const float* __restrict__ tmp, const float* __restrict__ hcur,
+                                float* __restrict__ gy, Scatter sc) {
+  const int b = blockIdx.y;
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const size_t o = (size_t)b * E + e;
+  const float v = tmp[o], h = hcur[b];
+  gy[o] = fmaf(1.0f, v, gy[o]);
+  for (int j = 0; j < sc.n; ++j) sc.gk[j][o] = fmaf(h, sc.a[j] * v, sc.gk[j][o]);
 }
 
 // row k of a per-step trajectory [B, G, E]: out = (accumulate ? out : 0) + traj[:, k]
@@ -739,9 +765,14 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
       }
     }
     // reverse: gK_i = h b_i lam (+ the stage's extra cotangent) ; gy = lam
-    for (int i = 0; i < tab.stages; ++i)
-      hipLaunchKernelGGL(v_seed, ge, dim3(256), 0, st, B, E, G - 1, tab.stages, k, i, tab.b[i], w.lam, w.hcur,
-                         gstage, w.gK[i]);
+    {
+      Seeds sd{};
+      for (int i = 0; i < tab.stages; ++i) {
+        sd.out[i] = w.gK[i];
+        sd.b[i] = tab.b[i];
+      }
+      hipLaunchKernelGGL(v_seed_all, ge, dim3(256), 0, st, B, E, G - 1, tab.stages, k, w.lam, w.hcur, gstage, sd);
+    }
     (void)hipMemcpyAsync(w.gyacc, w.lam, (size_t)B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
     for (int i = tab.stages - 1; i >= 0; --i) {
       hipLaunchKernelGGL(v_stage_time, dim3(gb), dim3(256), 0, st, B, tab.c[i], w.tcur, w.hcur, w.tst);
@@ -754,21 +785,14 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
       } else {
         vf_vjp(p, w.tst, w.U[i], w.gK[i], w.tmp, gdata, w, st);
       }
-      // gy += tmp ; gK_j += h a_ij tmp
-      Lin one{};
-      one.x[0] = w.tmp;
-      one.a[0] = 1.0f;
-      one.nx = 1;
-      hipLaunchKernelGGL(v_lincomb, ge, dim3(256), 0, st, B, E, nullptr, one, w.hcur, w.gyacc, 1);
+      // gy += tmp ; gK_j += h a_ij tmp (one launch)
+      Scatter sc{};
       for (int j = 0; j < i; ++j)
         if (tab.a[i][j] != 0.f) {
-          Lin lc{};
-          lc.x[0] = w.tmp;
-          lc.a[0] = tab.a[i][j];
-          lc.nx = 1;
-          lc.scale_h = 1;
-          hipLaunchKernelGGL(v_lincomb, ge, dim3(256), 0, st, B, E, nullptr, lc, w.hcur, w.gK[j], 1);
+          sc.gk[sc.n] = w.gK[j];
+          sc.a[sc.n++] = tab.a[i][j];
         }
+      hipLaunchKernelGGL(v_stage_scatter, ge, dim3(256), 0, st, B, E, w.tmp, w.hcur, w.gyacc, sc);
     }
     (void)hipMemcpyAsync(w.lam, w.gyacc, (size_t)B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
     if (s.save_mode == GNCDE_SAVE_STEPS)
