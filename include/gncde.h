@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GNCDE_ABI_VERSION 5
+#define GNCDE_ABI_VERSION 6
 #define GNCDE_MAX_LAYERS 8
 #define GNCDE_FC 24
 
@@ -82,7 +82,9 @@ enum {
   GNCDE_ERR_SHAPE = 2,        /* inconsistent dims (e.g. CDE width != h*de*2) */
   GNCDE_ERR_UNSUPPORTED = 3,  /* configuration outside what any kernel implements */
   GNCDE_ERR_WORKSPACE = 4,    /* workspace smaller than gncde_workspace_bytes() */
-  GNCDE_ERR_HIP = 5           /* a HIP runtime call failed (launch error) */
+  GNCDE_ERR_HIP = 5,          /* a HIP runtime call failed (launch error) */
+  GNCDE_ERR_BARRIER = 6       /* a one-launch evaluation's group barrier gave up: the results are invalid (see
+                                 gncde_integrate) */
 };
 
 enum { GNCDE_RK4 = 0, GNCDE_TSIT5 = 1 };

@@ -15,10 +15,12 @@ int validate_problem(const GncdeProblem* p) {
   if (p->B < 0 || p->n <= 0 || p->T < 2 || p->L < 1 || p->L > GNCDE_MAX_LAYERS) return GNCDE_ERR_SHAPE;
   for (int l = 0; l <= p->L; ++l)
     if (p->dims[l] <= 0) return GNCDE_ERR_SHAPE;
-  if (!p->ts || !p->coef || !p->tcoef || !p->fusion || !p->params) return GNCDE_ERR_ARG;
+  // (an empty shard may pass NULL data pointers: torch gives empty tensors a null data_ptr)
+  if (p->B > 0 && (!p->ts || !p->coef || !p->tcoef)) return GNCDE_ERR_ARG;
+  if (!p->fusion || !p->params) return GNCDE_ERR_ARG;
   if (p->compute < GNCDE_COMPUTE_FP32 || p->compute > GNCDE_COMPUTE_BF16_MFMA) return GNCDE_ERR_ARG;
   if (p->cde_hidden > 0) {
-    if (p->cde_embed <= 0 || !p->data_coef) return GNCDE_ERR_ARG;
+    if (p->cde_embed <= 0 || (p->B > 0 && !p->data_coef)) return GNCDE_ERR_ARG;
     if (p->dims[p->L] != p->cde_hidden * p->cde_embed * 2) return GNCDE_ERR_SHAPE;
     if (p->dims[0] != p->cde_hidden) return GNCDE_ERR_SHAPE;
   } else if (p->cde_hidden < 0) {
@@ -111,6 +113,7 @@ const char* gncde_strerror(int code) {
     case GNCDE_ERR_UNSUPPORTED: return "configuration not supported by any kernel";
     case GNCDE_ERR_WORKSPACE: return "workspace too small";
     case GNCDE_ERR_HIP: return "HIP runtime error";
+    case GNCDE_ERR_BARRIER: return "a one-launch evaluation's group barrier gave up (results invalid)";
     default: return "unknown gncde error";
   }
 }
@@ -136,9 +139,13 @@ int gncde_integrate_path(const GncdeProblem* prob, const GncdeSolver* solver, ch
   rc = validate_solver(prob, solver);
   if (rc) return rc;
   if (!buf || buf_len == 0) return GNCDE_ERR_ARG;
-  if (!use_fused(*prob, *solver, buf, buf_len))
-    snprintf(buf, buf_len,
-             prob->compute == GNCDE_COMPUTE_BF16_MFMA ? "rows_bf16" : prob->compute != GNCDE_COMPUTE_FP32 ? "generic_bf16" : "generic");
+  if (use_fused(*prob, *solver, buf, buf_len)) return GNCDE_OK;
+  if (rows_pid_supported(*prob, *solver))
+    rows_pid_name(*prob, buf, buf_len);
+  else if (prob->compute == GNCDE_COMPUTE_FP32)  // generic_rows: every evaluation is one k_rows launch
+    snprintf(buf, buf_len, rows_supported(*prob) ? "generic_rows" : "generic");
+  else
+    snprintf(buf, buf_len, prob->compute == GNCDE_COMPUTE_BF16_MFMA ? "rows_bf16" : "generic_bf16");
   return GNCDE_OK;
 }
 
@@ -149,8 +156,9 @@ int gncde_vf_eval(const GncdeProblem* prob, const float* t, const float* y, floa
   if (prob->B == 0) return GNCDE_OK;
   if (!t || !y || !dy) return GNCDE_ERR_ARG;
   if (workspace_bytes < generic_vf_workspace(*prob) || !workspace) return GNCDE_ERR_WORKSPACE;
-  return generic_vf_eval(*prob, t, y, dy, static_cast<char*>(workspace),
-                         static_cast<hipStream_t>(stream));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int rc2 = generic_vf_eval(*prob, t, y, dy, static_cast<char*>(workspace), st);
+  return rc2 ? rc2 : rows_fault_status(*prob, static_cast<char*>(workspace), st, rows_supported(*prob));
 }
 
 int gncde_integrate(const GncdeProblem* prob, const GncdeSolver* solver, const float* y0, float* ys,

@@ -33,25 +33,6 @@ typedef __attribute__((address_space(4))) const float CFloat;  // constant addre
 
 constexpr int kTMax = 256;  // knots per sample held in LDS
 
-// Tsit5 row a[s][0..5] for stage s = 1..6 (row 6 = b_sol) and c[s], as compile-time immediates
-// selected by a wave-uniform switch (no constant-memory table).
-__device__ __forceinline__ void tsit5_row(int s, float (&a)[6], float& c) {
-  a[0] = a[1] = a[2] = a[3] = a[4] = a[5] = 0.f;
-  c = 1.f;
-  switch (s) {
-    case 1: a[0] = TSIT5_A21; c = TSIT5_C2; break;
-    case 2: a[0] = TSIT5_A31; a[1] = TSIT5_A32; c = TSIT5_C3; break;
-    case 3: a[0] = TSIT5_A41; a[1] = TSIT5_A42; a[2] = TSIT5_A43; c = TSIT5_C4; break;
-    case 4: a[0] = TSIT5_A51; a[1] = TSIT5_A52; a[2] = TSIT5_A53; a[3] = TSIT5_A54; c = TSIT5_C5; break;
-    case 5:
-      a[0] = TSIT5_A61; a[1] = TSIT5_A62; a[2] = TSIT5_A63; a[3] = TSIT5_A64; a[4] = TSIT5_A65;
-      break;
-    default:
-      a[0] = TSIT5_B1; a[1] = TSIT5_B2; a[2] = TSIT5_B3; a[3] = TSIT5_B4; a[4] = TSIT5_B5; a[5] = TSIT5_B6;
-      break;
-  }
-}
-
 struct FusedArgs {
   int B, n, T, G, save_mode;
   const float* ts;
@@ -77,19 +58,6 @@ struct FusedArgs {
 };
 
 constexpr int kTsit5Pid = 2;  // internal METHOD id: Tsit5 + PIDController (diffrax defaults)
-
-// Tsit5 free interpolant weights b_i(theta): y(t + theta h) = y + h * sum_i b_i(theta) f_i
-// (restated in oracle/gncde_oracle.py:tsit5_dense_weights).
-__device__ __forceinline__ void tsit5_dense(float th, float (&w)[7]) {
-  const float t2 = th * th;
-  w[0] = -1.0530884977290216f * th * (th - 1.3299890189751412f) * (t2 - 1.4364028541716351f * th + 0.7139816917074209f);
-  w[1] = 0.1017f * t2 * (t2 - 2.1966568338249754f * th + 1.2949852507374631f);
-  w[2] = 2.490627285651252793f * t2 * (t2 - 2.38535645472061657f * th + 1.57803468208092486f);
-  w[3] = -16.54810288924490272f * (th - 1.21712927295533244f) * (th - 0.61620406037800089f) * t2;
-  w[4] = 47.37952196281928122f * (th - 1.203071208372362603f) * (th - 0.658047292653547382f) * t2;
-  w[5] = -34.87065786149660974f * (th - 1.2f) * (th - 0.666666666666666667f) * t2;
-  w[6] = 2.5f * (th - 1.0f) * (th - 0.6f) * t2;
-}
 
 // A(t)/dA(t) LDS images use a padded row stride NP+1: row AND column walks are bank-conflict free
 // and every address is lane base + compile-time offset (no per-element address registers).

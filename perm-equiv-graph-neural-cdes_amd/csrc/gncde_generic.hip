@@ -638,7 +638,8 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   // the one-launch evaluation reads a node block's column strip [:, R] as rows R of the transposed planes (whole
   // cache lines, like its rows block) instead of 16-column segments of every row
   const size_t planes = B * (size_t)(p.T - 1) * 4 * nn;
-  w.coefT = take(rows_supported(p) || rows_vjp_supported(p) ? (coef_is_bf16(p) ? (planes + 1) / 2 : planes) : 1);
+  const bool strip = rows_supported(p) || rows_vjp_supported(p) || rows_solve_shape(p);
+  w.coefT = take(strip ? (coef_is_bf16(p) ? (planes + 1) / 2 : planes) : 1);
   return off;
 }
 
@@ -747,7 +748,7 @@ void generic_vf_transpose(const GncdeProblem& p, char* ws, hipStream_t st) {
                        reinterpret_cast<float*>(w.coefT));
 }
 
-void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
+void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool rows_layout) {
   VfWs w;
   carve_vf(p, ws, w);
   (void)hipMemsetAsync(w.sync, 0, ((size_t)p.B + 4) * sizeof(unsigned), st);
@@ -757,7 +758,7 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st) {
                        reinterpret_cast<const uint16_t*>(p.coef), w.csum);
   else
     hipLaunchKernelGGL(k_coef_sums<float>, gs, dim3(256), 0, st, p.n, p.T, p.coef, w.csum);
-  const bool rows = rows_supported(p);
+  const bool rows = rows_supported(p) || rows_layout;
   if (rows) generic_vf_transpose(p, ws, st);
   size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
@@ -918,6 +919,27 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }
 
+int rows_fault_status(const GncdeProblem& p, char* vf_ws, hipStream_t st, bool ran_rows) {
+  if (!ran_rows) return GNCDE_OK;
+  int fault = 0;
+  if (hipMemcpyAsync(&fault, generic_vf_fault(p, vf_ws), sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return GNCDE_ERR_HIP;
+  return fault ? GNCDE_ERR_BARRIER : GNCDE_OK;
+}
+
+// Tsit5 + PID as ONE persistent launch on the one-launch evaluation (gncde_rows.hip)
+int generic_rows_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats, char* ws,
+                     hipStream_t st) {
+  VfWs w;
+  carve_vf(p, ws, w);
+  generic_vf_prepare(p, ws, st, true);
+  float* part = reinterpret_cast<float*>(ws + generic_vf_workspace(p));
+  const int rc = rows_integrate_pid(p, s, y0, ys, stats, ws, part, w.csum, w.coefT, w.wp, w.bf, w.Z0, w.Z1, w.sync, st);
+  if (rc) return rc;
+  return rows_fault_status(p, ws, st, true);
+}
+
 size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s) {
   if (s.controller == GNCDE_CTRL_PID) return generic_pid_workspace(p);
   const size_t B = p.B, E = (size_t)p.n * state_dim(p);
@@ -929,7 +951,11 @@ size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s) 
 
 int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
                       char* ws, hipStream_t st) {
-  if (s.controller == GNCDE_CTRL_PID) return generic_integrate_pid(p, s, y0, ys, stats, ws, st);
+  if (s.controller == GNCDE_CTRL_PID) {
+    if (rows_pid_supported(p, s)) return generic_rows_pid(p, s, y0, ys, stats, ws, st);
+    const int rc = generic_integrate_pid(p, s, y0, ys, stats, ws, st);
+    return rc ? rc : rows_fault_status(p, ws, st, rows_supported(p));
+  }
   if (s.controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
   const int B = p.B;
   const size_t E = (size_t)p.n * state_dim(p);
@@ -1042,7 +1068,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     hipLaunchKernelGGL(k_grid_stats, dim3(gb), dim3(256), 0, st, B, s.method, s.nsteps, generic_vf_fault(p, ws),
                        stats);
   if (hipGetLastError() != hipSuccess) return GNCDE_ERR_HIP;
-  return rc;
+  return rc ? rc : rows_fault_status(p, ws, st, rows_supported(p));
 }
 
 }  // namespace gncde

@@ -49,6 +49,38 @@ __device__ __forceinline__ float stage_time(float t, float c, float h) {
   return __fadd_rn(t, __fmul_rn(c, h));
 }
 
+// Tsit5 row a[s][0..5] for stage s = 1..6 (row 6 = b_sol) and c[s], as compile-time immediates
+// selected by a wave-uniform switch (no constant-memory table).
+__device__ __forceinline__ void tsit5_row(int s, float (&a)[6], float& c) {
+  a[0] = a[1] = a[2] = a[3] = a[4] = a[5] = 0.f;
+  c = 1.f;
+  switch (s) {
+    case 1: a[0] = TSIT5_A21; c = TSIT5_C2; break;
+    case 2: a[0] = TSIT5_A31; a[1] = TSIT5_A32; c = TSIT5_C3; break;
+    case 3: a[0] = TSIT5_A41; a[1] = TSIT5_A42; a[2] = TSIT5_A43; c = TSIT5_C4; break;
+    case 4: a[0] = TSIT5_A51; a[1] = TSIT5_A52; a[2] = TSIT5_A53; a[3] = TSIT5_A54; c = TSIT5_C5; break;
+    case 5:
+      a[0] = TSIT5_A61; a[1] = TSIT5_A62; a[2] = TSIT5_A63; a[3] = TSIT5_A64; a[4] = TSIT5_A65;
+      break;
+    default:
+      a[0] = TSIT5_B1; a[1] = TSIT5_B2; a[2] = TSIT5_B3; a[3] = TSIT5_B4; a[4] = TSIT5_B5; a[5] = TSIT5_B6;
+      break;
+  }
+}
+
+// Tsit5 free interpolant weights b_i(theta): y(t + theta h) = y + h * sum_i b_i(theta) f_i
+// (restated in oracle/gncde_oracle.py:tsit5_dense_weights).
+__device__ __forceinline__ void tsit5_dense(float th, float (&w)[7]) {
+  const float t2 = th * th;
+  w[0] = -1.0530884977290216f * th * (th - 1.3299890189751412f) * (t2 - 1.4364028541716351f * th + 0.7139816917074209f);
+  w[1] = 0.1017f * t2 * (t2 - 2.1966568338249754f * th + 1.2949852507374631f);
+  w[2] = 2.490627285651252793f * t2 * (t2 - 2.38535645472061657f * th + 1.57803468208092486f);
+  w[3] = -16.54810288924490272f * (th - 1.21712927295533244f) * (th - 0.61620406037800089f) * t2;
+  w[4] = 47.37952196281928122f * (th - 1.203071208372362603f) * (th - 0.658047292653547382f) * t2;
+  w[5] = -34.87065786149660974f * (th - 1.2f) * (th - 0.666666666666666667f) * t2;
+  w[6] = 2.5f * (th - 1.0f) * (th - 0.6f) * t2;
+}
+
 // Sum over the four 16-lane rows of a wave64 (lane ^ 16, lane ^ 32) on the gfx950 row-swap VALU ops:
 // no LDS round trip.  Written as asm because the clang builtins of this toolchain drop the second
 // (vsrc) result of the swap; the leading s_nop covers the VALU-write -> permlane-read hazard.
@@ -187,7 +219,9 @@ size_t vf_forms_scratch(const GncdeProblem& p);
 // wrapper, [B, n, 2 de]) the data spline's derivative at t.
 void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float* tg, float* red, float* part,
               float* abar, hipStream_t st, float* qrow = nullptr, float* dx = nullptr);
-void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st);
+// rows_layout: also lay out what the one-launch evaluation reads (transposed planes, every W' permuted) for a caller
+// that runs it although rows_supported(p) is false (the persistent solve at batches past one co-resident round)
+void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool rows_layout = false);
 // bars: the solve's count of per-group barriers done by one-launch evaluations so far (gncde_rows.hip); nullptr
 // only together with prepared = false (a standalone evaluation)
 // keep (optional, [L-1, B, n, d]): every hidden layer's output Z_{l+1} kept for the reverse mode (uniform width d)
@@ -223,6 +257,21 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
                 const float* csum, const float* wf, const float* bfold, char* ws, char* vf_ws, unsigned* bars,
                 hipStream_t st);
 void rows_vjp_finish(const GncdeProblem& p, char* ws, float* gparams, float* gfusion, hipStream_t st);
+
+// the persistent Tsit5 + PIDController solve on the one-launch evaluation (gncde_rows.hip): n <= 256, one width
+bool rows_pid_supported(const GncdeProblem& p, const GncdeSolver& s);
+bool rows_solve_shape(const GncdeProblem& p);  // the shape part of rows_pid_supported
+size_t rows_pid_scratch(const GncdeProblem& p);
+// sync: the evaluation workspace's [B] arrival counters, fault word and ticket counter (zeroed by generic_vf_prepare)
+int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
+                       char* vf_ws, float* part, const float* csum, const void* coefT, const float* wperm,
+                       const float* bf, float* z0, float* z1, unsigned* sync, hipStream_t st);
+void rows_pid_name(const GncdeProblem& p, char* buf, size_t len);
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device, kernel, size) for launches above 64 KB of LDS
+bool ensure_dyn_lds(const void* fn, size_t smem);
+// a one-launch evaluation's group barrier gave up in this call: GNCDE_ERR_BARRIER (reads the workspace's fault word
+// back, one stream synchronisation; GNCDE_OK without one-launch evaluations)
+int rows_fault_status(const GncdeProblem& p, char* vf_ws, hipStream_t st, bool ran_rows);
 
 // generic Tsit5 + PIDController (any shape, CDE wrapper): gncde_pid.hip
 size_t generic_pid_workspace(const GncdeProblem& p);

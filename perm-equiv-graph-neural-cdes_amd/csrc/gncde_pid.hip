@@ -57,32 +57,6 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return tot;
 }
 
-__device__ __forceinline__ void tsit5_dense_w(float th, float (&w)[7]) {
-  const float t2 = th * th;
-  w[0] = -1.0530884977290216f * th * (th - 1.3299890189751412f) * (t2 - 1.4364028541716351f * th + 0.7139816917074209f);
-  w[1] = 0.1017f * t2 * (t2 - 2.1966568338249754f * th + 1.2949852507374631f);
-  w[2] = 2.490627285651252793f * t2 * (t2 - 2.38535645472061657f * th + 1.57803468208092486f);
-  w[3] = -16.54810288924490272f * (th - 1.21712927295533244f) * (th - 0.61620406037800089f) * t2;
-  w[4] = 47.37952196281928122f * (th - 1.203071208372362603f) * (th - 0.658047292653547382f) * t2;
-  w[5] = -34.87065786149660974f * (th - 1.2f) * (th - 0.666666666666666667f) * t2;
-  w[6] = 2.5f * (th - 1.0f) * (th - 0.6f) * t2;
-}
-
-__device__ __forceinline__ void stage_row(int s, float (&a)[6], float& c) {
-  for (int j = 0; j < 6; ++j) a[j] = 0.f;
-  c = 1.f;
-  switch (s) {
-    case 1: a[0] = TSIT5_A21; c = TSIT5_C2; break;
-    case 2: a[0] = TSIT5_A31; a[1] = TSIT5_A32; c = TSIT5_C3; break;
-    case 3: a[0] = TSIT5_A41; a[1] = TSIT5_A42; a[2] = TSIT5_A43; c = TSIT5_C4; break;
-    case 4: a[0] = TSIT5_A51; a[1] = TSIT5_A52; a[2] = TSIT5_A53; a[3] = TSIT5_A54; c = TSIT5_C5; break;
-    case 5: a[0] = TSIT5_A61; a[1] = TSIT5_A62; a[2] = TSIT5_A63; a[3] = TSIT5_A64; a[4] = TSIT5_A65; break;
-    default:
-      a[0] = TSIT5_B1; a[1] = TSIT5_B2; a[2] = TSIT5_B3; a[3] = TSIT5_B4; a[4] = TSIT5_B5; a[5] = TSIT5_B6;
-      break;
-  }
-}
-
 // initial state: t = t0, saved states at save_ts <= t0, first evaluation f(t0, y0)
 __global__ void k_pid_init(PidArgs a, const float* __restrict__ y0) {
   const int b = blockIdx.x;
@@ -190,7 +164,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
       // input reads (j < st + 1, the current one taken from K in registers) in one round trip per pass.
       const int ns1 = s.st + 1;
       float ar[6], cst;
-      stage_row(ns1, ar, cst);
+      tsit5_row(ns1, ar, cst);
       for (int ep = e0; ep < E; ep += stride * U2) {
         float kq[U2], yv[U2], kv[6][U2];
 #pragma unroll
@@ -270,7 +244,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
           const float* sts = a.save_ts + (size_t)b * a.S;
           while (s.si < a.S && sts[s.si] <= s.tn) {  // dense output inside (t, tn]
             float wts[7];
-            tsit5_dense_w((sts[s.si] - s.t) / s.h, wts);
+            tsit5_dense((sts[s.si] - s.t) / s.h, wts);
             float* dst = a.ys + ((size_t)b * a.S + s.si) * E;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -387,7 +361,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
           const float* sts = a.save_ts + (size_t)b * a.S;
           while (s.si < a.S && sts[s.si] <= s.tn) {  // dense output inside (t, tn]
             float wts[7];
-            tsit5_dense_w((sts[s.si] - s.t) / s.h, wts);
+            tsit5_dense((sts[s.si] - s.t) / s.h, wts);
             float* dst = a.ys + ((size_t)b * a.S + s.si) * E;
             for (int e = tid; e < E; e += blockDim.x) {
               float acc = 0.f;
@@ -450,7 +424,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
   if (s.phase == 2) {  // next stage input and time
     const int ns1 = s.st + 1;
     float ar[6], cst;
-    stage_row(ns1, ar, cst);
+    tsit5_row(ns1, ar, cst);
     __syncthreads();
     for (int e0 = tid; e0 < E; e0 += P) {
       // every stage buffer's loads issued at once (the ones past ns1 are loaded and not used: allocated memory,

@@ -25,6 +25,8 @@
 // fault word (reported as solver status 4) instead of hanging.  Groups are laid out so a group's workgroups share
 // blockIdx % 8 (one XCD under the observed round-robin placement: its coefficient strips and Z re-reads stay in one
 // L2) — a speed choice, never needed for correctness.
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 
 #include "gncde_internal.h"
@@ -33,20 +35,36 @@ namespace gncde {
 namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
-typedef float floatx4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned rows (n = 129, 255)
+typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 #ifdef GNCDE_ROWS_STAMPS
 __device__ unsigned long long g_rows_stamps[4096 * 16];
 #define ROWS_STAMP(k) \
-  do { if (threadIdx.x == 0 && it == 0) g_rows_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+  do { if (threadIdx.x == 0) g_rows_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define ROWS_STAMP(k) do {} while (0)
 #endif
 constexpr int kRB = 16;      // node rows per workgroup
 constexpr int kMaxN = 256;   // per wave: four 16-column K chunks (fp32) or two 32-column chunks (bf16)
 constexpr int kStrip = 17;   // LDS row stride of the transposed column strip
+
+// The persistent solve's controller inputs and outputs (GncdeSolver, PID controller)
+struct SolveArgs {
+  int S, max_steps, auto_dt, step_len;
+  float rtol, atol;
+  const float* t0;       // [B]
+  const float* t1;       // [B]
+  const float* dt0;      // [B] (auto_dt = 0)
+  const float* save_ts;  // [B, S] (SAVE_TS) or nullptr
+  const float* y0;       // [B, n, H]
+  float* ys;             // [B, S, n, H] or [B, n, H]
+  float* step_ts;        // [B, step_len] or nullptr
+  int32_t* stats;        // [B, 4] or nullptr
+  float* part;           // [B, 2, nb, 2] the group sums' partials (two buffers, by publication parity)
+};
 
 struct RowsArgs {
   int B, n, T, L, G, rounds, nb, big;  // big: floats of the LDS region shared by the strip, Z_l and the partials
@@ -70,6 +88,10 @@ struct RowsArgs {
   unsigned* bar;           // [G] arrivals per group, monotonic within a solve
   unsigned bar0;           // barriers every group completed before this launch
   int* fault;              // set when a barrier wait gives up
+  unsigned spin_limit;     // polls before a barrier wait gives up
+  unsigned* ticket;        // solve: start-order tickets -> (sample, row block)
+  unsigned ticket0;        // tickets taken before this launch
+  SolveArgs s;             // solve only
 };
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
@@ -131,8 +153,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
 // BF (GNCDE_COMPUTE_BF16_MFMA): bfloat16 coefficients, and every product — (I + Abar_l) diag(inv) Z, the Linears, the
 // read-out — on v_mfma_f32_16x16x32_bf16 with single-plane bf16 operands rounded from the fp32 values (fp32
 // accumulation); the spline, the reductions, RMSNorm and all sums outside the MFMAs stay fp32.
-template <int H, int MODE, bool BF>
-__global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
+// SOLVE: the persistent Tsit5 + PIDController solve (gncde_rows.hip header); otherwise one evaluation per launch.
+template <int H, int MODE, bool BF, bool SOLVE>
+__global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int ZS = rows_zs(H);
   constexpr int CT = H / 16;           // column tiles of a width-H operand / output
@@ -150,62 +173,84 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
   float* sDx = sTg + 16;
   float* sOut = sDx + 16 * kStrip;
   floatx4* red = reinterpret_cast<floatx4*>(sOut + 16 * ZS);
+  int* sFlag = reinterpret_cast<int*>(red + 4 * 64);  // [0] barrier gave up, [1] ticket
 
-  const int x = blockIdx.x;
+  // ---- which rows of which sample ------------------------------------------------------------------------------
+  // One evaluation (k_rows): the grid holds G co-resident groups that loop over the samples in rounds.  Solve: one
+  // group per sample, the grid is B groups, and a workgroup takes its (sample, row block) from a ticket in start
+  // order, so the workgroups of a group are always ones that have started: a group waits only for members that
+  // are already running, and groups of later samples start as earlier solves finish (no co-residency assumption).
   int g, rb;
-  if (a.G % 8 == 0) {  // a group's workgroups share blockIdx % 8 (bijective for G % 8 == 0)
+  if constexpr (SOLVE) {
+    if (threadIdx.x == 0)
+      sFlag[1] = (int)(__hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.ticket0);
+    __syncthreads();
+    g = sFlag[1] / nb;
+    rb = sFlag[1] % nb;
+  } else if (a.G % 8 == 0) {  // a group's workgroups share blockIdx % 8 (bijective for G % 8 == 0)
+    const int x = blockIdx.x;
     g = (x & 7) + 8 * (x / (8 * nb));
     rb = (x >> 3) % nb;
   } else {
-    g = x / nb;
-    rb = x % nb;
+    g = blockIdx.x / nb;
+    rb = blockIdx.x % nb;
   }
   const int r0 = rb * kRB;
   const size_t nn = (size_t)n * n;
   const size_t zgroup = (size_t)n * H;
   unsigned epoch = a.bar0;
+  unsigned pub = 0;  // publications of this launch (stage inputs, hidden outputs, partial sums): buffer parity
 
   auto arrive = [&]() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores have reached memory
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(a.bar + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ++pub;
   };
-  auto wait_all = [&]() {
+  // wait until every workgroup of the group has arrived `epoch` times; a bounded spin: past the limit (or when
+  // another workgroup has given up) the fault word is set and the wait returns false in every thread
+  auto wait_all = [&]() -> bool {
     ++epoch;
     if (threadIdx.x == 0) {
       const unsigned target = epoch * (unsigned)nb;
       unsigned spins = 0;
+      int gave_up = 0;
       while (__hip_atomic_load(a.bar + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
-        if ((++spins & 1023u) == 0 &&
-            (spins > (1u << 22) || __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        ++spins;
+        if (spins > a.spin_limit ||
+            ((spins & 1023u) == 0 && __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
           __hip_atomic_store(a.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          gave_up = 1;
           break;
         }
       }
+      sFlag[0] = gave_up;
     }
     __syncthreads();
+    return sFlag[0] == 0;
   };
 
-  for (int it = 0; it < a.rounds; ++it) {
-    // the lane's indices through an opaque move each round: otherwise every per-lane address and bounds mask of the
-    // form and the layers is hoisted out of the round loop and held in registers for the whole kernel
+  // ---- one vector-field evaluation of sample b at time tb ----------------------------------------------------
+  // Layer 0 reads the stage input z0: with plain loads (written before this launch), or, with `handoff`, as a
+  // publication of the group (a barrier wait first, sc1 loads).  The output tile dy[R, 0 .. H-1] lands in sOut.
+  // Returns false when a barrier wait gave up.
+  auto evaluate = [&](const int b, const float tb, const float* z0, const bool handoff, const bool live)
+      __attribute__((always_inline)) -> bool {
+    bool ok = true;
+    // the lane's indices through an opaque move per evaluation: otherwise every per-lane address and bounds mask
+    // of the form and the layers is hoisted out of the enclosing loop and held in registers for the whole kernel
     int tid;
     asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
     const int w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
     const int ri = r0 + lo;  // this lane's operand row
-    ROWS_STAMP(0);
-    const int bs = g + it * a.G;
-    const bool live = bs < a.B;
-    const int b = live ? bs : a.B - 1;  // an idle round computes on a valid sample, keeps its barriers, stores no dy
-    const float tb = a.t[b];
     const float* tsb = a.ts + (size_t)b * T;
     const int idx = interval_index_wave(tsb, T, tb);
     const float f = tb - tsb[idx];
     using CT_ = typename std::conditional<BF, uint16_t, float>::type;
     const CT_* cb = reinterpret_cast<const CT_*>(a.coef) + ((size_t)b * (T - 1) + idx) * 4 * nn;
 
-    // ---- form ---------------------------------------------------------------------------------------------------
+    // ---- form -------------------------------------------------------------------------------------------------
     // Both coefficient reads are unconditional coalesced dwordx4 buffer loads from this (sample, interval)'s four
     // planes (the descriptor's range check zero-fills anything past plane a); values outside the matrix are
     // selected to 0 before they reach LDS, so no load sits in a divergent branch.
@@ -214,8 +259,7 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
     float* sAr = big + 2 * NP * kStrip;    // rows block A(t)[R, :] [16][RS], then dA/dt [16][RS]
     // 1. issue the rows block (thread = (row tid / 16, columns 4 (tid % 16) + 64 u): 256 coalesced bytes per row
     //    and u), the column strip and every small load of the form (node-vector plane sums, time channel, data
-    //    spline) at once: one memory round trip (L2 is cold at every launch, so the strip's second read of the
-    //    same lines is not cheaper later)
+    //    spline) at once: one memory round trip
     const int rr = tid >> 4;
     // fp32: 4 columns per 16-byte load (row rr = tid / 16, columns 4 (tid % 16) + 64 u, u < 4); bf16: 8 per load
     // (columns 8 (tid % 16) + 128 u, u < 2); the strip the same over the transposed planes
@@ -357,15 +401,16 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
     __syncthreads();  // the strip's region becomes Z_l
     ROWS_STAMP(2);
 
-    // ---- layers ----------------------------------------------------------------------------------------------
-    // Z_l -> LDS (the stage input with plain loads: written before this launch; a hidden output of the group with
-    // sc1 loads after the barrier) and the RMSNorm factors of its rows
+    // ---- layers --------------------------------------------------------------------------------------------
+    // Z_l -> LDS (a stage input written before this launch with plain loads; a publication of the group with sc1
+    // loads after the barrier) and the RMSNorm factors of its rows
+    const int zslot = SOLVE ? b : g;  // the group's hand-off buffers (solve: one group per sample)
     auto load_z = [&](int l) __attribute__((always_inline)) {
       float* Zs = big;
       constexpr int G4 = H / 4, U = 8;
       const int tot = NP * G4, valid = n * G4;
-      if (l == 0) {
-        const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.y + (size_t)b * zgroup);
+      if (l == 0 && !handoff) {
+        const floatx4* Z4 = reinterpret_cast<const floatx4*>(z0);
         for (int e0 = tid; e0 < tot; e0 += 256 * U) {
           floatx4 v[U];
 #pragma unroll
@@ -380,11 +425,12 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
           }
         }
       } else {
-        wait_all();
-        // hidden outputs alternate buffers by their step index within the launch, so a buffer is rewritten only
-        // after a barrier that every reader of its previous contents has passed (also across rounds, for L = 2)
-        const float* zin = a.keep && live ? a.keep + ((size_t)(l - 1) * a.B + b) * zgroup
-                                  : a.zbuf[(it * (L - 1) + l - 1) & 1] + (size_t)g * zgroup;
+        ok = wait_all() && ok;
+        // publications alternate buffers, so a buffer is rewritten only after a barrier that every reader of its
+        // previous contents has passed
+        const float* zin = l == 0 ? z0
+                         : a.keep && live ? a.keep + ((size_t)(l - 1) * a.B + b) * zgroup
+                                          : a.zbuf[(pub - 1) & 1] + (size_t)zslot * zgroup;
         const auto rs = rsrc(zin, (unsigned)(zgroup * sizeof(float)));
         for (int e0 = tid; e0 < tot; e0 += 256 * U) {
           floatx4 v[U];
@@ -546,8 +592,7 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
       }
       __syncthreads();
       // (an idle round keeps to its group's own buffers: the sample it recomputes is another group's)
-      float* zout = a.keep && live ? a.keep + ((size_t)l * a.B + b) * zgroup
-                                   : a.zbuf[(it * (L - 1) + l) & 1] + (size_t)g * zgroup;
+      float* zout = a.keep && live ? a.keep + ((size_t)l * a.B + b) * zgroup : a.zbuf[pub & 1] + (size_t)zslot * zgroup;
       const auto rs = rsrc(zout, (unsigned)(zgroup * sizeof(float)));
       constexpr int G4 = H / 4;
       if (tid < 16 * G4) {  // write-through 16-byte stores of this workgroup's rows, then one arrival
@@ -590,12 +635,8 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
       if constexpr (MODE == 1) {  // ODE: dy[R] = tg (P W'^T + q b'^T)
         for (int tile = w; tile < CT; tile += 4) {
           const floatx4 v = linear(l, tile);
-          if (live)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int R = 4 * hi + r;
-              if (r0 + R < n) a.dy[((size_t)b * n + r0 + R) * H + 16 * tile + lo] = v[r] * sTg[R];
-            }
+          for (int r = 0; r < 4; ++r) sOut[(4 * hi + r) * ZS + 16 * tile + lo] = v[r] * sTg[4 * hi + r];
         }
       } else {
         // CDE read-out: dy[R, m] = tg (sum_{c, j} P[., c] dX[., j] W'[16 m + j, c] + q sum_j b'[16 m + j] dX[., j])
@@ -652,15 +693,274 @@ __global__ void __launch_bounds__(256, MODE == 2 ? 2 : 3) k_rows(RowsArgs a) {
 #pragma unroll
             for (int p = 1; p < KP; ++p) acc += red[(w + p * CT) * 64 + lane];
         }
-        if (kp == 0 && live)
+        if (kp == 0)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int R = 4 * hi + r;
-            if (r0 + R < n) a.dy[((size_t)b * n + r0 + R) * H + m] = sTg[R] * acc[r];
-          }
+          for (int r = 0; r < 4; ++r) sOut[(4 * hi + r) * ZS + m] = sTg[4 * hi + r] * acc[r];
       }
-      __syncthreads();  // P (aliasing Z_l) and the LDS vectors are rewritten by the next round's form
+      __syncthreads();  // the output tile is complete; P (aliasing Z_l) and the LDS vectors are free again
       ROWS_STAMP(14);
+    }
+    return ok;
+  };
+
+  if constexpr (!SOLVE) {
+    for (int it = 0; it < a.rounds; ++it) {
+      const int bs = g + it * a.G;
+      const bool live = bs < a.B;
+      const int b = live ? bs : a.B - 1;  // an idle round computes on a valid sample, keeps its barriers, stores no dy
+      ROWS_STAMP(0);
+      evaluate(b, a.t[b], a.y + (size_t)b * zgroup, false, live);
+      // dy rows R: 16-byte stores of the output tile
+      constexpr int G4 = H / 4;
+      const int tid = threadIdx.x;
+      if (live && tid < 16 * G4) {
+        const int R = tid / G4, q = tid % G4;
+        if (r0 + R < n)
+          *reinterpret_cast<floatx4*>(a.dy + ((size_t)b * n + r0 + R) * H + 4 * q) =
+              *reinterpret_cast<const floatx4*>(sOut + R * ZS + 4 * q);
+      }
+      __syncthreads();  // sOut is rewritten by the next round
+    }
+  } else {
+    // ---- the persistent Tsit5 + PIDController solve of sample g (gncde_pid.hip's k_pid_advance state machine,
+    // graph_neural_cde.py:94-104 semantics): every workgroup of the group runs the controller redundantly on
+    // identical inputs (the group sums are added in row-block order by everyone), so all take the same decisions
+    const SolveArgs& s = a.s;
+    const int b = g;
+    const int tid = threadIdx.x;
+    // a thread owns 4 consecutive elements of the 16 x H row tile (threads < 4H), kept in registers all solve
+    const int orow = (4 * tid) / H, ocol = (4 * tid) % H;
+    const bool mine = tid < 4 * H && r0 + orow < n;
+    const size_t oel = ((size_t)b * n + r0 + orow) * H + ocol;
+    const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+    const float rtol = s.rtol, atol = s.atol;
+    const float t0 = s.t0[b], t1 = s.t1[b];
+    const float inv_cnt = 1.0f / (float)(n * H);
+    const size_t E = (size_t)n * H;
+    floatx4 y = mine ? *reinterpret_cast<const floatx4*>(s.y0 + oel) : zero;
+    floatx4 y1 = zero, kk[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) kk[j] = zero;
+    // the stage input of the next evaluation, published to the group (sc1 16-byte stores + one arrival)
+    auto publish = [&](const floatx4 u) {
+      if (mine)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, u),
+                                               rsrc(a.zbuf[pub & 1] + (size_t)b * zgroup, (unsigned)(E * 4)),
+                                               (int)(((r0 + orow) * H + ocol) * 4), 0, 16);
+      arrive();
+    };
+    // (sum of v0, sum of v1) over the group's rows: workgroup sums (waves in order), published, and every
+    // workgroup adds the nb partials in row-block order
+    float* sr = reinterpret_cast<float*>(red);  // free between evaluations
+    auto group_sum2 = [&](float v0, float v1, float& s0, float& s1) -> bool {
+      for (int o = 32; o > 0; o >>= 1) {
+        v0 += __shfl_xor(v0, o);
+        v1 += __shfl_xor(v1, o);
+      }
+      if ((tid & 63) == 0) {
+        sr[2 * (tid >> 6)] = v0;
+        sr[2 * (tid >> 6) + 1] = v1;
+      }
+      __syncthreads();
+      float* part = s.part + (size_t)(2 * b + (pub & 1)) * nb * 2;
+      if (tid == 0) {
+        const float p0 = ((sr[0] + sr[2]) + sr[4]) + sr[6], p1 = ((sr[1] + sr[3]) + sr[5]) + sr[7];
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, floatx2{p0, p1}),
+                                              rsrc(part, (unsigned)(nb * 8)), rb * 8, 0, 16);
+      }
+      arrive();
+      const bool ok = wait_all();
+      const auto rs = rsrc(part, (unsigned)(nb * 8));
+      float a0 = 0.f, a1 = 0.f;
+      for (int q = 0; q < nb; ++q) {
+        const floatx2 v = __builtin_bit_cast(floatx2, __builtin_amdgcn_raw_buffer_load_b64(rs, q * 8, 0, 16));
+        a0 += v.x;
+        a1 += v.y;
+      }
+      s0 = a0;
+      s1 = a1;
+      return ok;
+    };
+    int phase = 0, st = 0, steps = 0, rejects = 0, evals = 0, status = 0, si = 0;
+    float t = t0, tn = t0, h = 0.f, dt = s.auto_dt ? 0.f : s.dt0[b], h0 = 0.f, d1 = 0.f, tst = t0;
+    const float* sts = s.S > 0 ? s.save_ts + (size_t)b * s.S : nullptr;
+    while (si < s.S && sts[si] <= t0) {  // saved states at save_ts <= t0
+      if (mine) *reinterpret_cast<floatx4*>(s.ys + ((size_t)b * s.S + si) * E + (oel - (size_t)b * E)) = y;
+      ++si;
+    }
+    if (rb == 0 && tid == 0 && s.step_ts) s.step_ts[(size_t)b * s.step_len] = t0;
+    bool fault = false;
+    publish(y);  // f(t0, y0): the FSAL k0 and the initial-step heuristic's f0
+    for (;;) {
+      if (!evaluate(b, tst, a.zbuf[(pub - 1) & 1] + (size_t)b * zgroup, true, true)) {
+        fault = true;
+        break;
+      }
+      const floatx4 K = mine ? *reinterpret_cast<const floatx4*>(sOut + orow * ZS + ocol) : zero;
+      ++evals;
+      bool start = false;
+      if (phase == 0) {
+        kk[0] = K;
+        phase = 2;
+        if (s.auto_dt) {  // Hairer's initial step (diffrax dt0 = None): d0 = rms(y0 / sc), d1 = rms(f0 / sc)
+          float p0 = 0.f, p1 = 0.f;
+          if (mine)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float sc = fmaf(fabsf(y[e]), rtol, atol);
+              const float u = y[e] / sc, v = K[e] / sc;
+              p0 = fmaf(u, u, p0);
+              p1 = fmaf(v, v, p1);
+            }
+          float P0, P1;
+          if (!group_sum2(p0, p1, P0, P1)) {
+            fault = true;
+            break;
+          }
+          const float d0 = sqrtf(P0 * inv_cnt);
+          d1 = sqrtf(P1 * inv_cnt);
+          h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : 0.01f * (d0 / d1);
+          floatx4 u;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) u[e] = fmaf(h0, K[e], y[e]);
+          publish(u);
+          tst = t0 + h0;
+          phase = 1;
+          continue;
+        }
+        start = true;
+      } else if (phase == 1) {  // f(t0 + h0, y0 + h0 f0): d2 and the first step
+        float p2 = 0.f;
+        if (mine)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float sc = fmaf(fabsf(y[e]), rtol, atol);
+            const float v = (K[e] - kk[0][e]) / sc;
+            p2 = fmaf(v, v, p2);
+          }
+        float P2, unused;
+        if (!group_sum2(p2, 0.f, P2, unused)) {
+          fault = true;
+          break;
+        }
+        const float d2 = sqrtf(P2 * inv_cnt) / h0;
+        const float md = fmaxf(d1, d2);
+        const float h1 = md <= 1e-15f ? fmaxf(1e-6f, h0 * 1e-3f) : powf(0.01f / md, 0.2f);
+        dt = fminf(100.0f * h0, h1);
+        phase = 2;
+        start = true;
+      } else if (st < 6) {  // stage st (1 .. 5) of the attempt evaluated: the next stage's input
+#pragma unroll
+        for (int j = 1; j < 6; ++j)
+          if (j == st) kk[j] = K;
+        const int ns1 = st + 1;
+        float ar[6], cst;
+        tsit5_row(ns1, ar, cst);
+        floatx4 u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float acc = 0.f;  // k_pid_advance's summation order
+#pragma unroll
+          for (int j = 0; j < 6; ++j) acc = j < ns1 ? fmaf(ar[j], kk[j][e], acc) : acc;
+          u[e] = fmaf(h, acc, y[e]);
+        }
+        if (ns1 == 6) y1 = u;  // the FSAL stage's input is the step's candidate solution
+        publish(u);
+        tst = ns1 >= 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);
+        st = ns1;
+        continue;
+      } else {  // the attempt is complete: K = f(tn, y1); embedded error, accept / reject, next step size
+        float pe = 0.f;
+        if (mine)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float err = h * (TSIT5_E1 * kk[0][e] + TSIT5_E2 * kk[1][e] + TSIT5_E3 * kk[2][e] +
+                                   TSIT5_E4 * kk[3][e] + TSIT5_E5 * kk[4][e] + TSIT5_E6 * kk[5][e] + TSIT5_E7 * K[e]);
+            const float sc = fmaf(fmaxf(fabsf(y[e]), fabsf(y1[e])), rtol, atol);
+            const float v = err / sc;
+            pe = fmaf(v, v, pe);
+          }
+        float PE, unused;
+        if (!group_sum2(pe, 0.f, PE, unused)) {
+          fault = true;
+          break;
+        }
+        const float err = sqrtf(PE * inv_cnt);
+        const bool finite = isfinite(err);
+        const bool keep = finite && err < 1.0f;
+        float factor;
+        if (!finite) {
+          factor = 0.2f;
+        } else {
+          const float f1 = err == 0.f ? 10.0f : 0.9f * powf(1.0f / err, 0.2f);
+          factor = fminf(fmaxf(f1, keep ? 1.0f : 0.2f), 10.0f);
+        }
+        if (keep) {
+          while (si < s.S && sts[si] <= tn) {  // dense output inside (t, tn]
+            float wts[7];
+            tsit5_dense((sts[si] - t) / h, wts);
+            if (mine) {
+              floatx4 o;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                float acc = 0.f;
+#pragma unroll
+                for (int j = 0; j < 6; ++j) acc = fmaf(wts[j], kk[j][e], acc);
+                acc = fmaf(wts[6], K[e], acc);
+                o[e] = fmaf(h, acc, y[e]);
+              }
+              *reinterpret_cast<floatx4*>(s.ys + ((size_t)b * s.S + si) * E + (oel - (size_t)b * E)) = o;
+            }
+            ++si;
+          }
+          y = y1;
+          kk[0] = K;  // FSAL
+          if (rb == 0 && tid == 0 && s.step_ts && steps + 1 < s.step_len)
+            s.step_ts[(size_t)b * s.step_len + steps + 1] = tn;
+          t = tn;
+          ++steps;
+        } else {
+          ++rejects;
+        }
+        dt = factor * h;
+        st = 0;
+        start = true;
+      }
+      if (start) {  // begin the next attempt, or finish
+        bool finish = false;
+        if (!(t < t1)) {
+          finish = true;
+        } else if (steps + rejects >= s.max_steps) {
+          status = 1;
+          finish = true;
+        }
+        if (finish) {
+          if (s.step_ts && status == 0 && steps + 1 > s.step_len) status = 3;  // step record truncated
+          if (mine) {
+            if (s.S == 0) *reinterpret_cast<floatx4*>(s.ys + oel) = y;
+            for (int q = si; q < s.S; ++q)  // SAVE_TS: only on failure
+              *reinterpret_cast<floatx4*>(s.ys + ((size_t)b * s.S + q) * E + (oel - (size_t)b * E)) = y;
+          }
+          break;
+        }
+        tn = t + dt;
+        if (tn > t1 - 1e-6f) tn = t1;  // diffrax _clip_to_end
+        h = tn - t;
+        floatx4 u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] = fmaf(h, fmaf(TSIT5_A21, kk[0][e], 0.f), y[e]);
+        publish(u);
+        tst = stage_time(t, TSIT5_C2, h);
+        st = 1;
+      }
+    }
+    if (rb == 0 && tid == 0 && s.stats) {
+      const bool bad = fault || __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int32_t* o = s.stats + (size_t)b * 4;
+      o[GNCDE_STAT_STEPS] = steps;
+      o[GNCDE_STAT_REJECTS] = rejects;
+      o[GNCDE_STAT_EVALS] = evals;
+      o[GNCDE_STAT_STATUS] = bad ? 4 : status;
     }
   }
 }
@@ -670,28 +970,28 @@ struct Inst {
   void (*launch)(const RowsArgs&, int, size_t, hipStream_t);
 };
 
-template <int H, int MODE, bool BF>
+template <int H, int MODE, bool BF, bool SOLVE>
 void launch_rows(const RowsArgs& a, int grid, size_t smem, hipStream_t st) {
-  hipLaunchKernelGGL((k_rows<H, MODE, BF>), dim3(grid), dim3(256), smem, st, a);
+  hipLaunchKernelGGL((k_rows<H, MODE, BF, SOLVE>), dim3(grid), dim3(256), smem, st, a);
 }
 
-template <int H, int MODE, bool BF>
+template <int H, int MODE, bool BF, bool SOLVE>
 Inst inst() {
-  return Inst{reinterpret_cast<const void*>(&k_rows<H, MODE, BF>), &launch_rows<H, MODE, BF>};
+  return Inst{reinterpret_cast<const void*>(&k_rows<H, MODE, BF, SOLVE>), &launch_rows<H, MODE, BF, SOLVE>};
 }
 
-template <bool BF>
+template <bool BF, bool SOLVE>
 bool find_inst_t(int H, int mode, Inst& out) {
   if (mode == 1) {
-    if (H == 16) out = inst<16, 1, BF>();
-    else if (H == 32) out = inst<32, 1, BF>();
-    else if (H == 64) out = inst<64, 1, BF>();
+    if (H == 16) out = inst<16, 1, BF, SOLVE>();
+    else if (H == 32) out = inst<32, 1, BF, SOLVE>();
+    else if (H == 64) out = inst<64, 1, BF, SOLVE>();
     else return false;
   } else {
-    if (H == 16) out = inst<16, 2, BF>();
-    else if (H == 32) out = inst<32, 2, BF>();
-    else if constexpr (BF) {  // (fp32: the H = 64 read-out keeps the multi-kernel path)
-      if (H == 64) out = inst<64, 2, BF>();
+    if (H == 16) out = inst<16, 2, BF, SOLVE>();
+    else if (H == 32) out = inst<32, 2, BF, SOLVE>();
+    else if constexpr (BF && !SOLVE) {  // (fp32: the H = 64 read-out keeps the multi-kernel path)
+      if (H == 64) out = inst<64, 2, BF, SOLVE>();
       else return false;
     } else {
       return false;
@@ -699,9 +999,14 @@ bool find_inst_t(int H, int mode, Inst& out) {
   }
   return true;
 }
-bool find_inst(int H, int mode, bool bf, Inst& out) { return bf ? find_inst_t<true>(H, mode, out) : find_inst_t<false>(H, mode, out); }
+bool find_inst(int H, int mode, bool bf, Inst& out) {
+  return bf ? find_inst_t<true, false>(H, mode, out) : find_inst_t<false, false>(H, mode, out);
+}
 
-// workgroups of one instance resident per CU at this LDS size (occupancy query, cached per device) x CUs
+// 256-thread workgroups of one instance resident at this LDS size: min(occupancy query, what the SGPR file admits)
+// per CU, less one per CU of margin, x CUs (cached per device).  The occupancy API reports one workgroup per CU too
+// many for kernels with 97-112 SGPRs (MI355X_MICROARCH.md, residency): every k_rows instance has 106, and
+// floor(800 / (ceil(sgpr / 16) * 16 + 16)) = 6 covers any SGPR count up to 112.
 int resident_blocks(const Inst& k, size_t smem) {
   struct Entry {
     int dev;
@@ -719,16 +1024,54 @@ int resident_blocks(const Inst& k, size_t smem) {
     if (cache[i].dev == dev && cache[i].fn == k.fn && cache[i].smem == smem) return cache[i].blocks;
   int cus = 0, per = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (smem > 64 * 1024 &&
-      hipFuncSetAttribute(k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
-    return 0;
+  if (!ensure_dyn_lds(k.fn, smem)) return 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k.fn, 256, smem) != hipSuccess) return 0;
-  const int blocks = per * cus;
+  constexpr int kSgprCap = 800 / (112 + 16);
+  per = per < kSgprCap ? per : kSgprCap;
+  const int blocks = (per > 1 ? per - 1 : per) * cus;
   if (used < 64) cache[used++] = Entry{dev, k.fn, smem, blocks};
   return blocks;
 }
 
+// polls before a group barrier wait gives up (each poll is an L2 round trip plus s_sleep 1: seconds in all);
+// GNCDE_DEBUG_BARRIER_SPINS overrides it so tests can force the fault path
+unsigned spin_limit() {
+  const char* e = getenv("GNCDE_DEBUG_BARRIER_SPINS");
+  return e ? (unsigned)strtoul(e, nullptr, 10) : (1u << 22);
+}
+
+bool rows_shape(const GncdeProblem& p, bool bf) {
+  if (p.n > kMaxN || p.n < 1) return false;
+  const int H = p.dims[0];
+  if (H != 16 && H != 32 && H != 64) return false;
+  for (int l = 0; l < p.L; ++l)
+    if (p.dims[l] != H) return false;
+  if (p.cde_hidden > 0) return p.cde_embed == 8 && p.cde_hidden == H && (H <= 32 || bf) && p.dims[p.L] == 16 * H;
+  return p.dims[p.L] == H;
+}
+
 }  // namespace
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) for launches above 64 KB of LDS, once per (device, kernel, size)
+bool ensure_dyn_lds(const void* fn, size_t smem) {
+  if (smem <= 64 * 1024) return true;
+  struct Entry {
+    int dev;
+    const void* fn;
+    size_t smem;
+  };
+  static std::mutex mu;
+  static Entry done[128];
+  static int used = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  std::lock_guard<std::mutex> lock(mu);
+  for (int i = 0; i < used; ++i)
+    if (done[i].dev == dev && done[i].fn == fn && done[i].smem >= smem) return true;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess) return false;
+  if (used < 128) done[used++] = Entry{dev, fn, smem};
+  return true;
+}
 
 // The one-launch evaluation's envelope: every hidden width H in {16, 32, 64}, n <= 256, fp32, and an ODE output of
 // width H or the de = 8 CDE read-out with cde_hidden = H <= 32.  At H = 64 the CDE read-out weight is 256 KB (n x 16h
@@ -742,18 +1085,11 @@ int resident_blocks(const Inst& k, size_t smem) {
 // (config 5 at B = 64: 42.7 ms per solve on this kernel's two rounds against 36.9 ms multi-kernel).
 bool rows_supported(const GncdeProblem& p) {
   const bool bf = p.compute == GNCDE_COMPUTE_BF16_MFMA;
-  if ((p.compute != GNCDE_COMPUTE_FP32 && !bf) || p.n > kMaxN || p.n < 1) return false;
-  const int H = p.dims[0];
-  if (H != 16 && H != 32 && H != 64) return false;
-  for (int l = 0; l < p.L; ++l)
-    if (p.dims[l] != H) return false;
-  bool shape;
-  if (p.cde_hidden > 0)
-    shape = p.cde_embed == 8 && p.cde_hidden == H && (H <= 32 || bf) && p.dims[p.L] == 16 * H;
-  else
-    shape = p.dims[p.L] == H;
-  if (!shape || bf) return shape;
+  if (p.compute != GNCDE_COMPUTE_FP32 && !bf) return false;
+  if (!rows_shape(p, bf)) return false;
+  if (bf) return true;
   Inst k;
+  const int H = p.dims[0];
   if (!find_inst(H, p.cde_hidden > 0 ? 2 : 1, false, k)) return false;
   const int nb = (p.n + kRB - 1) / kRB;
   return resident_blocks(k, rows_smem(p.n, H, p.L, false)) / nb >= p.B;
@@ -814,9 +1150,97 @@ int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* d
   a.bar = bar;
   a.bar0 = bars_done;
   a.fault = fault;
+  a.spin_limit = spin_limit();
   k.launch(a, G * nb, smem, st);
   bars_done += (unsigned)(a.rounds * (p.L - 1));
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+}
+
+// ---- the persistent Tsit5 + PIDController solve ----------------------------------------------------------------
+// Envelope: the one-launch evaluation's fp32 shapes for any batch (a group only waits for workgroups that have
+// started, so no residency condition beyond one group), Tsit5 + PID, SaveAt(t1) or SaveAt(ts), and the default
+// dispatch (GNCDE_FLAG_GENERIC takes the host-paced gncde_pid.hip path instead).
+bool rows_solve_shape(const GncdeProblem& p) {
+  Inst k;
+  return p.compute == GNCDE_COMPUTE_FP32 && rows_shape(p, false) &&
+         find_inst_t<false, true>(p.dims[0], p.cde_hidden > 0 ? 2 : 1, k);
+}
+
+bool rows_pid_supported(const GncdeProblem& p, const GncdeSolver& s) {
+  if (!rows_solve_shape(p)) return false;
+  if (s.method != GNCDE_TSIT5 || s.controller != GNCDE_CTRL_PID || (s.flags & GNCDE_FLAG_GENERIC)) return false;
+  if (s.save_mode != GNCDE_SAVE_T1 && s.save_mode != GNCDE_SAVE_TS) return false;
+  Inst k;
+  const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
+  find_inst_t<false, true>(H, mode, k);
+  const int nb = (p.n + kRB - 1) / kRB;
+  return resident_blocks(k, rows_smem(p.n, H, p.L, false)) >= nb;
+}
+
+size_t rows_pid_scratch(const GncdeProblem& p) {
+  const int nb = (p.n + kRB - 1) / kRB;
+  return align_up((size_t)p.B * 2 * nb * 2 * sizeof(float), 256);
+}
+
+int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
+                       char* vf_ws, float* part, const float* csum, const void* coefT, const float* wperm,
+                       const float* bf, float* z0, float* z1, unsigned* sync, hipStream_t st) {
+  Inst k;
+  const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
+  if (!find_inst_t<false, true>(H, mode, k)) return GNCDE_ERR_UNSUPPORTED;
+  (void)vf_ws;
+  const size_t smem = rows_smem(p.n, H, p.L, false);
+  if (!ensure_dyn_lds(k.fn, smem)) return GNCDE_ERR_HIP;
+  const int nb = (p.n + kRB - 1) / kRB;
+  RowsArgs a{};
+  a.B = p.B;
+  a.n = p.n;
+  a.T = p.T;
+  a.L = p.L;
+  a.G = p.B;
+  a.rounds = 1;
+  a.nb = nb;
+  a.big = rows_big(p.n, H, false);
+  a.np = rows_np(p.n, false);
+  a.ts = p.ts;
+  a.coef = p.coef;
+  a.coefT = coefT;
+  a.csum = csum;
+  a.tcoef = p.tcoef;
+  a.data_coef = p.data_coef;
+  a.fusion = p.fusion;
+  a.wperm = wperm;
+  a.bf = bf;
+  a.zbuf[0] = z0;
+  a.zbuf[1] = z1;
+  a.bar = sync;                                   // [B] per-sample arrivals (zeroed by generic_vf_prepare)
+  a.fault = reinterpret_cast<int*>(sync + p.B);   // the workspace's fault word
+  a.ticket = sync + p.B + 1;
+  a.ticket0 = 0;
+  a.bar0 = 0;
+  a.spin_limit = spin_limit();
+  SolveArgs& v = a.s;
+  v.S = s.save_mode == GNCDE_SAVE_TS ? s.n_save : 0;
+  v.max_steps = s.max_steps;
+  v.auto_dt = s.dt0 == nullptr;
+  v.step_len = s.step_ts_len;
+  v.rtol = s.rtol;
+  v.atol = s.atol;
+  v.t0 = s.t0;
+  v.t1 = s.t1;
+  v.dt0 = s.dt0;
+  v.save_ts = s.save_ts;
+  v.y0 = y0;
+  v.ys = ys;
+  v.step_ts = s.step_ts;
+  v.stats = stats;
+  v.part = part;
+  k.launch(a, p.B * nb, smem, st);
+  return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+}
+
+void rows_pid_name(const GncdeProblem& p, char* buf, size_t len) {
+  snprintf(buf, len, "rows_pid<%d,%s>", p.dims[0], p.cde_hidden > 0 ? "cde" : "ode");
 }
 
 }  // namespace gncde

@@ -810,15 +810,10 @@ void launch_layer(const BwdArgs& a, int grid, size_t smem, hipStream_t st) {
 }
 
 bool set_smem(int H, size_t smem) {
-  static bool done[3] = {false, false, false};
-  const int k = H == 16 ? 0 : (H == 32 ? 1 : 2);
-  if (done[k] || smem <= 64 * 1024) return true;
   const void* fn = H == 16 ? reinterpret_cast<const void*>(&k_bwd_layer<16>)
                            : (H == 32 ? reinterpret_cast<const void*>(&k_bwd_layer<32>)
                                       : reinterpret_cast<const void*>(&k_bwd_layer<64>));
-  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) return false;
-  done[k] = true;
-  return true;
+  return ensure_dyn_lds(fn, smem);
 }
 
 }  // namespace
@@ -977,11 +972,8 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     if (H == 16) hipLaunchKernelGGL(k_bwd_readout<16>, dim3(w.ro_chunks, 1), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
     else if (H == 32) hipLaunchKernelGGL(k_bwd_readout<32>, dim3(w.ro_chunks, 2), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
     else {
-      static bool attr = false;  // 82 KB of LDS at H = 64
-      if (!attr && hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bwd_readout<64>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)rsm) != hipSuccess)
+      if (!ensure_dyn_lds(reinterpret_cast<const void*>(&k_bwd_readout<64>), rsm))  // 82 KB of LDS at H = 64
         return GNCDE_ERR_HIP;
-      attr = true;
       hipLaunchKernelGGL(k_bwd_readout<64>, dim3(w.ro_chunks, 4), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
     }
     if (gdata)
@@ -1004,7 +996,8 @@ void rows_vjp_finish(const GncdeProblem& p, char* ws, float* gparams, float* gfu
 
 }  // namespace gncde
 
-// Diagnostic (not part of include/gncde.h): one evaluation with the hidden outputs kept, for tests.
+#ifdef GNCDE_DIAG
+// Diagnostic builds only (-DGNCDE_DIAG; not part of include/gncde.h): one evaluation with the hidden outputs kept.
 extern "C" int gncde_diag_keep(const GncdeProblem* prob, const float* t, const float* y, float* dy, float* keep,
                                void* ws, size_t ws_bytes, void* stream) {
   using namespace gncde;
@@ -1067,3 +1060,4 @@ extern "C" size_t gncde_diag_vf_vjp_bytes(const GncdeProblem* prob) {
   }
   return align_up((wfs + bfs) * sizeof(float), 256) + rows_vjp_workspace(p) + generic_vf_workspace(p);
 }
+#endif  // GNCDE_DIAG

@@ -806,7 +806,8 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
     hipLaunchKernelGGL(v_batch_sum, dim3(cdiv((size_t)p.L * GNCDE_FC, 256)), dim3(256), 0, st, B,
                        (size_t)p.L * GNCDE_FC, w.gfc, gfusion);
   }
-  return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+  if (hipGetLastError() != hipSuccess) return GNCDE_ERR_HIP;
+  return rows_fault_status(p, vf_ws, st, rows_supported(p));  // the keep forwards ran one-launch evaluations
 }
 
 }  // namespace gncde

@@ -12,7 +12,7 @@ from ctypes import POINTER, c_char_p, c_float, c_int32, c_size_t, c_void_p
 
 MAX_LAYERS = 8
 FC = 24
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 RK4, TSIT5 = 0, 1
 CTRL_GRID, CTRL_PID = 0, 1

@@ -388,10 +388,20 @@ class WindowDataCfg:
         return cls(**{k: v for k, v in (d or {}).items() if k in names})
 
 
+def window_nodes(name: str) -> int:
+    """Nodes of the snapshot graphs ``synthetic_snapshots`` generates for a dataset name (england-covid: the 129
+    NHS regions; tgbn-trade: 255 countries)."""
+    if name.startswith("england"):
+        return 129
+    if name.startswith("tgbn-trade") or name.startswith("trade"):
+        return 255
+    raise NotImplementedError(f"dataset {name}: england-covid and tgbn-trade shapes are generated here")
+
+
 def synthetic_snapshots(name: str, rng: np.random.Generator, num_snapshots: int = 0):
     """Snapshot sequence (list of dicts adj [n,n], x, y, src) shaped like the reference's datasets."""
     if name.startswith("england"):
-        n, S, F = 129, num_snapshots or 61, 8
+        n, S, F = window_nodes(name), num_snapshots or 61, 8
         base = community_graph(n, int(rng.integers(1 << 30)))
         signal = np.abs(rng.standard_normal(n)) * 10.0
         hist = [signal.copy() for _ in range(F)]
@@ -406,7 +416,7 @@ def synthetic_snapshots(name: str, rng: np.random.Generator, num_snapshots: int 
             signal = nxt
         return snaps
     if name.startswith("tgbn-trade") or name.startswith("trade"):
-        n, S = 255, num_snapshots or 32
+        n, S = window_nodes(name), num_snapshots or 32
         pattern = rng.random((n, n)) < 0.08
         np.fill_diagonal(pattern, False)
         vol = rng.lognormal(2.0, 2.0, (n, n))

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import time
 
@@ -41,6 +42,18 @@ def _mse(pred, y, idx):
         return float("nan")
     sel = torch.as_tensor(idx, device=pred.device)
     return float(((pred[:, sel] - y[:, sel]) ** 2).mean())
+
+
+def _optimiser(cfg: dict) -> dict:
+    """The ``optimiser:`` block (optimiser_configs.py:53-88) as numbers.  The reference YAMLs write ``1e-4`` and
+    ``10e-2``, which YAML 1.1 (yaml.safe_load) reads as strings; optax receives them through pydantic's float
+    coercion, so they are floats here too."""
+    opt_cfg = cfg.get("optimiser", {})
+    sched = opt_cfg.get("schedule", {"name": "constant_schedule", "value": 1e-3})
+    if sched.get("name", "constant_schedule") != "constant_schedule":
+        raise NotImplementedError("only constant_schedule is wired (optimiser_configs.py)")
+    return {"learning_rate": float(sched.get("value", 1e-3)), "weight_decay": float(opt_cfg.get("weight_decay", 0.0)),
+            "gradient_clipping": bool(opt_cfg.get("gradient_clipping", True))}
 
 
 class Trainer:
@@ -71,6 +84,21 @@ class Trainer:
             with open(self.out, "a") as fh:
                 fh.write(line + "\n")
 
+    def describe(self) -> dict:
+        """What ``run`` would build from this config, derived from the YAML alone (no GPU, no data): nodes n
+        (grid: ceil(sqrt(num_nodes))^2, ode_dataset.py:56), hidden width h, layers L, data_embed_dim, the
+        optimiser numbers and the solve (graph_neural_cde.py:53-54,86,94-104)."""
+        m, vfc = self.model_cfg, self.model_cfg.get("vector_field", {})
+        dc = data.DynDataCfg.from_dict(self.cfg.get("dataset", {}))
+        n = int(math.ceil(math.sqrt(dc.num_nodes))) ** 2 if dc.graph_type == "grid" else int(dc.num_nodes)
+        h = int(m.get("hidden_dim", 16))
+        solve = ({"method": "tsit5", "controller": "pid", "rtol": 1e-3, "atol": 1e-6, "dt0": None}
+                 if self.steps_per_interval is None else
+                 {"method": "rk4", "controller": "grid", "steps_per_interval": self.steps_per_interval})
+        return {"model": "graph_neural_cde", "vector_field": vfc.get("name", "PermEquivGraphVectorField"), "n": n,
+                "h": h, "L": int(vfc.get("num_layers", 2)), "data_embed_dim": 1, "batch": int(dc.batch_size),
+                **_optimiser(self.cfg), "solve": solve}
+
     def build(self):
         torch.manual_seed(self.seed)
         ds = data.DynDataset(data.DynDataCfg.from_dict(self.cfg.get("dataset", {})))
@@ -87,13 +115,7 @@ class Trainer:
     def run(self) -> dict:
         ds, model = self.build()
         rank, world = train.dist_world()
-        opt_cfg = self.cfg.get("optimiser", {})
-        sched = opt_cfg.get("schedule", {"name": "constant_schedule", "value": 1e-3})
-        if sched.get("name", "constant_schedule") != "constant_schedule":
-            raise NotImplementedError("only constant_schedule is wired (optimiser_configs.py)")
-        opt = train.ClipAdamW(model, learning_rate=float(sched.get("value", 1e-3)),
-                              weight_decay=float(opt_cfg.get("weight_decay", 0.0)),
-                              gradient_clipping=bool(opt_cfg.get("gradient_clipping", True)))
+        opt = train.ClipAdamW(model, **_optimiser(self.cfg))
         # training control over the training knots (the reference's train_graph_path_coeffs), validation over all
         ts_tr, coef_tr, tcoef_tr = ds.graph_path(ds.id_train)
         ts_all, coef_all, tcoef_all = ds.graph_path(list(range(ds.t.shape[1])))
@@ -109,6 +131,8 @@ class Trainer:
         # accepted step counts (balanced_partition) when the ranks' work differs by more than 10 %.
         def shard(own):
             st = dict(own=list(own))
+            if not own:  # more ranks than samples: this rank contributes a zero gradient and zero sums
+                return st
             st["prob"] = prob_tr_all.take(own) if world > 1 else prob_tr_all
             st["x0"] = ds.x0[torch.as_tensor(own, device=ds.x0.device)] if world > 1 else ds.x0
             st["y"] = y_tr_all[torch.as_tensor(own, device=y_tr_all.device)] if world > 1 else y_tr_all
@@ -121,12 +145,17 @@ class Trainer:
         sh = shard(parts[rank])
 
         def loss_terms():
+            if not sh["own"]:
+                return sum(p.sum() * 0.0 for p in model.parameters()), 0
             pred = model.predict_packed(sh["prob"], sh["x0"], sh["spec"]).squeeze(-1)
             return ((pred - sh["y"]) ** 2).sum(), pred.numel()
 
         def validate():
             """interpolation / extrapolation MSE over all samples (each rank its own, summed over ranks)."""
             own = sh["own"]
+            if not own:
+                v_s, v_c, e_s, e_c = train.all_reduce_sum([0.0, 0.0, 0.0, 0.0], ds.x0.device)
+                return (v_s / v_c if v_c else float("nan")), (e_s / e_c if e_c else float("nan"))
             with torch.no_grad():
                 pa = prob_all_full.take(own) if world > 1 else prob_all_full
                 pred = model.forward_packed(pa, sh["x0"], pa.ts).squeeze(-1)  # PID, SaveAt(ts)
@@ -137,7 +166,7 @@ class Trainer:
                     sel = torch.as_tensor(ids, device=pred.device)
                     sums += [float(((pred[:, sel] - yt[:, sel]) ** 2).sum()), pred[:, sel].numel()]
                 else:
-                    sums += [float("nan"), 0.0]
+                    sums += [0.0, 0.0]
             v_s, v_c, e_s, e_c = train.all_reduce_sum(sums, pred.device)
             return (v_s / v_c if v_c else float("nan")), (e_s / e_c if e_c else float("nan"))
 
@@ -150,7 +179,7 @@ class Trainer:
             torch.cuda.synchronize()
             step_time = time.time() - t0
             if adaptive and world > 1:
-                steps = sh["spec"].stats_out[:, _lib.STAT_STEPS].tolist()
+                steps = sh["spec"].stats_out[:, _lib.STAT_STEPS].tolist() if sh["own"] else []
                 costs = train.global_costs(sh["own"], steps, B, ds.x0.device)
                 loads = [sum(costs[i] for i in p) for p in parts]
                 if max(loads) > 1.1 * max(min(loads), 1.0):
@@ -205,6 +234,27 @@ class WindowTrainer:
 
     _log = Trainer._log
 
+    def describe(self) -> dict:
+        """As Trainer.describe for the PGT / TGB drivers (pgt_graph_neural_cde.py:119-129: ConstantStepSize 0.1;
+        tgb_graph_neural_cde.py:152-162: 0.01, or the build-only ``solver: pid``)."""
+        from .models import PGTGraphNeuralCDE, TGBGraphNeuralCDE
+        import inspect
+        m, vfc = self.model_cfg, self.model_cfg.get("vector_field", {})
+        dc = data.WindowDataCfg.from_dict(self.cfg.get("dataset", {}))
+        n = data.window_nodes(dc.name)
+        if "num_nodes" in vfc and int(vfc["num_nodes"]) != n:
+            raise ValueError(f"vector_field.num_nodes {vfc['num_nodes']} != the {dc.name} graph's {n} nodes")
+        h = int(m.get("hidden_dim", 32))
+        cls = TGBGraphNeuralCDE if self.tgb else PGTGraphNeuralCDE
+        dt0 = inspect.signature(cls.__init__).parameters["dt0"].default
+        solve = {"method": "tsit5", "controller": "constant", "dt0": dt0}
+        if self.tgb and m.get("solver") == "pid":
+            solve = {"method": "tsit5", "controller": "pid", "rtol": 1e-3, "atol": 1e-6, "dt0": None}
+        return {"model": self.model_cfg.get("name"), "vector_field": vfc.get("name", "PermEquivGraphVectorField"),
+                "n": n, "h": h, "L": int(vfc.get("num_layers", 2)), "data_embed_dim": int(vfc.get("data_embed_dim", 8)),
+                "window_size": int(dc.window_size), "windows_per_step": self.window_batch, **_optimiser(self.cfg),
+                "solve": solve, "compute": m.get("compute", "fp32")}
+
     def build(self):
         from .models import PGTGraphNeuralCDE, TGBGraphNeuralCDE
         torch.manual_seed(self.seed)
@@ -255,19 +305,19 @@ class WindowTrainer:
     def run(self) -> dict:
         from safetensors.torch import save_file
         ds, model = self.build()
-        opt_cfg = self.cfg.get("optimiser", {})
-        sched = opt_cfg.get("schedule", {"name": "constant_schedule", "value": 1e-3})
-        if sched.get("name", "constant_schedule") != "constant_schedule":
-            raise NotImplementedError("only constant_schedule is wired (optimiser_configs.py)")
-        opt = train.ClipAdamW(model, learning_rate=float(sched.get("value", 1e-3)),
-                              weight_decay=float(opt_cfg.get("weight_decay", 0.0)),
-                              gradient_clipping=bool(opt_cfg.get("gradient_clipping", True)))
+        opt = train.ClipAdamW(model, **_optimiser(self.cfg))
         # Data parallelism: each optimiser step takes `window_batch` windows (at least one per rank),
         # split over the ranks (balanced_partition by the windows' costs: the adaptive TGB solve's accepted step
         # counts from the previous epoch, else equal), with one gradient all-reduce per step (train.make_step
         # normalises by the global element count).
         rank, world = train.dist_world()
-        wb = max(self.window_batch, world)
+        # the global window batch stays --window-batch (the same training as one GPU): with fewer windows per step
+        # than ranks the surplus ranks contribute zero gradients every step
+        wb = self.window_batch
+        if wb < world and rank == 0:
+            import warnings
+            warnings.warn(f"--window-batch {wb} < world size {world}: {world - wb} of {world} ranks idle every "
+                          "optimiser step (pass --window-batch >= world to use them)", stacklevel=2)
         chunks = self._chunks(list(ds.train), wb)
         cost = {w: 1.0 for w in ds.train}
 
@@ -327,7 +377,8 @@ class WindowTrainer:
                     if self.patience > 0 and bad * self.eval_freq >= self.patience and epoch > self.min_epochs:
                         break
         key = "best_validation_ndcg@10" if self.tgb else "best_validation_loss"
-        res = {key: best_val, "corr_test_loss": test_loss, "best_epoch": best_epoch, "checkpoint": ckpt}
+        res = {key: best_val, "corr_test_loss": test_loss, "best_epoch": best_epoch, "checkpoint": ckpt,
+               "windows_per_step": wb}
         if self.tgb:
             res["corr_test_ndcg"] = test_ndcg
         self._log(res)
@@ -348,6 +399,20 @@ def init_distributed():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         dist.init_process_group(backend)
+
+
+def single_run(default_config: str, argv=None):
+    """The body of the ``src/run/{dyn,pgt,tgb}/single_run.py`` shims: the reference's hard-coded YAML path (relative
+    to the working directory, as in the reference, e.g. src/run/dyn/single_run.py:23-24) unless ``--config`` is
+    given; every other flag of ``main`` passes through."""
+    import sys
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not any(a == "--config" or a.startswith("--config=") for a in argv):
+        if not os.path.exists(default_config):
+            raise SystemExit(f"{default_config} not found (run from the directory holding configs/, as the "
+                             "reference's single_run.py expects, or pass --config <yaml>)")
+        argv = ["--config", default_config] + argv
+    return main(argv)
 
 
 def main(argv=None):

@@ -1,0 +1,267 @@
+"""GPU parity at BASELINE configs 3 and 5's exact shapes, against the fp64 oracle (oracle/gncde_oracle*.py).
+
+* Config 3 (PGT England, pgt_graph_neural_cde.py:119-129): undirected fusion, n = 129, dims [64, 64, 64, 1024], de = 8,
+  L = 3, ts = 0..3, Tsit5 + ConstantStepSize(0.1) -> 30 steps on the generic path, B = 64.  Every step state of two
+  samples of the batch against the oracle's trajectory (RTOL_SOLVE), and the discrete adjoint of those two samples
+  (the other 62 carry a zero cotangent) against the oracle's (RTOL_GRAD).
+* Config 5 (TGB trade, tgb_graph_neural_cde.py:152-162 with BASELINE's adaptive controller): n = 255, h = 32, L = 4,
+  de = 8 (d_L = 512), Tsit5 + PIDController(1e-3, 1e-6) from dt0 = 0.01 on [0, 1], B = 16.  The GPU records its
+  accepted steps (GncdeSolver.step_ts); two samples' steps are replayed in the oracle (RTOL_SOLVE).
+
+Inputs are drawn with numpy (oracle.make_graph_control: a dynamic graph's normalised-Laplacian path, node data from
+a standard normal) so the oracle sees exactly what the GPU reads.  Samples whose gradient moves under a 1e-6
+relative change of y0 (a ReLU pre-activation within fp32 reach of its kink) are skipped for the gradient check
+(the test fails if fewer than two stable samples exist among the candidates).
+"""
+import dataclasses
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gncde_oracle as O
+from oracle import gncde_oracle_grad as OG
+
+pytestmark = pytest.mark.gpu
+
+RTOL_SOLVE = 1e-4
+RTOL_GRAD = 5e-4
+
+
+def rel_err(x, ref):
+    x, ref = np.asarray(x, np.float64), np.asarray(ref, np.float64)
+    return float(np.max(np.abs(x - ref)) / max(np.max(np.abs(ref)), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def G():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    import gncde
+    gncde._lib.load()
+    return gncde
+
+
+def cde_inputs(seed, B, n, T, t1, H, de, L, kind="undirected", scale=1.0, distinct=None):
+    """numpy inputs of a CDE-wrapper problem (operator spline, data spline, parameters, y0).  ``distinct``: draw
+    that many windows and cycle them over the batch (config 3's 49 England windows cycled to B = 64); every sample
+    keeps its own y0."""
+    rng = np.random.default_rng(seed)
+    ts_all, co_all, dco = [], [], []
+    for _ in range(distinct or B):
+        ts, X = O.make_graph_control(rng, n, T, t0=0.0, t1=t1, irregular=False)
+        ts_all.append(ts)
+        co_all.append(O.backward_hermite_coefficients(ts, X))
+        x = rng.standard_normal((T, n, de))
+        Xd = np.stack([np.broadcast_to(ts[:, None, None], x.shape), x], axis=-1)
+        dco.append(O.backward_hermite_coefficients(ts, Xd))
+    P = O.init_vf_params(rng, kind, [H] * L + [2 * H * de])
+    for lay in P.layers:
+        for nm in OG.FUSION_NAMES[kind]:
+            lay[nm] = lay[nm] * scale
+    cyc = [b % len(ts_all) for b in range(B)]
+    ts_all, co_all, dco = [ts_all[i] for i in cyc], [co_all[i] for i in cyc], [dco[i] for i in cyc]
+    ts = np.stack(ts_all)
+    coeffs = tuple(np.stack([c[q] for c in co_all]) for q in range(4))
+    dcoeffs = tuple(np.stack([c[q] for c in dco]) for q in range(4))
+    y0 = rng.standard_normal((B, n, H))
+    return rng, ts, coeffs, dcoeffs, dco, P, y0
+
+
+def oracle_fns(ts, coeffs, dco, P, H, de, b):
+    ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
+    cx = O.CubicInterpolation(ts[b], dco[b])
+    f = lambda t, y: O.cde_wrapper(P, H, de, t, y, ctrl, cx)  # noqa: E731
+    fv = lambda t, y, g: OG.cde_wrapper_vjp(P, H, de, t, y, ctrl, cx, g)  # noqa: E731
+    return f, fv
+
+
+def test_config3_exact_shape_trajectory_and_gradient(G):
+    B, n, T, H, de, L = 64, 129, 4, 64, 8, 3
+    rng, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(31, B, n, T, 3.0, H, de, L, scale=3.0, distinct=10)
+    prob = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
+    grids = [O.constant_grid(0.0, 3.0, 0.1)] * B
+    assert len(grids[0]) == 31
+    grid, ns = G.layout.stack_grids(grids)
+    spec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS, grid=grid, nsteps=ns)
+    assert G.integrate_path(prob, spec) == "generic"
+    ys, st = G.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda"), stats=True)
+    st = st.cpu().numpy()
+    assert np.all(st[:, 0] == 30) and np.all(st[:, 2] == 181) and np.all(st[:, 3] == 0)
+    # candidates spread over the batch; the first two whose oracle gradient is kink-stable are checked
+    gfin = np.zeros((B, n, H))
+    chosen, refs = [], []
+    for b in (5, 40, 63, 17, 28, 51):  # windows 5, 0, 3, 7, 8, 1
+        f, fv = oracle_fns(ts, coeffs, dco, P, H, de, b)
+        g = rng.standard_normal((n, H))
+        g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g)
+        g1, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b] * (1 + 1e-6), "tsit5", g_final=g)
+        if np.max(np.abs(g1 - g0)) > 1e-5 * np.max(np.abs(g0)):
+            print(f"  sample {b}: gradient not kink-stable, skipped")
+            continue
+        traj, _ = O.solve_fixed_grid(f, grids[b], y0[b], "tsit5", save_every_step=True, time_dtype=np.float32)
+        err = rel_err(ys[b].cpu().numpy(), traj)
+        per_step = max(rel_err(ys[b, k].cpu().numpy(), traj[k]) for k in range(1, 31))
+        print(f"  config 3 sample {b}: trajectory vs oracle {err:.2e} (worst step-relative {per_step:.2e})")
+        assert err <= RTOL_SOLVE
+        gfin[b] = g
+        chosen.append(b)
+        refs.append((g0, gr))
+        if len(chosen) == 2:
+            break
+    assert len(chosen) == 2, "fewer than two kink-stable samples among the candidates"
+    spec.save_mode = G._lib.SAVE_T1
+    gy0, gp, gf = G.integrate_vjp(prob, spec, ys, torch.tensor(gfin, dtype=torch.float32, device="cuda"))
+    total = OG._acc(OG._acc(None, refs[0][1]), refs[1][1])
+    errs = {f"gy0[{b}]": rel_err(gy0[b].cpu().numpy(), r[0]) for b, r in zip(chosen, refs)}
+    others = [b for b in range(B) if b not in chosen]
+    assert float(gy0[others].abs().max()) == 0.0  # zero cotangent -> exactly zero adjoint
+    gp = gp.cpu().numpy()
+    off = 0
+    for l in range(L):
+        for k in ("rms_w", "rms_b", "W", "b"):
+            sz = total[l][k].size
+            errs[f"{k}{l}"] = rel_err(gp[off:off + sz].reshape(total[l][k].shape), total[l][k])
+            off += sz
+    names, _, M = G.layout.fusion_map(P.kind, n)
+    ref_f = np.stack([np.concatenate([total[l][nm] for nm in names]) for l in range(L)])
+    errs["fusion"] = rel_err(gf.double().cpu().numpy() @ M.numpy().T, ref_f)
+    worst = max(errs, key=errs.get)
+    print(f"  config 3 gradient of samples {chosen}: worst {worst} {errs[worst]:.2e}")
+    for k, e in errs.items():
+        assert e <= RTOL_GRAD, (k, e)
+
+
+def test_config5_exact_shape_pid_replay(G):
+    B, n, T, H, de, L = 16, 255, 3, 32, 8, 4
+    _, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(55, B, n, T, 1.0, H, de, L)
+    prob = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
+    tsd = torch.tensor(ts, dtype=torch.float32, device="cuda")
+    rec = torch.empty(B, 4097, device="cuda")
+    spec = G.SolverSpec(method=G._lib.TSIT5, controller=G._lib.CTRL_PID, save_mode=G._lib.SAVE_T1, rtol=1e-3,
+                        atol=1e-6, t0=tsd[:, 0].contiguous(), t1=tsd[:, -1].contiguous(),
+                        dt0=torch.full((B,), 0.01, device="cuda"), step_ts=rec)
+    path = G.integrate_path(prob, spec)
+    assert path == "rows_pid<32,cde>"  # the persistent solve: the whole controller loop in one launch
+    ys, st = G.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda"), stats=True)
+    st = st.cpu().numpy()
+    print(f"  config 5 [{path}]: steps {st[:, 0].tolist()} rejects {st[:, 1].tolist()}")
+    assert np.all(st[:, 3] == 0)
+    assert np.all(st[:, 2] == 1 + 6 * (st[:, 0] + st[:, 1]))
+    for b in (3, 12):
+        f, _ = oracle_fns(ts, coeffs, dco, P, H, de, b)
+        grid = rec[b, :st[b, 0] + 1].cpu().numpy().astype(np.float64)
+        assert grid[0] == 0.0 and grid[-1] == 1.0 and np.all(np.diff(grid) > 0)
+        ref = OG.solve_grid_dense(f, grid, y0[b], ts[b, -1:], time_dtype=np.float32)
+        err = rel_err(ys[b].cpu().numpy()[None], ref)
+        print(f"  config 5 sample {b}: replay of {st[b, 0]} accepted steps in the oracle {err:.2e}")
+        assert err <= RTOL_SOLVE
+
+
+def _config5(G, B, seed=55):
+    from gncde import synthetic
+    prob, y0 = synthetic.cde_batch(B, 255, 3, 32, 8, 4, 1.0, seed=seed)
+    spec = G.SolverSpec(method=G._lib.TSIT5, controller=G._lib.CTRL_PID, save_mode=G._lib.SAVE_T1, rtol=1e-3,
+                        atol=1e-6, t0=prob.ts[:, 0].contiguous(), t1=prob.ts[:, -1].contiguous(),
+                        dt0=torch.full((B,), 0.01, device="cuda"))
+    return prob, y0, spec
+
+
+def test_rows_pid_against_host_paced(G):
+    """The persistent solve and the host-paced controller (gncde_pid.hip: one evaluation launch + one k_pid_advance
+    launch per stage, GNCDE_FLAG_GENERIC) take the same decisions up to the last bits of the error norm's summation
+    order: equal evaluation bookkeeping, accepted steps within 25 %, and outputs within the solver tolerance."""
+    prob, y0, spec = _config5(G, 16)
+    ys, st = G.integrate(prob, spec, y0, stats=True)
+    gspec = dataclasses.replace(spec, flags=G._lib.FLAG_GENERIC)
+    assert G.integrate_path(prob, gspec) == "generic_rows"
+    yg, sg = G.integrate(prob, gspec, y0, stats=True)
+    st, sg = st.cpu().numpy(), sg.cpu().numpy()
+    print(f"  persistent steps {st[:, 0].tolist()} rejects {st[:, 1].tolist()}; host-paced steps "
+          f"{sg[:, 0].tolist()} rejects {sg[:, 1].tolist()}")
+    assert np.all(st[:, 3] == 0) and np.all(sg[:, 3] == 0)
+    assert np.all(st[:, 2] == 1 + 6 * (st[:, 0] + st[:, 1]))
+    assert np.all(np.abs(st[:, 0] - sg[:, 0]) <= 0.25 * sg[:, 0])
+    err = rel_err(ys.cpu().numpy(), yg.cpu().numpy())
+    print(f"  persistent vs host-paced outputs: {err:.2e}")
+    assert err <= 2e-2
+
+
+def test_rows_pid_batch_independent(G):
+    """A sample's solve is the same computation whatever the batch: at B = 64 (more groups than the chip holds at
+    once: later samples' workgroups start as earlier solves finish, taking start-order tickets) every sample's
+    output, step counts and step record equal, bitwise, those of the same sample solved in a batch of 16 and of a
+    solve of that sample alone; and repeated runs are bitwise equal."""
+    prob, y0, spec = _config5(G, 64, seed=56)
+    rec = torch.zeros(64, 256, device="cuda")
+    ys, st = G.integrate(prob, dataclasses.replace(spec, step_ts=rec), y0, stats=True)
+    ys2, st2 = G.integrate(prob, spec, y0, stats=True)
+    assert torch.equal(ys, ys2) and torch.equal(st, st2)
+    assert torch.all(st[:, 3] == 0)
+    idx = list(range(40, 56))
+    sub = prob.take(idx)
+    sspec = dataclasses.replace(spec, t0=spec.t0[idx].contiguous(), t1=spec.t1[idx].contiguous(),
+                                dt0=spec.dt0[idx].contiguous(), step_ts=torch.zeros(16, 256, device="cuda"))
+    ys16, st16 = G.integrate(sub, sspec, y0[idx].contiguous(), stats=True)
+    assert torch.equal(ys16, ys[idx]) and torch.equal(st16, st[idx]) and torch.equal(sspec.step_ts, rec[idx])
+    one = prob.take([47])
+    ospec = dataclasses.replace(spec, t0=spec.t0[47:48].contiguous(), t1=spec.t1[47:48].contiguous(),
+                                dt0=spec.dt0[47:48].contiguous())
+    assert torch.equal(G.integrate(one, ospec, y0[47:48].contiguous()), ys[47:48])
+
+
+def test_rows_eval_largest_resident_batch(G):
+    """The one-evaluation-per-launch kernel (fixed grids, and the keep forwards of the reverse mode) needs every
+    sample's group co-resident; its grid is sized from the occupancy query capped by the SGPR file, with one
+    workgroup per CU of margin.  At config 5's shape the largest batch it admits runs with status 0 and matches the
+    oracle on one evaluation; one sample more takes the multi-kernel path."""
+    from gncde import layout
+    prob, _, _ = _config5(G, 64)
+
+    def admitted(b):  # (path queries are host-only)
+        g, n_ = layout.stack_grids([layout.constant_step_grid(0.0, 1.0, 0.25)] * b)
+        sp = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=g, nsteps=n_)
+        return G.integrate_path(prob.shard(0, b), sp) == "generic_rows"
+    lo, hi = 1, 64
+    assert admitted(lo) and not admitted(hi)
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        lo, hi = (mid, hi) if admitted(mid) else (lo, mid)
+    bmax = lo
+    print(f"  config 5 shape: one-launch evaluation admits B <= {bmax}")
+    _, ts, coeffs, dcoeffs, dco, P, yn = cde_inputs(57, bmax, 255, 3, 1.0, 32, 8, 4, distinct=4)
+    probm = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=32, cde_embed=8)
+    g, n_ = layout.stack_grids([layout.constant_step_grid(0.0, 1.0, 0.25)] * bmax)
+    sp = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=g, nsteps=n_)
+    assert G.integrate_path(probm, sp) == "generic_rows"
+    ysm, stm = G.integrate(probm, sp, torch.tensor(yn, dtype=torch.float32, device="cuda"), stats=True)
+    assert torch.all(stm[:, 3] == 0)
+    t = torch.full((bmax,), 0.37, device="cuda")
+    dy = G.vf_eval(probm, t, torch.tensor(yn, dtype=torch.float32, device="cuda")).cpu().numpy()
+    for b in (0, bmax - 1):
+        f, _ = oracle_fns(ts, coeffs, dco, P, 32, 8, b)
+        err = rel_err(dy[b], f(0.37, yn[b]))
+        print(f"  sample {b}: one evaluation vs oracle {err:.2e}")
+        assert err <= 2e-5
+
+
+def test_barrier_fault_is_reported(G, monkeypatch):
+    """A one-launch evaluation whose group barrier gives up returns GNCDE_ERR_BARRIER (6) from the call instead of
+    results it knows are invalid: the persistent solve, the fixed-grid forward and the reverse sweep.  The fault is
+    forced by a zero poll budget (GNCDE_DEBUG_BARRIER_SPINS=0: a wait that has to poll even once gives up)."""
+    from gncde import layout
+    prob, y0, spec = _config5(G, 16)
+    grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, 1.0, 0.1)] * 16)
+    fspec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS, grid=grid, nsteps=ns)
+    ys_ok = G.integrate(prob, fspec, y0)  # (the reverse sweep's checkpoints, computed with the default budget)
+    monkeypatch.setenv("GNCDE_DEBUG_BARRIER_SPINS", "0")
+    with pytest.raises(G._lib.GncdeError, match="gncde error 6"):
+        G.integrate(prob, spec, y0)
+    with pytest.raises(G._lib.GncdeError, match="gncde error 6"):
+        G.integrate(prob, fspec, y0)
+    with pytest.raises(G._lib.GncdeError, match="gncde error 6"):
+        G.integrate_vjp(prob, dataclasses.replace(fspec, save_mode=G._lib.SAVE_T1), ys_ok, torch.ones_like(y0))
+    monkeypatch.delenv("GNCDE_DEBUG_BARRIER_SPINS")
+    _, st = G.integrate(prob, spec, y0, stats=True)  # the next solve starts clean
+    assert torch.all(st[:, 3] == 0)

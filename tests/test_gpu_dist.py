@@ -139,7 +139,7 @@ def _run_trainer(kind, cfg):
     train.reduce_gradients = reduce_keep
     train.balanced_partition = bp
     try:
-        if kind in ("dyn", "dyn_rk4"):
+        if kind.startswith("dyn"):
             spi = None if kind == "dyn" else 2
             res = run.Trainer(cfg, epochs=3, steps_per_interval=spi).run()["best_validation_loss"]
         else:
@@ -151,7 +151,7 @@ def _run_trainer(kind, cfg):
     return res, captured["opt"].flat.detach().cpu(), captured["grads"][0], captured["parts"]
 
 
-@pytest.mark.parametrize("kind", ["dyn", "dyn_rk4", "pgt"])
+@pytest.mark.parametrize("kind", ["dyn", "dyn_rk4", "dyn_rk4_b1", "pgt"])
 def test_two_rank_trainers_equal_single_process(tmp_path, kind):
     """gncde.run's trainers in data-parallel mode: the dyn Trainer shards its samples and the PGT
     WindowTrainer splits each step's windows over two gloo ranks sharing the GPU.
@@ -166,7 +166,10 @@ def test_two_rank_trainers_equal_single_process(tmp_path, kind):
       decisions are discontinuous in them: a sample may take a different (equally valid, rtol-accurate) step
       sequence, which moves its gradient by ~rtol.  So parameters are held to Adam's per-step bound (|update| <=
       lr, 3 steps) and the metric to 5 %; tools/diag_partition.py checks that the gradient is additive over any
-      partition of the samples at fixed parameters (measured 5e-8 .. 9e-8)."""
+      partition of the samples at fixed parameters (measured 5e-8 .. 9e-8).
+    * ``dyn_rk4_b1``: one sample on two ranks (the reference dyn YAML's batch_size 4 on 8 GPUs is the same case):
+      the rank without samples contributes a zero gradient and zero validation sums, and the run equals the
+      single process's."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a HIP device")
     import yaml
@@ -178,7 +181,7 @@ def test_two_rank_trainers_equal_single_process(tmp_path, kind):
         cfg["dataset"]["num_snapshots"] = 26
         cfg["eval_freq"] = 2
     else:
-        cfg["dataset"].update(num_nodes=16, time_tick=16, batch_size=5)
+        cfg["dataset"].update(num_nodes=16, time_tick=16, batch_size=1 if kind.endswith("_b1") else 5)
         cfg["eval_freq"] = 3
     cfg["checkpoint_dir"] = str(tmp_path)
     ref_metric, ref, ref_g1, _ = _run_trainer(kind, cfg)

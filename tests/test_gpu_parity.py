@@ -253,7 +253,8 @@ def test_pid_cde8_matches_golden(gncde, golden_dir, name, compute, save):
     prob = problem_from(G, z, params, data=True).with_compute(compute)
     ts = torch.tensor(z["ts"], dtype=torch.float32, device="cuda")
     spec = pid_spec(G, ts, z, save)
-    assert G.integrate_path(prob, spec) == ("generic" if compute == "fp32" else "generic_bf16")
+    # fp32: the persistent solve (the whole Tsit5 + PID loop in one launch, gncde_rows.hip)
+    assert G.integrate_path(prob, spec) == (f"rows_pid<{int(z['h'])},cde>" if compute == "fp32" else "generic_bf16")
     ys, st = G.integrate(prob, spec, torch.tensor(z["y0"], dtype=torch.float32, device="cuda"), stats=True)
     st = st.cpu().numpy()
     sel = (lambda x: x) if save == "ts" else (lambda x: x[:, -1])
@@ -284,7 +285,7 @@ def test_config5_pid_full_size(gncde, compute):
     prob32, y0 = synthetic.cde_batch(B, n, 3, 32, 8, 4, 1.0, seed=55)
     prob = prob32.with_compute(compute)
     spec = pid_spec(G, prob.ts, dt0=0.01)
-    assert G.integrate_path(prob, spec) == ("generic" if compute == "fp32" else "generic_bf16")
+    assert G.integrate_path(prob, spec) == ("rows_pid<32,cde>" if compute == "fp32" else "generic_bf16")
     ys1, st1 = G.integrate(prob, spec, y0, stats=True)
     ys2, st2 = G.integrate(prob, spec, y0, stats=True)
     assert torch.equal(ys1, ys2) and torch.equal(st1, st2)
@@ -422,7 +423,7 @@ def test_generic_cde_full_size_properties(gncde, B, n, T, h, L, t1, dt):
     err_vf = rel_err(dyP.cpu().numpy(), dy[:, P].cpu().numpy())
     grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, t1, dt)] * B)
     spec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=grid, nsteps=ns)
-    assert G.integrate_path(prob, spec) == "generic"
+    assert G.integrate_path(prob, spec) == ("generic" if h == 64 else "generic_rows")
     ys1 = G.integrate(prob, spec, y0)
     ys2 = G.integrate(prob, spec, y0)
     assert torch.equal(ys1, ys2)
@@ -503,7 +504,7 @@ def test_generic_cde_fixed_grid_solve_vs_oracle(gncde, method):
     grid, ns = layout.stack_grids(grids)
     spec = gncde.SolverSpec(method=gncde._lib.RK4 if method == "rk4" else gncde._lib.TSIT5,
                             save_mode=gncde._lib.SAVE_STEPS, grid=grid, nsteps=ns)
-    assert gncde.integrate_path(prob, spec) == "generic"
+    assert gncde.integrate_path(prob, spec) == "generic_rows"
     ys = gncde.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda")).cpu().numpy()
     for b in range(B):
         ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
