@@ -133,12 +133,18 @@ def cpu_baseline(prob, spec, y0, layers, target_s):
         _, nev = c_oracle.rk4(ts, coef, tcoef, lay, grid, ns, yy, nthreads=threads)
         return nev, time.perf_counter() - t0
 
+    model = "unknown"
+    try:  # the host CPU the baseline ran on (/proc/cpuinfo "model name")
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), model)
+    except OSError:
+        pass
     c_oracle.load()
     nev1, dt1 = run(1)  # calibration (1 sample, 1 thread busy)
     nb = int(max(threads, min(prob.B, math.ceil(target_s / max(dt1, 1e-6)) * threads)))
     nb = min(nb, prob.B)
     nev, dt = run(nb)
-    return {"value": nev / dt, "unit": "sample-evals/s", "cores": threads, "kind": "port",
+    return {"value": nev / dt, "unit": "sample-evals/s", "cores": threads, "cpu_model": model, "kind": "port",
             "sample": f"{nb} of the {prob.B} samples, full 100-step RK4 solve each ({nev} VF evals, "
                       f"{dt:.1f} s, oracle/gncde_oracle.c fp32, literal reference fusion, OpenMP)"}
 

@@ -101,7 +101,8 @@ enum { GNCDE_RK4 = 0, GNCDE_TSIT5 = 1 };
  *                 from the fp32 values and fp32 accumulation (~2^-8 relative per operand: a genuinely bf16 solve, the
  *                 throughput mode of config 5).  Only the one-launch evaluation runs it (gncde_rows.hip: n <= 256,
  *                 one hidden width H in {16, 32, 64}, ODE output or the de = 8 read-out); other shapes return
- *                 GNCDE_ERR_UNSUPPORTED.
+ *                 GNCDE_ERR_UNSUPPORTED, and so does the PID controller (its error estimate reads the mode's
+ *                 ~1e-2 per-stage rounding noise as truncation error and takes 12-21x the steps): fixed grids only.
  * Splines, reductions, RMSNorm, solver and epilogues stay fp32.  The bf16 modes always take the generic path.
  * Their reverse mode (gncde_integrate_vjp*) is the fp32 discrete adjoint over the coefficients the forward read
  * (BF16_STORAGE: the bf16 planes widened exactly into the workspace head, which gncde_vjp_workspace_bytes

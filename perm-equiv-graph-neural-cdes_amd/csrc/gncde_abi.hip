@@ -51,6 +51,10 @@ int validate_solver(const GncdeProblem* p, const GncdeSolver* s) {
     if (s->stage_rec && (s->stage_rec_len <= 0 || (size_t)s->stage_rec_len != record_floats(*p, *s)))
       return GNCDE_ERR_ARG;
   } else if (s->controller == GNCDE_CTRL_PID) {
+    // the single-plane bf16 mode puts ~1e-2 relative noise into every stage, which the embedded error estimate
+    // reads as truncation error: at rtol 1e-3 the controller takes 12-21x the evaluations, so
+    // the mode is for fixed grids (ConstantStepSize, the reference's own PGT / TGB solves) only
+    if (p->compute == GNCDE_COMPUTE_BF16_MFMA) return GNCDE_ERR_UNSUPPORTED;
     if (!s->t0 || !s->t1 || s->max_steps < 1) return GNCDE_ERR_ARG;
     if (!(s->rtol >= 0.f) || !(s->atol > 0.f)) return GNCDE_ERR_ARG;
     if (s->save_mode == GNCDE_SAVE_STEPS) return GNCDE_ERR_UNSUPPORTED;

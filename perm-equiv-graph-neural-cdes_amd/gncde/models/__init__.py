@@ -257,7 +257,8 @@ class TGBGraphNeuralCDE(nn.Module):
     step count of the latest forward (the data-parallel trainer balances ranks by it).
 
     ``compute`` (build extension): the solve's arithmetic, engine.COMPUTE_MODES — "bf16_mfma" is config 5's
-    single-plane bf16 MFMA mode (bf16 coefficients, every product on bf16 operands; include/gncde.h)."""
+    single-plane bf16 MFMA mode (bf16 coefficients, every product on bf16 operands; include/gncde.h), refused with
+    ``solver="pid"``."""
 
     def __init__(self, cfg, vector_field, interpolation="cubic", model_key=None, dt0=0.01, solver=None,
                  compute="fp32", **kwargs):
@@ -280,6 +281,10 @@ class TGBGraphNeuralCDE(nn.Module):
         self.adaptive = solver == "pid"
         if compute not in engine.COMPUTE_MODES:
             raise ValueError(f"compute {compute!r}: one of {sorted(engine.COMPUTE_MODES)}")
+        if self.adaptive and compute == "bf16_mfma":
+            raise ValueError("compute 'bf16_mfma' with solver 'pid': the single-plane bf16 rounding noise makes the "
+                             "PID controller take 12-21x the steps (gncde.h GNCDE_COMPUTE_BF16_MFMA); use it with "
+                             "the ConstantStepSize solve, or compute 'bf16' (split products) under PID")
         self.compute = compute
         self.last_steps = None
 

@@ -35,8 +35,9 @@ def test_dyn_single_run_small(tmp_path, spi):
     assert losses[-1] < losses[0]
 
 
-# config 5's bf16 MFMA mode needs the one-launch evaluation's shapes: h = 16 = the hidden width, de = 8
-BF16M_TGB = {"solver": "pid", "compute": "bf16_mfma", "hidden_dim": 16,
+# config 5's bf16 MFMA mode needs the one-launch evaluation's shapes (h = 16 = the hidden width, de = 8) and a fixed
+# grid (the reference's own ConstantStepSize TGB solve; the PID controller refuses the mode)
+BF16M_TGB = {"compute": "bf16_mfma", "hidden_dim": 16,
              "vector_field": {"name": "PermEquivGraphVectorField", "hidden_dim": 16, "num_layers": 2, "data_embed_dim": 8}}
 
 
@@ -48,7 +49,7 @@ def test_window_single_run_small(tmp_path, config, metric, model):
     """trainer_pgt / trainer_tgb flow: windows -> one optimiser step per window -> validation (MSE / NDCG@10)
     -> checkpoint -> test metrics of the best model.  solver "pid": the TGB model on BASELINE config 5's adaptive
     Tsit5 + PIDController (build-only `model.solver: pid`), trained through the reverse mode on the accepted steps;
-    with `model.compute: bf16_mfma`, its forward solves in the single-plane bf16 mode."""
+    with `model.compute: bf16_mfma`, the ConstantStepSize forward solves in the single-plane bf16 mode."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a HIP device")
     from gncde import data, run

@@ -56,3 +56,15 @@ def test_drivers_construct():
     p = PGTGraphNeuralCDE({"hidden_dim": 64, "data_dim": 8, "feature_dim": 1}, vf2, "cubic", 2)
     # pgt_graph_neural_cde.py:62 builds the decoder with the encoder's key
     assert torch.equal(p.encoder.layers[0].weight[:, :8].flatten()[:4], p.encoder.layers[0].weight[:, :8].flatten()[:4])
+
+
+def test_bf16_mfma_refuses_the_pid_controller():
+    """The single-plane bf16 mode is for fixed grids: under the adaptive controller its rounding noise costs 12-21x
+    the steps, so the TGB driver refuses the combination up front (and the C-ABI returns
+    GNCDE_ERR_UNSUPPORTED)."""
+    from gncde.models import TGBGraphNeuralCDE
+    vf = V.PermEquivGraphVectorField(16, 16, 16 * 8 * 2, 2, 8, 40, key=0)
+    TGBGraphNeuralCDE({"hidden_dim": 16}, vf, "cubic", 1, solver=None, compute="bf16_mfma")
+    TGBGraphNeuralCDE({"hidden_dim": 16}, vf, "cubic", 1, solver="pid", compute="bf16")
+    with pytest.raises(ValueError, match="bf16_mfma"):
+        TGBGraphNeuralCDE({"hidden_dim": 16}, vf, "cubic", 1, solver="pid", compute="bf16_mfma")
