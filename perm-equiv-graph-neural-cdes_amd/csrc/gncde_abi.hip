@@ -147,7 +147,7 @@ int gncde_integrate_path(const GncdeProblem* prob, const GncdeSolver* solver, ch
   if (rows_pid_supported(*prob, *solver))
     rows_pid_name(*prob, buf, buf_len);
   else if (prob->compute == GNCDE_COMPUTE_FP32)  // generic_rows: every evaluation is one k_rows launch
-    snprintf(buf, buf_len, rows_supported(*prob) ? "generic_rows" : "generic");
+    snprintf(buf, buf_len, rows_eval_used(*prob) ? "generic_rows" : "generic");
   else
     snprintf(buf, buf_len, prob->compute == GNCDE_COMPUTE_BF16_MFMA ? "rows_bf16" : "generic_bf16");
   return GNCDE_OK;
@@ -162,7 +162,7 @@ int gncde_vf_eval(const GncdeProblem* prob, const float* t, const float* y, floa
   if (workspace_bytes < generic_vf_workspace(*prob) || !workspace) return GNCDE_ERR_WORKSPACE;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int rc2 = generic_vf_eval(*prob, t, y, dy, static_cast<char*>(workspace), st);
-  return rc2 ? rc2 : rows_fault_status(*prob, static_cast<char*>(workspace), st, rows_supported(*prob));
+  return rc2 ? rc2 : rows_fault_status(*prob, static_cast<char*>(workspace), st, rows_eval_used(*prob));
 }
 
 int gncde_integrate(const GncdeProblem* prob, const GncdeSolver* solver, const float* y0, float* ys,

@@ -626,7 +626,7 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.Z1 = take(B * n * D);
   w.m = take(B * n * D);
   // (I + Abar_l) for every layer (not needed by the one-launch evaluation)
-  w.abar = take(rows_supported(p) ? 1 : (size_t)p.L * B * nn);
+  w.abar = take(rows_eval_used(p) ? 1 : (size_t)p.L * B * nn);
   w.wf = take(wsum);  // W' = W diag(rms_w) per layer, back to back
   w.wp = take(wsum);  // W' in k_layer's operand order (layers with layer_mode >= 0)
   w.bf = take(bsum);  // bias' = bias + W rms_b per layer
@@ -758,7 +758,7 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool ro
                        reinterpret_cast<const uint16_t*>(p.coef), w.csum);
   else
     hipLaunchKernelGGL(k_coef_sums<float>, gs, dim3(256), 0, st, p.n, p.T, p.coef, w.csum);
-  const bool rows = rows_supported(p) || rows_layout;
+  const bool rows = rows_eval_used(p) || rows_layout;
   if (rows) generic_vf_transpose(p, ws, st);
   size_t wo = 0, bo = 0;
   for (int l = 0; l < p.L; ++l) {
@@ -788,14 +788,29 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   carve_vf(p, ws, w);
   unsigned local = 0;
   if (!prepared) generic_vf_prepare(p, ws, st);
-  if (rows_supported(p)) {  // one launch: spline, fusion, every layer and the read-out (gncde_rows.hip)
+  if (rows_eval_used(p)) {  // one launch: spline, fusion, every layer (and the read-out) (gncde_rows.hip)
     if (!bars) {
       if (prepared) return GNCDE_ERR_ARG;
       bars = &local;
     }
     // (the workspace holds no (I + Abar_l) planes for these problems: there is no multi-kernel fallback here)
-    return rows_vf_eval(p, t, y, dy, w.csum, w.coefT, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync, reinterpret_cast<int*>(w.sync + B), *bars,
-                        st, keep);
+    if (rows_supported(p))
+      return rows_vf_eval(p, t, y, dy, w.csum, w.coefT, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync,
+                          reinterpret_cast<int*>(w.sync + B), *bars, st, keep);
+    // the H = 64 CDE read-out: the hidden stack writes P, q, tg, dX (in w.m), then one GEMM over all B n rows
+    const int H = p.dims[0];
+    float* P = w.m;
+    float* aux = w.m + (size_t)B * n * H;
+    const int rc = rows_vf_eval(p, t, y, dy, w.csum, w.coefT, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync,
+                                reinterpret_cast<int*>(w.sync + B), *bars, st, keep, P, aux);
+    if (rc) return rc;
+    size_t wo = 0, bo = 0;
+    for (int l = 0; l + 1 < p.L; ++l) {
+      wo += (size_t)p.dims[l] * p.dims[l + 1];
+      bo += p.dims[l + 1];
+    }
+    readout_rows(B * n, H, P, aux, w.wp + wo, w.bf + bo, dy, st);
+    return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
   }
   vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st);
   const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
@@ -954,7 +969,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   if (s.controller == GNCDE_CTRL_PID) {
     if (rows_pid_supported(p, s)) return generic_rows_pid(p, s, y0, ys, stats, ws, st);
     const int rc = generic_integrate_pid(p, s, y0, ys, stats, ws, st);
-    return rc ? rc : rows_fault_status(p, ws, st, rows_supported(p));
+    return rc ? rc : rows_fault_status(p, ws, st, rows_eval_used(p));
   }
   if (s.controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
   const int B = p.B;
@@ -1068,7 +1083,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     hipLaunchKernelGGL(k_grid_stats, dim3(gb), dim3(256), 0, st, B, s.method, s.nsteps, generic_vf_fault(p, ws),
                        stats);
   if (hipGetLastError() != hipSuccess) return GNCDE_ERR_HIP;
-  return rc ? rc : rows_fault_status(p, ws, st, rows_supported(p));
+  return rc ? rc : rows_fault_status(p, ws, st, rows_eval_used(p));
 }
 
 }  // namespace gncde

@@ -829,7 +829,7 @@ bool rows_vjp_supported(const GncdeProblem& p) {
   if (p.cde_hidden > 0) return p.cde_embed == 8 && p.cde_hidden == H && p.dims[p.L] == 16 * H;
   if (p.dims[p.L] != H) return false;
   // the forward keep needs every layer on the one-launch path or on k_layer (gncde_generic.hip generic_vf_eval)
-  if (rows_supported(p)) return true;
+  if (rows_eval_used(p)) return true;
   for (int l = 0; l < p.L; ++l)
     if (layer_mode(p, l) < 0) return false;
   return true;

@@ -712,7 +712,7 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
   char* vf_ws = rows_ws + (rows ? rows_vjp_workspace(p) : 0);
   const Tableau tab = s.method == GNCDE_RK4 ? rk4_tab() : tsit5_tab();
   generic_vf_prepare(p, vf_ws, st);
-  if (!rows_supported(p) && rows_vjp_supported(p)) generic_vf_transpose(p, vf_ws, st);
+  if (!rows_eval_used(p) && rows_vjp_supported(p)) generic_vf_transpose(p, vf_ws, st);
   unsigned bars = 0;  // barriers of one-launch stage evaluations (generic_vf_eval)
   {
     size_t wo = 0, bo = 0;
@@ -807,7 +807,7 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
                        (size_t)p.L * GNCDE_FC, w.gfc, gfusion);
   }
   if (hipGetLastError() != hipSuccess) return GNCDE_ERR_HIP;
-  return rows_fault_status(p, vf_ws, st, rows_supported(p));  // the keep forwards ran one-launch evaluations
+  return rows_fault_status(p, vf_ws, st, rows_eval_used(p));  // the keep forwards ran one-launch evaluations
 }
 
 }  // namespace gncde
