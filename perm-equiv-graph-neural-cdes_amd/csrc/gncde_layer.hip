@@ -477,16 +477,20 @@ __global__ void __launch_bounds__(256, 2) k_readout_rows(int rows, const float* 
     const int R = e / AX, c = e % AX;
     sAux[R][c] = r0 + R < rows ? aux[(size_t)(r0 + R) * AX + c] : 0.f;
   }
-  // K loop: per 16-deep c chunk all 16 j operand loads (one coalesced 1 KB wave load each) are issued a chunk ahead
+  // K loop: per 16-deep c chunk all 16 j operand loads (one coalesced 1 KB wave load each) are issued a chunk ahead;
+  // the scheduling barriers keep the compiler from sinking each load to its first use (which waits out one L2
+  // round trip per load: 64 per wave)
   floatx4 acc[2][2] = {{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}};
   floatx4 wv[2][16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) wv[0][j] = W4[((ct * 16 + j) * NCC + 0) * 64 + lane];
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int cc = 0; cc < NCC; ++cc) {
     if (cc + 1 < NCC)
 #pragma unroll
       for (int j = 0; j < 16; ++j) wv[(cc + 1) & 1][j] = W4[((ct * 16 + j) * NCC + cc + 1) * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const floatx4 a0 = pr[0][cc] * dxr[0][j], a1 = pr[1][cc] * dxr[1][j];
@@ -496,6 +500,7 @@ __global__ void __launch_bounds__(256, 2) k_readout_rows(int rows, const float* 
         acc[1][j & 1] = mfma4(a1[s], wv[cc & 1][j][s], acc[1][j & 1]);
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();  // sAux
   const int m = 16 * ct + lo;

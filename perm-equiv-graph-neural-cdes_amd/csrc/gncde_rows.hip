@@ -42,8 +42,10 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 #ifdef GNCDE_ROWS_STAMPS
 __device__ unsigned long long g_rows_stamps[4096 * 16];
+// (solve: the evaluation kStampEval of every workgroup, slot = its ticket)
+constexpr int kStampEval = 20;
 #define ROWS_STAMP(k) \
-  do { if (threadIdx.x == 0) g_rows_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+  do { if (threadIdx.x == 0 && stamp_on) g_rows_stamps[stamp_slot * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define ROWS_STAMP(k) do {} while (0)
 #endif
@@ -182,11 +184,18 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
 
   // ---- which rows of which sample ------------------------------------------------------------------------------
   // One evaluation (k_rows): the grid holds G co-resident groups that loop over the samples in rounds.  Solve: one
-  // group per sample, the grid is B groups, and a workgroup takes its (sample, row block) from a ticket in start
-  // order, so the workgroups of a group are always ones that have started: a group waits only for members that
-  // are already running, and groups of later samples start as earlier solves finish (no co-residency assumption).
+  // group per sample.  When every group is resident at once (G = B, a multiple of 8), the groups take the
+  // XCD-affine blockIdx layout (a sample's workgroups on one XCD: its coefficients, weights and hand-offs stay in
+  // one L2 across the solve's evaluations); otherwise a workgroup takes its (sample, row block) from a ticket in
+  // start order, so the workgroups of a group are always ones that have started: a group waits only for members
+  // that are already running, and groups of later samples start as earlier solves finish (no co-residency
+  // assumption).
   int g, rb;
-  if constexpr (SOLVE) {
+  if (SOLVE && a.G > 0 && a.G % 8 == 0) {  // every group resident at once (rows_integrate_pid checked): the XCD-affine layout
+    const int x = blockIdx.x;
+    g = (x & 7) + 8 * (x / (8 * nb));
+    rb = (x >> 3) % nb;
+  } else if constexpr (SOLVE) {
     if (threadIdx.x == 0)
       sFlag[1] = (int)(__hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.ticket0);
     __syncthreads();
@@ -205,6 +214,10 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
   const size_t zgroup = (size_t)n * H;
   unsigned epoch = a.bar0;
   unsigned pub = 0;  // publications of this launch (stage inputs, hidden outputs, partial sums): buffer parity
+#ifdef GNCDE_ROWS_STAMPS
+  bool stamp_on = true;
+  const int stamp_slot = SOLVE ? g * nb + rb : (int)blockIdx.x;
+#endif
 
   auto arrive = [&]() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores have reached memory
@@ -236,6 +249,9 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
     return sFlag[0] == 0;
   };
 
+  // the solve's knots, one per lane (T <= 64)
+  const float ts_lane = SOLVE && (int)(threadIdx.x & 63) < T ? a.ts[(size_t)g * T + (threadIdx.x & 63)] : 0.f;
+
   // ---- one vector-field evaluation of sample b at time tb ----------------------------------------------------
   // Layer 0 reads the stage input z0: with plain loads (written before this launch), or, with `handoff`, as a
   // publication of the group (a barrier wait first, sc1 loads).  The output tile dy[R, 0 .. H-1] lands in sOut.
@@ -243,6 +259,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
   auto evaluate = [&](const int b, const float tb, const float* z0, const bool handoff, const bool live)
       __attribute__((always_inline)) -> bool {
     bool ok = true;
+    ROWS_STAMP(0);
     // the lane's indices through an opaque move per evaluation: otherwise every per-lane address and bounds mask
     // of the form and the layers is hoisted out of the enclosing loop and held in registers for the whole kernel
     int tid;
@@ -250,8 +267,16 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
     const int w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
     const int ri = r0 + lo;  // this lane's operand row
     const float* tsb = a.ts + (size_t)b * T;
-    const int idx = interval_index_wave(tsb, T, tb);
-    const float f = tb - tsb[idx];
+    int idx;
+    float f;
+    if (SOLVE && T <= 64) {  // the knots held in registers for the whole solve (no L2 round trip before the form)
+      idx = __popcll(__ballot(lane < T && ts_lane < tb)) - 1;
+      idx = idx < 0 ? 0 : (idx > T - 2 ? T - 2 : idx);
+      f = tb - __shfl(ts_lane, idx);
+    } else {
+      idx = interval_index_wave(tsb, T, tb);
+      f = tb - tsb[idx];
+    }
     using CT_ = typename std::conditional<BF, uint16_t, float>::type;
     const CT_* cb = reinterpret_cast<const CT_*>(a.coef) + ((size_t)b * (T - 1) + idx) * 4 * nn;
 
@@ -618,16 +643,21 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
       const int ct = w % CT, kp = w / CT, j0 = kp * JP;
       const floatx4* W4 = reinterpret_cast<const floatx4*>(a.wperm + (size_t)l * H * H);
       constexpr bool F32R = MODE == 2 && !BF, BFR = MODE == 2 && BF;
+      // (the persistent solve requests its slice after the product instead: held across the barrier wait, its 64
+      // VGPRs push the solve's stage values into scratch; its W' is L2-resident across the evaluations)
+      constexpr bool PREF = F32R && !SOLVE;
       floatx4 wv[F32R ? CT : 1][F32R ? JP : 1];
       // bf16: W'[16 m + j, 32 cc + 8 hi ..], m = 16 ct + lo; at H = 64 the first K chunk (64 VGPRs) is prefetched,
       // the second is requested after the product
       constexpr int KPF = H == 64 ? 1 : KC;
       bf16x8 wb[BFR ? KC : 1][BFR ? JP : 1];
-      if constexpr (F32R)
+      auto load_wv = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int cc = 0; cc < CT; ++cc)
 #pragma unroll
           for (int j = 0; j < JP; ++j) wv[cc][j] = W4[((ct * 16 + j0 + j) * CT + cc) * 64 + lane];
+      };
+      if constexpr (PREF) load_wv();
       if constexpr (BFR)
 #pragma unroll
         for (int cc = 0; cc < KPF; ++cc)
@@ -636,6 +666,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
       load_z(l);
       ROWS_STAMP(12);
       product(l);
+      if constexpr (F32R && !PREF) load_wv();
       ROWS_STAMP(13);
       if constexpr (MODE == 3) {
         // the read-out's inputs for rows R (gncde_layer.hip k_readout_rows): P = (I + Abar_L)[R, :] diag(inv) Z_L
@@ -738,7 +769,6 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
       const int bs = g + it * a.G;
       const bool live = bs < a.B;
       const int b = live ? bs : a.B - 1;  // an idle round computes on a valid sample, keeps its barriers, stores no dy
-      ROWS_STAMP(0);
       evaluate(b, a.t[b], a.y + (size_t)b * zgroup, false, live);
       // dy rows R: 16-byte stores of the output tile (MODE 3 wrote the read-out's inputs itself)
       constexpr int G4 = H / 4;
@@ -822,6 +852,9 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
     bool fault = false;
     publish(y);  // f(t0, y0): the FSAL k0 and the initial-step heuristic's f0
     for (;;) {
+#ifdef GNCDE_ROWS_STAMPS
+      stamp_on = evals == kStampEval;
+#endif
       if (!evaluate(b, tst, a.zbuf[(pub - 1) & 1] + (size_t)b * zgroup, true, true)) {
         fault = true;
         break;
@@ -1248,7 +1281,8 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   a.n = p.n;
   a.T = p.T;
   a.L = p.L;
-  a.G = p.B;
+  // G = B (a multiple of 8) selects the XCD-affine layout: only when every group is resident at once
+  a.G = p.B % 8 == 0 && resident_blocks(k, smem) >= p.B * nb ? p.B : 0;
   a.rounds = 1;
   a.nb = nb;
   a.big = rows_big(p.n, H, false);

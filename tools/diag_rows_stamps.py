@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Diagnostic (GPU, experiment build only): per-phase wall time of one k_rows evaluation at BASELINE config 5's
-shape, from s_memrealtime stamps (100 MHz) that a -DGNCDE_ROWS_STAMPS build of gncde_rows.hip writes for round 0
-of every workgroup.  Run with GNCDE_LIB pointing at that build."""
+shape, from s_memrealtime stamps (100 MHz) that a -DGNCDE_ROWS_STAMPS build of gncde_rows.hip writes (the last
+round of every workgroup; with DIAG_SOLVE=1 the persistent Tsit5 + PID solve's 20th evaluation of every workgroup,
+slots by ticket).  Run with GNCDE_LIB pointing at that build."""
 import ctypes
 import os
 import sys
@@ -25,12 +26,19 @@ def main():
     prob, y0 = synthetic.cde_batch(B, 255, 3, 32, 8, 4, 1.0)
     prob = prob.with_compute(compute)
     t = torch.full((B,), 0.37, dtype=torch.float32, device="cuda")
+    solve = os.environ.get("DIAG_SOLVE") == "1"
+    spec = gncde.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_PID, save_mode=_lib.SAVE_T1, rtol=1e-3, atol=1e-6,
+                            t0=prob.ts[:, 0].contiguous(), t1=prob.ts[:, -1].contiguous(),
+                            dt0=torch.full((B,), 0.01, device="cuda"))
     lib = ctypes.CDLL(_lib.LIB_PATH)
     fn = lib.gncde_debug_rows_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
     nwg = B * 16
     for rep in range(3):
-        gncde.vf_eval(prob, t, y0)
+        if solve:
+            gncde.integrate(prob, spec, y0)
+        else:
+            gncde.vf_eval(prob, t, y0)
         torch.cuda.synchronize()
     buf = np.zeros(nwg * 16, dtype=np.uint64)
     assert fn(buf.ctypes.data, buf.size) == 0
@@ -45,8 +53,9 @@ def main():
     # the group count is a multiple of 8, else x / 16)
     G = B
     x = np.arange(nwg)
-    g = (x & 7) + 8 * (x // (8 * 16)) if G % 8 == 0 else x // 16
-    for name, pub, z in (("barrier 1", 5, 6), ("barrier 2", 8, 9), ("barrier 3", 11, 12)):
+    g = (x & 7) + 8 * (x // (8 * 16)) if G % 8 == 0 and not solve else x // 16
+    for name, pub, z in ((("stage input", 0, 3),) if solve else ()) + (("barrier 1", 5, 6), ("barrier 2", 8, 9),
+                                                                         ("barrier 3", 11, 12)):
         last = np.array([rel[g == q, pub].max() for q in range(G)])
         first_z = np.array([rel[g == q, z].min() for q in range(G)])
         skew = np.array([rel[g == q, pub].max() - rel[g == q, pub].min() for q in range(G)])
