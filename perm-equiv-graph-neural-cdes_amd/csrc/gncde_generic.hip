@@ -804,6 +804,8 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     const int rc = rows_vf_eval(p, t, y, dy, w.csum, w.coefT, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync,
                                 reinterpret_cast<int*>(w.sync + B), *bars, st, keep, P, aux);
     if (rc) return rc;
+    // a keep forward serves the reverse sweep, which reads the kept hidden layers and never dy: no read-out
+    if (keep) return GNCDE_OK;
     size_t wo = 0, bo = 0;
     for (int l = 0; l + 1 < p.L; ++l) {
       wo += (size_t)p.dims[l] * p.dims[l + 1];

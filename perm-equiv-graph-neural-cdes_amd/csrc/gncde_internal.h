@@ -224,7 +224,8 @@ void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float*
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool rows_layout = false);
 // bars: the solve's count of per-group barriers done by one-launch evaluations so far (gncde_rows.hip); nullptr
 // only together with prepared = false (a standalone evaluation)
-// keep (optional, [L-1, B, n, d]): every hidden layer's output Z_{l+1} kept for the reverse mode (uniform width d)
+// keep (optional, [L-1, B, n, d]): every hidden layer's output Z_{l+1} kept for the reverse mode (uniform width d);
+// dy is then not needed by the caller, and the stack split skips its read-out
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared = false, unsigned* bars = nullptr, float* keep = nullptr);
 // the workspace's fault word (a one-launch evaluation's barrier gave up): solver status 4 when set

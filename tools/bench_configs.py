@@ -23,9 +23,20 @@ FP32_PEAK = 157.3
 
 
 def flops_per_eval(n, dims, de=0):
+    """the (I + Abar) m product of every layer charged at that layer's output width."""
     f = 19 * n * n
     for l in range(1, len(dims)):
         f += 22 * n * n + 2 * n * n * dims[l] + 2 * n * dims[l - 1] * dims[l] + 6 * n * dims[l]
+    return f + (4 * n * dims[-1] if de else 0)
+
+
+def executed_flops_per_eval(n, dims, de=0):
+    """The same model as the generic path executes it: a widening layer (the CDE read-out, d_L = 16 h) runs the n x n
+    product at its input width in the reassociated order ((I + Abar) diag(inv) Z) W'^T (gncde_generic.hip)."""
+    f = 19 * n * n
+    for l in range(1, len(dims)):
+        w = min(dims[l], dims[l - 1])
+        f += 22 * n * n + 2 * n * n * w + 2 * n * dims[l - 1] * dims[l] + 6 * n * dims[l]
     return f + (4 * n * dims[-1] if de else 0)
 
 
@@ -45,6 +56,8 @@ def run(name, prob, spec, y0, reps, ref=None):
            "sample_evals_per_s": round(evals / dt, 1), "evals_per_sample": evals / prob.B,
            "tflops_algorithmic": round(evals * fpe / dt / 1e12, 3),
            "mfma_frac": round(evals * fpe / dt / 1e12 / FP32_PEAK, 4),
+           "executed_frac": round(evals * executed_flops_per_eval(prob.n, prob.dims, prob.cde_embed) / dt / 1e12
+                                  / FP32_PEAK, 4),
            "finite": bool(torch.isfinite(ys).all())}
     if ref is not None:  # deviation of this arithmetic from the fp32 solve of the same problem
         out["rel_dev_vs_fp32"] = float((ys - ref).abs().max() / ref.abs().max())
