@@ -266,3 +266,35 @@ def test_barrier_fault_is_reported(G, monkeypatch):
     monkeypatch.delenv("GNCDE_DEBUG_BARRIER_SPINS")
     _, st = G.integrate(prob, spec, y0, stats=True)  # the next solve starts clean
     assert torch.all(st[:, 3] == 0)
+
+
+@pytest.mark.parametrize("config", ["2", "4"])
+def test_fused_configs_exact_shape_vs_oracle(G, config):
+    """BASELINE configs 2 and 4 at their exact per-GPU shapes on the fused persistent kernel: config 2 (heat grid
+    n = 64, h = 16, L = 3, B = 1024, 100 RK4 steps) and config 4's per-GPU forward (community graph n = 128, h = 16,
+    L = 2, B = 1024, 100 RK4 steps).  Four samples spread over the batch against the fp64 oracle's solve on the same
+    grid (RTOL_SOLVE)."""
+    from gncde import layout, synthetic
+    if config == "2":
+        prob, y0, layers = synthetic.heat_batch(1024, num_nodes=64, hidden=16, num_layers=3, seed=1234)
+        path = "fused<64,16,3,rk4>"
+    else:
+        prob, y0, layers = synthetic.heat_batch(1024, num_nodes=128, hidden=16, num_layers=2, T=80, seed=4321,
+                                                graph="community")
+        path = "fused<128,16,2,rk4>"
+    grids = [layout.rk4_grid(float(prob.ts[b, 0]), float(prob.ts[b, -1]), 100) for b in range(prob.B)]
+    grid, ns = layout.stack_grids(grids)
+    spec = G.SolverSpec(method=G._lib.RK4, save_mode=G._lib.SAVE_T1, grid=grid, nsteps=ns)
+    assert G.integrate_path(prob, spec) == path
+    ys, st = G.integrate(prob, spec, y0, stats=True)
+    assert torch.all(st[:, 2] == 400) and torch.all(st[:, 3] == 0)
+    params = O.VFParams("undirected", [{k: v.numpy() for k, v in lay.items()} for lay in layers])
+    y0n = y0.cpu().numpy().astype(np.float64)
+    for b in (0, 341, 702, 1023):
+        ts, coeffs = synthetic.to_reference_coeffs(prob, b)
+        ctrl = O.CubicInterpolation(ts, coeffs)
+        f = lambda t, y, c=ctrl: O.vector_field(params, t, y, c)  # noqa: E731
+        ref, _ = O.solve_fixed_grid(f, grids[b], y0n[b], "rk4", time_dtype=np.float32)
+        err = rel_err(ys[b].cpu().numpy(), ref)
+        print(f"  config {config} sample {b}: 100 RK4 steps vs fp64 oracle {err:.2e}")
+        assert err <= RTOL_SOLVE
