@@ -145,7 +145,7 @@ int gncde_integrate_path(const GncdeProblem* prob, const GncdeSolver* solver, ch
   if (!buf || buf_len == 0) return GNCDE_ERR_ARG;
   if (use_fused(*prob, *solver, buf, buf_len)) return GNCDE_OK;
   if (rows_pid_supported(*prob, *solver))
-    rows_pid_name(*prob, buf, buf_len);
+    rows_pid_name(*prob, *solver, buf, buf_len);
   else if (prob->compute == GNCDE_COMPUTE_FP32)  // generic_rows: every evaluation is one k_rows launch
     snprintf(buf, buf_len, rows_eval_used(*prob) ? "generic_rows" : "generic");
   else

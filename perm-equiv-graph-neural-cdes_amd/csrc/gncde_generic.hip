@@ -945,7 +945,7 @@ int rows_fault_status(const GncdeProblem& p, char* vf_ws, hipStream_t st, bool r
   return fault ? GNCDE_ERR_BARRIER : GNCDE_OK;
 }
 
-// Tsit5 + PID as ONE persistent launch on the one-launch evaluation (gncde_rows.hip)
+// the whole solve (Tsit5 + PID, or a fixed grid) as ONE persistent launch on the one-launch evaluation (gncde_rows.hip)
 int generic_rows_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats, char* ws,
                      hipStream_t st) {
   VfWs w;
@@ -974,6 +974,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     return rc ? rc : rows_fault_status(p, ws, st, rows_eval_used(p));
   }
   if (s.controller != GNCDE_CTRL_GRID) return GNCDE_ERR_UNSUPPORTED;
+  if (rows_pid_supported(p, s)) return generic_rows_pid(p, s, y0, ys, stats, ws, st);  // the whole grid: one launch
   const int B = p.B;
   const size_t E = (size_t)p.n * state_dim(p);
   char* cur = ws + generic_vf_workspace(p);

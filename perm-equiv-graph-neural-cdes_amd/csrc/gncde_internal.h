@@ -269,7 +269,8 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
                 hipStream_t st);
 void rows_vjp_finish(const GncdeProblem& p, char* ws, float* gparams, float* gfusion, hipStream_t st);
 
-// the persistent Tsit5 + PIDController solve on the one-launch evaluation (gncde_rows.hip): n <= 256, one width
+// the persistent solve on the one-launch evaluation (gncde_rows.hip): n <= 256, one width; Tsit5 + PIDController
+// or a fixed grid (GRID controller)
 bool rows_pid_supported(const GncdeProblem& p, const GncdeSolver& s);
 bool rows_solve_shape(const GncdeProblem& p);  // the shape part of rows_pid_supported
 size_t rows_pid_scratch(const GncdeProblem& p);
@@ -277,7 +278,7 @@ size_t rows_pid_scratch(const GncdeProblem& p);
 int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
                        char* vf_ws, float* part, const float* csum, const void* coefT, const float* wperm,
                        const float* bf, float* z0, float* z1, unsigned* sync, hipStream_t st);
-void rows_pid_name(const GncdeProblem& p, char* buf, size_t len);
+void rows_pid_name(const GncdeProblem& p, const GncdeSolver& s, char* buf, size_t len);
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device, kernel, size) for launches above 64 KB of LDS
 bool ensure_dyn_lds(const void* fn, size_t smem);
 // a one-launch evaluation's group barrier gave up in this call: GNCDE_ERR_BARRIER (reads the workspace's fault word

@@ -56,6 +56,11 @@ constexpr int kAux = 20;     // MODE 3: floats per row of the read-out's per-row
 
 // The persistent solve's controller inputs and outputs (GncdeSolver, PID controller)
 struct SolveArgs {
+  int grid_mode;         // 1: GRID controller (grid, nsteps, method, save_steps, rec); 0: PID
+  int method, G, save_steps;
+  const float* grid;     // [B, G]
+  const int32_t* nsteps; // [B]
+  float* rec;            // [B, G-1, S-1, n, H] stage record or nullptr
   int S, max_steps, auto_dt, step_len;
   float rtol, atol;
   const float* t0;       // [B]
@@ -160,9 +165,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
 // BF (GNCDE_COMPUTE_BF16_MFMA): bfloat16 coefficients, and every product — (I + Abar_l) diag(inv) Z, the Linears, the
 // read-out — on v_mfma_f32_16x16x32_bf16 with single-plane bf16 operands rounded from the fp32 values (fp32
 // accumulation); the spline, the reductions, RMSNorm and all sums outside the MFMAs stay fp32.
-// SOLVE: the persistent Tsit5 + PIDController solve (gncde_rows.hip header); otherwise one evaluation per launch.
-template <int H, int MODE, bool BF, bool SOLVE>
-__global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsArgs a) {
+// SOLVE: 0 one evaluation per launch; the persistent solve with 1 the Tsit5 + PIDController controller, 2 a fixed
+// step grid (§ the solve below).
+template <int H, int MODE, bool BF, int SOLVE>
+__global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int ZS = rows_zs(H);
   constexpr int CT = H / 16;           // column tiles of a width-H operand / output
@@ -191,11 +197,11 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
   // that are already running, and groups of later samples start as earlier solves finish (no co-residency
   // assumption).
   int g, rb;
-  if (SOLVE && a.G > 0 && a.G % 8 == 0) {  // every group resident at once (rows_integrate_pid checked): the XCD-affine layout
+  if (SOLVE != 0 && a.G > 0 && a.G % 8 == 0) {  // every group resident at once (rows_integrate_pid checked): the XCD-affine layout
     const int x = blockIdx.x;
     g = (x & 7) + 8 * (x / (8 * nb));
     rb = (x >> 3) % nb;
-  } else if constexpr (SOLVE) {
+  } else if constexpr (SOLVE != 0) {
     if (threadIdx.x == 0)
       sFlag[1] = (int)(__hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.ticket0);
     __syncthreads();
@@ -216,7 +222,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
   unsigned pub = 0;  // publications of this launch (stage inputs, hidden outputs, partial sums): buffer parity
 #ifdef GNCDE_ROWS_STAMPS
   bool stamp_on = true;
-  const int stamp_slot = SOLVE ? g * nb + rb : (int)blockIdx.x;
+  const int stamp_slot = SOLVE != 0 ? g * nb + rb : (int)blockIdx.x;
 #endif
 
   auto arrive = [&]() {
@@ -250,7 +256,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
   };
 
   // the solve's knots, one per lane (T <= 64)
-  const float ts_lane = SOLVE && (int)(threadIdx.x & 63) < T ? a.ts[(size_t)g * T + (threadIdx.x & 63)] : 0.f;
+  const float ts_lane = SOLVE != 0 && (int)(threadIdx.x & 63) < T ? a.ts[(size_t)g * T + (threadIdx.x & 63)] : 0.f;
 
   // ---- one vector-field evaluation of sample b at time tb ----------------------------------------------------
   // Layer 0 reads the stage input z0: with plain loads (written before this launch), or, with `handoff`, as a
@@ -269,7 +275,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
     const float* tsb = a.ts + (size_t)b * T;
     int idx;
     float f;
-    if (SOLVE && T <= 64) {  // the knots held in registers for the whole solve (no L2 round trip before the form)
+    if (SOLVE != 0 && T <= 64) {  // the knots held in registers for the whole solve (no L2 round trip before the form)
       idx = __popcll(__ballot(lane < T && ts_lane < tb)) - 1;
       idx = idx < 0 ? 0 : (idx > T - 2 ? T - 2 : idx);
       f = tb - __shfl(ts_lane, idx);
@@ -434,7 +440,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
     // ---- layers --------------------------------------------------------------------------------------------
     // Z_l -> LDS (a stage input written before this launch with plain loads; a publication of the group with sc1
     // loads after the barrier) and the RMSNorm factors of its rows
-    const int zslot = SOLVE ? b : g;  // the group's hand-off buffers (solve: one group per sample)
+    const int zslot = SOLVE != 0 ? b : g;  // the group's hand-off buffers (solve: one group per sample)
     auto load_z = [&](int l) __attribute__((always_inline)) {
       float* Zs = big;
       constexpr int G4 = H / 4, U = 8;
@@ -645,7 +651,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
       constexpr bool F32R = MODE == 2 && !BF, BFR = MODE == 2 && BF;
       // (the persistent solve requests its slice after the product instead: held across the barrier wait, its 64
       // VGPRs push the solve's stage values into scratch; its W' is L2-resident across the evaluations)
-      constexpr bool PREF = F32R && !SOLVE;
+      constexpr bool PREF = F32R && SOLVE == 0;
       floatx4 wv[F32R ? CT : 1][F32R ? JP : 1];
       // bf16: W'[16 m + j, 32 cc + 8 hi ..], m = 16 ct + lo; at H = 64 the first K chunk (64 VGPRs) is prefetched,
       // the second is requested after the product
@@ -764,7 +770,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
     return ok;
   };
 
-  if constexpr (!SOLVE) {
+  if constexpr (SOLVE == 0) {
     for (int it = 0; it < a.rounds; ++it) {
       const int bs = g + it * a.G;
       const bool live = bs < a.B;
@@ -794,7 +800,8 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
     const size_t oel = ((size_t)b * n + r0 + orow) * H + ocol;
     const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
     const float rtol = s.rtol, atol = s.atol;
-    const float t0 = s.t0[b], t1 = s.t1[b];
+    constexpr bool GRIDC = SOLVE == 2;  // the controller, fixed per instance (one evaluation call site each)
+    const float t0 = GRIDC ? 0.f : s.t0[b], t1 = GRIDC ? 0.f : s.t1[b];
     const float inv_cnt = 1.0f / (float)(n * H);
     const size_t E = (size_t)n * H;
     floatx4 y = mine ? *reinterpret_cast<const floatx4*>(s.y0 + oel) : zero;
@@ -841,26 +848,98 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
       s1 = a1;
       return ok;
     };
-    int phase = 0, st = 0, steps = 0, rejects = 0, evals = 0, status = 0, si = 0;
-    float t = t0, tn = t0, h = 0.f, dt = s.auto_dt ? 0.f : s.dt0[b], h0 = 0.f, d1 = 0.f, tst = t0;
-    const float* sts = s.S > 0 ? s.save_ts + (size_t)b * s.S : nullptr;
-    while (si < s.S && sts[si] <= t0) {  // saved states at save_ts <= t0
-      if (mine) *reinterpret_cast<floatx4*>(s.ys + ((size_t)b * s.S + si) * E + (oel - (size_t)b * E)) = y;
-      ++si;
-    }
-    if (rb == 0 && tid == 0 && s.step_ts) s.step_ts[(size_t)b * s.step_len] = t0;
+    int steps = 0, rejects = 0, evals = 0, status = 0;
     bool fault = false;
-    publish(y);  // f(t0, y0): the FSAL k0 and the initial-step heuristic's f0
-    for (;;) {
-#ifdef GNCDE_ROWS_STAMPS
-      stamp_on = evals == kStampEval;
-#endif
-      if (!evaluate(b, tst, a.zbuf[(pub - 1) & 1] + (size_t)b * zgroup, true, true)) {
-        fault = true;
-        break;
+    // ONE evaluation call site (the evaluation body is large: a second inlined copy costs registers); each
+    // controller is a step function that takes the evaluation's K, publishes the next stage input and returns
+    // false, or returns true when the sample is done.
+    floatx4 K = zero;
+
+    // ---- a fixed step grid (GRID controller: RK4, or Tsit5 at ConstantStepSize): the generic path's arithmetic
+    // (gncde_generic.hip generic_integrate: k_combo's summation order, stage times), SaveAt(t1) or every step, and
+    // the stage record the reverse sweep reads (GncdeSolver.stage_rec)
+    const int Gl = s.G;
+    const float* gr = GRIDC ? s.grid + (size_t)b * Gl : nullptr;
+    int ns = GRIDC ? s.nsteps[b] : 0;
+    ns = ns < 0 ? 0 : (ns > Gl - 1 ? Gl - 1 : ns);
+    const bool rk4 = s.method == GNCDE_RK4;
+    const int S1 = rk4 ? 3 : 5;  // recorded stage inputs per step
+    const size_t own = oel - (size_t)b * E;
+    auto save_col = [&](int k) {
+      if (s.save_steps && mine) *reinterpret_cast<floatx4*>(s.ys + ((size_t)b * Gl + k) * E + own) = y;
+    };
+    auto record = [&](int k, int i, const floatx4 u) {  // stage input U_i of step k -> slot (k, i - 1)
+      if (s.rec && mine) *reinterpret_cast<floatx4*>(s.rec + (((size_t)b * (Gl - 1) + k) * S1 + i - 1) * E + own) = u;
+    };
+    int gk = 0;
+    // the PID controller's state (graph_neural_cde.py:94-104 semantics)
+    int phase = 0, st = 0, si = 0;
+    float t = t0, tn = t0, h = 0.f, dt = 0.f, h0 = 0.f, d1 = 0.f, tst = t0;
+    const float* sts = s.S > 0 ? s.save_ts + (size_t)b * s.S : nullptr;
+
+    auto grid_step = [&]() -> bool {
+      if (rk4) {
+        if (st < 3) {  // k1 .. k3 evaluated: y + h (0.5 k1 | 0.5 k2 | k3)
+          const float cf = st < 2 ? 0.5f : 1.0f;
+          floatx4 u;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) u[e] = fmaf(h, fmaf(cf, K[e], 0.f), y[e]);
+          record(gk, st + 1, u);
+          publish(u);
+          tst = stage_time(t, cf, h);
+          ++st;
+          return false;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // y + h/6 (k1 + 2 k2 + 2 k3 + k4)
+          float acc = fmaf(1.0f / 6.0f, kk[0][e], 0.f);
+          acc = fmaf(2.0f / 6.0f, kk[1][e], acc);
+          acc = fmaf(2.0f / 6.0f, kk[2][e], acc);
+          acc = fmaf(1.0f / 6.0f, kk[3][e], acc);
+          y[e] = fmaf(h, acc, y[e]);
+        }
+        ++gk;
+        save_col(gk);
+        if (gk >= ns) return true;
+        t = gr[gk];
+        h = gr[gk + 1] - t;
+        tst = t;
+        st = 0;
+        publish(y);
+        return false;
       }
-      const floatx4 K = mine ? *reinterpret_cast<const floatx4*>(sOut + orow * ZS + ocol) : zero;
-      ++evals;
+      if (st == 6) {  // y1 accepted; its evaluation is the next step's k1 (FSAL)
+        y = y1;
+        kk[0] = K;
+        ++gk;
+        save_col(gk);
+        st = 0;
+      }
+      if (gk >= ns) return true;
+      if (st == 0) {
+        t = gr[gk];
+        h = gr[gk + 1] - t;
+      }
+      const int ns1 = st + 1;
+      float ar[6], cst;
+      tsit5_row(ns1, ar, cst);
+      floatx4 u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) acc = j < ns1 ? fmaf(ar[j], kk[j][e], acc) : acc;
+        u[e] = fmaf(h, acc, y[e]);
+      }
+      if (ns1 <= 5) record(gk, ns1, u);
+      else y1 = u;
+      publish(u);
+      tst = ns1 >= 5 ? stage_time(t, 1.0f, h) : stage_time(t, cst, h);
+      st = ns1;
+      return false;
+    };
+
+    auto pid_step = [&]() -> bool {
       bool start = false;
       if (phase == 0) {
         kk[0] = K;
@@ -878,7 +957,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
           float P0, P1;
           if (!group_sum2(p0, p1, P0, P1)) {
             fault = true;
-            break;
+            return true;
           }
           const float d0 = sqrtf(P0 * inv_cnt);
           d1 = sqrtf(P1 * inv_cnt);
@@ -889,7 +968,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
           publish(u);
           tst = t0 + h0;
           phase = 1;
-          continue;
+          return false;
         }
         start = true;
       } else if (phase == 1) {  // f(t0 + h0, y0 + h0 f0): d2 and the first step
@@ -904,7 +983,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
         float P2, unused;
         if (!group_sum2(p2, 0.f, P2, unused)) {
           fault = true;
-          break;
+          return true;
         }
         const float d2 = sqrtf(P2 * inv_cnt) / h0;
         const float md = fmaxf(d1, d2);
@@ -931,7 +1010,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
         publish(u);
         tst = ns1 >= 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);
         st = ns1;
-        continue;
+        return false;
       } else {  // the attempt is complete: K = f(tn, y1); embedded error, accept / reject, next step size
         float pe = 0.f;
         if (mine)
@@ -946,7 +1025,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
         float PE, unused;
         if (!group_sum2(pe, 0.f, PE, unused)) {
           fault = true;
-          break;
+          return true;
         }
         const float err = sqrtf(PE * inv_cnt);
         const bool finite = isfinite(err);
@@ -1004,7 +1083,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
             for (int q = si; q < s.S; ++q)  // SAVE_TS: only on failure
               *reinterpret_cast<floatx4*>(s.ys + ((size_t)b * s.S + q) * E + (oel - (size_t)b * E)) = y;
           }
-          break;
+          return true;
         }
         tn = t + dt;
         if (tn > t1 - 1e-6f) tn = t1;  // diffrax _clip_to_end
@@ -1016,6 +1095,53 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE ? 2 : 3) k_rows(RowsAr
         tst = stage_time(t, TSIT5_C2, h);
         st = 1;
       }
+      return false;
+    };
+
+    if constexpr (GRIDC) {
+      save_col(0);
+      t = ns > 0 ? gr[0] : gr[ns];
+      h = ns > 0 ? gr[1] - gr[0] : 0.f;
+      tst = t;
+    } else {
+      dt = s.auto_dt ? 0.f : s.dt0[b];
+      while (si < s.S && sts[si] <= t0) {  // saved states at save_ts <= t0
+        if (mine) *reinterpret_cast<floatx4*>(s.ys + ((size_t)b * s.S + si) * E + (oel - (size_t)b * E)) = y;
+        ++si;
+      }
+      if (rb == 0 && tid == 0 && s.step_ts) s.step_ts[(size_t)b * s.step_len] = t0;
+    }
+    // RK4 on an empty grid evaluates nothing; Tsit5 evaluates its FSAL k0 even then (stats: 1 + 6 ns)
+    if (!GRIDC || !rk4 || ns > 0) {
+      publish(y);  // the first evaluation's input: f(t0, y0) (PID: the FSAL k0 and the initial-step heuristic's f0)
+      for (;;) {
+#ifdef GNCDE_ROWS_STAMPS
+        stamp_on = evals == kStampEval;
+#endif
+        if (!evaluate(b, tst, a.zbuf[(pub - 1) & 1] + (size_t)b * zgroup, true, true)) {
+          fault = true;
+          break;
+        }
+        K = mine ? *reinterpret_cast<const floatx4*>(sOut + orow * ZS + ocol) : zero;
+        ++evals;
+        if constexpr (GRIDC) {
+#pragma unroll
+          for (int j = 0; j < 7; ++j)
+            if (j == st) kk[j] = K;
+          if (grid_step()) break;
+        } else {
+          if (pid_step()) break;
+        }
+      }
+    }
+    if constexpr (GRIDC) {
+      // padded steps (past this sample's grid): every stage input and saved state is the final state
+      for (int kp = ns; kp < Gl - 1; ++kp) {
+        for (int i = 1; i <= S1; ++i) record(kp, i, y);
+        save_col(kp + 1);
+      }
+      if (!s.save_steps && mine) *reinterpret_cast<floatx4*>(s.ys + oel) = y;
+      steps = ns;
     }
     if (rb == 0 && tid == 0 && s.stats) {
       const bool bad = fault || __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1033,17 +1159,17 @@ struct Inst {
   void (*launch)(const RowsArgs&, int, size_t, hipStream_t);
 };
 
-template <int H, int MODE, bool BF, bool SOLVE>
+template <int H, int MODE, bool BF, int SOLVE>
 void launch_rows(const RowsArgs& a, int grid, size_t smem, hipStream_t st) {
   hipLaunchKernelGGL((k_rows<H, MODE, BF, SOLVE>), dim3(grid), dim3(256), smem, st, a);
 }
 
-template <int H, int MODE, bool BF, bool SOLVE>
+template <int H, int MODE, bool BF, int SOLVE>
 Inst inst() {
   return Inst{reinterpret_cast<const void*>(&k_rows<H, MODE, BF, SOLVE>), &launch_rows<H, MODE, BF, SOLVE>};
 }
 
-template <bool BF, bool SOLVE>
+template <bool BF, int SOLVE>
 bool find_inst_t(int H, int mode, Inst& out) {
   if (mode == 1) {
     if (H == 16) out = inst<16, 1, BF, SOLVE>();
@@ -1053,7 +1179,7 @@ bool find_inst_t(int H, int mode, Inst& out) {
   } else {
     if (H == 16) out = inst<16, 2, BF, SOLVE>();
     else if (H == 32) out = inst<32, 2, BF, SOLVE>();
-    else if constexpr (BF && !SOLVE) {  // (fp32: the H = 64 read-out keeps the multi-kernel path)
+    else if constexpr (BF && SOLVE == 0) {  // (fp32: the H = 64 read-out keeps the multi-kernel path)
       if (H == 64) out = inst<64, 2, BF, SOLVE>();
       else return false;
     } else {
@@ -1065,10 +1191,10 @@ bool find_inst_t(int H, int mode, Inst& out) {
 bool find_inst(int H, int mode, bool bf, Inst& out) {
   if (mode == 3) {  // the hidden stack of the H = 64 read-out (fp32)
     if (bf || H != 64) return false;
-    out = inst<64, 3, false, false>();
+    out = inst<64, 3, false, 0>();
     return true;
   }
-  return bf ? find_inst_t<true, false>(H, mode, out) : find_inst_t<false, false>(H, mode, out);
+  return bf ? find_inst_t<true, 0>(H, mode, out) : find_inst_t<false, 0>(H, mode, out);
 }
 
 // 256-thread workgroups of one instance resident at this LDS size, x CUs (cached per device): min(occupancy query,
@@ -1240,25 +1366,36 @@ int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* d
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }
 
-// ---- the persistent Tsit5 + PIDController solve ----------------------------------------------------------------
+// ---- the persistent solve ------------------------------------------------------------------------------------
 // Envelope: the one-launch evaluation's fp32 shapes for any batch (a group only waits for workgroups that have
-// started, so no residency condition beyond one group), Tsit5 + PID, SaveAt(t1) or SaveAt(ts), and the default
-// dispatch (GNCDE_FLAG_GENERIC takes the host-paced gncde_pid.hip path instead).
+// started, so no residency condition beyond one group); Tsit5 + PID with SaveAt(t1) or SaveAt(ts), or a fixed grid
+// (RK4 / Tsit5) with SaveAt(t1) or every step (+ the stage record); the default dispatch (GNCDE_FLAG_GENERIC takes
+// the host-paced paths instead).
 bool rows_solve_shape(const GncdeProblem& p) {
   Inst k;
   return p.compute == GNCDE_COMPUTE_FP32 && rows_shape(p, false) &&
-         find_inst_t<false, true>(p.dims[0], p.cde_hidden > 0 ? 2 : 1, k);
+         find_inst_t<false, 1>(p.dims[0], p.cde_hidden > 0 ? 2 : 1, k);
+}
+
+// the persistent solve's instance for this controller
+bool find_solve_inst(const GncdeProblem& p, const GncdeSolver& s, Inst& k) {
+  const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
+  return s.controller == GNCDE_CTRL_GRID ? find_inst_t<false, 2>(H, mode, k) : find_inst_t<false, 1>(H, mode, k);
 }
 
 bool rows_pid_supported(const GncdeProblem& p, const GncdeSolver& s) {
-  if (!rows_solve_shape(p)) return false;
-  if (s.method != GNCDE_TSIT5 || s.controller != GNCDE_CTRL_PID || (s.flags & GNCDE_FLAG_GENERIC)) return false;
-  if (s.save_mode != GNCDE_SAVE_T1 && s.save_mode != GNCDE_SAVE_TS) return false;
+  if (!rows_solve_shape(p) || (s.flags & GNCDE_FLAG_GENERIC)) return false;
+  if (s.controller == GNCDE_CTRL_PID) {
+    if (s.method != GNCDE_TSIT5 || (s.save_mode != GNCDE_SAVE_T1 && s.save_mode != GNCDE_SAVE_TS)) return false;
+  } else if (s.controller == GNCDE_CTRL_GRID) {
+    if (s.save_mode != GNCDE_SAVE_T1 && s.save_mode != GNCDE_SAVE_STEPS) return false;
+  } else {
+    return false;
+  }
   Inst k;
-  const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
-  find_inst_t<false, true>(H, mode, k);
+  if (!find_solve_inst(p, s, k)) return false;
   const int nb = (p.n + kRB - 1) / kRB;
-  return resident_blocks(k, rows_smem(p.n, H, p.L, false)) >= nb;
+  return resident_blocks(k, rows_smem(p.n, p.dims[0], p.L, false)) >= nb;
 }
 
 size_t rows_pid_scratch(const GncdeProblem& p) {
@@ -1270,8 +1407,8 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
                        char* vf_ws, float* part, const float* csum, const void* coefT, const float* wperm,
                        const float* bf, float* z0, float* z1, unsigned* sync, hipStream_t st) {
   Inst k;
-  const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
-  if (!find_inst_t<false, true>(H, mode, k)) return GNCDE_ERR_UNSUPPORTED;
+  const int H = p.dims[0];
+  if (!find_solve_inst(p, s, k)) return GNCDE_ERR_UNSUPPORTED;
   (void)vf_ws;
   const size_t smem = rows_smem(p.n, H, p.L, false);
   if (!ensure_dyn_lds(k.fn, smem)) return GNCDE_ERR_HIP;
@@ -1305,6 +1442,13 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   a.bar0 = 0;
   a.spin_limit = spin_limit();
   SolveArgs& v = a.s;
+  v.grid_mode = s.controller == GNCDE_CTRL_GRID;
+  v.method = s.method;
+  v.G = s.grid_len;
+  v.save_steps = s.save_mode == GNCDE_SAVE_STEPS;
+  v.grid = s.grid;
+  v.nsteps = s.nsteps;
+  v.rec = s.grid_len >= 2 ? s.stage_rec : nullptr;
   v.S = s.save_mode == GNCDE_SAVE_TS ? s.n_save : 0;
   v.max_steps = s.max_steps;
   v.auto_dt = s.dt0 == nullptr;
@@ -1324,8 +1468,12 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }
 
-void rows_pid_name(const GncdeProblem& p, char* buf, size_t len) {
-  snprintf(buf, len, "rows_pid<%d,%s>", p.dims[0], p.cde_hidden > 0 ? "cde" : "ode");
+void rows_pid_name(const GncdeProblem& p, const GncdeSolver& s, char* buf, size_t len) {
+  if (s.controller == GNCDE_CTRL_PID)
+    snprintf(buf, len, "rows_pid<%d,%s>", p.dims[0], p.cde_hidden > 0 ? "cde" : "ode");
+  else
+    snprintf(buf, len, "rows_grid<%d,%s,%s>", p.dims[0], p.cde_hidden > 0 ? "cde" : "ode",
+             s.method == GNCDE_RK4 ? "rk4" : "tsit5");
 }
 
 }  // namespace gncde

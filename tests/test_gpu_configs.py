@@ -220,9 +220,9 @@ def test_rows_eval_largest_resident_batch(G):
     from gncde import layout
     prob, _, _ = _config5(G, 64)
 
-    def admitted(b):  # (path queries are host-only)
+    def admitted(b):  # (path queries are host-only; FLAG_GENERIC: one evaluation per launch, not the whole grid)
         g, n_ = layout.stack_grids([layout.constant_step_grid(0.0, 1.0, 0.25)] * b)
-        sp = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=g, nsteps=n_)
+        sp = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=g, nsteps=n_, flags=G._lib.FLAG_GENERIC)
         return G.integrate_path(prob.shard(0, b), sp) == "generic_rows"
     lo, hi = 1, 64
     assert admitted(lo) and not admitted(hi)
@@ -234,7 +234,7 @@ def test_rows_eval_largest_resident_batch(G):
     _, ts, coeffs, dcoeffs, dco, P, yn = cde_inputs(57, bmax, 255, 3, 1.0, 32, 8, 4, distinct=4)
     probm = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=32, cde_embed=8)
     g, n_ = layout.stack_grids([layout.constant_step_grid(0.0, 1.0, 0.25)] * bmax)
-    sp = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=g, nsteps=n_)
+    sp = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=g, nsteps=n_, flags=G._lib.FLAG_GENERIC)
     assert G.integrate_path(probm, sp) == "generic_rows"
     ysm, stm = G.integrate(probm, sp, torch.tensor(yn, dtype=torch.float32, device="cuda"), stats=True)
     assert torch.all(stm[:, 3] == 0)
@@ -298,3 +298,43 @@ def test_fused_configs_exact_shape_vs_oracle(G, config):
         err = rel_err(ys[b].cpu().numpy(), ref)
         print(f"  config {config} sample {b}: 100 RK4 steps vs fp64 oracle {err:.2e}")
         assert err <= RTOL_SOLVE
+
+
+@pytest.mark.parametrize("method,save", [("rk4", "steps"), ("tsit5", "steps"), ("tsit5", "t1")])
+def test_rows_grid_against_host_paced_and_oracle(G, method, save):
+    """The persistent fixed-grid solve (the whole grid in one launch, gncde_rows.hip GRID controller) at config 5's
+    shape with ragged step counts: against the host-paced path (one k_rows launch per evaluation + k_combo,
+    GNCDE_FLAG_GENERIC: the same arithmetic, so equal to fp32 summation order) and two samples against the fp64
+    oracle; the stage record it writes equals the host-paced one's."""
+    from gncde import layout
+    B, n, T, H, de, L = 16, 255, 3, 32, 8, 4
+    _, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(58, B, n, T, 1.0, H, de, L, distinct=4)
+    prob = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
+    grids = [O.rk4_grid(0.0, 1.0, 5 + b % 4) if method == "rk4" else O.constant_grid(0.0, 1.0, 0.1 + 0.02 * (b % 3))
+             for b in range(B)]
+    grid, ns = layout.stack_grids(grids)
+    m = G._lib.RK4 if method == "rk4" else G._lib.TSIT5
+    mode = G._lib.SAVE_STEPS if save == "steps" else G._lib.SAVE_T1
+    spec = G.SolverSpec(method=m, save_mode=mode, grid=grid, nsteps=ns)
+    assert G.integrate_path(prob, spec) == f"rows_grid<32,cde,{method}>"
+    yd = torch.tensor(y0, dtype=torch.float32, device="cuda")
+    floats = G.engine.stage_record_floats(prob, spec)
+    rec = torch.zeros(B, floats, device="cuda") if floats else None
+    ys, st = G.integrate(prob, dataclasses.replace(spec, stage_rec=rec), yd, stats=True)
+    gspec = dataclasses.replace(spec, flags=G._lib.FLAG_GENERIC)
+    grec = torch.zeros(B, floats, device="cuda") if floats else None
+    yg, sg = G.integrate(prob, dataclasses.replace(gspec, stage_rec=grec), yd, stats=True)
+    assert torch.equal(st, sg)
+    err = rel_err(ys.cpu().numpy(), yg.cpu().numpy())
+    print(f"  rows_grid {method} save={save}: vs host-paced {err:.2e}")
+    assert err <= 1e-5
+    if rec is not None:
+        assert rel_err(rec.cpu().numpy(), grec.cpu().numpy()) <= 1e-5
+    for b in (1, 14):
+        f, _ = oracle_fns(ts, coeffs, dco, P, H, de, b)
+        traj, _ = O.solve_fixed_grid(f, grids[b], y0[b], method, save_every_step=True, time_dtype=np.float32)
+        got = ys[b, :len(traj)].cpu().numpy() if save == "steps" else ys[b].cpu().numpy()
+        ref = traj if save == "steps" else traj[-1]
+        e = rel_err(got, ref)
+        print(f"  sample {b} ({len(grids[b]) - 1} steps) vs fp64 oracle {e:.2e}")
+        assert e <= RTOL_SOLVE

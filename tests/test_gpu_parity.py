@@ -423,7 +423,8 @@ def test_generic_cde_full_size_properties(gncde, B, n, T, h, L, t1, dt):
     err_vf = rel_err(dyP.cpu().numpy(), dy[:, P].cpu().numpy())
     grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, t1, dt)] * B)
     spec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=grid, nsteps=ns)
-    assert G.integrate_path(prob, spec) == "generic_rows"
+    # config 3 (H = 64 read-out): the stack split per evaluation; config 5: the whole grid in one launch
+    assert G.integrate_path(prob, spec) == ("generic_rows" if h == 64 else "rows_grid<32,cde,tsit5>")
     ys1 = G.integrate(prob, spec, y0)
     ys2 = G.integrate(prob, spec, y0)
     assert torch.equal(ys1, ys2)
@@ -504,7 +505,7 @@ def test_generic_cde_fixed_grid_solve_vs_oracle(gncde, method):
     grid, ns = layout.stack_grids(grids)
     spec = gncde.SolverSpec(method=gncde._lib.RK4 if method == "rk4" else gncde._lib.TSIT5,
                             save_mode=gncde._lib.SAVE_STEPS, grid=grid, nsteps=ns)
-    assert gncde.integrate_path(prob, spec) == "generic_rows"
+    assert gncde.integrate_path(prob, spec) == f"rows_grid<16,cde,{method}>"
     ys = gncde.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda")).cpu().numpy()
     for b in range(B):
         ctrl = O.CubicInterpolation(ts[b], tuple(c[b] for c in coeffs))
