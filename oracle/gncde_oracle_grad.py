@@ -159,11 +159,15 @@ def _acc(total, grads):
     return total
 
 
-def solve_fixed_grid_vjp(f, f_vjp, grid, y0, method="rk4", g_final=None, g_steps=None, time_dtype=np.float32):
+def solve_fixed_grid_vjp(f, f_vjp, grid, y0, method="rk4", g_final=None, g_steps=None, time_dtype=np.float32,
+                         y_lin=None):
     """Reverse mode of oracle.solve_fixed_grid (same stage times, same grid).
 
     f(t, y) -> dy; f_vjp(t, y, g) -> (g_y, grads).  Cotangent of the final state ``g_final`` [n, d] or of
     every saved step state ``g_steps`` [G, n, d].  Returns (g_y0, summed parameter grads).
+    ``y_lin`` [G, n, d]: step states to linearise at instead of this function's own fp64 forward (e.g. the GPU's
+    fp32 trajectory, so that both adjoints see the same side of every ReLU kink; the stage inputs are re-formed
+    from them in fp64).
     """
     cs, a, b = _tableau(method)
     y = np.asarray(y0, np.float64)
@@ -182,6 +186,8 @@ def solve_fixed_grid_vjp(f, f_vjp, grid, y0, method="rk4", g_final=None, g_steps
         else:
             y, _, _ = O.tsit5_step(f, t, y, h, time_dtype=time_dtype)
         ys.append(y)
+    if y_lin is not None:
+        ys = [np.asarray(v, np.float64) for v in y_lin]
     lam = np.array(g_steps[-1] if g_steps is not None else g_final, np.float64)
     total = None
     S = len(cs)

@@ -129,7 +129,11 @@ def test_bf16_pid_cde(gncde, golden_dir):
     assert np.all(np.abs(st[:, 0] - z["stats"][:, 0]) <= 0.25 * z["stats"][:, 0])
 
 
-RTOL_BF16_CFG5_VF = 1e-3
+# one evaluation of the single-plane mode at L = 4: each of the L + 1 products rounds both operands to bf16 (unit
+# roundoff 2^-8 each, so <= 2^-7 per product term relative to sum |a b|), and the errors add to first order through
+# the stack (RMSNorm renormalises, it does not amplify): (L + 1) 2^-7 = 3.9e-2 when the sums do not cancel
+# (measured 1.4e-2 at n = 255, 7.7e-3 at n = 64)
+RTOL_BF16_CFG5_VF = 5 * 2.0 ** -7
 
 
 @pytest.mark.parametrize("n", [255, 64])
@@ -149,7 +153,9 @@ def test_bf16_mfma_config5_shape_vs_fp32(gncde, n):
     ref = gncde.vf_eval(prob, t, y0).cpu().numpy()
     got = gncde.vf_eval(prob.with_compute("bf16_mfma"), t, y0).cpu().numpy()
     err = rel_err(got, ref)
-    grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, 1.0, 0.05)] * prob.B)
+    # a grid in fixed-step Tsit5's stable regime on this problem (h = 0.015; at h >= 0.05 the fp32 solve itself
+    # amplifies a 1-ulp change of y0 x2000: see tests/test_gpu_configs.py)
+    grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, 0.3, 0.015)] * prob.B)
     spec = gncde.SolverSpec(method=gncde._lib.TSIT5, save_mode=gncde._lib.SAVE_T1, grid=grid, nsteps=ns)
     yr = gncde.integrate(prob, spec, y0).cpu().numpy()
     ym = gncde.integrate(prob.with_compute("bf16_mfma"), spec, y0).cpu().numpy()
@@ -161,5 +167,5 @@ def test_bf16_mfma_config5_shape_vs_fp32(gncde, n):
     print(f"config-5 shape n={n}: one eval bf16_mfma vs fp32 {err:.3e}; 20-step solve: bf16_mfma {dev:.3e} "
           f"(bound {bound:.3e} from the fp32 1-ulp response {sens:.3e}), bf16_storage {rel_err(yq, yr):.3e}")
     assert np.isfinite(ym).all()
-    assert err <= RTOL_BF16M_EXACT
+    assert err <= RTOL_BF16_CFG5_VF
     assert dev <= bound

@@ -9,9 +9,10 @@
   accepted steps (GncdeSolver.step_ts); two samples' steps are replayed in the oracle (RTOL_SOLVE).
 
 Inputs are drawn with numpy (oracle.make_graph_control: a dynamic graph's normalised-Laplacian path, node data from
-a standard normal) so the oracle sees exactly what the GPU reads.  Samples whose gradient moves under a 1e-6
-relative change of y0 (a ReLU pre-activation within fp32 reach of its kink) are skipped for the gradient check
-(the test fails if fewer than two stable samples exist among the candidates).
+a standard normal) so the oracle sees exactly what the GPU reads.  The config-3 oracle adjoint is linearised at the
+GPU's step states (OG.solve_fixed_grid_vjp y_lin); samples whose gradient still moves under a 1e-6 relative change
+of those states (a ReLU pre-activation within fp32 reach of its kink) are skipped for the gradient check (the test
+fails if fewer than two stable samples exist among the candidates).
 """
 import dataclasses
 import os
@@ -96,8 +97,12 @@ def test_config3_exact_shape_trajectory_and_gradient(G):
     for b in (5, 40, 63, 17, 28, 51, 22, 34, 9, 56):  # windows 5, 0, 3, 7, 8, 1, 2, 4, 9, 6
         f, fv = oracle_fns(ts, coeffs, dco, P, H, de, b)
         g = rng.standard_normal((n, H))
-        g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g)
-        g1, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b] * (1 + 1e-6), "tsit5", g_final=g)
+        # the oracle adjoint is linearised at the GPU's own step states: over 30 x 6 x 3 ReLU layers an fp32
+        # trajectory 1e-5 away from fp64 crosses kinks a fp64 forward does not, which moves the gradient by more
+        # than the adjoint's own rounding
+        lin = ys[b].cpu().numpy()
+        g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g, y_lin=lin)
+        g1, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g, y_lin=lin * (1 + 1e-6))
         if np.max(np.abs(g1 - g0)) > 1e-5 * np.max(np.abs(g0)):
             print(f"  sample {b}: gradient not kink-stable, skipped")
             continue
@@ -310,7 +315,11 @@ def test_rows_grid_against_host_paced_and_oracle(G, method, save):
     B, n, T, H, de, L = 16, 255, 3, 32, 8, 4
     _, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(58, B, n, T, 1.0, H, de, L, distinct=4)
     prob = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
-    grids = [O.rk4_grid(0.0, 1.0, 5 + b % 4) if method == "rk4" else O.constant_grid(0.0, 1.0, 0.1 + 0.02 * (b % 3))
+    # Tsit5 at fixed h >= 0.05 is outside its stability region on this problem (the fp64 oracle's own one-step
+    # Jacobian amplifies x6 at h = 0.05 where RK4's is x1.08, linearly in the perturbation: an oscillatory mode
+    # with |h lambda| near RK4's imaginary-axis limit), so any two fp32 summation orders drift apart by percents;
+    # its grids here stay in the stable regime (h <= 0.016, amplification <= x6 over the whole solve)
+    grids = [O.rk4_grid(0.0, 1.0, 5 + b % 4) if method == "rk4" else O.constant_grid(0.0, 0.3, 0.012 + 0.002 * (b % 3))
              for b in range(B)]
     grid, ns = layout.stack_grids(grids)
     m = G._lib.RK4 if method == "rk4" else G._lib.TSIT5
@@ -327,6 +336,19 @@ def test_rows_grid_against_host_paced_and_oracle(G, method, save):
     assert torch.equal(st, sg)
     err = rel_err(ys.cpu().numpy(), yg.cpu().numpy())
     print(f"  rows_grid {method} save={save}: vs host-paced {err:.2e}")
+    if err > 1e-5:  # localise the divergence: per sample, and the first stage-record slot that differs
+        S1 = 3 if method == "rk4" else 5
+        for b in range(B):
+            eb = rel_err(ys[b].cpu().numpy(), yg[b].cpu().numpy())
+            first = None
+            if rec is not None:
+                r = rec[b].view(grid.shape[1] - 1, S1, -1).cpu().numpy()
+                q = grec[b].view(grid.shape[1] - 1, S1, -1).cpu().numpy()
+                for k in range(r.shape[0]):
+                    for i in range(S1):
+                        if first is None and rel_err(r[k, i], q[k, i]) > 1e-6:
+                            first = (k, i + 1, rel_err(r[k, i], q[k, i]))
+            print(f"    sample {b} ({int(ns[b])} steps): {eb:.2e}, first differing stage input {first}")
     assert err <= 1e-5
     if rec is not None:
         assert rel_err(rec.cpu().numpy(), grec.cpu().numpy()) <= 1e-5
