@@ -794,25 +794,8 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
       bars = &local;
     }
     // (the workspace holds no (I + Abar_l) planes for these problems: there is no multi-kernel fallback here)
-    if (rows_supported(p))
-      return rows_vf_eval(p, t, y, dy, w.csum, w.coefT, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync,
-                          reinterpret_cast<int*>(w.sync + B), *bars, st, keep);
-    // the H = 64 CDE read-out: the hidden stack writes P, q, tg, dX (in w.m), then one GEMM over all B n rows
-    const int H = p.dims[0];
-    float* P = w.m;
-    float* aux = w.m + (size_t)B * n * H;
-    const int rc = rows_vf_eval(p, t, y, dy, w.csum, w.coefT, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync,
-                                reinterpret_cast<int*>(w.sync + B), *bars, st, keep, P, aux);
-    if (rc) return rc;
-    // a keep forward serves the reverse sweep, which reads the kept hidden layers and never dy: no read-out
-    if (keep) return GNCDE_OK;
-    size_t wo = 0, bo = 0;
-    for (int l = 0; l + 1 < p.L; ++l) {
-      wo += (size_t)p.dims[l] * p.dims[l + 1];
-      bo += p.dims[l + 1];
-    }
-    readout_rows(B * n, H, P, aux, w.wp + wo, w.bf + bo, dy, st);
-    return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+    return rows_vf_eval(p, t, y, dy, w.csum, w.coefT, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync,
+                        reinterpret_cast<int*>(w.sync + B), *bars, st, keep);
   }
   vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st);
   const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
@@ -823,6 +806,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     const int din = p.dims[l], dout = p.dims[l + 1];
     float* Zout = keep && l + 1 < p.L ? keep + (size_t)l * B * n * p.dims[l + 1] : bufs[l & 1];
     const bool last = l == p.L - 1;
+    if (keep && last) break;  // a keep forward serves the reverse sweep: it reads the kept layers, never dy
     // A widening layer (d_out > d_in: the CDE wrapper's h -> h*de*2 read-out layer) is evaluated in the
     // reassociated order (I + Abar)(diag(inv) Z W'^T + 1 b'^T) = ((I + Abar) diag(inv) Z) W'^T + q b'^T with
     // q = (I + Abar) 1: the n x n product runs at width d_in instead of d_out (configs 3 / 5: 16x / 16x fewer
@@ -928,7 +912,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     bo += dout;
     Zin = Zout;
   }
-  if (fused_out) return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+  if (fused_out || keep) return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
   const int dout = out_dim(p);
   hipLaunchKernelGGL(k_finalize, dim3(cdiv((size_t)n * dout, 256), B), dim3(256), 0, st, n,
                      p.dims[p.L], p.cde_hidden, p.cde_embed, p.T, p.ts, p.data_coef, t, w.tg, Zin,

@@ -225,7 +225,7 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool ro
 // bars: the solve's count of per-group barriers done by one-launch evaluations so far (gncde_rows.hip); nullptr
 // only together with prepared = false (a standalone evaluation)
 // keep (optional, [L-1, B, n, d]): every hidden layer's output Z_{l+1} kept for the reverse mode (uniform width d);
-// dy is then not needed by the caller, and the stack split skips its read-out
+// dy is then not needed by the caller
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared = false, unsigned* bars = nullptr, float* keep = nullptr);
 // the workspace's fault word (a one-launch evaluation's barrier gave up): solver status 4 when set
@@ -237,19 +237,11 @@ bool rows_supported(const GncdeProblem& p);
 inline bool coef_is_bf16(const GncdeProblem& p) {
   return p.compute == GNCDE_COMPUTE_BF16_STORAGE || p.compute == GNCDE_COMPUTE_BF16_MFMA;
 }
-// pout / aux (the stack split, rows_stack_supported): the hidden stack writes the read-out's inputs there instead of dy
 int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum, const void* coefT,
                  const float* wperm, const uint16_t* wbf, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
-                 unsigned& bars_done, hipStream_t st, float* keep = nullptr, float* pout = nullptr,
-                 float* aux = nullptr);
-// the fp32 H = 64 CDE read-out split: a one-launch hidden stack (k_rows MODE 3) + readout_rows over all B n rows
-bool rows_stack_supported(const GncdeProblem& p);
-// an evaluation of this problem runs on k_rows (rows_supported or the stack split): group barriers, a fault word
+                 unsigned& bars_done, hipStream_t st, float* keep = nullptr);
+// an evaluation of this problem runs on k_rows: group barriers, a fault word
 bool rows_eval_used(const GncdeProblem& p);
-// dy[i, m] = tg_i (sum_{c,j} P[i, c] dX[i, j] W'[16 m + j, c] + q_i sum_j b'[16 m + j] dX[i, j]) over rows i < rows
-// (aux = [dX[16], q, tg, pad 2] per row; wperm: the read-out W' in permute_linear's CDE order): gncde_layer.hip
-void readout_rows(int rows, int H, const float* P, const float* aux, const float* wperm, const float* bf, float* dy,
-                  hipStream_t st);
 int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys,
                       int32_t* stats, char* ws, hipStream_t st);
 // k_coef_sums' per-plane reductions in a prepared evaluation workspace

@@ -439,88 +439,6 @@ __global__ void k_permute_linear(int rows, int din, int cde, const float* __rest
   out[e] = W[(size_t)row * din + 16 * cc + 4 * hi + s];
 }
 
-// The CDE wrapper's read-out (cde_wrapper_vector_field.py:19-26, de = 8) as ONE GEMM over the node rows of every
-// sample, after the one-launch hidden stack (gncde_rows.hip MODE 3) wrote P = (I + Abar_L) diag(inv) Z_L and
-// [dX[16], q_L, tg] per row:
-//   dy[i, m] = tg_i (sum_{c,j} P[i, c] dX[i, j] W'[16 m + j, c] + q_i sum_j b'[16 m + j] dX[i, j])
-// K = (c, j) = 16 H deep, the A operand P[i, c] dX[i, j] formed in registers per MFMA step (the same contraction as
-// k_layer's MODE 2).  A workgroup takes 32 consecutive rows of [B n] (rows of any samples: the read-out is row-wise),
-// so no row block is padded (n = 129: 258 full blocks at B = 64 instead of 64 one-row blocks), and wave w the 16
-// channels m = 16 w .. (H = 64: four column tiles) over both 16-row tiles; each W' operand load serves 32 rows.
-template <int H>
-__global__ void __launch_bounds__(256, 2) k_readout_rows(int rows, const float* __restrict__ P,
-                                                         const float* __restrict__ aux, const float* __restrict__ wperm,
-                                                         const float* __restrict__ bfv, float* __restrict__ dy) {
-  static_assert(H == 64, "one column tile per wave");
-  constexpr int NCC = H / 16, AX = 20;  // aux row: dX[16], q, tg, pad
-  __shared__ float sAux[32][AX + 1];
-  const int r0 = blockIdx.x * 32;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
-  const int ct = w;
-  const floatx4* W4 = reinterpret_cast<const floatx4*>(wperm);
-  // this lane's A-operand rows (16 t + lo): P[row][16 cc + 4 hi .. +3] and dX[row][0 .. 15], all in registers
-  floatx4 pr[2][NCC];
-  float dxr[2][16];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int row = r0 + 16 * t + lo < rows ? r0 + 16 * t + lo : rows - 1;  // clamped loads, masked stores
-#pragma unroll
-    for (int cc = 0; cc < NCC; ++cc) pr[t][cc] = *reinterpret_cast<const floatx4*>(P + (size_t)row * H + 16 * cc + 4 * hi);
-#pragma unroll
-    for (int j4 = 0; j4 < 4; ++j4) {
-      const floatx4 d = *reinterpret_cast<const floatx4*>(aux + (size_t)row * AX + 4 * j4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) dxr[t][4 * j4 + e] = d[e];
-    }
-  }
-  for (int e = tid; e < 32 * AX; e += 256) {
-    const int R = e / AX, c = e % AX;
-    sAux[R][c] = r0 + R < rows ? aux[(size_t)(r0 + R) * AX + c] : 0.f;
-  }
-  // K loop: per 16-deep c chunk all 16 j operand loads (one coalesced 1 KB wave load each) are issued a chunk ahead;
-  // the scheduling barriers keep the compiler from sinking each load to its first use (which waits out one L2
-  // round trip per load: 64 per wave)
-  floatx4 acc[2][2] = {{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}};
-  floatx4 wv[2][16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) wv[0][j] = W4[((ct * 16 + j) * NCC + 0) * 64 + lane];
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int cc = 0; cc < NCC; ++cc) {
-    if (cc + 1 < NCC)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) wv[(cc + 1) & 1][j] = W4[((ct * 16 + j) * NCC + cc + 1) * 64 + lane];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const floatx4 a0 = pr[0][cc] * dxr[0][j], a1 = pr[1][cc] * dxr[1][j];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {  // even / odd j into independent chains: no exposed MFMA result latency
-        acc[0][j & 1] = mfma4(a0[s], wv[cc & 1][j][s], acc[0][j & 1]);
-        acc[1][j & 1] = mfma4(a1[s], wv[cc & 1][j][s], acc[1][j & 1]);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  __syncthreads();  // sAux
-  const int m = 16 * ct + lo;
-  float bm[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) bm[j] = bfv[16 * m + j];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const floatx4 v = acc[t][0] + acc[t][1];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int R = 16 * t + 4 * hi + r;
-      float sb = 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) sb = fmaf(bm[j], sAux[R][j], sb);
-      if (r0 + R < rows) dy[(size_t)(r0 + R) * H + m] = sAux[R][17] * fmaf(sAux[R][16], sb, v[r]);
-    }
-  }
-}
-
 template <int DIN>
 size_t layer_smem(int n, bool bf) {
   constexpr int ZS = zs_stride<DIN>();
@@ -578,12 +496,6 @@ int layer_mode(const GncdeProblem& p, int l) {
 void permute_linear(int rows, int din, bool cde, const float* W, float* out, hipStream_t st) {
   const int tot = rows * din;
   hipLaunchKernelGGL(k_permute_linear, dim3((tot + 255) / 256), dim3(256), 0, st, rows, din, cde ? 1 : 0, W, out);
-}
-
-void readout_rows(int rows, int H, const float* P, const float* aux, const float* wperm, const float* bf, float* dy,
-                  hipStream_t st) {
-  if (H == 64)
-    hipLaunchKernelGGL(k_readout_rows<64>, dim3((rows + 31) / 32), dim3(256), 0, st, rows, P, aux, wperm, bf, dy);
 }
 
 void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, const float* Z, const float* wperm,

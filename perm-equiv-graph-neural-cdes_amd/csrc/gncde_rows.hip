@@ -52,7 +52,6 @@ constexpr int kStampEval = 20;
 constexpr int kRB = 16;      // node rows per workgroup
 constexpr int kMaxN = 256;   // per wave: four 16-column K chunks (fp32) or two 32-column chunks (bf16)
 constexpr int kStrip = 17;   // LDS row stride of the transposed column strip
-constexpr int kAux = 20;     // MODE 3: floats per row of the read-out's per-row inputs (dX[16], q_L, tg; 16-byte rows)
 
 // The persistent solve's controller inputs and outputs (GncdeSolver, PID controller)
 struct SolveArgs {
@@ -96,8 +95,6 @@ struct RowsArgs {
   unsigned* bar;           // [G] arrivals per group, monotonic within a solve
   unsigned bar0;           // barriers every group completed before this launch
   int* fault;              // set when a barrier wait gives up
-  float* pout;             // MODE 3: [B, n, H] the last layer's product P
-  float* aux;              // MODE 3: [B, n, kAux] dX[16], q_L, tg per row
   unsigned spin_limit;     // polls before a barrier wait gives up
   unsigned* ticket;        // solve: start-order tickets -> (sample, row block)
   unsigned ticket0;        // tickets taken before this launch
@@ -159,9 +156,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
 }
 
 // MODE 1: ODE output layer.  MODE 2: CDE read-out (de = 8, cde_hidden = H).  Three workgroups per CU (168 VGPRs)
-// for the ODE output, two for the CDE read-out (its weight slice is prefetched into registers).  MODE 3: the hidden
-// stack of a CDE vector field whose read-out runs as its own GEMM over all samples' rows (H = 64, config 3: a 16-row
-// workgroup would stream the whole 256 KB read-out weight per evaluation): the last layer stops at its product P.
+// for the ODE output, two for the CDE read-out (its weight slice is prefetched into registers).
 // BF (GNCDE_COMPUTE_BF16_MFMA): bfloat16 coefficients, and every product — (I + Abar_l) diag(inv) Z, the Linears, the
 // read-out — on v_mfma_f32_16x16x32_bf16 with single-plane bf16 operands rounded from the fp32 values (fp32
 // accumulation); the spline, the reductions, RMSNorm and all sums outside the MFMAs stay fp32.
@@ -674,32 +669,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       product(l);
       if constexpr (F32R && !PREF) load_wv();
       ROWS_STAMP(13);
-      if constexpr (MODE == 3) {
-        // the read-out's inputs for rows R (gncde_layer.hip k_readout_rows): P = (I + Abar_L)[R, :] diag(inv) Z_L
-        // (the four K parts summed in the fixed order of prow), and [dX[0 .. 15], q_L, tg] per row
-        constexpr int G4 = H / 4;
-        if (live) {
-          for (int e = tid; e < 16 * G4; e += 256) {
-            const int R = e / G4, c = 4 * (e % G4);
-            if (r0 + R < n) {
-              const float* p = big + R * ZS + c;
-              floatx4 v = *reinterpret_cast<const floatx4*>(p);
-#pragma unroll
-              for (int kp = 1; kp < 4; ++kp) v += *reinterpret_cast<const floatx4*>(p + kp * 16 * ZS);
-              *reinterpret_cast<floatx4*>(a.pout + ((size_t)b * n + r0 + R) * H + c) = v;
-            }
-          }
-          const int R = tid >> 4, j = tid & 15;
-          if (r0 + R < n) {
-            float* ax = a.aux + ((size_t)b * n + r0 + R) * kAux;
-            ax[j] = sDx[R * kStrip + j];
-            if (j == 0) {
-              ax[16] = sRow[(2 * L + l) * 16 + R];
-              ax[17] = sTg[R];
-            }
-          }
-        }
-      } else if constexpr (MODE == 1) {  // ODE: dy[R] = tg (P W'^T + q b'^T)
+      if constexpr (MODE == 1) {  // ODE: dy[R] = tg (P W'^T + q b'^T)
         for (int tile = w; tile < CT; tile += 4) {
           const floatx4 v = linear(l, tile);
 #pragma unroll
@@ -776,10 +746,10 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       const bool live = bs < a.B;
       const int b = live ? bs : a.B - 1;  // an idle round computes on a valid sample, keeps its barriers, stores no dy
       evaluate(b, a.t[b], a.y + (size_t)b * zgroup, false, live);
-      // dy rows R: 16-byte stores of the output tile (MODE 3 wrote the read-out's inputs itself)
+      // dy rows R: 16-byte stores of the output tile
       constexpr int G4 = H / 4;
       const int tid = threadIdx.x;
-      if (MODE != 3 && live && tid < 16 * G4) {
+      if (live && tid < 16 * G4) {
         const int R = tid / G4, q = tid % G4;
         if (r0 + R < n)
           *reinterpret_cast<floatx4*>(a.dy + ((size_t)b * n + r0 + R) * H + 4 * q) =
@@ -1189,11 +1159,6 @@ bool find_inst_t(int H, int mode, Inst& out) {
   return true;
 }
 bool find_inst(int H, int mode, bool bf, Inst& out) {
-  if (mode == 3) {  // the hidden stack of the H = 64 read-out (fp32)
-    if (bf || H != 64) return false;
-    out = inst<64, 3, false, 0>();
-    return true;
-  }
   return bf ? find_inst_t<true, 0>(H, mode, out) : find_inst_t<false, 0>(H, mode, out);
 }
 
@@ -1290,18 +1255,7 @@ bool rows_supported(const GncdeProblem& p) {
   return resident_blocks(k, rows_smem(p.n, H, p.L, false)) / nb >= p.B;
 }
 
-// The hidden stack + read-out GEMM split for the fp32 H = 64 CDE read-out (config 3): every other condition of the
-// one-launch evaluation, the stack's groups co-resident (one round per launch).
-bool rows_stack_supported(const GncdeProblem& p) {
-  if (p.compute != GNCDE_COMPUTE_FP32 || !rows_shape(p, true)) return false;
-  if (p.cde_hidden != 64) return false;
-  Inst k;
-  if (!find_inst(64, 3, false, k)) return false;
-  const int nb = (p.n + kRB - 1) / kRB;
-  return resident_blocks(k, rows_smem(p.n, 64, p.L, false)) / nb >= p.B;
-}
-
-bool rows_eval_used(const GncdeProblem& p) { return rows_supported(p) || rows_stack_supported(p); }
+bool rows_eval_used(const GncdeProblem& p) { return rows_supported(p); }
 
 #ifdef GNCDE_ROWS_STAMPS
 extern "C" int gncde_debug_rows_stamps(unsigned long long* host, int count) {
@@ -1314,9 +1268,9 @@ size_t rows_sync_ints(const GncdeProblem& p) { return align_up((size_t)p.B + 4, 
 // Launch one evaluation (RowsState: the group layout, fixed per problem, and the barriers done so far).
 int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum, const void* coefT,
                  const float* wperm, const uint16_t* wbf, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
-                 unsigned& bars_done, hipStream_t st, float* keep, float* pout, float* aux) {
+                 unsigned& bars_done, hipStream_t st, float* keep) {
   Inst k;
-  const int H = p.dims[0], mode = p.cde_hidden > 0 ? (pout ? 3 : 2) : 1;
+  const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
   const bool bfm = p.compute == GNCDE_COMPUTE_BF16_MFMA;
   if (!find_inst(H, mode, bfm, k)) return GNCDE_ERR_UNSUPPORTED;
   const size_t smem = rows_smem(p.n, H, p.L, bfm);
@@ -1355,8 +1309,6 @@ int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* d
   a.zbuf[0] = z0;
   a.zbuf[1] = z1;
   a.keep = keep;
-  a.pout = pout;
-  a.aux = aux;
   a.bar = bar;
   a.bar0 = bars_done;
   a.fault = fault;
