@@ -32,6 +32,8 @@
 // to the reference's W, b, rms_w, rms_b.
 #include "gncde_internal.h"
 
+#include <cstdlib>
+
 namespace gncde {
 namespace {
 
@@ -57,19 +59,23 @@ __device__ __forceinline__ float u2f(unsigned x) { return __builtin_bit_cast(flo
 
 __host__ __device__ constexpr int bwd_zs(int H) { return H + 4; }
 __host__ __device__ inline int bwd_np(int n) { return (n + 15) & ~15; }
-// rows of the two big regions: every node (NP), at least 80 (the 64 partial rows of the products + 16 result rows)
-__host__ __device__ inline int bwd_rows(int n) { return bwd_np(n) > 80 ? bwd_np(n) : 80; }
-// floats of region 1 (the form's strip + rows block, then zhat of every node, then the P partials and P[R])
-__host__ __device__ inline int bwd_big(int n, int H) {
-  const int np = bwd_np(n), z = bwd_rows(n) * bwd_zs(H), s = 2 * np * kStrip + 32 * (np + 4);
-  return ((z > s ? z : s) + 3) & ~3;
+constexpr int kMaxRbw = 3;  // row blocks per workgroup (one 256-thread group each)
+// floats of one group's form scratch: the column strip [2][NP][17] and the rows block [2][16][NP + 4]
+__host__ __device__ inline int bwd_form(int n) { return (2 * bwd_np(n) * kStrip + 32 * (bwd_np(n) + 4) + 3) & ~3; }
+// The union region, used in turn as (1) every group's form scratch, (2) zhat and g_P of every node [NP][H+4] each,
+// shared by the groups, (3) every group's product partials: P rows [80][H+4] (64 partial rows, 16 result rows),
+// then the g_zhat rows [80][H+4]
+__host__ __device__ inline int bwd_union(int n, int H, int rbw) {
+  const int f = rbw * bwd_form(n), z = 2 * bwd_np(n) * bwd_zs(H), e = rbw * 160 * bwd_zs(H);
+  const int m = f > z ? f : z;
+  return ((m > e ? m : e) + 3) & ~3;
 }
-inline size_t bwd_smem(int n, int H) {
+inline size_t bwd_smem(int n, int H, int rbw) {
   const int np = bwd_np(n);
-  // big | gP region [rows][H+4] | inv, gq, r, rd, c, cd, dg, dgd, v, w [10][NP] | u, q [2][16] | scratch [1280]
-  // | fusion sums [24][4]
-  return sizeof(float) * ((size_t)bwd_big(n, H) + (size_t)bwd_rows(n) * bwd_zs(H) + 10 * (size_t)np + 32 + 1280 +
-                          GNCDE_FC * 4);
+  // union | inv, gq, r, rd, c, cd, dg, dgd, v, w [10][NP] | u, q [kMaxRbw][2][16] | scratch [1280]
+  // | fusion sums [kMaxRbw][24][4]
+  return sizeof(float) * ((size_t)bwd_union(n, H, rbw) + 10 * (size_t)np + 32 * kMaxRbw + 1280 +
+                          (size_t)kMaxRbw * GNCDE_FC * 4);
 }
 
 struct BwdArgs {
@@ -97,28 +103,42 @@ struct BwdArgs {
   int cde_out;             // layer l is the CDE read-out layer
 };
 
-// One ConvLayer's reverse mode for a 16-row block R of one sample (see the file comment).
+// One ConvLayer's reverse mode for rbw = blockDim.x / 256 row blocks R of one sample (see the file comment): each
+// 256-thread group owns one 16-row block; the groups share the staging of every node's zhat and g_P (the widest
+// part of the launch's memory traffic) and the per-node reductions.  At config 3 (B = 64, nb = 9) three groups per
+// workgroup make the grid 192 workgroups, one round on 256 CUs, where one block per workgroup took three rounds (its
+// 90 KB of LDS admits one workgroup per CU).
 template <int H>
-__global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
+__global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int ZS = bwd_zs(H);
   constexpr int CT = H / 16;
   constexpr int KH = H / 4;  // MFMA K steps over a width-H contraction
   const int n = a.n, T = a.T, l = a.l;
-  const int NP = bwd_np(n), nch = NP >> 4, RWS = bwd_rows(n);
-  float* big = sm;
-  float* sG = big + bwd_big(n, H);     // g_P of every node [RWS][ZS]; later the g_zhat partials and g_zhat[R]
-  float* sInv = sG + (size_t)RWS * ZS;
+  const int NP = bwd_np(n), nch = NP >> 4;
+  const int NT = (int)blockDim.x, rbw = NT >> 8, grp = (int)threadIdx.x >> 8;
+  float* U = sm;
+  float* fs = U + grp * bwd_form(n);       // this group's form scratch
+  float* big = U;                          // zhat of every node [NP][ZS] (shared)
+  float* sG = U + (size_t)NP * ZS;         // g_P of every node [NP][ZS] (shared)
+  float* epP = U + (size_t)grp * 160 * ZS;  // this group's P partials [64][ZS] + P[R] [16][ZS]
+  float* epG = epP + 80 * ZS;               // this group's g_zhat partials + g_zhat[R]
+  float* sInv = U + bwd_union(n, H, rbw);
   float* sGq = sInv + NP;
   float* sF = sGq + NP;                // r, rd, c, cd, dg, dgd [6][NP]
   float* sV = sF + 6 * NP;             // v_l [NP]
   float* sW = sV + NP;                 // w_l [NP]
-  float* sRow = sW + NP;               // u_l [16], q_l [16] of the block's rows
-  float* sScr = sRow + 32;             // [1280] reduction scratch
-  float* sFus = sScr + 1280;           // [GNCDE_FC][4]
+  float* sRow = sW + NP + 32 * grp;    // u_l [16], q_l [16] of this group's rows
+  float* sScr = sW + NP + 32 * kMaxRbw;  // [1280] reduction scratch
+  float* sFus = sScr + 1280 + grp * GNCDE_FC * 4;  // [GNCDE_FC][4] of this group
 
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
-  const int b = blockIdx.x / a.nb, rb = blockIdx.x % a.nb;
+  const int tid = (int)threadIdx.x & 255, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
+  const int nbw = (a.nb + rbw - 1) / rbw;
+  const int b = blockIdx.x / nbw, rbr = (blockIdx.x % nbw) * rbw + grp;
+  // a group past the sample's last block recomputes that block (every barrier is the whole workgroup's) and stores
+  // nothing
+  const bool gact = rbr < a.nb;
+  const int rb = gact ? rbr : a.nb - 1, slot = b * a.nb + rb;
   const int r0 = rb * kRB, ri = r0 + lo;
   const size_t nn = (size_t)n * n, zgroup = (size_t)n * H;
   const float tb = a.t[b];
@@ -131,7 +151,7 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
   const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
   const auto crs = rsrc(cb, (unsigned)(4 * nn * sizeof(float)));
   const int RS = NP + 4;
-  float* sAr = big + 2 * NP * kStrip;
+  float* sAr = fs + 2 * NP * kStrip;
   const int rr = tid >> 4, cq = 4 * (tid & 15);
   const auto crt = rsrc(a.coefT + ((size_t)b * (T - 1) + idx) * 4 * nn, (unsigned)(4 * nn * sizeof(float)));
   u32x4 rc[4][4], sc[4][4];
@@ -175,8 +195,8 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
         const bool in = r0 + rr < n && kk < n;
         const unsigned x0 = sc[u][0][e], x1 = sc[u][1][e], x2 = sc[u][2][e], x3 = sc[u][3][e];
         const float cc[4] = {u2f(x0), u2f(x1), u2f(x2), u2f(x3)};
-        big[kk * kStrip + rr] = in ? cubic(cc, f) : 0.f;
-        big[(NP + kk) * kStrip + rr] = in ? dcubic(cc, f) : 0.f;
+        fs[kk * kStrip + rr] = in ? cubic(cc, f) : 0.f;
+        fs[(NP + kk) * kStrip + rr] = in ? dcubic(cc, f) : 0.f;
       }
   }
   // node features and this layer's families at every node (thread = node)
@@ -186,7 +206,7 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
     const float r = nin ? cubic(pv[0], f) : 0.f, rd = nin ? dcubic(pv[0], f) : 0.f;
     const float c = nin ? cubic(pv[1], f) : 0.f, cd = nin ? dcubic(pv[1], f) : 0.f;
     const float dg = nin ? cubic(pv[2], f) : 0.f, dgd = nin ? dcubic(pv[2], f) : 0.f;
-    if (tid < NP) {
+    if (grp == 0 && tid < NP) {  // the node vectors: one group writes them
       sF[tid] = r;
       sF[NP + tid] = rd;
       sF[2 * NP + tid] = c;
@@ -228,11 +248,11 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
     for (int s = 0; s < 4; ++s) {
       Ar[j][s] = ar[s];
       dAr[j][s] = dr[s];
-      At[j][s] = in ? big[(k0 + s) * kStrip + lo] : 0.f;
-      dAt[j][s] = in ? big[(NP + k0 + s) * kStrip + lo] : 0.f;
+      At[j][s] = in ? fs[(k0 + s) * kStrip + lo] : 0.f;
+      dAt[j][s] = in ? fs[(NP + k0 + s) * kStrip + lo] : 0.f;
     }
   }
-  __syncthreads();  // the strip's region becomes zhat
+  __syncthreads();  // the form scratch becomes zhat and g_P
 
   // ---- Z_l and g_P of every node ----------------------------------------------------------------------------
   {
@@ -240,27 +260,27 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
     const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.zin + (size_t)b * zgroup);
     const floatx4* P4 = reinterpret_cast<const floatx4*>(a.gP + (size_t)b * zgroup);
     const int tot = NP * G4, valid = n * G4;
-    for (int e0 = tid; e0 < tot; e0 += 256 * 4) {
+    for (int e0 = (int)threadIdx.x; e0 < tot; e0 += NT * 4) {
       floatx4 vz[4], vp[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int e = e0 + 256 * u;
+        const int e = e0 + NT * u;
         vz[u] = e < valid ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
         vp[u] = e < valid ? P4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int e = e0 + 256 * u;
+        const int e = e0 + NT * u;
         if (e < tot) {
           *reinterpret_cast<floatx4*>(big + (e / G4) * ZS + 4 * (e % G4)) = vz[u];
           *reinterpret_cast<floatx4*>(sG + (e / G4) * ZS + 4 * (e % G4)) = vp[u];
         }
       }
     }
-    for (int k = tid; k < NP; k += 256) sGq[k] = k < n ? a.gq[(size_t)b * n + k] : 0.f;
+    for (int k = (int)threadIdx.x; k < NP; k += NT) sGq[k] = k < n ? a.gq[(size_t)b * n + k] : 0.f;
   }
   __syncthreads();
-  for (int k = tid; k < NP; k += 256) {
+  for (int k = (int)threadIdx.x; k < NP; k += NT) {
     float ss = 0.f;
 #pragma unroll
     for (int q = 0; q < H / 4; ++q) {
@@ -271,7 +291,7 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
   }
   __syncthreads();
   // zsum = sum_k zhat_k and zf_x = sum_k zhat_k x_k (x = r, rd, c, cd): column c = tid % H, rows k = g mod NG
-  {
+  if (grp == 0) {
     constexpr int NG = 256 / H;
     const int c = tid % H, g = tid / H;
     float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -286,7 +306,7 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
   }
   __syncthreads();
   float* sZv = sScr + 1280 - 5 * H;  // zsum, zf_r, zf_rd, zf_c, zf_cd [5][H] (after the group partials)
-  for (int e = tid; e < 5 * H; e += 256) {
+  for (int e = tid; grp == 0 && e < 5 * H; e += 256) {
     // (NG * 5 H = 1280 floats: the total for (x, c) lands in the last group's slot for (x, c), which only this
     // thread reads, after reading it)
     constexpr int NG = 256 / H;
@@ -334,16 +354,16 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
       dsum[2] = fmaf(g, At[j][s], dsum[2]);
       dsum[3] = fmaf(g, dAt[j][s], dsum[3]);
     }
-    float bz[4][CT], bg[4][CT];
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        bz[s][ct] = big[(k0 + s) * ZS + 16 * ct + lo];
-        bg[s][ct] = sG[(k0 + s) * ZS + 16 * ct + lo];
-      }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
+      // (the B operands one k at a time: at H = 64 all four k's at once cost the registers a 3-group workgroup
+      // does not have)
+      float bz[1][CT], bg[1][CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        bz[0][ct] = big[(k0 + s) * ZS + 16 * ct + lo];
+        bg[0][ct] = sG[(k0 + s) * ZS + 16 * ct + lo];
+      }
       float v = fmaf(eA, Ar[j][s], fmaf(edA, dAr[j][s], fmaf(eTA, At[j][s], fmaf(eTdA, dAt[j][s], wi + vk[s]))));
       float vt = fmaf(eA, At[j][s], fmaf(edA, dAt[j][s], fmaf(eTA, Ar[j][s], fmaf(eTdA, dAr[j][s], wk[s] + vi))));
       if (k0 + s == ri) {
@@ -353,8 +373,8 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
       const float op = v * iv[s];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-        accP[ct] = mfma4(op, bz[s][ct], accP[ct]);
-        accT[ct] = mfma4(vt, bg[s][ct], accT[ct]);
+        accP[ct] = mfma4(op, bz[0][ct], accP[ct]);
+        accT[ct] = mfma4(vt, bg[0][ct], accT[ct]);
       }
     }
   }
@@ -405,13 +425,13 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
   facc[GNCDE_FC_ET_DA] += dsum[3];
   // this layer's own g_zhat / zhat rows are needed after the partials overwrite the node regions: the rows' Z and
   // inv stay available through HBM (zin) and sInv
-  __syncthreads();  // every read of zhat / g_P of all nodes done: the partial rows alias them
+  __syncthreads();  // every group's reads of zhat / g_P of all nodes done: the partial rows alias them
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      big[(w * 16 + 4 * hi + r) * ZS + 16 * ct + lo] = accP[ct][r];
-      sG[(w * 16 + 4 * hi + r) * ZS + 16 * ct + lo] = accT[ct][r];
+      epP[(w * 16 + 4 * hi + r) * ZS + 16 * ct + lo] = accP[ct][r];
+      epG[(w * 16 + 4 * hi + r) * ZS + 16 * ct + lo] = accT[ct][r];
     }
   // fusion sums: a butterfly per wave, then the four wave partials in order
 #pragma unroll
@@ -422,41 +442,41 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
     if (lane == 0) sFus[q * 4 + w] = v;
   }
   __syncthreads();
-  if (tid < GNCDE_FC) {
-    float* dst = a.gfc + ((size_t)blockIdx.x * a.L + l) * GNCDE_FC + tid;
+  if (gact && tid < GNCDE_FC) {
+    float* dst = a.gfc + ((size_t)slot * a.L + l) * GNCDE_FC + tid;
     *dst += (sFus[tid * 4] + sFus[tid * 4 + 1]) + (sFus[tid * 4 + 2] + sFus[tid * 4 + 3]);
   }
   // P[R], g_zhat[R]: the four K parts in a fixed order, into rows 64..79 of the two regions
   for (int e = tid; e < 16 * H; e += 256) {
     const int i = e / H, c = e % H;
-    float p = big[i * ZS + c], g = sG[i * ZS + c];
+    float p = epP[i * ZS + c], g = epG[i * ZS + c];
 #pragma unroll
     for (int kp = 1; kp < 4; ++kp) {
-      p += big[(kp * 16 + i) * ZS + c];
-      g += sG[(kp * 16 + i) * ZS + c];
+      p += epP[(kp * 16 + i) * ZS + c];
+      g += epG[(kp * 16 + i) * ZS + c];
     }
-    big[(64 + i) * ZS + c] = p;
-    sG[(64 + i) * ZS + c] = g;
+    epP[(64 + i) * ZS + c] = p;
+    epG[(64 + i) * ZS + c] = g;
   }
   __syncthreads();
-  const float* sP = big + 64 * ZS;   // P[R] [16][ZS]
-  const float* sGz = sG + 64 * ZS;   // g_zhat[R]
+  const float* sP = epP + 64 * ZS;   // P[R] [16][ZS]
+  const float* sGz = epG + 64 * ZS;  // g_zhat[R]
   // ---- parameter partials: g_W' += g_out[R]^T P[R], g_b' += g_out[R]^T q[R] (d_out = H), or P | q out (CDE) ----
   if (a.cde_out) {
     for (int e = tid; e < 16 * (H + 1); e += 256) {
       const int i = e / (H + 1), c = e % (H + 1);
-      if (r0 + i < n) a.pq[((size_t)b * n + r0 + i) * (H + 1) + c] = c < H ? sP[i * ZS + c] : sRow[16 + i];
+      if (gact && r0 + i < n) a.pq[((size_t)b * n + r0 + i) * (H + 1) + c] = c < H ? sP[i * ZS + c] : sRow[16 + i];
     }
   } else {
-    float* go = sG;  // g_out[R] staged in rows 0..15 of the g_P region (the partials are consumed)
+    float* go = epG;  // g_out[R] staged in rows 0..15 of the group's g partial region (the partials are consumed)
     for (int e = tid; e < 16 * H; e += 256) {
       const int i = e / H, c = e % H;
       go[i * ZS + c] = r0 + i < n ? a.gout[((size_t)b * n + r0 + i) * H + c] : 0.f;
     }
     __syncthreads();
-    float* gw = a.gw + (size_t)blockIdx.x * a.gw_stride + a.gw_off;
+    float* gw = a.gw + (size_t)slot * a.gw_stride + a.gw_off;
     // g_W'[j][c] += sum_{i in R} g_out[i][j] P[i][c]: CT x CT MFMA tiles over the waves, K = the 16 rows
-    for (int tile = w; tile < CT * CT; tile += 4) {
+    for (int tile = w; gact && tile < CT * CT; tile += 4) {
       const int jt = tile / CT, ct = tile % CT;
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -464,7 +484,7 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) gw[(16 * jt + 4 * hi + r) * H + 16 * ct + lo] += acc[r];
     }
-    if (tid < H) {
+    if (gact && tid < H) {
       float acc = 0.f;
 #pragma unroll
       for (int i = 0; i < kRB; ++i) acc = fmaf(go[i * ZS + tid], sRow[16 + i], acc);
@@ -477,7 +497,7 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
   {
     const int i = tid >> 4, cl = tid & 15;
     constexpr int U = H / 16;
-    const bool iin = r0 + i < n;
+    const bool iin = gact && r0 + i < n;
     const float inv = iin ? sInv[r0 + i] : 0.f;
     float z[U], gzh[U];
     float dot = 0.f;
@@ -498,7 +518,7 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) a.gz[((size_t)b * n + r0 + i) * H + cl + 16 * u] = gZ[u];
     } else {
-      float* go = sG;  // g_out_{l-1}[R] = g_Z * [Z_l > 0]
+      float* go = epG;  // g_out_{l-1}[R] = g_Z * [Z_l > 0]
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const float g = z[u] > 0.f ? gZ[u] : 0.f;
@@ -510,9 +530,9 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
   if (l == 0) return;
   __syncthreads();
   {
-    const float* go = sG;
+    const float* go = epG;
     // g_P_{l-1}[i][c] = sum_j g_out[i][j] W'_{l-1}[j][c]: wave ct's 16 x 16 tile, K = H (W' rows from L2)
-    if (w < CT) {
+    if (gact && w < CT) {
       const int ct = w;
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -522,7 +542,7 @@ __global__ void __launch_bounds__(256, 1) k_bwd_layer(BwdArgs a) {
       for (int r = 0; r < 4; ++r)
         if (r0 + 4 * hi + r < n) a.gP_next[((size_t)b * n + r0 + 4 * hi + r) * H + 16 * ct + lo] = acc[r];
     }
-    if (tid < kRB && r0 + tid < n) {
+    if (gact && tid < kRB && r0 + tid < n) {
       float acc = 0.f;
       for (int jo = 0; jo < H; ++jo) acc = fmaf(go[tid * ZS + jo], a.bprev[jo], acc);
       a.gq_next[(size_t)b * n + r0 + tid] = acc;
@@ -805,8 +825,27 @@ __global__ void k_bwd_params(int L, int H, int dlast, const float* __restrict__ 
 }
 
 template <int H>
-void launch_layer(const BwdArgs& a, int grid, size_t smem, hipStream_t st) {
-  hipLaunchKernelGGL((k_bwd_layer<H>), dim3(grid), dim3(256), smem, st, a);
+void launch_layer(const BwdArgs& a, int grid, int rbw, size_t smem, hipStream_t st) {
+  hipLaunchKernelGGL((k_bwd_layer<H>), dim3(grid), dim3(256 * rbw), smem, st, a);
+}
+
+// Row blocks per k_bwd_layer workgroup: the fewest that put the grid in one round on the device's CUs (one
+// workgroup per CU: the LDS), within kMaxRbw and the LDS limit.
+int bwd_rbw(const GncdeProblem& p, int nb) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0, v = 0;
+    cus = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+  }
+  if (const char* e = getenv("GNCDE_BWD_RBW")) {  // test hook: a fixed count (the partials do not depend on it)
+    const int v = atoi(e);
+    if (v >= 1 && v <= kMaxRbw && bwd_smem(p.n, p.dims[0], v) <= 160 * 1024) return v;
+  }
+  int r = 1;
+  while (r < kMaxRbw && (size_t)p.B * ((nb + r - 1) / r) > (size_t)cus && bwd_smem(p.n, p.dims[0], r + 1) <= 160 * 1024)
+    ++r;
+  return r;
 }
 
 bool set_smem(int H, size_t smem) {
@@ -929,7 +968,8 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     else if (H == 32) hipLaunchKernelGGL(k_bwd_head<32>, dim3(B * w.nb), dim3(256), 0, st, h);
     else hipLaunchKernelGGL(k_bwd_head<64>, dim3(B * w.nb), dim3(256), 0, st, h);
   }
-  const size_t smem = bwd_smem(n, H);
+  const int rbw = bwd_rbw(p, w.nb), grid = B * ((w.nb + rbw - 1) / rbw);
+  const size_t smem = bwd_smem(n, H, rbw);
   if (!set_smem(H, smem)) return GNCDE_ERR_HIP;
   int cur = 0;
   for (int l = L - 1; l >= 0; --l) {
@@ -962,9 +1002,9 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     a.gw_stride = w.gw_stride;
     a.gw_off = l * (H * H + H);
     a.cde_out = (cde && l == L - 1) ? 1 : 0;
-    if (H == 16) launch_layer<16>(a, B * w.nb, smem, st);
-    else if (H == 32) launch_layer<32>(a, B * w.nb, smem, st);
-    else launch_layer<64>(a, B * w.nb, smem, st);
+    if (H == 16) launch_layer<16>(a, grid, rbw, smem, st);
+    else if (H == 32) launch_layer<32>(a, grid, rbw, smem, st);
+    else launch_layer<64>(a, grid, rbw, smem, st);
     cur ^= 1;
   }
   if (cde) {

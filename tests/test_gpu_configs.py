@@ -361,3 +361,29 @@ def test_rows_grid_against_host_paced_and_oracle(G, method, save):
         e = rel_err(got, ref)
         print(f"  sample {b} ({len(grids[b]) - 1} steps) vs fp64 oracle {e:.2e}")
         assert e <= RTOL_SOLVE
+
+
+def test_bwd_row_blocks_per_workgroup_bitwise(G, monkeypatch):
+    """k_bwd_layer at config 3's shape (B = 64, n = 129: nine 16-row blocks per sample) with one, two and three row
+    blocks per workgroup (GNCDE_BWD_RBW; the default picks three there, one round on 256 CUs): every sample's
+    gradient is bitwise the same — the groups share only the staging of zhat and g_P, and each row block's partials
+    keep their own slots and summation order."""
+    B, n, T, H, de, L = 64, 129, 4, 64, 8, 3
+    rng, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(33, B, n, T, 3.0, H, de, L, distinct=4)
+    prob = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
+    grid, ns = G.layout.stack_grids([O.constant_grid(0.0, 0.3, 0.1)] * B)
+    spec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS, grid=grid, nsteps=ns)
+    ys = G.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda"))
+    gfin = torch.tensor(rng.standard_normal((B, n, H)), dtype=torch.float32, device="cuda")
+    spec.save_mode = G._lib.SAVE_T1
+    outs = {}
+    for r in ("1", "2", "3", None):
+        if r is None:
+            monkeypatch.delenv("GNCDE_BWD_RBW", raising=False)
+        else:
+            monkeypatch.setenv("GNCDE_BWD_RBW", r)
+        outs[r] = [x.clone() for x in G.integrate_vjp(prob, spec, ys, gfin)[:3]]
+    for r in ("2", "3", None):
+        for k in range(3):
+            assert torch.equal(outs[r][k], outs["1"][k]), (r, k)
+    assert all(torch.isfinite(x).all() for x in outs["1"])
