@@ -98,6 +98,7 @@ struct RowsArgs {
   unsigned spin_limit;     // polls before a barrier wait gives up
   unsigned* ticket;        // solve: start-order tickets -> (sample, row block)
   unsigned ticket0;        // tickets taken before this launch
+  int b0;                  // solve: the first sample of this launch (the batch runs in resident chunks)
   SolveArgs s;             // solve only
 };
 
@@ -139,15 +140,17 @@ __device__ __forceinline__ float coef_el(u32x4 v, int e) {
 __host__ __device__ constexpr int rows_zs(int H) { return H + 4; }
 __host__ __device__ inline int rows_np(int n, bool bf) { return bf ? (n + 31) & ~31 : (n + 15) & ~15; }
 // floats of the shared region: the strip [2][NP][17] and the rows block [2][16][NP+4] during the form, then Z_l
-// [NP][H+4] and the partials [4][16][H+4]
+// [NP][H+4]; after a layer's product the partials [4][16][H+4] (rows 0 .. 63) and the output tile [16][H+4] (rows
+// 64 .. 79: Z_l is consumed by then, and the tile is read before the next form writes the region)
 __host__ __device__ inline int rows_big(int n, int H, bool bf) {
-  const int np = rows_np(n, bf), z = (np > 64 ? np : 64) * rows_zs(H), s = 2 * np * kStrip + 32 * (np + 4);
+  const int np = rows_np(n, bf), z = (np > 80 ? np : 80) * rows_zs(H), s = 2 * np * kStrip + 32 * (np + 4);
   return ((z > s ? z : s) + 3) & ~3;
 }
 inline size_t rows_smem(int n, int H, int L, bool bf) {
   const int np = rows_np(n, bf);
-  // big | inv [NP] | v_l [L][NP] | w, u, q [3][L][16] | tg [16] | dX [16][17] | out tile [16][H+4] | red [4][64] x4
-  return sizeof(float) * ((size_t)rows_big(n, H, bf) + np + (size_t)L * np + 48 * L + 16 + 16 * kStrip + 16 * rows_zs(H) +
+  // big | inv [NP] | v_l [L][NP] | w, u, q [3][L][16] | tg [16] | dX [16][17] | red [4][64] x4
+  // (config 5, n = 255 h = 32 L = 4: 77.4 KiB, two workgroups per CU)
+  return sizeof(float) * ((size_t)rows_big(n, H, bf) + np + (size_t)L * np + 48 * L + 16 + 16 * kStrip +
                           4 * 64 * 4 + 4);
 }
 
@@ -179,8 +182,8 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
   float* sRow = sV + (size_t)L * NP;  // w_l [L][16], u_l [L][16], q_l [L][16]
   float* sTg = sRow + 48 * L;
   float* sDx = sTg + 16;
-  float* sOut = sDx + 16 * kStrip;
-  floatx4* red = reinterpret_cast<floatx4*>(sOut + 16 * ZS);
+  float* sOut = big + 64 * ZS;  // the output tile [16][ZS] (rows_big)
+  floatx4* red = reinterpret_cast<floatx4*>(sDx + 16 * kStrip);
   int* sFlag = reinterpret_cast<int*>(red + 4 * 64);  // [0] barrier gave up, [1] ticket
 
   // ---- which rows of which sample ------------------------------------------------------------------------------
@@ -210,6 +213,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     g = blockIdx.x / nb;
     rb = blockIdx.x % nb;
   }
+  if constexpr (SOLVE != 0) g += a.b0;  // the solve's groups are samples b0 .. b0 + G - 1 of the batch
   const int r0 = rb * kRB;
   const size_t nn = (size_t)n * n;
   const size_t zgroup = (size_t)n * H;
@@ -1087,6 +1091,8 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       for (;;) {
 #ifdef GNCDE_ROWS_STAMPS
         stamp_on = evals == kStampEval;
+        if (evals == kStampEval + 1 && threadIdx.x == 0)  // the next evaluation's start: the whole iteration
+          g_rows_stamps[stamp_slot * 16 + 15] = __builtin_amdgcn_s_memrealtime();
 #endif
         if (!evaluate(b, tst, a.zbuf[(pub - 1) & 1] + (size_t)b * zgroup, true, true)) {
           fault = true;
@@ -1191,6 +1197,18 @@ int resident_blocks(const Inst& k, size_t smem) {
   const int blocks = per * cus;
   if (used < 64) cache[used++] = Entry{dev, k.fn, smem, blocks};
   return blocks;
+}
+
+// compute units of the current device (cached per device)
+int cu_count() {
+  static std::mutex mu;
+  static int cached[64] = {0};
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!cached[dev] && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+    cached[dev] = cus;
+  return cached[dev];
 }
 
 // polls before a group barrier wait gives up (each poll is an L2 round trip plus s_sleep 1: seconds in all);
@@ -1319,8 +1337,8 @@ int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* d
 }
 
 // ---- the persistent solve ------------------------------------------------------------------------------------
-// Envelope: the one-launch evaluation's fp32 shapes for any batch (a group only waits for workgroups that have
-// started, so no residency condition beyond one group); Tsit5 + PID with SaveAt(t1) or SaveAt(ts), or a fixed grid
+// Envelope: the one-launch evaluation's fp32 shapes for any batch (run in chunks of co-resident groups: one group
+// must fit); Tsit5 + PID with SaveAt(t1) or SaveAt(ts), or a fixed grid
 // (RK4 / Tsit5) with SaveAt(t1) or every step (+ the stage record); the default dispatch (GNCDE_FLAG_GENERIC takes
 // the host-paced paths instead).
 bool rows_solve_shape(const GncdeProblem& p) {
@@ -1370,8 +1388,6 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   a.n = p.n;
   a.T = p.T;
   a.L = p.L;
-  // G = B (a multiple of 8) selects the XCD-affine layout: only when every group is resident at once
-  a.G = p.B % 8 == 0 && resident_blocks(k, smem) >= p.B * nb ? p.B : 0;
   a.rounds = 1;
   a.nb = nb;
   a.big = rows_big(p.n, H, false);
@@ -1416,7 +1432,25 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   v.step_ts = s.step_ts;
   v.stats = stats;
   v.part = part;
-  k.launch(a, p.B * nb, smem, st);
+  // The batch runs in chunks of co-resident groups, one launch each, at most one workgroup per CU.  A launch past
+  // residency starts later groups only as earlier solves finish, its resident groups sharing CUs with a
+  // start-order skew (config 5 at B = 64: 53.5 ms); and two workgroups per CU, though resident, double the
+  // coefficient stream each evaluation's form pulls through HBM / MALL at ~6 TB/s (130 KB per workgroup) and slow
+  // every group: config 5 at B = 32 took 93 us per iteration against 29.6 us at B = 16 (profiles/
+  // r04_config5_solve_stamps*.txt), so B = 64 runs as four B = 16 launches.  A chunk of a multiple of 8 samples takes
+  // the XCD-affine layout (G = its sample count); otherwise its workgroups take start-order tickets.
+  const int cap = std::min(resident_blocks(k, smem), cu_count()) / nb;
+  int bc = p.B < cap ? p.B : cap;
+  if (bc >= 8) bc &= ~7;
+  unsigned tickets = 0;
+  for (int c0 = 0; c0 < p.B; c0 += bc) {
+    const int nbc = p.B - c0 < bc ? p.B - c0 : bc;
+    a.b0 = c0;
+    a.G = nbc % 8 == 0 ? nbc : 0;
+    a.ticket0 = tickets;
+    if (a.G == 0) tickets += (unsigned)(nbc * nb);
+    k.launch(a, nbc * nb, smem, st);
+  }
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }
 

@@ -424,7 +424,7 @@ def test_generic_cde_full_size_properties(gncde, B, n, T, h, L, t1, dt):
     grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, t1, dt)] * B)
     spec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=grid, nsteps=ns)
     # config 3 (H = 64 read-out): the stack split per evaluation; config 5: the whole grid in one launch
-    assert G.integrate_path(prob, spec) == ("generic_rows" if h == 64 else "rows_grid<32,cde,tsit5>")
+    assert G.integrate_path(prob, spec) == ("generic" if h == 64 else "rows_grid<32,cde,tsit5>")
     ys1 = G.integrate(prob, spec, y0)
     ys2 = G.integrate(prob, spec, y0)
     assert torch.equal(ys1, ys2)

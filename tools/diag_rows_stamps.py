@@ -44,7 +44,14 @@ def main():
     assert fn(buf.ctypes.data, buf.size) == 0
     full = buf.reshape(nwg, 16).astype(np.float64)
     st = full[:, :15]
-    print(f"  rows-block Horner done (coefficient loads landed) at median {np.median((full[:, 15] - full[:, 0]) * 0.01):.2f} us")
+    if solve:  # slot 15: the start of the next evaluation
+        it = (full[:, 15] - full[:, 0]) * 0.01
+        ctl = (full[:, 15] - full[:, 14]) * 0.01
+        print(f"  solve iteration (evaluation start -> next evaluation start) median {np.median(it):.2f} us, of which "
+              f"controller + stage publication (read-out end -> next start) median {np.median(ctl):.2f} us")
+    else:
+        print(f"  rows-block Horner done (coefficient loads landed) at median "
+              f"{np.median((full[:, 15] - full[:, 0]) * 0.01):.2f} us")
     t0 = st[:, 0].min()
     rel = (st - t0) * 0.01  # us
     print(f"B={B} {compute}: launch span {rel[:, 14].max():.2f} us; first WG start {0:.2f}, last WG start "
