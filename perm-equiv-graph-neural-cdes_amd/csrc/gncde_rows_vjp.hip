@@ -24,8 +24,9 @@
 //                   zhat g_P^T, which meets A, dA, A^T, dA^T in registers for the dense contractions; then g_W'
 //                   partials, RMSNorm^T, the ReLU mask and the next layer's g_out, g_P, g_q (or the stage input's
 //                   cotangent at l = 0)
-//   k_bwd_readout   (CDE) the read-out weight and bias gradient on MFMA, split over 64-row slices of all samples
-//                   and H / 16 output-row groups
+//   k_bwd_head_gemm (CDE) g_P, g_q of the read-out layer as one GEMM over all samples' rows
+//   k_bwd_readout   (CDE) the read-out weight and bias gradient on MFMA, K = all samples' rows in a few chunks,
+//                   one workgroup per (chunk, 4 output m)
 //   k_bwd_data      (CDE data-spline cotangent, TGB) g_dX_ij = tg_i sum_m gF_im (P_i . W'[16m+j,:] + q_i b'[16m+j])
 // Parameter and fusion partials accumulate in per-(sample, row block) / per-chunk slots that only their owner
 // workgroup updates (fixed order, no atomics); k_bwd_finish reduces them once per reverse sweep and maps g_W', g_b'
@@ -43,7 +44,6 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kRB = 16;
 constexpr int kMaxN = 256;
 constexpr int kStrip = 17;
-constexpr int kRoRows = 64;   // rows per read-out gradient slice (with the m split below: 128 workgroups at config 5)
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -576,10 +576,7 @@ __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
   const int n = a.n, T = a.T, tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const int i = tid >> 4, cl = tid & 15;
-  __shared__ float sgo[kRB][H + 1];  // ODE g_out rows / CDE tg gF rows
-  __shared__ float sdx[kRB][17];
-  __shared__ float sK[kRB][H];       // CDE: sum_j dX_ij b'[16m + j] per (row, m)
-  __shared__ float spart[4][kRB][H + 1];
+  __shared__ float sgo[kRB][H + 1];  // ODE g_out rows
   const float tb = a.t[b];
   const float* tsb = a.ts + (size_t)b * T;
   const int idx = interval_index_wave(tsb, T, tb);
@@ -593,12 +590,12 @@ __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
     sgo[i][c] = g;
     if (iin) (a.cde ? a.tgF : a.gout)[((size_t)b * n + row) * H + c] = g;
   }
-  if (a.cde) {
+  if (a.cde) {  // tg gF and dX only: g_P, g_q are k_bwd_head_gemm's GEMM over all samples' rows
     const size_t blk = (size_t)n * 16;
     const float* dc = a.data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)row * 16 + cl;
     const float dx = iin ? fmaf(f, fmaf(3.0f * f, dc[0], 2.0f * dc[blk]), dc[2 * blk]) : 0.f;
-    sdx[i][cl] = dx;
     if (iin) a.dxo[((size_t)b * n + row) * 16 + cl] = dx;
+    return;
   }
   __syncthreads();
   if (!a.cde) {
@@ -619,117 +616,172 @@ __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
     }
     return;
   }
-  // CDE: g_P[i][c] = sum_{j, m} (tgF_im dX_ij) W'[16 m + j][c] — wave w takes j = w, w + 4, ..., K = m per j
-  {
-    floatx4 acc[CT];
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int jq = 0; jq < 4; ++jq) {
-      const int jj = w + 4 * jq;
-      const float dx = sdx[lo][jj];
-#pragma unroll
-      for (int s = 0; s < KH; ++s) {
-        const float av = sgo[lo][4 * s + hi] * dx;
-        const float* wr = a.wl + (size_t)(16 * (4 * s + hi) + jj) * H + lo;
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma4(av, wr[16 * ct], acc[ct]);
-      }
-    }
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) spart[w][4 * hi + r][16 * ct + lo] = acc[ct][r];
-  }
-  for (int m = cl; m < H; m += 16) {
-    float acc = 0.f;
-#pragma unroll
-    for (int jj = 0; jj < 16; ++jj) acc = fmaf(sdx[i][jj], a.bl[16 * m + jj], acc);
-    sK[i][m] = acc;
-  }
-  __syncthreads();
-  for (int c = cl; c < H; c += 16) {
-    const float g = (spart[0][i][c] + spart[1][i][c]) + (spart[2][i][c] + spart[3][i][c]);
-    if (iin) a.gP[((size_t)b * n + row) * H + c] = g;
-  }
-  if (cl == 0) {
-    float acc = 0.f;
-    for (int m = 0; m < H; ++m) acc = fmaf(sgo[i][m], sK[i][m], acc);
-    if (iin) a.gq[(size_t)b * n + row] = acc;
-  }
 }
 
-// CDE read-out weight / bias gradient over a kRoRows-row slice of all samples' nodes, on MFMA:
-//   part[slot][(16 m + j) (H + 1) + c] += sum_rows (tgF[r][m] dX[r][j]) (P | q)[r][c]
-// one 16-row output tile per m (its rows are the 16 j), N tiles over c = 0..H (zero past H), K = the slice's rows;
-// wave w takes m = w, w + 4, ... in batches of 4.
+// The CDE read-out layer's input cotangents as ONE GEMM over the node rows of every sample (the read-out is
+// row-wise; k_bwd_head wrote tgF = tg gF and dX per row):
+//   g_P[i][c] = sum_{m, j} (tgF_im dX_ij) W'[16 m + j][c],   g_q[i] = sum_m tgF_im sum_j dX_ij b'[16 m + j]
+// A workgroup takes 16 consecutive rows of [B n] (no padded per-sample blocks: n = 129 left a one-row block per
+// sample), wave w the output columns 16 (w % CT) .. and the m range of its K part (H < 64: the waves split m, summed
+// in LDS in a fixed order).  The A operand tgF_im dX_ij is formed in registers (dX_i. held for the whole K loop); W'
+// operands are issued a batch of m ahead, held apart from their use by scheduling barriers (the compiler otherwise
+// sinks each load to its MFMA: one L2 round trip per MFMA).
 template <int H>
-__global__ void __launch_bounds__(256) k_bwd_readout(int rows, const float* __restrict__ tgF,
-                                                     const float* __restrict__ dx, const float* __restrict__ pq,
-                                                     float* __restrict__ part) {
-  constexpr int NT = (H + 1 + 15) / 16, NC = NT * 16;
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* st = sm;                      // [kRoRows][H + 1]
-  float* sx = st + kRoRows * (H + 1);  // [kRoRows][17]
-  float* sp = sx + kRoRows * 17;       // [kRoRows][NC + 1]
-  const int r0 = blockIdx.x * kRoRows;
-  const int cnt = rows - r0 < kRoRows ? rows - r0 : kRoRows;
+__global__ void __launch_bounds__(256) k_bwd_head_gemm(int rows, const float* __restrict__ tgF,
+                                                       const float* __restrict__ dxo, const float* __restrict__ wl,
+                                                       const float* __restrict__ bl, float* __restrict__ gP,
+                                                       float* __restrict__ gq) {
+  constexpr int CT = H / 16, KP = 4 / CT, MP = H / KP;  // column tiles, waves per tile, m per wave
+  constexpr int MB = MP < 8 ? MP : 8;                   // m per W' batch
+  __shared__ float sg[16][H + 1];
+  __shared__ float sx[16][17];
+  __shared__ floatx4 red[4][64];
+  const int r0 = blockIdx.x * 16;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
-  for (int e = tid; e < kRoRows * H; e += 256) {
-    const int r = e / H, c = e % H;
-    st[r * (H + 1) + c] = r < cnt ? tgF[(size_t)(r0 + r) * H + c] : 0.f;
+  const int ct = w % CT, kp = w / CT, m0 = kp * MP;
+  // this wave's W' operands: row 16 m + 4 s + hi, column 16 ct + lo (issued before the staging waits)
+  const float* wb = wl + (size_t)(16 * m0 + hi) * H + 16 * ct + lo;
+  float wv[2][MB][4];
+#pragma unroll
+  for (int mm = 0; mm < MB; ++mm)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wv[0][mm][q] = wb[(size_t)(16 * mm + 4 * q) * H];
+  for (int e = tid; e < 16 * H; e += 256) {
+    const int R = e / H, c = e % H;
+    sg[R][c] = r0 + R < rows ? tgF[(size_t)(r0 + R) * H + c] : 0.f;
   }
-  for (int e = tid; e < kRoRows * 16; e += 256) {
-    const int r = e / 16, c = e % 16;
-    sx[r * 17 + c] = r < cnt ? dx[(size_t)(r0 + r) * 16 + c] : 0.f;
-  }
-  for (int e = tid; e < kRoRows * NC; e += 256) {
-    const int r = e / NC, c = e % NC;
-    sp[r * (NC + 1) + c] = (r < cnt && c <= H) ? pq[(size_t)(r0 + r) * (H + 1) + c] : 0.f;
+  {
+    const int R = tid >> 4, j = tid & 15;
+    sx[R][j] = r0 + R < rows ? dxo[(size_t)(r0 + R) * 16 + j] : 0.f;
   }
   __syncthreads();
-  float* dst = part + (size_t)blockIdx.x * 16 * H * (H + 1);
-  // gridDim.y = H / 16 workgroups share the slice, each the output rows m of its own m0 (disjoint partial rows)
-  for (int m0 = w + 16 * (int)blockIdx.y; m0 < H; m0 += 16 * (int)gridDim.y) {  // batch: m = m0, m0 + 4, m0 + 8, m0 + 12
-    floatx4 acc[4][NT];
+  float dxr[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 4; ++q) dxr[q] = sx[lo][4 * q + hi];
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[q][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < kRoRows / 4; ++s) {
-      const int r = 4 * s + hi;
-      const float xv = sx[r * 17 + lo];
-      float bv[NT];
+  for (int mb = 0; mb < MP; mb += MB) {
+    const int cur = (mb / MB) & 1;
+    if (mb + MB < MP)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bv[nt] = sp[r * (NC + 1) + 16 * nt + lo];
+      for (int mm = 0; mm < MB; ++mm)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = m0 + 4 * q;
-        if (m < H) {
-          const float av = st[r * (H + 1) + m] * xv;
+        for (int q = 0; q < 4; ++q) wv[cur ^ 1][mm][q] = wb[(size_t)(16 * (mb + MB + mm) + 4 * q) * H];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt) acc[q][nt] = mfma4(av, bv[nt], acc[q][nt]);
-        }
-      }
+    for (int mm = 0; mm < MB; ++mm) {
+      const float g = sg[lo][m0 + mb + mm];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = mfma4(g * dxr[q], wv[cur][mm][q], acc);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (KP > 1) {
+    red[w][lane] = acc;
+    __syncthreads();
+    if (kp == 0)
+#pragma unroll
+      for (int p = 1; p < KP; ++p) acc += red[w + p * CT][lane];
+  }
+  if (kp == 0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r0 + 4 * hi + r < rows) gP[(size_t)(r0 + 4 * hi + r) * H + 16 * ct + lo] = acc[r];
+  // g_q: row R = tid / 16, m = cl, cl + 16, ... then the 16 lanes of the row in a fixed butterfly
+  {
+    const int R = tid >> 4, cl = tid & 15;
+    float p = 0.f;
+    for (int m = cl; m < H; m += 16) {
+      float k = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) k = fmaf(sx[R][jj], bl[16 * m + jj], k);
+      p = fmaf(sg[R][m], k, p);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int m = m0 + 4 * q;
-      if (m < H)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int c = 16 * nt + lo;
-            if (c <= H) dst[(size_t)(16 * m + 4 * hi + rr) * (H + 1) + c] += acc[q][nt][rr];
-          }
-    }
+    for (int o = 8; o > 0; o >>= 1) p += __shfl_xor(p, o);
+    if (cl == 0 && r0 + R < rows) gq[r0 + R] = p;
   }
 }
 
-inline size_t readout_smem(int H) {
-  const int nc = ((H + 1 + 15) / 16) * 16;
-  return sizeof(float) * (size_t)kRoRows * ((H + 1) + 17 + nc + 1);
+// CDE read-out weight / bias gradient on MFMA, K = the node rows of every sample:
+//   part[slot][(16 m + j) (H + 1) + c] += sum_rows (tgF[r][m] dX[r][j]) (P | q)[r][c]
+// Workgroup (row chunk kc, m group): wave w owns m = 4 blockIdx.y + w, its 16 x 16 output tiles (rows j, columns c
+// = 0 .. H, zero past H) over the chunk's rows; the four waves share the chunk's dX and (P | q) rows, staged in LDS in
+// 64-row blocks whose global loads are issued one block ahead.  The chunks are few (one partial slot each, summed
+// by k_bwd_reduce once per sweep): the per-evaluation partial traffic is chunks x 16 H (H + 1) floats, and the grid
+// is chunks x H / 4 workgroups (~256).
+constexpr int kRoBlk = 64;
+inline int readout_chunks(int rows, int H) {
+  const int groups = H / 4, blocks = (rows + kRoBlk - 1) / kRoBlk;
+  int kc = (256 + groups - 1) / groups;
+  return kc < blocks ? kc : (blocks > 0 ? blocks : 1);
+}
+template <int H>
+__global__ void __launch_bounds__(256) k_bwd_readout(int rows, int rpc, const float* __restrict__ tgF,
+                                                     const float* __restrict__ dxo, const float* __restrict__ pq,
+                                                     float* __restrict__ part) {
+  constexpr int NT = (H + 1 + 15) / 16, NC = NT * 16, RB = kRoBlk;
+  constexpr int NPQ = (RB * (H + 1) + 255) / 256;
+  __shared__ float sx[RB][17];
+  __shared__ float sp[RB][NC + 1];
+  __shared__ float sg[RB][4];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
+  const int kc = blockIdx.x, mg = 4 * (int)blockIdx.y, m = mg + w;
+  const int rbeg = kc * rpc, rend = rows < rbeg + rpc ? rows : rbeg + rpc;
+  for (int e = tid; e < RB * (NC + 1); e += 256) (&sp[0][0])[e] = 0.f;  // columns past H stay zero
+  float rdx[4], rpq[NPQ], rtg;
+  auto gload = [&](int rb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u, row = rb + (e >> 4);
+      rdx[u] = row < rend ? dxo[(size_t)row * 16 + (e & 15)] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < NPQ; ++u) {
+      const int e = tid + 256 * u, row = rb + e / (H + 1);
+      rpq[u] = (e < RB * (H + 1) && row < rend) ? pq[(size_t)row * (H + 1) + e % (H + 1)] : 0.f;
+    }
+    const int row = rb + (tid >> 2);
+    rtg = row < rend ? tgF[(size_t)row * H + mg + (tid & 3)] : 0.f;
+  };
+  floatx4 acc[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) acc[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (rbeg < rend) gload(rbeg);
+  for (int rb = rbeg; rb < rend; rb += RB) {
+    __syncthreads();  // the previous block's reads are done (and the zero fill)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u;
+      sx[e >> 4][e & 15] = rdx[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NPQ; ++u) {
+      const int e = tid + 256 * u;
+      if (e < RB * (H + 1)) sp[e / (H + 1)][e % (H + 1)] = rpq[u];
+    }
+    sg[tid >> 2][tid & 3] = rtg;
+    __syncthreads();
+    if (rb + RB < rend) gload(rb + RB);  // the next block's loads fly under this block's MFMAs
+#pragma unroll 4
+    for (int s4 = 0; s4 < RB / 4; ++s4) {
+      const int r = 4 * s4 + hi;
+      const float av = sg[r][w] * sx[r][lo];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma4(av, sp[r][16 * nt + lo], acc[nt]);
+    }
+  }
+  if (m < H) {
+    float* dst = part + (size_t)kc * 16 * H * (H + 1);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int c = 16 * nt + lo;
+        if (c <= H) dst[(size_t)(16 * m + 4 * hi + rr) * (H + 1) + c] += acc[nt][rr];
+      }
+  }
 }
 
 // CDE data-spline cotangent (TGB): g_dX[i][j] = sum_m tgF_im (P_i . W'[16m+j, :] + q_i b'[16m+j]), scattered onto
@@ -885,7 +937,7 @@ size_t carve_rows_vjp(const GncdeProblem& p, char* ws, RowsVjpWs& w) {
   w.nb = (int)((n + kRB - 1) / kRB);
   w.slots = (int)B * w.nb;
   w.gw_stride = (int)((cde ? p.L - 1 : p.L) * (H * H + H));
-  w.ro_chunks = cde ? (int)((B * n + kRoRows - 1) / kRoRows) : 0;
+  w.ro_chunks = cde ? readout_chunks((int)(B * n), (int)H) : 0;
   size_t off = 0;
   auto take = [&](size_t floats) {
     float* ptr = ws ? reinterpret_cast<float*>(ws + off) : nullptr;
@@ -967,6 +1019,12 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     if (H == 16) hipLaunchKernelGGL(k_bwd_head<16>, dim3(B * w.nb), dim3(256), 0, st, h);
     else if (H == 32) hipLaunchKernelGGL(k_bwd_head<32>, dim3(B * w.nb), dim3(256), 0, st, h);
     else hipLaunchKernelGGL(k_bwd_head<64>, dim3(B * w.nb), dim3(256), 0, st, h);
+    if (cde) {
+      const dim3 g((B * n + 15) / 16);
+      if (H == 16) hipLaunchKernelGGL(k_bwd_head_gemm<16>, g, dim3(256), 0, st, B * n, w.tgF, w.dx, h.wl, h.bl, h.gP, h.gq);
+      else if (H == 32) hipLaunchKernelGGL(k_bwd_head_gemm<32>, g, dim3(256), 0, st, B * n, w.tgF, w.dx, h.wl, h.bl, h.gP, h.gq);
+      else hipLaunchKernelGGL(k_bwd_head_gemm<64>, g, dim3(256), 0, st, B * n, w.tgF, w.dx, h.wl, h.bl, h.gP, h.gq);
+    }
   }
   const int rbw = bwd_rbw(p, w.nb), grid = B * ((w.nb + rbw - 1) / rbw);
   const size_t smem = bwd_smem(n, H, rbw);
@@ -1008,14 +1066,11 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     cur ^= 1;
   }
   if (cde) {
-    const size_t rsm = readout_smem(H);
-    if (H == 16) hipLaunchKernelGGL(k_bwd_readout<16>, dim3(w.ro_chunks, 1), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
-    else if (H == 32) hipLaunchKernelGGL(k_bwd_readout<32>, dim3(w.ro_chunks, 2), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
-    else {
-      if (!ensure_dyn_lds(reinterpret_cast<const void*>(&k_bwd_readout<64>), rsm))  // 82 KB of LDS at H = 64
-        return GNCDE_ERR_HIP;
-      hipLaunchKernelGGL(k_bwd_readout<64>, dim3(w.ro_chunks, 4), dim3(256), rsm, st, B * n, w.tgF, w.dx, w.pq, w.gwo);
-    }
+    const int rows = B * n, rpc = ((rows + w.ro_chunks - 1) / w.ro_chunks + kRoBlk - 1) / kRoBlk * kRoBlk;
+    const dim3 g(w.ro_chunks, H / 4);
+    if (H == 16) hipLaunchKernelGGL(k_bwd_readout<16>, g, dim3(256), 0, st, rows, rpc, w.tgF, w.dx, w.pq, w.gwo);
+    else if (H == 32) hipLaunchKernelGGL(k_bwd_readout<32>, g, dim3(256), 0, st, rows, rpc, w.tgF, w.dx, w.pq, w.gwo);
+    else hipLaunchKernelGGL(k_bwd_readout<64>, g, dim3(256), 0, st, rows, rpc, w.tgF, w.dx, w.pq, w.gwo);
     if (gdata)
       hipLaunchKernelGGL(k_bwd_data, dim3((n * 16 + 255) / 256, B), dim3(256), 0, st, B, n, H, p.T, p.ts, t, w.tgF,
                          w.pq, wf + wo_last, bfold + bo_last, gdata);
