@@ -710,11 +710,11 @@ __global__ void __launch_bounds__(256) k_bwd_head_gemm(int rows, const float* __
 // = 0 .. H, zero past H) over the chunk's rows; the four waves share the chunk's dX and (P | q) rows, staged in LDS in
 // 64-row blocks whose global loads are issued one block ahead.  The chunks are few (one partial slot each, summed
 // by k_bwd_reduce once per sweep): the per-evaluation partial traffic is chunks x 16 H (H + 1) floats, and the grid
-// is chunks x H / 4 workgroups (~256).
+// is chunks x H / 4 workgroups (~512: two per CU hide each other's LDS and staging latency).
 constexpr int kRoBlk = 64;
 inline int readout_chunks(int rows, int H) {
   const int groups = H / 4, blocks = (rows + kRoBlk - 1) / kRoBlk;
-  int kc = (256 + groups - 1) / groups;
+  int kc = (512 + groups - 1) / groups;
   return kc < blocks ? kc : (blocks > 0 ? blocks : 1);
 }
 template <int H>
