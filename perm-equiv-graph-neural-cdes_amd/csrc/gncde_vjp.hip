@@ -298,27 +298,30 @@ __global__ void v_batch_sum(int B, size_t P, const float* __restrict__ x, float*
 }
 
 // ---- solver helpers ------------------------------------------------------------------------------------
+// step k's (t, h) per sample and, with `tc` (the tableau's stage fractions), every stage's time tst[i B + b]
+struct StageFracs {
+  int stages;
+  float c[7];
+};
 __global__ void v_step_geom(int B, int G, int k, const float* __restrict__ grid, const int32_t* __restrict__ nsteps,
-                            float* __restrict__ tcur, float* __restrict__ hcur) {
+                            float* __restrict__ tcur, float* __restrict__ hcur, StageFracs tc, float* __restrict__ tst) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   int ns = nsteps[b];
   ns = ns < 0 ? 0 : (ns > G - 1 ? G - 1 : ns);
   const float* g = grid + (size_t)b * G;
+  float t, h;
   if (k < ns) {
-    tcur[b] = g[k];
-    hcur[b] = g[k + 1] - g[k];
+    t = g[k];
+    h = g[k + 1] - g[k];
   } else {
-    tcur[b] = g[ns];
-    hcur[b] = 0.f;
+    t = g[ns];
+    h = 0.f;
   }
-}
-
-__global__ void v_stage_time(int B, float c, const float* __restrict__ tcur, const float* __restrict__ hcur,
-                             float* __restrict__ tst) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  tst[b] = stage_time(tcur[b], c, hcur[b]);
+  tcur[b] = t;
+  hcur[b] = h;
+  if (tst)
+    for (int i = 0; i < tc.stages; ++i) tst[(size_t)i * B + b] = stage_time(t, tc.c[i], h);
 }
 
 struct Lin {
@@ -410,7 +413,7 @@ struct VjpWs {
   float *cpart, *kpart, *dpart, *fpart;  // column-sum, split-K and dense-fusion partials
   float* rcpart;                 // per-tile row / column partial sums of G: [B, tiles1, 2, n]
   float *gsum, *gfc;             // batch-summed parameter gradient [P]; per-sample fusion gradient [B, L, 24]
-  float *y, *lam, *gyacc, *tmp;
+  float *y, *lam, *tmp;
   float* U[7];                   // stage inputs
   float* K[7];                   // stage values
   float* gK[7];                  // stage cotangents
@@ -467,7 +470,6 @@ void carve(const GncdeProblem& p, char* ws, VjpWs& w, size_t* bytes) {
   w.gfc = tk(B * p.L * GNCDE_FC);
   w.y = tk(B * E);
   w.lam = tk(B * E);
-  w.gyacc = tk(B * E);
   w.tmp = tk(B * E);
   for (int j = 0; j < 7; ++j) {
     w.U[j] = tk(B * E);
@@ -476,7 +478,7 @@ void carve(const GncdeProblem& p, char* ws, VjpWs& w, size_t* bytes) {
   }
   w.tcur = tk(B);
   w.hcur = tk(B);
-  w.tst = tk(B);
+  w.tst = tk(7 * (size_t)B);  // every stage's time of the current step [stage][B]
   *bytes = c.off;
 }
 
@@ -711,6 +713,9 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
   char* rows_ws = ws + bytes;
   char* vf_ws = rows_ws + (rows ? rows_vjp_workspace(p) : 0);
   const Tableau tab = s.method == GNCDE_RK4 ? rk4_tab() : tsit5_tab();
+  StageFracs tfr{};
+  tfr.stages = tab.stages;
+  for (int i = 0; i < tab.stages; ++i) tfr.c[i] = tab.c[i];
   generic_vf_prepare(p, vf_ws, st);
   if (!rows_eval_used(p) && rows_vjp_supported(p)) generic_vf_transpose(p, vf_ws, st);
   unsigned bars = 0;  // barriers of one-launch stage evaluations (generic_vf_eval)
@@ -738,7 +743,7 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
   else
     (void)hipMemcpyAsync(w.lam, gys, (size_t)B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
   for (int k = G - 2; k >= 0; --k) {
-    hipLaunchKernelGGL(v_step_geom, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, w.tcur, w.hcur);
+    hipLaunchKernelGGL(v_step_geom, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, w.tcur, w.hcur, tfr, w.tst);
     // checkpoint y_k (the forward's SAVE_STEPS output)
     hipLaunchKernelGGL(v_step_row, ge, dim3(256), 0, st, B, E, G, k, ys, w.y, 0);
     if (s.stage_rec) {  // the forward's stage record: U_0 = y_k, U_i (i >= 1) from slot (k, i-1); no recompute
@@ -758,9 +763,8 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
           lc.a[lc.nx++] = tab.a[i][j];
         }
       hipLaunchKernelGGL(v_lincomb, ge, dim3(256), 0, st, B, E, w.y, lc, w.hcur, w.U[i], 0);
-      hipLaunchKernelGGL(v_stage_time, dim3(gb), dim3(256), 0, st, B, tab.c[i], w.tcur, w.hcur, w.tst);
       if (i + 1 < tab.stages) {  // the last stage's value is not needed for the reverse sweep
-        const int rc = generic_vf_eval(p, w.tst, w.U[i], w.K[i], vf_ws, st, true, &bars);
+        const int rc = generic_vf_eval(p, w.tst + (size_t)i * B, w.U[i], w.K[i], vf_ws, st, true, &bars);
         if (rc) return rc;
       }
     }
@@ -773,17 +777,17 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
       }
       hipLaunchKernelGGL(v_seed_all, ge, dim3(256), 0, st, B, E, G - 1, tab.stages, k, w.lam, w.hcur, gstage, sd);
     }
-    (void)hipMemcpyAsync(w.gyacc, w.lam, (size_t)B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
+    // gy accumulates in lam itself: the seeds above are the only readers of the step's incoming lam
     for (int i = tab.stages - 1; i >= 0; --i) {
-      hipLaunchKernelGGL(v_stage_time, dim3(gb), dim3(256), 0, st, B, tab.c[i], w.tcur, w.hcur, w.tst);
-      // tmp = cotangent of U_i
-      (void)hipMemsetAsync(w.tmp, 0, (size_t)B * E * sizeof(float), st);
+      const float* tsti = w.tst + (size_t)i * B;
+      // tmp = cotangent of U_i (the per-layer reverse overwrites every element; the generic one accumulates)
       if (rows) {
-        const int rc = rows_vf_vjp(p, w.tst, w.U[i], w.gK[i], w.tmp, gdata, generic_vf_csum(p, vf_ws), w.wf, w.bf,
+        const int rc = rows_vf_vjp(p, tsti, w.U[i], w.gK[i], w.tmp, gdata, generic_vf_csum(p, vf_ws), w.wf, w.bf,
                                    rows_ws, vf_ws, &bars, st);
         if (rc) return rc;
       } else {
-        vf_vjp(p, w.tst, w.U[i], w.gK[i], w.tmp, gdata, w, st);
+        (void)hipMemsetAsync(w.tmp, 0, (size_t)B * E * sizeof(float), st);
+        vf_vjp(p, tsti, w.U[i], w.gK[i], w.tmp, gdata, w, st);
       }
       // gy += tmp ; gK_j += h a_ij tmp (one launch)
       Scatter sc{};
@@ -792,9 +796,8 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
           sc.gk[sc.n] = w.gK[j];
           sc.a[sc.n++] = tab.a[i][j];
         }
-      hipLaunchKernelGGL(v_stage_scatter, ge, dim3(256), 0, st, B, E, w.tmp, w.hcur, w.gyacc, sc);
+      hipLaunchKernelGGL(v_stage_scatter, ge, dim3(256), 0, st, B, E, w.tmp, w.hcur, w.lam, sc);
     }
-    (void)hipMemcpyAsync(w.lam, w.gyacc, (size_t)B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
     if (s.save_mode == GNCDE_SAVE_STEPS)
       hipLaunchKernelGGL(v_step_row, ge, dim3(256), 0, st, B, E, G, k, gys, w.lam, 1);
   }
