@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GNCDE_ABI_VERSION 6
+#define GNCDE_ABI_VERSION 7
 #define GNCDE_MAX_LAYERS 8
 #define GNCDE_FC 24
 
@@ -171,6 +171,15 @@ typedef struct GncdeSolver {
   float* stage_rec;
   int64_t stage_rec_len;
   int32_t flags;                     /* GNCDE_FLAG_* (0 = default dispatch) */
+  /* GRID only, optional (NULL = not recorded / recomputed; ABI 7): the activation record, [G-1, S, L-1, B, n, H] —
+   * every stage evaluation's hidden-layer outputs Z_1 .. Z_{L-1} (S = 4 RK4 / 6 Tsit5 stages of every step), each
+   * (step, stage) slab in the layout the per-layer reverse mode reads.  gncde_integrate WRITES it and
+   * gncde_integrate_vjp* READ it instead of re-running every stage's forward (288 GB of HBM per GPU: the forward
+   * keeps what the reverse would recompute).  Only where gncde_activation_record_floats() is nonzero (an fp32
+   * multi-kernel forward whose reverse takes the per-layer kernels: BASELINE config 3's shape); act_rec_len must
+   * equal it (else GNCDE_ERR_ARG).  Batch-major: a caller that shards the batch records per shard. */
+  float* act_rec;
+  int64_t act_rec_len;
 } GncdeSolver;
 
 /* Library / error helpers */
@@ -184,6 +193,11 @@ int gncde_integrate_path(const GncdeProblem* prob, const GncdeSolver* solver, ch
  * an fp32 GRID solve with G >= 2, else 0 (PID controller: its reverse mode replays the accepted steps as a GRID
  * solve, which takes the record; bf16 modes: their reverse sweep recomputes the stages, no record).  Never fails; 0 for invalid arguments. */
 size_t gncde_stage_record_floats(const GncdeProblem* prob, const GncdeSolver* solver);
+
+/* Floats of the activation record (GncdeSolver.act_rec, the whole batch) for this problem and solver:
+ * (G-1)*S*(L-1)*B*n*H where the forward takes the multi-kernel fixed-grid path and the reverse the per-layer
+ * kernels, else 0 (no record is written or read).  Never fails; 0 for invalid arguments.  (ABI 7) */
+size_t gncde_activation_record_floats(const GncdeProblem* prob, const GncdeSolver* solver);
 
 /* Workspace bytes needed by gncde_vf_eval (solver == NULL) or gncde_integrate. */
 size_t gncde_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* solver);

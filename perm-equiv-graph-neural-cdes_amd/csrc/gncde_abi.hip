@@ -38,6 +38,18 @@ size_t record_floats(const GncdeProblem& p, const GncdeSolver& s) {
   return (size_t)(s.grid_len - 1) * (S - 1) * (size_t)p.n * (size_t)p.dims[0];
 }
 
+// Floats of the activation record (gncde.h): the multi-kernel fixed-grid forward (not the fused kernel, not the
+// persistent solve) whose reverse sweep takes the per-layer kernels
+bool use_fused(const GncdeProblem& p, const GncdeSolver& s, char* name, size_t len);
+bool use_stage_vjp(const GncdeProblem& p, const GncdeSolver& s);
+size_t act_floats(const GncdeProblem& p, const GncdeSolver& s) {
+  if (s.controller != GNCDE_CTRL_GRID || p.compute != GNCDE_COMPUTE_FP32 || s.grid_len < 2 || p.L < 2) return 0;
+  if (use_fused(p, s, nullptr, 0) || use_stage_vjp(p, s) || rows_pid_supported(p, s) || !rows_vjp_supported(p))
+    return 0;
+  const size_t S = s.method == GNCDE_RK4 ? 4 : 6;
+  return (size_t)(s.grid_len - 1) * S * (size_t)(p.L - 1) * (size_t)p.B * (size_t)p.n * (size_t)p.dims[0];
+}
+
 int validate_solver(const GncdeProblem* p, const GncdeSolver* s) {
   if (!s) return GNCDE_ERR_ARG;
   if (s->flags & ~GNCDE_FLAG_GENERIC) return GNCDE_ERR_ARG;
@@ -50,7 +62,13 @@ int validate_solver(const GncdeProblem* p, const GncdeSolver* s) {
     // a record must be exactly the one this solve writes / its sweep reads (none exists for the bf16 modes)
     if (s->stage_rec && (s->stage_rec_len <= 0 || (size_t)s->stage_rec_len != record_floats(*p, *s)))
       return GNCDE_ERR_ARG;
+    if (s->act_rec) {
+      GncdeSolver q = *s;
+      q.act_rec = nullptr;
+      if (s->act_rec_len <= 0 || (size_t)s->act_rec_len != act_floats(*p, q)) return GNCDE_ERR_ARG;
+    }
   } else if (s->controller == GNCDE_CTRL_PID) {
+    if (s->act_rec) return GNCDE_ERR_ARG;
     // the single-plane bf16 mode puts ~1e-2 relative noise into every stage, which the embedded error estimate
     // reads as truncation error: at rtol 1e-3 the controller takes 12-21x the evaluations, so
     // the mode is for fixed grids (ConstantStepSize, the reference's own PGT / TGB solves) only
@@ -91,6 +109,8 @@ GncdeProblem fp32_view(const GncdeProblem& p, size_t& head) {
   return q;
 }
 
+}  // namespace
+
 // GNCDE_FLAG_GENERIC forces the generic forward and the generic reverse sweep (gncde.h)
 bool use_fused(const GncdeProblem& p, const GncdeSolver& s, char* name, size_t len) {
   return !(s.flags & GNCDE_FLAG_GENERIC) && fused_supported(p, s, name, len);
@@ -98,8 +118,6 @@ bool use_fused(const GncdeProblem& p, const GncdeSolver& s, char* name, size_t l
 bool use_stage_vjp(const GncdeProblem& p, const GncdeSolver& s) {
   return !(s.flags & GNCDE_FLAG_GENERIC) && stage_vjp_supported(p, s);
 }
-
-}  // namespace
 
 }  // namespace gncde
 
@@ -128,6 +146,15 @@ size_t gncde_stage_record_floats(const GncdeProblem* prob, const GncdeSolver* so
   s.stage_rec = nullptr;
   if (validate_solver(prob, &s) != GNCDE_OK) return 0;
   return record_floats(*prob, s);
+}
+
+size_t gncde_activation_record_floats(const GncdeProblem* prob, const GncdeSolver* solver) {
+  if (validate_problem(prob) != GNCDE_OK || !solver) return 0;
+  GncdeSolver s = *solver;  // the records themselves are not part of the question
+  s.stage_rec = nullptr;
+  s.act_rec = nullptr;
+  if (validate_solver(prob, &s) != GNCDE_OK) return 0;
+  return act_floats(*prob, s);
 }
 
 size_t gncde_workspace_bytes(const GncdeProblem* prob, const GncdeSolver* solver) {

@@ -781,7 +781,7 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool ro
 }
 
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st, bool prepared, unsigned* bars, float* keep) {
+                    hipStream_t st, bool prepared, unsigned* bars, float* keep, bool need_dy) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
   VfWs w;
@@ -806,7 +806,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     const int din = p.dims[l], dout = p.dims[l + 1];
     float* Zout = keep && l + 1 < p.L ? keep + (size_t)l * B * n * p.dims[l + 1] : bufs[l & 1];
     const bool last = l == p.L - 1;
-    if (keep && last) break;  // a keep forward serves the reverse sweep: it reads the kept layers, never dy
+    if (!need_dy && last) break;  // a reverse sweep's keep forward reads the kept layers, never dy
     // A widening layer (d_out > d_in: the CDE wrapper's h -> h*de*2 read-out layer) is evaluated in the
     // reassociated order (I + Abar)(diag(inv) Z W'^T + 1 b'^T) = ((I + Abar) diag(inv) Z) W'^T + q b'^T with
     // q = (I + Abar) 1: the n x n product runs at width d_in instead of d_out (configs 3 / 5: 16x / 16x fewer
@@ -912,7 +912,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     bo += dout;
     Zin = Zout;
   }
-  if (fused_out || keep) return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
+  if (fused_out || !need_dy) return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
   const int dout = out_dim(p);
   hipLaunchKernelGGL(k_finalize, dim3(cdiv((size_t)n * dout, 256), B), dim3(256), 0, st, n,
                      p.dims[p.L], p.cde_hidden, p.cde_embed, p.T, p.ts, p.data_coef, t, w.tg, Zin,
@@ -986,9 +986,17 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   // Every evaluation's stage time tst is written by the launch before it (k_grid_step for c = 0, k_combo for the
   // others); the step's y <- y_{k+1} and Tsit5's FSAL k1 <- k7 are pointer swaps, not copies.
   unsigned bars = 0;
-  auto eval = [&](const float* yin, float* out) { return generic_vf_eval(p, tst, yin, out, ws, st, true, &bars); };
-  // stage record (GncdeSolver.stage_rec): the stage input U_i of step k goes to slot (k, i-1) as it is formed
+  // activation record (GncdeSolver.act_rec): stage i of step k keeps its hidden outputs in slab (k, i)
   const int S = s.method == GNCDE_RK4 ? 4 : 6;
+  const size_t slab = (size_t)(p.L - 1) * B * E;
+  auto act = [&](int k, int i) -> float* {
+    return s.act_rec && k < G - 1 ? s.act_rec + ((size_t)k * S + i) * slab : nullptr;
+  };
+  float* keep_next = nullptr;  // the keep slab of the next evaluation
+  auto eval = [&](const float* yin, float* out) {
+    return generic_vf_eval(p, tst, yin, out, ws, st, true, &bars, keep_next);
+  };
+  // stage record (GncdeSolver.stage_rec): the stage input U_i of step k goes to slot (k, i-1) as it is formed
   float* rec = G >= 2 ? s.stage_rec : nullptr;
   int rec_k = 0, rec_i = 0;  // slot of the next combination's output (rec_i == 0: not recorded)
   auto combo = [&](std::initializer_list<std::pair<int, float>> terms, float* out, float c_next, bool has_next) {
@@ -1013,8 +1021,10 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   // K[j]).  (Folding the combination into the read-out k_layer's epilogue measured slower at config 3, 15.8 vs
   // 15.15 ms per solve: the epilogue's dependent K loads lengthen the critical launch by more than k_combo costs.)
   int rc = GNCDE_OK;
+  int cur_k = 0;  // the step eval_combo's evaluations belong to (activation slab (cur_k, j))
   auto eval_combo = [&](const float* yin, int j, std::initializer_list<std::pair<int, float>> terms, float* out,
                         float c_next, bool has_next) {
+    keep_next = act(cur_k, j);
     rc |= eval(yin, K[j]);
     combo(terms, out, c_next, has_next);
   };
@@ -1025,6 +1035,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
       hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst);
       rec_k = k;
       rec_i = 1;
+      cur_k = k;
       eval_combo(y, 0, {{0, 0.5f}}, yt, 0.5f, true);
       rec_i = 2;
       eval_combo(yt, 1, {{1, 0.5f}}, yt, 0.5f, true);
@@ -1039,9 +1050,11 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     }
   } else {  // Tsit5 on the grid (ConstantStepSize), FSAL
     hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, 0, s.grid, s.nsteps, tcur, hcur, tst);
+    keep_next = act(0, 0);
     rc |= eval(y, K[0]);
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
       hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst);
+      cur_k = k;
       rec_k = k;
       rec_i = 1;
       combo({{0, TSIT5_A21}}, yt, TSIT5_C2, true);  // K[0] is the FSAL value; k_grid_step set this step's h
@@ -1057,6 +1070,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
       rec_i = 0;
       eval_combo(yt, 5, {{0, TSIT5_B1}, {1, TSIT5_B2}, {2, TSIT5_B3}, {3, TSIT5_B4}, {4, TSIT5_B5}, {5, TSIT5_B6}},
                  yt, 1.0f, true);
+      keep_next = act(k + 1, 0);  // the FSAL evaluation is the next step's stage 0
       rc |= eval(yt, K[6]);
       std::swap(y, yt);
       std::swap(K[0], K[6]);

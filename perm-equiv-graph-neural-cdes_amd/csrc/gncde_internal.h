@@ -94,6 +94,20 @@ __device__ __forceinline__ float xor_sum_rows4(float v) {
   return x + y;
 }
 
+// Sum over all 64 lanes, result in every lane: DPP within each 16-lane row (quad swaps, then the half-row and row
+// mirrors), then the gfx950 row swaps (xor_sum_rows4).  No LDS and no lane-index arithmetic.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum64(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  return xor_sum_rows4(v);
+}
+
 // equinox RMSNorm scale rsqrt(mean(x^2) + eps) on the hardware reciprocal square root (1 ulp; the
 // parity tolerances are fp32-accumulation bounds).
 __device__ __forceinline__ float rms_inv(float sumsq, float inv_d) {
@@ -225,9 +239,10 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool ro
 // bars: the solve's count of per-group barriers done by one-launch evaluations so far (gncde_rows.hip); nullptr
 // only together with prepared = false (a standalone evaluation)
 // keep (optional, [L-1, B, n, d]): every hidden layer's output Z_{l+1} kept for the reverse mode (uniform width d);
-// dy is then not needed by the caller
+// need_dy = false (a reverse sweep's keep forward): dy is not wanted and the multi-kernel path skips the read-out
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st, bool prepared = false, unsigned* bars = nullptr, float* keep = nullptr);
+                    hipStream_t st, bool prepared = false, unsigned* bars = nullptr, float* keep = nullptr,
+                    bool need_dy = true);
 // the workspace's fault word (a one-launch evaluation's barrier gave up): solver status 4 when set
 const int* generic_vf_fault(const GncdeProblem& p, char* ws);
 
@@ -256,9 +271,11 @@ void generic_vf_transpose(const GncdeProblem& p, char* ws, hipStream_t st);
 bool rows_vjp_supported(const GncdeProblem& p);
 size_t rows_vjp_workspace(const GncdeProblem& p);
 void rows_vjp_begin(const GncdeProblem& p, char* ws, hipStream_t st);
+// kept (optional): the stage's hidden outputs [L-1, B, n, H] from the forward's activation record (GncdeSolver.act_rec);
+// without it the evaluation's forward runs first in keep mode
 int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* gF, float* gu, float* gdata,
                 const float* csum, const float* wf, const float* bfold, char* ws, char* vf_ws, unsigned* bars,
-                hipStream_t st);
+                hipStream_t st, const float* kept = nullptr);
 void rows_vjp_finish(const GncdeProblem& p, char* ws, float* gparams, float* gfusion, hipStream_t st);
 
 // the persistent solve on the one-launch evaluation (gncde_rows.hip): n <= 256, one width; Tsit5 + PIDController

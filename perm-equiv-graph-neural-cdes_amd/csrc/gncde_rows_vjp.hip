@@ -60,6 +60,16 @@ __device__ __forceinline__ float u2f(unsigned x) { return __builtin_bit_cast(flo
 __host__ __device__ constexpr int bwd_zs(int H) { return H + 4; }
 __host__ __device__ inline int bwd_np(int n) { return (n + 15) & ~15; }
 constexpr int kMaxRbw = 3;  // row blocks per workgroup (one 256-thread group each)
+
+// Phase stamps of k_bwd_layer (diagnostic build -DGNCDE_BWD_STAMPS only: tools/diag_bwd_stamps.py): the first wave
+// of every workgroup records s_memrealtime at 12 points of the last launch.
+#ifdef GNCDE_BWD_STAMPS
+__device__ unsigned long long g_bwd_stamps[1024 * 16];
+#define BWD_STAMP(k) \
+  do { if (threadIdx.x == 0 && a.l == 1 && blockIdx.x < 1024) g_bwd_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define BWD_STAMP(k) do {} while (0)
+#endif
 // floats of one group's form scratch: the column strip [2][NP][17] and the rows block [2][16][NP + 4]
 __host__ __device__ inline int bwd_form(int n) { return (2 * bwd_np(n) * kStrip + 32 * (bwd_np(n) + 4) + 3) & ~3; }
 // The union region, used in turn as (1) every group's form scratch, (2) zhat and g_P of every node [NP][H+4] each,
@@ -72,9 +82,9 @@ __host__ __device__ inline int bwd_union(int n, int H, int rbw) {
 }
 inline size_t bwd_smem(int n, int H, int rbw) {
   const int np = bwd_np(n);
-  // union | inv, gq, r, rd, c, cd, dg, dgd, v, w [10][NP] | u, q [kMaxRbw][2][16] | scratch [1280]
+  // union | inv, gq, r, rd, c, cd, dg, dgd, v, w [10][NP] | u, q [kMaxRbw][2][16] | scratch [1280 kMaxRbw]
   // | fusion sums [kMaxRbw][24][4]
-  return sizeof(float) * ((size_t)bwd_union(n, H, rbw) + 10 * (size_t)np + 32 * kMaxRbw + 1280 +
+  return sizeof(float) * ((size_t)bwd_union(n, H, rbw) + 10 * (size_t)np + 32 * kMaxRbw + 1280 * kMaxRbw +
                           (size_t)kMaxRbw * GNCDE_FC * 4);
 }
 
@@ -129,8 +139,8 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   float* sV = sF + 6 * NP;             // v_l [NP]
   float* sW = sV + NP;                 // w_l [NP]
   float* sRow = sW + NP + 32 * grp;    // u_l [16], q_l [16] of this group's rows
-  float* sScr = sW + NP + 32 * kMaxRbw;  // [1280] reduction scratch
-  float* sFus = sScr + 1280 + grp * GNCDE_FC * 4;  // [GNCDE_FC][4] of this group
+  float* sScr = sW + NP + 32 * kMaxRbw;  // [1280 kMaxRbw] reduction scratch (5 H floats per node group)
+  float* sFus = sScr + 1280 * kMaxRbw + grp * GNCDE_FC * 4;  // [GNCDE_FC][4] of this group
 
   const int tid = (int)threadIdx.x & 255, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const int nbw = (a.nb + rbw - 1) / rbw;
@@ -140,12 +150,23 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   const bool gact = rbr < a.nb;
   const int rb = gact ? rbr : a.nb - 1, slot = b * a.nb + rb;
   const int r0 = rb * kRB, ri = r0 + lo;
+  BWD_STAMP(0);
   const size_t nn = (size_t)n * n, zgroup = (size_t)n * H;
   const float tb = a.t[b];
   const float* tsb = a.ts + (size_t)b * T;
   const int idx = interval_index_wave(tsb, T, tb);
   const float f = tb - tsb[idx];
   const float* fc = a.fusion + l * GNCDE_FC;
+  // independent global reads of the epilogue issued now (their round trips overlap the form): the slot's fusion
+  // partial and this group's g_out rows
+  const float gfc_old = gact && tid < GNCDE_FC ? a.gfc[((size_t)slot * a.L + l) * GNCDE_FC + tid] : 0.f;
+  constexpr int GOU = 16 * H / 256;  // g_out[R] elements per thread
+  float gor[GOU];
+#pragma unroll
+  for (int u = 0; u < GOU; ++u) {
+    const int e = tid + 256 * u, i = e / H, c = e % H;
+    gor[u] = !a.cde_out && r0 + i < n ? a.gout[((size_t)b * n + r0 + i) * H + c] : 0.f;
+  }
 
   // ---- form: the interval's rows block and column strip (as the forward) --------------------------------------
   const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
@@ -236,6 +257,7 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     }
   }
   __syncthreads();
+  BWD_STAMP(1);
   // the operand elements: (ri, k) and (k, ri) of A and dA, k = 16 kc + 4 hi + s, kc = w + 4 j
   float Ar[4][4], dAr[4][4], At[4][4], dAt[4][4];
 #pragma unroll
@@ -253,6 +275,7 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     }
   }
   __syncthreads();  // the form scratch becomes zhat and g_P
+  BWD_STAMP(2);
 
   // ---- Z_l and g_P of every node ----------------------------------------------------------------------------
   {
@@ -280,6 +303,7 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     for (int k = (int)threadIdx.x; k < NP; k += NT) sGq[k] = k < n ? a.gq[(size_t)b * n + k] : 0.f;
   }
   __syncthreads();
+  BWD_STAMP(3);
   for (int k = (int)threadIdx.x; k < NP; k += NT) {
     float ss = 0.f;
 #pragma unroll
@@ -290,10 +314,12 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     sInv[k] = k < n ? rms_inv(ss, 1.0f / (float)H) : 0.f;
   }
   __syncthreads();
-  // zsum = sum_k zhat_k and zf_x = sum_k zhat_k x_k (x = r, rd, c, cd): column c = tid % H, rows k = g mod NG
-  if (grp == 0) {
-    constexpr int NG = 256 / H;
-    const int c = tid % H, g = tid / H;
+  BWD_STAMP(4);
+  // zsum = sum_k zhat_k and zf_x = sum_k zhat_k x_k (x = r, rd, c, cd): column c, node groups k = g mod NG with a
+  // fixed NG (the sums do not depend on the row blocks per workgroup), spread over every thread of the workgroup
+  constexpr int NG = 256 * kMaxRbw / H;
+  for (int g = (int)threadIdx.x / H; g < NG; g += NT / H) {
+    const int c = (int)threadIdx.x % H;
     float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     for (int k = g; k < n; k += NG) {
       const float z = big[k * ZS + c] * sInv[k];
@@ -305,17 +331,17 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     for (int x = 0; x < 5; ++x) sScr[(g * 5 + x) * H + c] = acc[x];
   }
   __syncthreads();
-  float* sZv = sScr + 1280 - 5 * H;  // zsum, zf_r, zf_rd, zf_c, zf_cd [5][H] (after the group partials)
-  for (int e = tid; grp == 0 && e < 5 * H; e += 256) {
-    // (NG * 5 H = 1280 floats: the total for (x, c) lands in the last group's slot for (x, c), which only this
-    // thread reads, after reading it)
-    constexpr int NG = 256 / H;
+  float* sZv = sScr + 5 * NG * H - 5 * H;  // zsum, zf_r, zf_rd, zf_c, zf_cd [5][H] (after the group partials)
+  for (int e = (int)threadIdx.x; e < 5 * H; e += NT) {
+    // (the total for (x, c) lands in the last group's slot for (x, c), which only this thread reads, after reading
+    // it)
     const int x = e / H, c = e % H;
     float v = 0.f;
     for (int g = 0; g < NG; ++g) v += sScr[(g * 5 + x) * H + c];
     sZv[x * H + c] = v;
   }
   __syncthreads();
+  BWD_STAMP(5);
 
   // ---- the K loop: P = (I+Abar) zhat, g_zhat = (I+Abar)^T g_P, G^T tiles meeting A, dA, A^T, dA^T ----------
   const float eA = fc[GNCDE_FC_E_A], edA = fc[GNCDE_FC_E_DA], eTA = fc[GNCDE_FC_ET_A], eTdA = fc[GNCDE_FC_ET_DA];
@@ -382,10 +408,12 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   float facc[GNCDE_FC];
 #pragma unroll
   for (int q = 0; q < GNCDE_FC; ++q) facc[q] = 0.f;
-  if (tid < kRB && r0 + tid < n) {
-    const int i = r0 + tid;
+  {  // row ir of the block: its 16 lanes take columns cl + 16 u, then a fixed 16-lane butterfly
+    const int ir = tid >> 4, cl = tid & 15, i = r0 + ir < n ? r0 + ir : n - 1;
     float gz = 0.f, gd = 0.f, gfr = 0.f, gfrd = 0.f, gfc_ = 0.f, gfcd = 0.f;
-    for (int c = 0; c < H; ++c) {
+#pragma unroll
+    for (int u = 0; u < H / 16; ++u) {
+      const int c = cl + 16 * u;
       const float g = sG[i * ZS + c];
       gz = fmaf(g, sZv[c], gz);
       gd = fmaf(g, big[i * ZS + c], gd);
@@ -394,30 +422,41 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
       gfc_ = fmaf(g, sZv[3 * H + c], gfc_);
       gfcd = fmaf(g, sZv[4 * H + c], gfcd);
     }
-    const float gqv = sGq[i];
-    const float R = fmaf((float)n, gqv, gz);
-    const float D = fmaf(gd, sInv[i], gqv);
-    const float r = sF[i], rd = sF[NP + i], c = sF[2 * NP + i], cd = sF[3 * NP + i];
-    const float dg = sF[4 * NP + i], dgd = sF[5 * NP + i];
-    facc[GNCDE_FC_WR_A] = R * r;
-    facc[GNCDE_FC_WR_DA] = R * rd;
-    facc[GNCDE_FC_WC_A] = R * c;
-    facc[GNCDE_FC_WC_DA] = R * cd;
-    facc[GNCDE_FC_WS_A] = R * s_t;
-    facc[GNCDE_FC_WS_DA] = R * sd_t;
-    facc[GNCDE_FC_UD_A] = D * dg;
-    facc[GNCDE_FC_UD_DA] = D * dgd;
-    facc[GNCDE_FC_UR_A] = D * r;
-    facc[GNCDE_FC_UR_DA] = D * rd;
-    facc[GNCDE_FC_UC_A] = D * c;
-    facc[GNCDE_FC_UC_DA] = D * cd;
-    facc[GNCDE_FC_US_A] = D * s_t;
-    facc[GNCDE_FC_US_DA] = D * sd_t;
-    facc[GNCDE_FC_IDC] = D;
-    facc[GNCDE_FC_VR_A] = fmaf(gqv, s_t, gfr);
-    facc[GNCDE_FC_VR_DA] = fmaf(gqv, sd_t, gfrd);
-    facc[GNCDE_FC_VC_A] = fmaf(gqv, s_t, gfc_);
-    facc[GNCDE_FC_VC_DA] = fmaf(gqv, sd_t, gfcd);
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      gz += __shfl_xor(gz, o);
+      gd += __shfl_xor(gd, o);
+      gfr += __shfl_xor(gfr, o);
+      gfrd += __shfl_xor(gfrd, o);
+      gfc_ += __shfl_xor(gfc_, o);
+      gfcd += __shfl_xor(gfcd, o);
+    }
+    if (cl == 0 && r0 + ir < n) {
+      const float gqv = sGq[i];
+      const float R = fmaf((float)n, gqv, gz);
+      const float D = fmaf(gd, sInv[i], gqv);
+      const float r = sF[i], rd = sF[NP + i], c = sF[2 * NP + i], cd = sF[3 * NP + i];
+      const float dg = sF[4 * NP + i], dgd = sF[5 * NP + i];
+      facc[GNCDE_FC_WR_A] = R * r;
+      facc[GNCDE_FC_WR_DA] = R * rd;
+      facc[GNCDE_FC_WC_A] = R * c;
+      facc[GNCDE_FC_WC_DA] = R * cd;
+      facc[GNCDE_FC_WS_A] = R * s_t;
+      facc[GNCDE_FC_WS_DA] = R * sd_t;
+      facc[GNCDE_FC_UD_A] = D * dg;
+      facc[GNCDE_FC_UD_DA] = D * dgd;
+      facc[GNCDE_FC_UR_A] = D * r;
+      facc[GNCDE_FC_UR_DA] = D * rd;
+      facc[GNCDE_FC_UC_A] = D * c;
+      facc[GNCDE_FC_UC_DA] = D * cd;
+      facc[GNCDE_FC_US_A] = D * s_t;
+      facc[GNCDE_FC_US_DA] = D * sd_t;
+      facc[GNCDE_FC_IDC] = D;
+      facc[GNCDE_FC_VR_A] = fmaf(gqv, s_t, gfr);
+      facc[GNCDE_FC_VR_DA] = fmaf(gqv, sd_t, gfrd);
+      facc[GNCDE_FC_VC_A] = fmaf(gqv, s_t, gfc_);
+      facc[GNCDE_FC_VC_DA] = fmaf(gqv, sd_t, gfcd);
+    }
   }
   facc[GNCDE_FC_E_A] += dsum[0];
   facc[GNCDE_FC_E_DA] += dsum[1];
@@ -426,6 +465,7 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   // this layer's own g_zhat / zhat rows are needed after the partials overwrite the node regions: the rows' Z and
   // inv stay available through HBM (zin) and sInv
   __syncthreads();  // every group's reads of zhat / g_P of all nodes done: the partial rows alias them
+  BWD_STAMP(6);
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
@@ -433,19 +473,17 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
       epP[(w * 16 + 4 * hi + r) * ZS + 16 * ct + lo] = accP[ct][r];
       epG[(w * 16 + 4 * hi + r) * ZS + 16 * ct + lo] = accT[ct][r];
     }
-  // fusion sums: a butterfly per wave, then the four wave partials in order
+  // fusion sums: a DPP / row-swap reduction per wave (no LDS), then the four wave partials in order
 #pragma unroll
   for (int q = 0; q < GNCDE_FC; ++q) {
-    float v = facc[q];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const float v = wave_sum64(facc[q]);
     if (lane == 0) sFus[q * 4 + w] = v;
   }
   __syncthreads();
-  if (gact && tid < GNCDE_FC) {
-    float* dst = a.gfc + ((size_t)slot * a.L + l) * GNCDE_FC + tid;
-    *dst += (sFus[tid * 4] + sFus[tid * 4 + 1]) + (sFus[tid * 4 + 2] + sFus[tid * 4 + 3]);
-  }
+  BWD_STAMP(7);
+  if (gact && tid < GNCDE_FC)
+    a.gfc[((size_t)slot * a.L + l) * GNCDE_FC + tid] =
+        gfc_old + ((sFus[tid * 4] + sFus[tid * 4 + 1]) + (sFus[tid * 4 + 2] + sFus[tid * 4 + 3]));
   // P[R], g_zhat[R]: the four K parts in a fixed order, into rows 64..79 of the two regions
   for (int e = tid; e < 16 * H; e += 256) {
     const int i = e / H, c = e % H;
@@ -459,6 +497,7 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     epG[(64 + i) * ZS + c] = g;
   }
   __syncthreads();
+  BWD_STAMP(8);
   const float* sP = epP + 64 * ZS;   // P[R] [16][ZS]
   const float* sGz = epG + 64 * ZS;  // g_zhat[R]
   // ---- parameter partials: g_W' += g_out[R]^T P[R], g_b' += g_out[R]^T q[R] (d_out = H), or P | q out (CDE) ----
@@ -469,9 +508,10 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     }
   } else {
     float* go = epG;  // g_out[R] staged in rows 0..15 of the group's g partial region (the partials are consumed)
-    for (int e = tid; e < 16 * H; e += 256) {
-      const int i = e / H, c = e % H;
-      go[i * ZS + c] = r0 + i < n ? a.gout[((size_t)b * n + r0 + i) * H + c] : 0.f;
+#pragma unroll
+    for (int u = 0; u < GOU; ++u) {
+      const int e = tid + 256 * u;
+      go[(e / H) * ZS + e % H] = gor[u];
     }
     __syncthreads();
     float* gw = a.gw + (size_t)slot * a.gw_stride + a.gw_off;
@@ -492,6 +532,7 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     }
     __syncthreads();  // go is reused below
   }
+  BWD_STAMP(9);
   // ---- RMSNorm^T of the block's rows and the next cotangents ------------------------------------------------
   // thread = (row tid / 16, columns (tid % 16) + 16 u): a row's 16 threads are 16 consecutive lanes
   {
@@ -529,6 +570,7 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   }
   if (l == 0) return;
   __syncthreads();
+  BWD_STAMP(10);
   {
     const float* go = epG;
     // g_P_{l-1}[i][c] = sum_j g_out[i][j] W'_{l-1}[j][c]: wave ct's 16 x 16 tile, K = H (W' rows from L2)
@@ -542,6 +584,7 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
       for (int r = 0; r < 4; ++r)
         if (r0 + 4 * hi + r < n) a.gP_next[((size_t)b * n + r0 + 4 * hi + r) * H + 16 * ct + lo] = acc[r];
     }
+    BWD_STAMP(11);
     if (gact && tid < kRB && r0 + tid < n) {
       float acc = 0.f;
       for (int jo = 0; jo < H; ++jo) acc = fmaf(go[tid * ZS + jo], a.bprev[jo], acc);
@@ -983,14 +1026,18 @@ void rows_vjp_begin(const GncdeProblem& p, char* ws, hipStream_t st) {
 // every layer back to back (generic_vf_prepare's fold).
 int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* gF, float* gu, float* gdata,
                 const float* csum, const float* wf, const float* bfold, char* ws, char* vf_ws, unsigned* bars,
-                hipStream_t st) {
+                hipStream_t st, const float* kept) {
   RowsVjpWs w;
   carve_rows_vjp(p, ws, w);
   const int B = p.B, n = p.n, H = p.dims[0], L = p.L;
   const bool cde = p.cde_hidden > 0;
-  // forward with the hidden outputs kept
-  int rc = generic_vf_eval(p, t, u, w.dy, vf_ws, st, true, bars, w.keep);
-  if (rc) return rc;
+  // the hidden outputs: the forward's activation record, or a forward in keep mode now
+  const float* keep = kept;
+  if (!keep) {
+    const int rc = generic_vf_eval(p, t, u, w.dy, vf_ws, st, true, bars, w.keep, false);
+    if (rc) return rc;
+    keep = w.keep;
+  }
   const size_t E = (size_t)B * n * H;
   size_t wo_last = 0, bo_last = 0;
   for (int l = 0; l + 1 < L; ++l) {
@@ -1044,7 +1091,7 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     a.csum = csum;
     a.fusion = p.fusion;
     a.t = t;
-    a.zin = l == 0 ? u : w.keep + (size_t)(l - 1) * E;
+    a.zin = l == 0 ? u : keep + (size_t)(l - 1) * E;
     a.gP = w.gP[cur];
     a.gq = w.gq[cur];
     a.gout = w.gout[cur];
@@ -1090,6 +1137,13 @@ void rows_vjp_finish(const GncdeProblem& p, char* ws, float* gparams, float* gfu
 }
 
 }  // namespace gncde
+
+#ifdef GNCDE_BWD_STAMPS
+extern "C" int gncde_debug_bwd_stamps(unsigned long long* host, int count) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gncde::g_bwd_stamps), sizeof(unsigned long long) * count) == hipSuccess ? 0
+                                                                                                                  : -1;
+}
+#endif
 
 #ifdef GNCDE_DIAG
 // Diagnostic builds only (-DGNCDE_DIAG; not part of include/gncde.h): one evaluation with the hidden outputs kept.

@@ -782,8 +782,10 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
       const float* tsti = w.tst + (size_t)i * B;
       // tmp = cotangent of U_i (the per-layer reverse overwrites every element; the generic one accumulates)
       if (rows) {
+        const float* kept =
+            s.act_rec ? s.act_rec + ((size_t)k * tab.stages + i) * (size_t)(p.L - 1) * B * E : nullptr;
         const int rc = rows_vf_vjp(p, tsti, w.U[i], w.gK[i], w.tmp, gdata, generic_vf_csum(p, vf_ws), w.wf, w.bf,
-                                   rows_ws, vf_ws, &bars, st);
+                                   rows_ws, vf_ws, &bars, st, kept);
         if (rc) return rc;
       } else {
         (void)hipMemsetAsync(w.tmp, 0, (size_t)B * E * sizeof(float), st);

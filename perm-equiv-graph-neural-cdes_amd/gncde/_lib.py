@@ -12,7 +12,7 @@ from ctypes import POINTER, c_char_p, c_float, c_int32, c_size_t, c_void_p
 
 MAX_LAYERS = 8
 FC = 24
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 RK4, TSIT5 = 0, 1
 CTRL_GRID, CTRL_PID = 0, 1
@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "gncde_strerror",
     "gncde_integrate_path",
     "gncde_stage_record_floats",
+    "gncde_activation_record_floats",
     "gncde_workspace_bytes",
     "gncde_vf_eval",
     "gncde_integrate",
@@ -91,6 +92,8 @@ class GncdeSolver(ctypes.Structure):
         ("stage_rec", c_void_p),
         ("stage_rec_len", ctypes.c_int64),
         ("flags", c_int32),
+        ("act_rec", c_void_p),
+        ("act_rec_len", ctypes.c_int64),
     ]
 
 
@@ -119,6 +122,8 @@ def load(path: str | None = None):
     lib.gncde_integrate_path.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver), c_char_p, c_size_t]
     lib.gncde_stage_record_floats.restype = c_size_t
     lib.gncde_stage_record_floats.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver)]
+    lib.gncde_activation_record_floats.restype = c_size_t
+    lib.gncde_activation_record_floats.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver)]
     lib.gncde_workspace_bytes.restype = c_size_t
     lib.gncde_workspace_bytes.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver)]
     lib.gncde_vf_eval.restype = c_int32

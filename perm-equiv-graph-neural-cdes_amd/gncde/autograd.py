@@ -28,7 +28,8 @@ STAGE_RECORD_SHARE = 0.25
 
 
 def with_stage_record(prob: engine.Problem, spec: engine.SolverSpec, want: bool = True) -> engine.SolverSpec:
-    """``spec`` with a freshly allocated stage record when the reverse sweep would read one and it fits."""
+    """``spec`` with a freshly allocated stage record (and, where the reverse sweep reads one, an activation
+    record) when it fits in STAGE_RECORD_SHARE of the free device memory."""
     if not want:
         return spec
     floats = engine.stage_record_floats(prob, spec)
@@ -37,8 +38,12 @@ def with_stage_record(prob: engine.Problem, spec: engine.SolverSpec, want: bool 
     free, _ = torch.cuda.mem_get_info(prob.params.device)
     if prob.B * floats * 4 > STAGE_RECORD_SHARE * free:
         return spec
-    return dataclasses.replace(spec, stage_rec=torch.empty(prob.B, floats, dtype=torch.float32,
-                                                           device=prob.params.device))
+    dev = prob.params.device
+    spec = dataclasses.replace(spec, stage_rec=torch.empty(prob.B, floats, dtype=torch.float32, device=dev))
+    act = engine.activation_record_floats(prob, spec)
+    if act and (prob.B * floats + act) * 4 <= STAGE_RECORD_SHARE * free:
+        spec = dataclasses.replace(spec, act_rec=torch.empty(act, dtype=torch.float32, device=dev))
+    return spec
 
 
 class _FixedGridSolve(torch.autograd.Function):
@@ -50,7 +55,7 @@ class _FixedGridSolve(torch.autograd.Function):
             p = dataclasses.replace(p, data_coef=data_coef.detach().to(torch.float32).contiguous())
         steps = with_stage_record(p, dataclasses.replace(spec, save_mode=_lib.SAVE_STEPS, stage_rec=None), record)
         ys = engine.integrate(p, steps, y0.detach())
-        ctx.prob, ctx.spec = p, dataclasses.replace(spec, stage_rec=steps.stage_rec)
+        ctx.prob, ctx.spec = p, dataclasses.replace(spec, stage_rec=steps.stage_rec, act_rec=steps.act_rec)
         ctx.dtypes = (y0.dtype, params.dtype, fusion.dtype)
         ctx.save_for_backward(ys)
         if spec.save_mode == _lib.SAVE_STEPS:
@@ -154,6 +159,13 @@ class _PidSolve(torch.autograd.Function):
         steps = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_STEPS, grid=grid,
                                   nsteps=nst, flags=spec.flags)
         want_data = ctx.needs_input_grad[3]
+        # The replay's forward keeps every stage's hidden outputs when the reverse sweep can read them (the
+        # host-paced replay, not the one-launch persistent one: config 5's shape spends 35 us per stage re-running
+        # the forward otherwise, against ~10 us the host-paced replay costs over the persistent one per evaluation)
+        if engine.integrate_path(ctx.prob, steps).startswith("rows_grid"):
+            gen = dataclasses.replace(steps, flags=steps.flags | _lib.FLAG_GENERIC)
+            if engine.activation_record_floats(ctx.prob, gen):
+                steps = gen
         steps = with_stage_record(ctx.prob, steps)
         ys = engine.integrate(ctx.prob, steps, y0)  # the checkpoints (and stage inputs): the accepted steps replayed
         if dense:

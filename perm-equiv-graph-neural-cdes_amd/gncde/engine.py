@@ -189,6 +189,9 @@ class SolverSpec:
     # host side only (not in GncdeSolver): autograd.solve copies the forward's stats [B, 4] here when given (the
     # trainers balance data-parallel shards by the adaptive solves' accepted step counts)
     stats_out: torch.Tensor | None = None
+    # GRID: activation record [activation_record_floats(prob, solver)] (the whole batch, [G-1, S, L-1, B, n, H]),
+    # written by integrate, read by integrate_vjp (ABI 7)
+    act_rec: torch.Tensor | None = None
 
     def c_struct(self) -> _lib.GncdeSolver:
         s = _lib.GncdeSolver()
@@ -214,10 +217,17 @@ class SolverSpec:
                 raise _lib.GncdeError("SolverSpec.stage_rec must be a contiguous fp32 CUDA tensor [B, floats]")
             s.stage_rec = _ptr(self.stage_rec).value
             s.stage_rec_len = int(self.stage_rec.shape[1])
+        if self.act_rec is not None:
+            if not (self.act_rec.is_cuda and self.act_rec.dtype == torch.float32 and self.act_rec.is_contiguous()):
+                raise _lib.GncdeError("SolverSpec.act_rec must be a contiguous fp32 CUDA tensor")
+            s.act_rec = _ptr(self.act_rec).value
+            s.act_rec_len = int(self.act_rec.numel())
         s.flags = int(self.flags)
         return s
 
     def shard(self, start, stop):
+        """The spec of samples [start, stop) (the activation record is batch-major and is not carried over: a
+        shard records its own)."""
         cut = lambda x: None if x is None else x[start:stop]  # noqa: E731
         return SolverSpec(self.method, self.controller, self.save_mode, cut(self.grid), cut(self.nsteps),
                           self.rtol, self.atol, self.max_steps, cut(self.t0), cut(self.t1), cut(self.dt0),
@@ -229,6 +239,13 @@ def stage_record_floats(prob: Problem, solver: SolverSpec) -> int:
     lib = _lib.load()
     ss = dataclasses.replace(solver, stage_rec=None).c_struct()
     return int(lib.gncde_stage_record_floats(ctypes.byref(prob.c_struct()), ctypes.byref(ss)))
+
+
+def activation_record_floats(prob: Problem, solver: SolverSpec) -> int:
+    """Floats of the activation record (the whole batch) the reverse sweep would read (0: none is kept)."""
+    lib = _lib.load()
+    ss = dataclasses.replace(solver, stage_rec=None, act_rec=None).c_struct()
+    return int(lib.gncde_activation_record_floats(ctypes.byref(prob.c_struct()), ctypes.byref(ss)))
 
 
 def integrate_path(prob: Problem, solver: SolverSpec) -> str:

@@ -44,10 +44,11 @@ def test_struct_layout_matches_c(tmp_path):
 #include <stddef.h>
 #include "{HEADER}"
 int main(void) {{
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(GncdeProblem), offsetof(GncdeProblem, ts),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(GncdeProblem), offsetof(GncdeProblem, ts),
          offsetof(GncdeProblem, params), sizeof(GncdeSolver), offsetof(GncdeSolver, save_ts),
          offsetof(GncdeSolver, step_ts), offsetof(GncdeSolver, step_ts_len), offsetof(GncdeSolver, stage_rec),
-         offsetof(GncdeSolver, stage_rec_len), offsetof(GncdeSolver, flags));
+         offsetof(GncdeSolver, stage_rec_len), offsetof(GncdeSolver, flags), offsetof(GncdeSolver, act_rec),
+         offsetof(GncdeSolver, act_rec_len));
   return 0;
 }}''')
     exe = tmp_path / "layout"
@@ -56,7 +57,7 @@ int main(void) {{
     P, S = _lib.GncdeProblem, _lib.GncdeSolver
     assert vals == [ctypes.sizeof(P), P.ts.offset, P.params.offset, ctypes.sizeof(S), S.save_ts.offset,
                     S.step_ts.offset, S.step_ts_len.offset, S.stage_rec.offset, S.stage_rec_len.offset,
-                    S.flags.offset]
+                    S.flags.offset, S.act_rec.offset, S.act_rec_len.offset]
 
 
 def _fake_problem(B=4, n=64, T=10, dims=(16, 16, 16, 16)):
@@ -129,6 +130,27 @@ def test_stage_record_floats():
     bad = _fake_problem()
     bad.T = 1
     assert f(bad, _fake_solver()) == 0
+
+
+def test_activation_record_floats():
+    """gncde_activation_record_floats: (G-1) S (L-1) B n H where the fixed-grid forward takes the multi-kernel path
+    and the reverse the per-layer kernels (BASELINE config 3's shape), else 0."""
+    lib = _lib.load()
+    f = lambda p, s: lib.gncde_activation_record_floats(ctypes.byref(p), ctypes.byref(s))  # noqa: E731
+    cfg3 = _fake_problem(B=64, n=129, T=4, dims=(64, 64, 64, 1024))
+    cfg3.cde_hidden, cfg3.cde_embed, cfg3.data_coef = 64, 8, 0x1000
+    s = _fake_solver(_lib.TSIT5)
+    s.grid_len = 31
+    assert f(cfg3, s) == 30 * 6 * 2 * 64 * 129 * 64
+    s.method = _lib.RK4
+    assert f(cfg3, s) == 30 * 4 * 2 * 64 * 129 * 64
+    assert f(_fake_problem(), _fake_solver()) == 0  # the fused forward / fused reverse sweep: no record
+    pid = _fake_solver(_lib.TSIT5)
+    pid.controller, pid.t0, pid.t1, pid.max_steps = _lib.CTRL_PID, 0x1000, 0x1000, 16
+    assert f(cfg3, pid) == 0
+    bf = _fake_problem(B=64, n=129, T=4, dims=(64, 64, 64, 1024))
+    bf.cde_hidden, bf.cde_embed, bf.data_coef, bf.compute = 64, 8, 0x1000, _lib.COMPUTE_BF16
+    assert f(bf, s) == 0
 
 
 def test_stage_record_length_is_checked():

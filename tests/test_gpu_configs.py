@@ -387,3 +387,40 @@ def test_bwd_row_blocks_per_workgroup_bitwise(G, monkeypatch):
         for k in range(3):
             assert torch.equal(outs[r][k], outs["1"][k]), (r, k)
     assert all(torch.isfinite(x).all() for x in outs["1"])
+
+
+@pytest.mark.parametrize("method", ["rk4", "tsit5"])
+def test_activation_record_matches_recompute(G, method):
+    """The activation record (GncdeSolver.act_rec, ABI 7) at config 3's shape: the reverse sweep reading the
+    forward's hidden-layer outputs gives the gradient of the sweep that re-runs every stage's forward — bitwise for
+    RK4 (every stage is evaluated at the same time in both); Tsit5's stage 0 comes from the forward's FSAL evaluation
+    at t_k + h_k, which can differ from the grid's t_{k+1} by an ulp, so there to fp32 rounding."""
+    B, n, T, H, de, L = 8, 129, 4, 64, 8, 3
+    rng, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(35, B, n, T, 3.0, H, de, L, distinct=4)
+    prob = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
+    grid, ns = G.layout.stack_grids([O.constant_grid(0.0, 0.3, 0.1)] * B)
+    m = G._lib.RK4 if method == "rk4" else G._lib.TSIT5
+    spec = G.SolverSpec(method=m, save_mode=G._lib.SAVE_STEPS, grid=grid, nsteps=ns)
+    floats = G.engine.stage_record_floats(prob, spec)
+    act = G.engine.activation_record_floats(prob, spec)
+    S = 4 if method == "rk4" else 6
+    assert act == 3 * S * (L - 1) * B * n * H
+    rec = torch.zeros(B, floats, device="cuda")
+    arec = torch.full((act,), float("nan"), device="cuda")  # every slab must be written by the forward
+    yd = torch.tensor(y0, dtype=torch.float32, device="cuda")
+    ys = G.integrate(prob, dataclasses.replace(spec, stage_rec=rec, act_rec=arec), yd)
+    assert bool(torch.isfinite(arec).all())
+    ys2 = G.integrate(prob, dataclasses.replace(spec, stage_rec=rec), yd)
+    assert torch.equal(ys, ys2)  # recording changes nothing in the forward
+    g = torch.tensor(rng.standard_normal((B, n, H)), dtype=torch.float32, device="cuda")
+    t1 = G._lib.SAVE_T1
+    with_rec = G.integrate_vjp(prob, dataclasses.replace(spec, save_mode=t1, stage_rec=rec, act_rec=arec), ys, g)
+    without = G.integrate_vjp(prob, dataclasses.replace(spec, save_mode=t1, stage_rec=rec), ys, g)
+    for a, b in zip(with_rec, without):
+        if method == "rk4":
+            assert torch.equal(a, b)
+        else:
+            assert rel_err(a.cpu().numpy(), b.cpu().numpy()) <= 1e-5
+    bad = torch.zeros(act - 1, device="cuda")
+    with pytest.raises(G._lib.GncdeError):
+        G.integrate(prob, dataclasses.replace(spec, stage_rec=rec, act_rec=bad), yd)
