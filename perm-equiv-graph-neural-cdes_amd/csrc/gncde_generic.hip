@@ -638,7 +638,7 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   // the one-launch evaluation reads a node block's column strip [:, R] as rows R of the transposed planes (whole
   // cache lines, like its rows block) instead of 16-column segments of every row
   const size_t planes = B * (size_t)(p.T - 1) * 4 * nn;
-  const bool strip = rows_supported(p) || rows_vjp_supported(p) || rows_solve_shape(p);
+  const bool strip = rows_supported(p) || rows_solve_shape(p);
   w.coefT = take(strip ? (coef_is_bf16(p) ? (planes + 1) / 2 : planes) : 1);
   return off;
 }
@@ -704,12 +704,6 @@ const float* generic_vf_csum(const GncdeProblem& p, char* ws) {
   VfWs w;
   carve_vf(p, ws, w);
   return w.csum;
-}
-
-const void* generic_vf_coefT(const GncdeProblem& p, char* ws) {
-  VfWs w;
-  carve_vf(p, ws, w);
-  return w.coefT;
 }
 
 const int* generic_vf_fault(const GncdeProblem& p, char* ws) {

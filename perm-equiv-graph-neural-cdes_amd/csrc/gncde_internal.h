@@ -261,10 +261,8 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
                       int32_t* stats, char* ws, hipStream_t st);
 // k_coef_sums' per-plane reductions in a prepared evaluation workspace
 const float* generic_vf_csum(const GncdeProblem& p, char* ws);
-// the transposed coefficient planes of the one-launch evaluation and the per-layer reverse kernels:
-// generic_vf_prepare fills them when rows_supported(p); a reverse sweep on a shape only rows_vjp_supported covers
-// calls generic_vf_transpose itself
-const void* generic_vf_coefT(const GncdeProblem& p, char* ws);
+// the transposed coefficient planes of the one-launch evaluation: generic_vf_prepare fills them when
+// rows_supported(p) (or for the persistent solve's rows layout)
 void generic_vf_transpose(const GncdeProblem& p, char* ws, hipStream_t st);
 
 // reverse mode of one evaluation, one launch per ConvLayer (n <= 256, one width H): gncde_rows_vjp.hip

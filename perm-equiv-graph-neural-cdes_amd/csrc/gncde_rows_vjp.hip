@@ -14,11 +14,12 @@
 // sum_k C_k f_k = sum_i (g_P_i . sum_k zhat_k f_k + g_q_i sum_k f_k) against the form's node features — all O(n H).
 //
 // Launches per stage (after the forward kept Z_1 .. Z_{L-1}, generic_vf_eval keep mode):
-//   k_bwd_head      per 16-row block: g_out, g_P, g_q of the output layer from the stage cotangent gF
-//                   (ODE g_out = tg gF; CDE g_P_i = tg_i sum_{m,j} gF_im dX_ij W'[16m+j, :] without the n x 16h
+//   k_bwd_head      per 16-row block: the interval's A, dA rows (Horner of the coefficient planes, once per
+//                   evaluation for every layer launch), g_out, g_P, g_q of the output layer from the stage cotangent
+//                   gF (ODE g_out = tg gF; CDE g_P_i = tg_i sum_{m,j} gF_im dX_ij W'[16m+j, :] without the n x 16h
 //                   g_out, and the factors tg gF, dX for the read-out weight gradient)
-//   k_bwd_layer<H>  per 16-row block, l = L-1 .. 0: the interval's rows block and column strip -> A, dA, A^T, dA^T in
-//                   the product's operand layout (the forward form), zhat and g_P of every node in LDS, then one K
+//   k_bwd_layer<H>  per 16-row block, l = L-1 .. 0: the block's rows and columns of A, dA -> A, dA, A^T, dA^T in
+//                   the product's operand layout, zhat and g_P of every node in LDS, then one K
 //                   loop over the block's node chunks that runs three MFMA products per chunk: P = (I+Abar) zhat,
 //                   g_zhat = (I+Abar)^T g_P (the same registers, the transposed coefficients) and the G^T tile
 //                   zhat g_P^T, which meets A, dA, A^T, dA^T in registers for the dense contractions; then g_W'
@@ -43,7 +44,6 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kRB = 16;
 constexpr int kMaxN = 256;
-constexpr int kStrip = 17;
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -67,18 +67,18 @@ constexpr int kMaxRbw = 3;  // row blocks per workgroup (one 256-thread group ea
 __device__ unsigned long long g_bwd_stamps[1024 * 16];
 #define BWD_STAMP(k) \
   do { if (threadIdx.x == 0 && a.l == 1 && blockIdx.x < 1024) g_bwd_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// a stamp once the value v has arrived
+#define BWD_STAMP_AFTER(k, v) \
+  do { asm volatile("" ::"v"(v)); BWD_STAMP(k); } while (0)
 #else
 #define BWD_STAMP(k) do {} while (0)
+#define BWD_STAMP_AFTER(k, v) do {} while (0)
 #endif
-// floats of one group's form scratch: the column strip [2][NP][17] and the rows block [2][16][NP + 4]
-__host__ __device__ inline int bwd_form(int n) { return (2 * bwd_np(n) * kStrip + 32 * (bwd_np(n) + 4) + 3) & ~3; }
-// The union region, used in turn as (1) every group's form scratch, (2) zhat and g_P of every node [NP][H+4] each,
-// shared by the groups, (3) every group's product partials: P rows [80][H+4] (64 partial rows, 16 result rows),
-// then the g_zhat rows [80][H+4]
+// The union region, used in turn as (1) zhat and g_P of every node [NP][H+4] each, shared by the groups, (2) every
+// group's product partials: P rows [80][H+4] (64 partial rows, 16 result rows), then the g_zhat rows [80][H+4]
 __host__ __device__ inline int bwd_union(int n, int H, int rbw) {
-  const int f = rbw * bwd_form(n), z = 2 * bwd_np(n) * bwd_zs(H), e = rbw * 160 * bwd_zs(H);
-  const int m = f > z ? f : z;
-  return ((m > e ? m : e) + 3) & ~3;
+  const int z = 2 * bwd_np(n) * bwd_zs(H), e = rbw * 160 * bwd_zs(H);
+  return ((z > e ? z : e) + 3) & ~3;
 }
 inline size_t bwd_smem(int n, int H, int rbw) {
   const int np = bwd_np(n);
@@ -91,8 +91,7 @@ inline size_t bwd_smem(int n, int H, int rbw) {
 struct BwdArgs {
   int B, n, T, L, l, nb;
   const float* ts;
-  const float* coef;       // [B, T-1, 4, n, n]
-  const float* coefT;      // the same planes transposed (generic_vf_prepare): the column strip as whole-line rows
+  const float* aev;        // A, dA at the evaluation time [B][2][NP][NP] (k_bwd_head; zero past n)
   const float* csum;       // k_coef_sums [B, T-1, 12 n + 4]
   const float* fusion;     // [L, GNCDE_FC]
   const float* t;          // [B] stage times
@@ -128,7 +127,6 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   const int NP = bwd_np(n), nch = NP >> 4;
   const int NT = (int)blockDim.x, rbw = NT >> 8, grp = (int)threadIdx.x >> 8;
   float* U = sm;
-  float* fs = U + grp * bwd_form(n);       // this group's form scratch
   float* big = U;                          // zhat of every node [NP][ZS] (shared)
   float* sG = U + (size_t)NP * ZS;         // g_P of every node [NP][ZS] (shared)
   float* epP = U + (size_t)grp * 160 * ZS;  // this group's P partials [64][ZS] + P[R] [16][ZS]
@@ -151,12 +149,13 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   const int rb = gact ? rbr : a.nb - 1, slot = b * a.nb + rb;
   const int r0 = rb * kRB, ri = r0 + lo;
   BWD_STAMP(0);
-  const size_t nn = (size_t)n * n, zgroup = (size_t)n * H;
+  const size_t zgroup = (size_t)n * H;
   const float tb = a.t[b];
   const float* tsb = a.ts + (size_t)b * T;
   const int idx = interval_index_wave(tsb, T, tb);
   const float f = tb - tsb[idx];
   const float* fc = a.fusion + l * GNCDE_FC;
+  BWD_STAMP_AFTER(12, f);
   // independent global reads of the epilogue issued now (their round trips overlap the form): the slot's fusion
   // partial and this group's g_out rows
   const float gfc_old = gact && tid < GNCDE_FC ? a.gfc[((size_t)slot * a.L + l) * GNCDE_FC + tid] : 0.f;
@@ -168,22 +167,26 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     gor[u] = !a.cde_out && r0 + i < n ? a.gout[((size_t)b * n + r0 + i) * H + c] : 0.f;
   }
 
-  // ---- form: the interval's rows block and column strip (as the forward) --------------------------------------
-  const float* cb = a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
-  const auto crs = rsrc(cb, (unsigned)(4 * nn * sizeof(float)));
-  const int RS = NP + 4;
-  float* sAr = fs + 2 * NP * kStrip;
-  const int rr = tid >> 4, cq = 4 * (tid & 15);
-  const auto crt = rsrc(a.coefT + ((size_t)b * (T - 1) + idx) * 4 * nn, (unsigned)(4 * nn * sizeof(float)));
-  u32x4 rc[4][4], sc[4][4];
+  // ---- form: the block's rows and columns of A, dA straight into the operand registers: (ri, k) and (k, ri),
+  // k = 16 kc + 4 hi + s, kc = w + 4 j (k_bwd_head evaluated the interval's cubics once for every layer launch)
+  const size_t pl = (size_t)NP * NP;
+  const float* A0 = a.aev + (size_t)b * 2 * pl;
+  const float* A1 = A0 + pl;
+  float Ar[4][4], dAr[4][4], At[4][4], dAt[4][4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
+  for (int j = 0; j < 4; ++j) {
+    const int kc = w + 4 * j, k0 = 16 * kc + 4 * hi;
+    const bool in = kc < nch;
+    const floatx4 ar = in ? *reinterpret_cast<const floatx4*>(A0 + (size_t)ri * NP + k0) : floatx4{0.f, 0.f, 0.f, 0.f};
+    const floatx4 dr = in ? *reinterpret_cast<const floatx4*>(A1 + (size_t)ri * NP + k0) : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = (int)((q * nn + (size_t)(r0 + rr) * n + cq + 64 * u) * 4);
-      rc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, e, 0, 0);
-      sc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crt, e, 0, 0);  // transposed row rr = column r0 + rr
+    for (int s = 0; s < 4; ++s) {
+      Ar[j][s] = ar[s];
+      dAr[j][s] = dr[s];
+      At[j][s] = in ? A0[(size_t)(k0 + s) * NP + ri] : 0.f;
+      dAt[j][s] = in ? A1[(size_t)(k0 + s) * NP + ri] : 0.f;
     }
+  }
   const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
   const int nd = tid < n ? tid : n - 1;
   float pv[3][4], pt[4];
@@ -193,33 +196,8 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     for (int kd = 0; kd < 3; ++kd) pv[kd][q] = cs[(q * 3 + kd) * n + nd];
     pt[q] = cs[12 * n + q];
   }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int c0 = cq + 64 * u;
-    if (c0 < NP)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool in = r0 + rr < n && c0 + e < n;
-        const unsigned x0 = rc[u][0][e], x1 = rc[u][1][e], x2 = rc[u][2][e], x3 = rc[u][3][e];
-        const float cc[4] = {u2f(x0), u2f(x1), u2f(x2), u2f(x3)};
-        sAr[rr * RS + c0 + e] = in ? cubic(cc, f) : 0.f;
-        sAr[(16 + rr) * RS + c0 + e] = in ? dcubic(cc, f) : 0.f;
-      }
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int c0 = cq + 64 * u;
-    if (c0 < NP)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int kk = c0 + e;
-        const bool in = r0 + rr < n && kk < n;
-        const unsigned x0 = sc[u][0][e], x1 = sc[u][1][e], x2 = sc[u][2][e], x3 = sc[u][3][e];
-        const float cc[4] = {u2f(x0), u2f(x1), u2f(x2), u2f(x3)};
-        fs[kk * kStrip + rr] = in ? cubic(cc, f) : 0.f;
-        fs[(NP + kk) * kStrip + rr] = in ? dcubic(cc, f) : 0.f;
-      }
-  }
+  BWD_STAMP_AFTER(13, dAt[3][3]);
+  BWD_STAMP_AFTER(14, pv[2][3]);
   // node features and this layer's families at every node (thread = node)
   const float s_t = cubic(pt, f), sd_t = dcubic(pt, f);
   {
@@ -258,23 +236,6 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   }
   __syncthreads();
   BWD_STAMP(1);
-  // the operand elements: (ri, k) and (k, ri) of A and dA, k = 16 kc + 4 hi + s, kc = w + 4 j
-  float Ar[4][4], dAr[4][4], At[4][4], dAt[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int kc = w + 4 * j, k0 = 16 * kc + 4 * hi;
-    const bool in = kc < nch;
-    const floatx4 ar = in ? *reinterpret_cast<const floatx4*>(sAr + lo * RS + k0) : floatx4{0.f, 0.f, 0.f, 0.f};
-    const floatx4 dr = in ? *reinterpret_cast<const floatx4*>(sAr + (16 + lo) * RS + k0) : floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      Ar[j][s] = ar[s];
-      dAr[j][s] = dr[s];
-      At[j][s] = in ? fs[(k0 + s) * kStrip + lo] : 0.f;
-      dAt[j][s] = in ? fs[(NP + k0 + s) * kStrip + lo] : 0.f;
-    }
-  }
-  __syncthreads();  // the form scratch becomes zhat and g_P
   BWD_STAMP(2);
 
   // ---- Z_l and g_P of every node ----------------------------------------------------------------------------
@@ -596,6 +557,7 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
 struct HeadArgs {
   int B, n, T, H, cde;
   const float* ts;
+  const float* coef;       // [B, T-1, 4, n, n]
   const float* tcoef;      // [B, T-1, 3, n]
   const float* data_coef;  // [B, T-1, 4, n, 8, 2]
   const float* t;
@@ -607,6 +569,7 @@ struct HeadArgs {
   float* gq;               // [B, n]
   float* tgF;              // CDE: tg gF [B, n, H]
   float* dxo;              // CDE: dX [B, n, 16]
+  float* aev;              // A, dA at the evaluation time [B][2][NP][NP]
 };
 
 // Output layer's cotangents for a 16-row block (thread = (row tid / 16, column tid % 16 + 16 u) for the elementwise
@@ -624,6 +587,37 @@ __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
   const float* tsb = a.ts + (size_t)b * T;
   const int idx = interval_index_wave(tsb, T, tb);
   const float f = tb - tsb[idx];
+  {
+    // the interval's A, dA rows r0 .. r0 + 15 at every column (zero past n), read by every layer launch: thread =
+    // (row tid / 16, columns 4 (tid % 16) + 64 u)
+    const size_t nn = (size_t)n * n;
+    const int NP = bwd_np(n), rr = tid >> 4, cq = 4 * (tid & 15);
+    const auto crs = rsrc(a.coef + ((size_t)b * (T - 1) + idx) * 4 * nn, (unsigned)(4 * nn * sizeof(float)));
+    u32x4 rc[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        rc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)((q * nn + (size_t)(r0 + rr) * n + cq + 64 * u) * 4), 0, 0);
+    float* a0 = a.aev + ((size_t)b * 2 * NP + r0 + rr) * NP;
+    float* a1 = a0 + (size_t)NP * NP;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c0 = cq + 64 * u;
+      if (c0 < NP) {
+        floatx4 va, vd;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool in = r0 + rr < n && c0 + e < n;
+          const float cc[4] = {u2f(rc[u][0][e]), u2f(rc[u][1][e]), u2f(rc[u][2][e]), u2f(rc[u][3][e])};
+          va[e] = in ? cubic(cc, f) : 0.f;
+          vd[e] = in ? dcubic(cc, f) : 0.f;
+        }
+        *reinterpret_cast<floatx4*>(a0 + c0) = va;
+        *reinterpret_cast<floatx4*>(a1 + c0) = vd;
+      }
+    }
+  }
   const bool iin = r0 + i < n;
   const int row = iin ? r0 + i : n - 1;
   const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n + row;
@@ -971,7 +965,7 @@ bool rows_vjp_supported(const GncdeProblem& p) {
 
 namespace {
 struct RowsVjpWs {
-  float *keep, *gP[2], *gq[2], *gout[2], *tgF, *dx, *pq, *gfc, *gw, *gwo, *gwp, *gbp, *dy;
+  float *keep, *gP[2], *gq[2], *gout[2], *tgF, *dx, *pq, *gfc, *gw, *gwo, *gwp, *gbp, *dy, *aev;
   int nb, slots, gw_stride, ro_chunks;
 };
 size_t carve_rows_vjp(const GncdeProblem& p, char* ws, RowsVjpWs& w) {
@@ -1003,6 +997,8 @@ size_t carve_rows_vjp(const GncdeProblem& p, char* ws, RowsVjpWs& w) {
   w.gwp = take((size_t)(p.L - 1) * H * H + (size_t)p.dims[p.L] * H);
   w.gbp = take((size_t)(p.L - 1) * H + p.dims[p.L]);
   w.dy = take(B * n * (size_t)out_dim(p));
+  const size_t np = bwd_np(p.n);
+  w.aev = take(B * 2 * np * np);
   return off;
 }
 }  // namespace
@@ -1052,6 +1048,8 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     h.H = H;
     h.cde = cde ? 1 : 0;
     h.ts = p.ts;
+    h.coef = p.coef;
+    h.aev = w.aev;
     h.tcoef = p.tcoef;
     h.data_coef = p.data_coef;
     h.t = t;
@@ -1086,8 +1084,7 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     a.l = l;
     a.nb = w.nb;
     a.ts = p.ts;
-    a.coef = p.coef;
-    a.coefT = static_cast<const float*>(generic_vf_coefT(p, vf_ws));
+    a.aev = w.aev;
     a.csum = csum;
     a.fusion = p.fusion;
     a.t = t;
@@ -1190,7 +1187,6 @@ extern "C" int gncde_diag_vf_vjp(const GncdeProblem* prob, const float* t, const
   }
   (void)H;
   generic_vf_prepare(p, vf_ws, st);
-  if (!rows_supported(p) && rows_vjp_supported(p)) generic_vf_transpose(p, vf_ws, st);
   rows_vjp_begin(p, rows_ws, st);
   unsigned bars = 0;
   const int rc = rows_vf_vjp(p, t, y, gF, gy, nullptr, generic_vf_csum(p, vf_ws), wf, bf, rows_ws, vf_ws, &bars, st);

@@ -717,7 +717,6 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
   tfr.stages = tab.stages;
   for (int i = 0; i < tab.stages; ++i) tfr.c[i] = tab.c[i];
   generic_vf_prepare(p, vf_ws, st);
-  if (!rows_eval_used(p) && rows_vjp_supported(p)) generic_vf_transpose(p, vf_ws, st);
   unsigned bars = 0;  // barriers of one-launch stage evaluations (generic_vf_eval)
   {
     size_t wo = 0, bo = 0;

@@ -39,8 +39,9 @@ def main():
         torch.cuda.synchronize()
     buf = np.zeros(1024 * 16, dtype=np.uint64)
     assert fn(buf.ctypes.data, buf.size) == 0
-    st = buf.reshape(1024, 16)[:, :12].astype(np.float64)
-    st = st[st[:, 0] > 0]
+    full = buf.reshape(1024, 16).astype(np.float64)
+    full = full[full[:, 0] > 0]
+    st = full[:, :12]
     t0 = st[:, 0].min()
     print(f"config {cfg}: {len(st)} workgroups; launch span {(st[:, 11].max() - t0) * 0.01:.2f} us, last start "
           f"{(st[:, 0].max() - t0) * 0.01:.2f} us")
@@ -48,6 +49,11 @@ def main():
         d = (st[:, k] - st[:, k - 1]) * 0.01
         print(f"  {PHASES[k - 1]:>38}: median {np.median(d):6.2f} us  max {d.max():6.2f}")
     print(f"  {'workgroup total':>38}: median {np.median((st[:, 11] - st[:, 0]) * 0.01):6.2f} us")
+    sub = full[:, 12:15]
+    if (sub > 0).all():  # form sub-stamps (from the launch start of each workgroup)
+        for k, name in enumerate(["interval found", "A, dA operands arrived", "coefficient sums arrived"]):
+            d = (sub[:, k] - st[:, 0]) * 0.01
+            print(f"  {'form: ' + name:>38}: median {np.median(d):6.2f} us  max {d.max():6.2f}")
 
 
 if __name__ == "__main__":
