@@ -56,6 +56,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
 __device__ __forceinline__ float u2f(unsigned x) { return __builtin_bit_cast(float, x); }
+// XCD-aware work index: workgroup s runs on XCD s % 8, so consecutive work indices (one sample's row blocks, which
+// read the same Z_l, g_P and A columns and wrote them in the previous launch) go to one XCD and its L2 (a bijection
+// of [0, G) when G % 8 == 0)
+__device__ __forceinline__ int xcd_work(int s, int G) { return G % 8 ? s : (s % 8) * (G / 8) + s / 8; }
 
 __host__ __device__ constexpr int bwd_zs(int H) { return H + 4; }
 __host__ __device__ inline int bwd_np(int n) { return (n + 15) & ~15; }
@@ -142,7 +146,8 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
 
   const int tid = (int)threadIdx.x & 255, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const int nbw = (a.nb + rbw - 1) / rbw;
-  const int b = blockIdx.x / nbw, rbr = (blockIdx.x % nbw) * rbw + grp;
+  const int wx = xcd_work((int)blockIdx.x, (int)gridDim.x);
+  const int b = wx / nbw, rbr = (wx % nbw) * rbw + grp;
   // a group past the sample's last block recomputes that block (every barrier is the whole workgroup's) and stores
   // nothing
   const bool gact = rbr < a.nb;
@@ -196,6 +201,31 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     for (int kd = 0; kd < 3; ++kd) pv[kd][q] = cs[(q * 3 + kd) * n + nd];
     pt[q] = cs[12 * n + q];
   }
+  // ---- Z_l and g_P of every node into LDS (their round trips overlap the operand loads') ----------------------
+  {
+    constexpr int G4 = H / 4;
+    const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.zin + (size_t)b * zgroup);
+    const floatx4* P4 = reinterpret_cast<const floatx4*>(a.gP + (size_t)b * zgroup);
+    const int tot = NP * G4, valid = n * G4;
+    for (int e0 = (int)threadIdx.x; e0 < tot; e0 += NT * 4) {
+      floatx4 vz[4], vp[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + NT * u;
+        vz[u] = e < valid ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
+        vp[u] = e < valid ? P4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + NT * u;
+        if (e < tot) {
+          *reinterpret_cast<floatx4*>(big + (e / G4) * ZS + 4 * (e % G4)) = vz[u];
+          *reinterpret_cast<floatx4*>(sG + (e / G4) * ZS + 4 * (e % G4)) = vp[u];
+        }
+      }
+    }
+    for (int k = (int)threadIdx.x; k < NP; k += NT) sGq[k] = k < n ? a.gq[(size_t)b * n + k] : 0.f;
+  }
   BWD_STAMP_AFTER(13, dAt[3][3]);
   BWD_STAMP_AFTER(14, pv[2][3]);
   // node features and this layer's families at every node (thread = node)
@@ -237,33 +267,6 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   __syncthreads();
   BWD_STAMP(1);
   BWD_STAMP(2);
-
-  // ---- Z_l and g_P of every node ----------------------------------------------------------------------------
-  {
-    constexpr int G4 = H / 4;
-    const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.zin + (size_t)b * zgroup);
-    const floatx4* P4 = reinterpret_cast<const floatx4*>(a.gP + (size_t)b * zgroup);
-    const int tot = NP * G4, valid = n * G4;
-    for (int e0 = (int)threadIdx.x; e0 < tot; e0 += NT * 4) {
-      floatx4 vz[4], vp[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = e0 + NT * u;
-        vz[u] = e < valid ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
-        vp[u] = e < valid ? P4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = e0 + NT * u;
-        if (e < tot) {
-          *reinterpret_cast<floatx4*>(big + (e / G4) * ZS + 4 * (e % G4)) = vz[u];
-          *reinterpret_cast<floatx4*>(sG + (e / G4) * ZS + 4 * (e % G4)) = vp[u];
-        }
-      }
-    }
-    for (int k = (int)threadIdx.x; k < NP; k += NT) sGq[k] = k < n ? a.gq[(size_t)b * n + k] : 0.f;
-  }
-  __syncthreads();
   BWD_STAMP(3);
   for (int k = (int)threadIdx.x; k < NP; k += NT) {
     float ss = 0.f;
@@ -276,20 +279,46 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   }
   __syncthreads();
   BWD_STAMP(4);
-  // zsum = sum_k zhat_k and zf_x = sum_k zhat_k x_k (x = r, rd, c, cd): column c, node groups k = g mod NG with a
-  // fixed NG (the sums do not depend on the row blocks per workgroup), spread over every thread of the workgroup
-  constexpr int NG = 256 * kMaxRbw / H;
-  for (int g = (int)threadIdx.x / H; g < NG; g += NT / H) {
-    const int c = (int)threadIdx.x % H;
-    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int k = g; k < n; k += NG) {
-      const float z = big[k * ZS + c] * sInv[k];
-      acc[0] += z;
+  // zsum = sum_k zhat_k and zf_x = sum_k zhat_k x_k (x = r, rd, c, cd) as one [16 x NP] x [NP x H] MFMA product
+  // (A rows 1, r, rd, c, cd times inv, rows 5.. zero; B = Z_l): work unit = (column tile ct, k quarter kq: the k steps
+  // 4 (kq + 4 i)), spread over every wave of the workgroup; the units' sums do not depend on the row blocks per
+  // workgroup
+  constexpr int NG = 4;
+  {
+    const int gw = (int)threadIdx.x >> 6, nw = NT >> 6;
+    const int x = lo < 5 ? lo : 0;
+    const float* fx = sF + (x > 0 ? x - 1 : 0) * NP;
+    constexpr int KS = kMaxN / 16;  // k steps of one unit at most
+    for (int u = gw; u < CT * NG; u += nw) {
+      const int ct = u / NG, kq = u % NG;
+      // eight k steps' operands read at a time (the steps past NP read row NP - 1 and contribute zero), two chains
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      for (int i0 = 0; i0 < KS && 4 * kq + 16 * i0 < NP; i0 += 8) {
+        float av[8], bv[8];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) acc[1 + x] = fmaf(z, sF[x * NP + k], acc[1 + x]);
+        for (int i = 0; i < 8; ++i) {
+          const int k4 = 4 * kq + 16 * (i0 + i), k = k4 + hi < NP ? k4 + hi : NP - 1;
+          const bool ok = k4 < NP;
+          const float iv = sInv[k], fv = x == 0 ? 1.f : fx[k];
+          const float bz = big[k * ZS + 16 * ct + lo];
+          av[i] = ok && lo < 5 ? fv * iv : 0.f;
+          bv[i] = ok ? bz : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+          acc = mfma4(av[i], bv[i], acc);
+          acc1 = mfma4(av[i + 1], bv[i + 1], acc1);
+        }
+      }
+      acc += acc1;
+      // rows 0..3 in the lanes of hi = 0, row 4 in acc[0] of hi = 1
+      if (hi == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sScr[(kq * 5 + r) * H + 16 * ct + lo] = acc[r];
+      } else if (hi == 1) {
+        sScr[(kq * 5 + 4) * H + 16 * ct + lo] = acc[0];
+      }
     }
-#pragma unroll
-    for (int x = 0; x < 5; ++x) sScr[(g * 5 + x) * H + c] = acc[x];
   }
   __syncthreads();
   float* sZv = sScr + 5 * NG * H - 5 * H;  // zsum, zf_r, zf_rd, zf_c, zf_cd [5][H] (after the group partials)
@@ -307,9 +336,12 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   // ---- the K loop: P = (I+Abar) zhat, g_zhat = (I+Abar)^T g_P, G^T tiles meeting A, dA, A^T, dA^T ----------
   const float eA = fc[GNCDE_FC_E_A], edA = fc[GNCDE_FC_E_DA], eTA = fc[GNCDE_FC_ET_A], eTdA = fc[GNCDE_FC_ET_DA];
   const float wi = sW[ri < NP ? ri : 0], vi = sV[ri < NP ? ri : 0], ui = sRow[lo], gqi = sGq[ri < NP ? ri : 0];
-  float gpr[KH];  // this lane's B operand of the G^T tiles: g_P[ri][4 s + hi]
+  // this lane's B operand of the G^T tiles, g_P[ri][4 s + hi]: held in registers below H = 64 (at H = 64 its 16
+  // registers would spill the 3-group workgroup's 170; read from LDS per chunk)
+  constexpr bool kGpr = H < 64;
+  float gpr[kGpr ? KH : 1];
 #pragma unroll
-  for (int s = 0; s < KH; ++s) gpr[s] = sG[ri * ZS + 4 * s + hi];
+  for (int s = 0; s < (kGpr ? KH : 0); ++s) gpr[s] = sG[ri * ZS + 4 * s + hi];
   floatx4 accP[CT], accT[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
@@ -331,7 +363,12 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
       const int kr = 16 * kc + lo;
       const float ik = sInv[kr];
 #pragma unroll
-      for (int s = 0; s < KH; ++s) gt = mfma4(big[kr * ZS + 4 * s + hi] * ik, gpr[s], gt);
+      for (int s = 0; s < KH; ++s) {
+        float gp;
+        if constexpr (kGpr) gp = gpr[s];
+        else gp = sG[ri * ZS + 4 * s + hi];
+        gt = mfma4(big[kr * ZS + 4 * s + hi] * ik, gp, gt);
+      }
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -578,7 +615,8 @@ template <int H>
 __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
   constexpr int CT = H / 16, KH = H / 4;
   const int nb = (a.n + kRB - 1) / kRB;
-  const int b = blockIdx.x / nb, r0 = (blockIdx.x % nb) * kRB;
+  const int wx = xcd_work((int)blockIdx.x, (int)gridDim.x);
+  const int b = wx / nb, r0 = (wx % nb) * kRB;
   const int n = a.n, T = a.T, tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const int i = tid >> 4, cl = tid & 15;
