@@ -144,7 +144,11 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   float* sScr = sW + NP + 32 * kMaxRbw;  // [1280 kMaxRbw] reduction scratch (5 H floats per node group)
   float* sFus = sScr + 1280 * kMaxRbw + grp * GNCDE_FC * 4;  // [GNCDE_FC][4] of this group
 
-  const int tid = (int)threadIdx.x & 255, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
+  // A group's four wave roles rotate by the group index: the waves of one role index share a SIMD, and the K loop's
+  // node chunks kc = w + 4 j do not split evenly over four waves (config 3: 9 chunks, 3 / 2 / 2 / 2), so the rotation
+  // spreads the long role over the SIMDs.  A permutation of the roles inside the group leaves every result unchanged.
+  const int tid = ((((int)threadIdx.x >> 6) + grp) & 3) << 6 | ((int)threadIdx.x & 63);
+  const int w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const int nbw = (a.nb + rbw - 1) / rbw;
   const int wx = xcd_work((int)blockIdx.x, (int)gridDim.x);
   const int b = wx / nbw, rbr = (wx % nbw) * rbw + grp;
