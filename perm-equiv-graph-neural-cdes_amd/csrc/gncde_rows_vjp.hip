@@ -284,43 +284,43 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
   __syncthreads();
   BWD_STAMP(4);
   // zsum = sum_k zhat_k and zf_x = sum_k zhat_k x_k (x = r, rd, c, cd) as one [16 x NP] x [NP x H] MFMA product
-  // (A rows 1, r, rd, c, cd times inv, rows 5.. zero; B = Z_l): work unit = (column tile ct, k quarter kq: the k steps
-  // 4 (kq + 4 i)), spread over every wave of the workgroup; the units' sums do not depend on the row blocks per
-  // workgroup
-  constexpr int NG = 4;
+  // (A rows 1, r, rd, c, cd times inv, rows 5.. zero; B = Z_l): work unit kq < NG = the k steps 4 (kq + NG i) for
+  // every column tile (the A operand shared), the units spread over every wave of the workgroup; NG is fixed, so the
+  // sums do not depend on the row blocks per workgroup
+  constexpr int NG = 4 * kMaxRbw;
   {
     const int gw = (int)threadIdx.x >> 6, nw = NT >> 6;
     const int x = lo < 5 ? lo : 0;
     const float* fx = sF + (x > 0 ? x - 1 : 0) * NP;
-    constexpr int KS = kMaxN / 16;  // k steps of one unit at most
-    for (int u = gw; u < CT * NG; u += nw) {
-      const int ct = u / NG, kq = u % NG;
-      // eight k steps' operands read at a time (the steps past NP read row NP - 1 and contribute zero), two chains
-      floatx4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      for (int i0 = 0; i0 < KS && 4 * kq + 16 * i0 < NP; i0 += 8) {
-        float av[8], bv[8];
+    constexpr int KS = (kMaxN / 4 + NG - 1) / NG;  // k steps of one unit at most
+    for (int kq = gw; kq < NG; kq += nw) {
+      // every operand of the unit read first (the steps past NP read row NP - 1 and contribute zero)
+      float av[KS];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int k4 = 4 * kq + 16 * (i0 + i), k = k4 + hi < NP ? k4 + hi : NP - 1;
-          const bool ok = k4 < NP;
-          const float iv = sInv[k], fv = x == 0 ? 1.f : fx[k];
-          const float bz = big[k * ZS + 16 * ct + lo];
-          av[i] = ok && lo < 5 ? fv * iv : 0.f;
-          bv[i] = ok ? bz : 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; i += 2) {
-          acc = mfma4(av[i], bv[i], acc);
-          acc1 = mfma4(av[i + 1], bv[i + 1], acc1);
-        }
+      for (int i = 0; i < KS; ++i) {
+        const int k4 = 4 * (kq + NG * i), k = k4 + hi < NP ? k4 + hi : NP - 1;
+        const float iv = sInv[k], fv = x == 0 ? 1.f : fx[k];
+        av[i] = k4 < NP && lo < 5 ? fv * iv : 0.f;
       }
-      acc += acc1;
-      // rows 0..3 in the lanes of hi = 0, row 4 in acc[0] of hi = 1
-      if (hi == 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sScr[(kq * 5 + r) * H + 16 * ct + lo] = acc[r];
-      } else if (hi == 1) {
-        sScr[(kq * 5 + 4) * H + 16 * ct + lo] = acc[0];
+      for (int ct = 0; ct < CT; ++ct) {
+        float bv[KS];
+#pragma unroll
+        for (int i = 0; i < KS; ++i) {
+          const int k4 = 4 * (kq + NG * i), k = k4 + hi < NP ? k4 + hi : NP - 1;
+          const float bz = big[k * ZS + 16 * ct + lo];
+          bv[i] = k4 < NP ? bz : 0.f;
+        }
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < KS; ++i) acc = mfma4(av[i], bv[i], acc);
+        // rows 0..3 in the lanes of hi = 0, row 4 in acc[0] of hi = 1
+        if (hi == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sScr[(kq * 5 + r) * H + 16 * ct + lo] = acc[r];
+        } else if (hi == 1) {
+          sScr[(kq * 5 + 4) * H + 16 * ct + lo] = acc[0];
+        }
       }
     }
   }
