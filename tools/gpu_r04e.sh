@@ -9,4 +9,5 @@ bash tools/gpu_session.sh bench prof pmc pmcsq || exit $?
 timeout -k 10 300 python tools/bench_configs.py --configs 3,4,5 > gpurun_out/configs_final.jsonl 2>&1 || exit $?
 timeout -k 10 300 python tools/bench_configs.py --configs 5 --batch5 64 > gpurun_out/cfg5_64.jsonl 2>&1 || exit $?
 timeout -k 10 300 python tools/bench_grad_configs.py --configs 3,5 > gpurun_out/grad_final.jsonl 2>&1 || exit $?
+bash tools/gpu_session.sh profgrad || exit $?
 echo r04e done
