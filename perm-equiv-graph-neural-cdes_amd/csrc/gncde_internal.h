@@ -129,6 +129,11 @@ __device__ __forceinline__ int interval_index(const float* ts, int T, float t) {
 // The same index from one round of loads: every lane of the wave reads a knot and the ballot counts the knots
 // below t (searchsorted 'left' on sorted knots), instead of log2(T) dependent loads.  Call with the whole wave
 // active (uniform control flow).
+// XCD-aware work index: workgroup s runs on XCD s % 8, so consecutive work indices (one sample's row blocks, which
+// read the same sample's Z, g_P and coefficient columns) go to one XCD and its L2 (a bijection of [0, G) when
+// G % 8 == 0)
+__device__ __forceinline__ int xcd_work(int s, int G) { return G % 8 ? s : (s % 8) * (G / 8) + s / 8; }
+
 __device__ __forceinline__ int interval_index_wave(const float* ts, int T, float t) {
   const int lane = threadIdx.x & 63;
   int cnt = 0;

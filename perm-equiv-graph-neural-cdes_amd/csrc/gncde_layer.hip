@@ -63,6 +63,19 @@ __host__ __device__ constexpr int zs_stride() {
 // MODE 0: hidden layer, ReLU.  MODE 1: ODE output layer, out = tg * Z_next.  MODE 2: CDE output layer (DOUT = h).
 // BF: the n x n product on v_mfma_f32_16x16x32_bf16 (GNCDE_COMPUTE_BF16*): (I + Abar) from its bf16 (hi, lo) planes,
 // diag(inv) Z split into (hi, lo) on the fly, three products (hi hi, hi lo, lo hi) with fp32 accumulation.
+// Phase stamps of the fp32 CDE read-out launch (diagnostic build -DGNCDE_LAYER_STAMPS only: tools/diag_layer_stamps.py):
+// the first wave of every workgroup records s_memrealtime at 7 points of the last such launch.
+#ifdef GNCDE_LAYER_STAMPS
+__device__ unsigned long long g_layer_stamps[1024 * 8];
+#define LAYER_STAMP(k)                                                                                              \
+  do {                                                                                                              \
+    const int wg_ = blockIdx.x + gridDim.x * blockIdx.y;                                                            \
+    if (MODE == 2 && !BF && threadIdx.x == 0 && wg_ < 1024) g_layer_stamps[wg_ * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define LAYER_STAMP(k) do {} while (0)
+#endif
+
 template <int DIN, int DOUT, int MODE, bool BF>
 __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -80,9 +93,13 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
   // MODE 2 splits the read-out's channels over kSplit workgroups per row block (each recomputes P: the product is
   // 1/16 of the read-out's MFMA work) so that the grid balances over the 256 CUs.
   constexpr int SPLIT = (MODE == 2 && DOUT / 16 >= kSplit) ? kSplit : 1;
-  const int b = blockIdx.y, r0 = (blockIdx.x / SPLIT) * kRows, ch = blockIdx.x % SPLIT;
+  // (one sample's workgroups on one XCD: they all stage that sample's Z)
+  const int wx = xcd_work((int)(blockIdx.x + gridDim.x * blockIdx.y), (int)(gridDim.x * gridDim.y));
+  const int bx = wx % (int)gridDim.x;
+  const int b = wx / (int)gridDim.x, r0 = (bx / SPLIT) * kRows, ch = bx % SPLIT;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const size_t nb = (size_t)b * n;
+  LAYER_STAMP(0);
 
   const bool two = r0 + 16 < n;  // the second row tile holds a valid row (else its MFMAs are skipped)
   // The fp32 product's first round of (I + Abar) operand loads is issued before Z is staged: the two HBM / L2 round
@@ -173,6 +190,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         sDx[row * 17 + j] = R < n ? a.dx[(nb + R) * 16 + j] : 0.f;
       }
     __syncthreads();
+    LAYER_STAMP(1);
     for (int r = tid; r < nk; r += 256) {
       float ss = 0.f;
 #pragma unroll
@@ -184,6 +202,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
     }
   }
   __syncthreads();
+  LAYER_STAMP(2);
 
   // ---- 2. P = (I + Abar)[R, :] Zs: wave w takes the 16-deep K chunks w, w + 4, ... for every column tile, so each
   // (I + Abar) element is loaded once per workgroup; the four K partials meet in LDS (aliasing Zs) in a fixed order.
@@ -289,6 +308,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         mm(std::false_type{});
     }
     __syncthreads();  // Zs reads done: the partials alias it
+    LAYER_STAMP(3);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -297,6 +317,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         for (int r = 0; r < 4; ++r) Ps[(w * kRows + 16 * t + 4 * hi + r) * ZS + 16 * ct + lo] = acc[t][ct][r];
   }
   __syncthreads();
+  LAYER_STAMP(4);
 
   // P row (16 t + lo), columns 16 cc + 4 hi .. +3, summed over the K parts in a fixed order
   auto prow = [&](int t, int cc) -> floatx4 {
@@ -379,6 +400,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
       kloop(std::true_type{});
     else
       kloop(std::false_type{});
+    LAYER_STAMP(5);
     // bias term of this wave's j range; rows 16 t + 4 hi + r, channel m = 16 ct + lo
     const int m = 16 * ct + lo;
 #pragma unroll
@@ -415,6 +437,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
           }
         }
     }
+    LAYER_STAMP(6);
   }
 }
 
@@ -526,3 +549,11 @@ void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, cons
 }
 
 }  // namespace gncde
+
+#ifdef GNCDE_LAYER_STAMPS
+extern "C" int gncde_debug_layer_stamps(unsigned long long* host, int count) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gncde::g_layer_stamps), sizeof(unsigned long long) * count) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif

@@ -56,10 +56,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
 __device__ __forceinline__ float u2f(unsigned x) { return __builtin_bit_cast(float, x); }
-// XCD-aware work index: workgroup s runs on XCD s % 8, so consecutive work indices (one sample's row blocks, which
-// read the same Z_l, g_P and A columns and wrote them in the previous launch) go to one XCD and its L2 (a bijection
-// of [0, G) when G % 8 == 0)
-__device__ __forceinline__ int xcd_work(int s, int G) { return G % 8 ? s : (s % 8) * (G / 8) + s / 8; }
 
 __host__ __device__ constexpr int bwd_zs(int H) { return H + 4; }
 __host__ __device__ inline int bwd_np(int n) { return (n + 15) & ~15; }
