@@ -274,11 +274,20 @@ void generic_vf_transpose(const GncdeProblem& p, char* ws, hipStream_t st);
 bool rows_vjp_supported(const GncdeProblem& p);
 size_t rows_vjp_workspace(const GncdeProblem& p);
 void rows_vjp_begin(const GncdeProblem& p, char* ws, hipStream_t st);
+// The step sweep's per-stage scatter of the stage input's cotangent v: gy += v, gk[j] += h a[j] v (h per sample).
+struct StageScatter {
+  float* gy;
+  const float* hcur;
+  float* gk[8];
+  float a[8];
+  int n;
+};
 // kept (optional): the stage's hidden outputs [L-1, B, n, H] from the forward's activation record (GncdeSolver.act_rec);
-// without it the evaluation's forward runs first in keep mode
+// without it the evaluation's forward runs first in keep mode.  scat (optional): the layer-0 launch applies that
+// scatter to the stage input's cotangent instead of writing it to gu (one launch per stage fewer, same arithmetic)
 int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* gF, float* gu, float* gdata,
                 const float* csum, const float* wf, const float* bfold, char* ws, char* vf_ws, unsigned* bars,
-                hipStream_t st, const float* kept = nullptr);
+                hipStream_t st, const float* kept = nullptr, const StageScatter* scat = nullptr);
 void rows_vjp_finish(const GncdeProblem& p, char* ws, float* gparams, float* gfusion, hipStream_t st);
 
 // the persistent solve on the one-launch evaluation (gncde_rows.hip): n <= 256, one width; Tsit5 + PIDController

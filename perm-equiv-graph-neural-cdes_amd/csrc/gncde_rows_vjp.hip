@@ -110,6 +110,8 @@ struct BwdArgs {
   float* gw;               // [B * nb, gw_stride] accumulated; this layer's H x H g_W' then H g_b' at gw_off
   int gw_stride, gw_off;
   int cde_out;             // layer l is the CDE read-out layer
+  int scatter;             // l = 0: apply sc to the stage input's cotangent instead of writing gz
+  StageScatter sc;
 };
 
 // One ConvLayer's reverse mode for rbw = blockDim.x / 256 row blocks R of one sample (see the file comment): each
@@ -553,9 +555,19 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u) gZ[u] = inv * (gzh[u] - z[u] * inv * cdot);
     if (l == 0) {
-      if (iin)
+      if (iin && a.scatter) {  // gncde_vjp.hip's v_stage_scatter arithmetic, fused
+        const float hb = a.sc.hcur[b];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const size_t o = ((size_t)b * n + r0 + i) * H + cl + 16 * u;
+          const float v = gZ[u];
+          a.sc.gy[o] = fmaf(1.0f, v, a.sc.gy[o]);
+          for (int j = 0; j < a.sc.n; ++j) a.sc.gk[j][o] = fmaf(hb, a.sc.a[j] * v, a.sc.gk[j][o]);
+        }
+      } else if (iin) {
 #pragma unroll
         for (int u = 0; u < U; ++u) a.gz[((size_t)b * n + r0 + i) * H + cl + 16 * u] = gZ[u];
+      }
     } else {
       float* go = epG;  // g_out_{l-1}[R] = g_Z * [Z_l > 0]
 #pragma unroll
@@ -1060,7 +1072,7 @@ void rows_vjp_begin(const GncdeProblem& p, char* ws, hipStream_t st) {
 // every layer back to back (generic_vf_prepare's fold).
 int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const float* gF, float* gu, float* gdata,
                 const float* csum, const float* wf, const float* bfold, char* ws, char* vf_ws, unsigned* bars,
-                hipStream_t st, const float* kept) {
+                hipStream_t st, const float* kept, const StageScatter* scat) {
   RowsVjpWs w;
   carve_rows_vjp(p, ws, w);
   const int B = p.B, n = p.n, H = p.dims[0], L = p.L;
@@ -1136,6 +1148,8 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     a.gq_next = w.gq[cur ^ 1];
     a.gout_next = w.gout[cur ^ 1];
     a.gz = gu;
+    a.scatter = scat != nullptr;
+    if (scat) a.sc = *scat;
     a.pq = w.pq;
     a.gfc = w.gfc;
     a.gw = w.gw;

@@ -783,21 +783,30 @@ int generic_integrate_vjp(const GncdeProblem& p, const GncdeSolver& s, const flo
       if (rows) {
         const float* kept =
             s.act_rec ? s.act_rec + ((size_t)k * tab.stages + i) * (size_t)(p.L - 1) * B * E : nullptr;
+        // gy += tmp ; gK_j += h a_ij tmp inside the layer-0 launch
+        StageScatter ss{};
+        ss.gy = w.lam;
+        ss.hcur = w.hcur;
+        for (int j = 0; j < i; ++j)
+          if (tab.a[i][j] != 0.f) {
+            ss.gk[ss.n] = w.gK[j];
+            ss.a[ss.n++] = tab.a[i][j];
+          }
         const int rc = rows_vf_vjp(p, tsti, w.U[i], w.gK[i], w.tmp, gdata, generic_vf_csum(p, vf_ws), w.wf, w.bf,
-                                   rows_ws, vf_ws, &bars, st, kept);
+                                   rows_ws, vf_ws, &bars, st, kept, &ss);
         if (rc) return rc;
       } else {
         (void)hipMemsetAsync(w.tmp, 0, (size_t)B * E * sizeof(float), st);
         vf_vjp(p, tsti, w.U[i], w.gK[i], w.tmp, gdata, w, st);
+        // gy += tmp ; gK_j += h a_ij tmp (one launch)
+        Scatter sc{};
+        for (int j = 0; j < i; ++j)
+          if (tab.a[i][j] != 0.f) {
+            sc.gk[sc.n] = w.gK[j];
+            sc.a[sc.n++] = tab.a[i][j];
+          }
+        hipLaunchKernelGGL(v_stage_scatter, ge, dim3(256), 0, st, B, E, w.tmp, w.hcur, w.lam, sc);
       }
-      // gy += tmp ; gK_j += h a_ij tmp (one launch)
-      Scatter sc{};
-      for (int j = 0; j < i; ++j)
-        if (tab.a[i][j] != 0.f) {
-          sc.gk[sc.n] = w.gK[j];
-          sc.a[sc.n++] = tab.a[i][j];
-        }
-      hipLaunchKernelGGL(v_stage_scatter, ge, dim3(256), 0, st, B, E, w.tmp, w.hcur, w.lam, sc);
     }
     if (s.save_mode == GNCDE_SAVE_STEPS)
       hipLaunchKernelGGL(v_step_row, ge, dim3(256), 0, st, B, E, G, k, gys, w.lam, 1);
