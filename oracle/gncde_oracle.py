@@ -403,7 +403,8 @@ def solve_fixed_grid(f, grid, y0, method="rk4", save_every_step=False, time_dtyp
             if fk is None:
                 fk = f(t, y)
                 nevals += 1
-            y, _, ks = tsit5_step(f, t, y, h, k1=h * fk, time_dtype=time_dtype)
+            t_end = float(grid[k + 1]) if time_dtype is None else float(time_dtype(grid[k + 1]))
+            y, _, ks = tsit5_step(f, t, y, h, k1=h * fk, time_dtype=time_dtype, t_end=t_end)
             fk = ks[6] / h if h != 0 else f(t + h, y)
             nevals += 6
         else:
@@ -412,9 +413,13 @@ def solve_fixed_grid(f, grid, y0, method="rk4", save_every_step=False, time_dtyp
     return (np.stack(ys) if save_every_step else y), nevals
 
 
-def tsit5_step(f, t, y, h, k1=None, time_dtype=None):
-    """One Tsit5 step.  Returns (y1, y_err, ks) with ks the 7 increments (dt * f); ks[6] = h f(t+h, y1)."""
+def tsit5_step(f, t, y, h, k1=None, time_dtype=None, t_end=None):
+    """One Tsit5 step.  Returns (y1, y_err, ks) with ks the 7 increments (dt * f); ks[6] = h f(t_end, y1): the FSAL
+    stage is evaluated at the step's end time t_end (the grid knot / the controller's t + dt; t + h if not given),
+    where it is reused as the next step's first stage."""
     tst = _stage_times(t, h, list(TSIT5_C), time_dtype)
+    if t_end is not None:
+        tst[6] = float(t_end)
     ks = []
     if k1 is None:
         k1 = h * f(tst[0], y)
@@ -482,7 +487,7 @@ def solve_tsit5_pid(f, t0, t1, y0, rtol=1e-3, atol=1e-6, dt0=None, save_ts=None,
         if tn > t1 - 1e-6:
             tn = float(t1)
         h = tn - t
-        y1, yerr, ks = tsit5_step(f, t, y, h, k1=h * fk)
+        y1, yerr, ks = tsit5_step(f, t, y, h, k1=h * fk, t_end=tn)
         evals += 6
         scale = atol + rtol * np.maximum(np.abs(y), np.abs(y1))
         err = rms(yerr / scale)

@@ -233,9 +233,11 @@ def _grid_geometry(grid, time_dtype):
     return geo
 
 
-def _tsit5_stages(f, t, h, y, time_dtype):
-    """The 7 stage inputs / values of a Tsit5 step (stage 7: f(t + h, y1)) and y1."""
+def _tsit5_stages(f, t, h, y, time_dtype, t_end=None):
+    """The 7 stage inputs / values of a Tsit5 step (stage 7: f(t_end, y1), the step's end knot) and y1."""
     tst = O._stage_times(t, h, list(O.TSIT5_C), time_dtype)
+    if t_end is not None:
+        tst[6] = float(t_end)
     U, K = [], []
     for i in range(7):
         if i < 6:
@@ -247,14 +249,19 @@ def _tsit5_stages(f, t, h, y, time_dtype):
     return tst, U, K
 
 
+def _end_knots(grid, time_dtype):
+    """Each step's end knot as the kernels see it (the FSAL stage's time)."""
+    return [float(grid[k + 1]) if time_dtype is None else float(time_dtype(grid[k + 1])) for k in range(len(grid) - 1)]
+
+
 def solve_grid_dense(f, grid, y0, save_ts, time_dtype=np.float32):
     """Tsit5 on the accepted step sequence ``grid`` with SaveAt(ts) through the dense interpolant: what an adaptive
     solve outputs once its steps are fixed.  Returns [S, n, d]."""
     y = np.asarray(y0, np.float64)
     geo = _grid_geometry(grid, time_dtype)
     ys, stages = [y], []
-    for t, h in geo:
-        _, _, K = _tsit5_stages(f, t, h, ys[-1], time_dtype)
+    for (t, h), te in zip(geo, _end_knots(grid, time_dtype)):
+        _, _, K = _tsit5_stages(f, t, h, ys[-1], time_dtype, te)
         stages.append(K)
         ys.append(ys[-1] + h * sum(O.TSIT5_B[j] * K[j] for j in range(6)))
     out = []
@@ -271,15 +278,16 @@ def solve_grid_dense(f, grid, y0, save_ts, time_dtype=np.float32):
 def solve_grid_dense_vjp(f, f_vjp, grid, y0, save_ts, g_saves, time_dtype=np.float32):
     """Reverse mode of solve_grid_dense for cotangents g_saves [S, n, d]: (g_y0, summed parameter grads).
 
-    Per save point s in step k: y(ts) = y_k + h_k sum_j b_j(th) K_j, j = 0..6, K_6 = f(t_k + h_k, y_{k+1}).  Going
+    Per save point s in step k: y(ts) = y_k + h_k sum_j b_j(th) K_j, j = 0..6, K_6 = f(t_{k+1}, y_{k+1}).  Going
     backwards over the steps, the cotangent of K_6 of step k is pulled back through f onto y_{k+1} first; then the
     usual Tsit5 adjoint of step k runs with stage seeds h_k (b_j lambda_{k+1} + sum_s b_j(th_s) g_s)."""
     y = np.asarray(y0, np.float64)
     geo = _grid_geometry(grid, time_dtype)
     gridd = np.asarray(grid, np.float64)
     ys = [y]
-    for t, h in geo:
-        _, _, K = _tsit5_stages(f, t, h, ys[-1], time_dtype)
+    tend = _end_knots(grid, time_dtype)
+    for (t, h), te in zip(geo, tend):
+        _, _, K = _tsit5_stages(f, t, h, ys[-1], time_dtype, te)
         ys.append(ys[-1] + h * sum(O.TSIT5_B[j] * K[j] for j in range(6)))
     N = len(geo)
     dense = [np.zeros((7,) + y.shape) for _ in range(N)]   # sum_s b_j(th_s) g_s per step
@@ -296,8 +304,8 @@ def solve_grid_dense_vjp(f, f_vjp, grid, y0, save_ts, g_saves, time_dtype=np.flo
     b = list(O.TSIT5_B[:6])
     for k in range(N - 1, -1, -1):
         t, h = geo[k]
-        tst, U, _ = _tsit5_stages(f, t, h, ys[k], time_dtype)
-        if np.any(dense[k][6]):  # K_6 = f(t + h, y_{k+1})
+        tst, U, _ = _tsit5_stages(f, t, h, ys[k], time_dtype, tend[k])
+        if np.any(dense[k][6]):  # K_6 = f(t_{k+1}, y_{k+1})
             gu, gr = f_vjp(tst[6], U[6], h * dense[k][6])
             total = _acc(total, gr)
             lam = lam + gu

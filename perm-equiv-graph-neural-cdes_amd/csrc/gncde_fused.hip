@@ -571,7 +571,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
           yt[fb][r] = fmaf(h, sacc, y[fb][r]);
         }
       if (a.rec && ns1 <= 5) store_from(a.rec + (((size_t)b * (G - 1) + k) * 5 + ns1 - 1) * E, yt);  // U_ns1
-      tst = ns1 >= 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);
+      tst = ns1 == 6 ? g[k + 1] : ns1 == 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);  // FSAL stage at the knot
       st = ns1;
     }
   }
@@ -766,7 +766,7 @@ __global__ void __launch_bounds__(NP * 4, (min_waves_per_eu<NP, H, L, METHOD>())
           for (int j = 0; j < 6; ++j) sacc = fmaf(arow[j], kk[j][fb][r], sacc);
           yt[fb][r] = fmaf(h, sacc, y[fb][r]);
         }
-      tst = ns1 >= 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);
+      tst = ns1 == 6 ? tn : ns1 == 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);  // FSAL stage at the step end
       st = ns1;
     }
     if (a.step_ts && status == 0 && steps + 1 > a.step_len) status = 3;  // step record truncated

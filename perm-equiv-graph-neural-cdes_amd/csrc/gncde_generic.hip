@@ -503,10 +503,11 @@ __global__ void k_finalize(int n, int dL, int h, int de, int T, const float* __r
 }
 
 // ---- solver helpers ---------------------------------------------------------------------------------
-// Per-sample step geometry for step k of the host-planned grid; tst = the first stage's time (c = 0).
+// Per-sample step geometry for step k of the host-planned grid; tst = the first stage's time (c = 0), tnx = the
+// step's end knot (Tsit5's FSAL stage is evaluated there: it is the next step's first stage).
 __global__ void k_grid_step(int B, int G, int k, const float* __restrict__ grid,
                             const int32_t* __restrict__ nsteps, float* __restrict__ tcur,
-                            float* __restrict__ hcur, float* __restrict__ tst) {
+                            float* __restrict__ hcur, float* __restrict__ tst, float* __restrict__ tnx) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const float* g = grid + (size_t)b * G;
@@ -515,9 +516,11 @@ __global__ void k_grid_step(int B, int G, int k, const float* __restrict__ grid,
   if (k < ns) {
     tcur[b] = g[k];
     hcur[b] = g[k + 1] - g[k];
+    tnx[b] = g[k + 1];
   } else {
     tcur[b] = g[ns];
     hcur[b] = 0.f;
+    tnx[b] = g[ns];
   }
   tst[b] = tcur[b];
 }
@@ -530,6 +533,7 @@ struct Combo {
   int nk;
   float c;
   const float* tcur;
+  const float* tend;  // non-null: the next stage is Tsit5's FSAL stage, evaluated at the step's end knot tend[b]
   float* tst;
   float* rec;         // stage record slot of this stage input ([B, G-1, S-1, E] at (k, i-1)) or nullptr
   size_t rec_stride;  // floats between consecutive samples' slots: (G-1)*(S-1)*E
@@ -541,7 +545,7 @@ __global__ void __launch_bounds__(256) k_combo(int B, size_t E, const float* __r
                                                const float* __restrict__ hcur, float* __restrict__ out) {
   const int b = blockIdx.y;
   const size_t e0 = (size_t)blockIdx.x * (blockDim.x * kComboU) + threadIdx.x;
-  if (cb.tst && e0 == 0) cb.tst[b] = stage_time(cb.tcur[b], cb.c, hcur[b]);
+  if (cb.tst && e0 == 0) cb.tst[b] = cb.tend ? cb.tend[b] : stage_time(cb.tcur[b], cb.c, hcur[b]);
   const float hb = hcur[b];
   float kv[7][kComboU], yv[kComboU];
 #pragma unroll
@@ -940,7 +944,7 @@ size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s) 
   const size_t B = p.B, E = (size_t)p.n * state_dim(p);
   size_t sz = generic_vf_workspace(p);
   sz += 9 * align_up(B * E * 4, 256);  // y, ytmp, K[7]
-  sz += 3 * align_up(B * 4, 256);      // tcur, hcur, tstage
+  sz += 4 * align_up(B * 4, 256);      // tcur, hcur, tstage, tnx
   return sz;
 }
 
@@ -968,6 +972,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   float* tcur = take(B);
   float* hcur = take(B);
   float* tst = take(B);
+  float* tnx = take(B);
   const int G = s.grid_len;
   const unsigned gb = cdiv(B, 256);
   const dim3 ge(cdiv(E, 256), B);
@@ -993,6 +998,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   // stage record (GncdeSolver.stage_rec): the stage input U_i of step k goes to slot (k, i-1) as it is formed
   float* rec = G >= 2 ? s.stage_rec : nullptr;
   int rec_k = 0, rec_i = 0;  // slot of the next combination's output (rec_i == 0: not recorded)
+  bool fsal_next = false;     // the combination forms Tsit5's FSAL stage input (its time: the step's end knot)
   auto combo = [&](std::initializer_list<std::pair<int, float>> terms, float* out, float c_next, bool has_next) {
     Combo cb{};
     if (rec && rec_i > 0) {
@@ -1007,6 +1013,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     }
     cb.c = c_next;
     cb.tcur = tcur;
+    cb.tend = fsal_next ? tnx : nullptr;
     cb.tst = has_next ? tst : nullptr;
     hipLaunchKernelGGL(k_combo, gc, dim3(256), 0, st, B, E, y, cb, hcur, out);
   };
@@ -1026,7 +1033,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   const int steps = G - 1;
   if (s.method == GNCDE_RK4) {
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
-      hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst);
+      hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst, tnx);
       rec_k = k;
       rec_i = 1;
       cur_k = k;
@@ -1043,11 +1050,11 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
         hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, k + 1, y, ys);
     }
   } else {  // Tsit5 on the grid (ConstantStepSize), FSAL
-    hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, 0, s.grid, s.nsteps, tcur, hcur, tst);
+    hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, 0, s.grid, s.nsteps, tcur, hcur, tst, tnx);
     keep_next = act(0, 0);
     rc |= eval(y, K[0]);
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
-      hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst);
+      hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst, tnx);
       cur_k = k;
       rec_k = k;
       rec_i = 1;
@@ -1062,8 +1069,10 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
       eval_combo(yt, 4, {{0, TSIT5_A61}, {1, TSIT5_A62}, {2, TSIT5_A63}, {3, TSIT5_A64}, {4, TSIT5_A65}}, yt, 1.0f,
                  true);
       rec_i = 0;
+      fsal_next = true;
       eval_combo(yt, 5, {{0, TSIT5_B1}, {1, TSIT5_B2}, {2, TSIT5_B3}, {3, TSIT5_B4}, {4, TSIT5_B5}, {5, TSIT5_B6}},
                  yt, 1.0f, true);
+      fsal_next = false;
       keep_next = act(k + 1, 0);  // the FSAL evaluation is the next step's stage 0
       rc |= eval(yt, K[6]);
       std::swap(y, yt);

@@ -28,6 +28,7 @@ struct PidState {
 
 struct PidArgs {
   int B, E, S, max_steps, auto_dt;
+  int n, d;     // E = n d: node rows of width d (the norms' canonical order, canon_sumsq)
   float rtol, atol;
   const float* t0;
   const float* t1;
@@ -44,16 +45,42 @@ struct PidArgs {
   float* tst;   // [B] time of each sample's next evaluation (written by init / advance)
   float* step_ts;  // [B, step_len] accepted step times (GncdeSolver.step_ts) or nullptr
   int step_len;
+  float* vbuf;  // [B, E] the norms' per-element values
+  float* rbuf;  // [B, n + ceil(n / 16)] their row and row-block sums
 };
 
-__device__ __forceinline__ float block_sum(float v, float* red) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+// sum of v_e^2 over one sample's [n, d] elements (v in vb, written by this workgroup before the call) in the
+// CANONICAL order the persistent solve uses too (gncde_rows.hip group_sumsq): a 4-element chunk of a row is an fma
+// chain from 0, a row sums its chunks in order, a 16-row block its rows in order, and the sample its blocks in
+// order.  The two controllers therefore see bitwise-equal error norms and take the same accept / reject decisions.
+__device__ float canon_sumsq(const float* vb, float* rb, int n, int d, float* red) {
+  __syncthreads();  // every element of vb written (global memory, this workgroup)
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float* r = vb + (size_t)i * d;
+    float s = 0.f;
+    for (int c = 0; c < d; c += 4) {
+      float p = 0.f;
+      for (int e = c; e < c + 4 && e < d; ++e) p = fmaf(r[e], r[e], p);
+      s = c == 0 ? p : s + p;
+    }
+    rb[i] = s;
+  }
   __syncthreads();
-  if (lane == 0) red[w] = v;
+  const int nb = (n + 15) / 16;
+  for (int q = threadIdx.x; q < nb; q += blockDim.x) {
+    float s = rb[16 * q];
+    for (int i = 16 * q + 1; i < 16 * q + 16 && i < n; ++i) s += rb[i];
+    rb[n + q] = s;
+  }
   __syncthreads();
-  float tot = 0.f;
-  for (int j = 0; j < (int)(blockDim.x >> 6); ++j) tot += red[j];
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int q = 0; q < nb; ++q) tot += rb[n + q];
+    red[0] = tot;
+  }
+  __syncthreads();
+  const float tot = red[0];
+  __syncthreads();  // (red and vb are reused by the next call)
   return tot;
 }
 
@@ -113,6 +140,8 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
   float* yt = a.yt + base;
   const float* K = a.K + base;
   auto kk = [&](int j) { return a.kk + (size_t)j * BE + base; };
+  float* vb = a.vbuf + base;
+  float* rb = a.rbuf + (size_t)b * (a.n + (a.n + 15) / 16);
   constexpr int U = kAdvU, P = kAdvThreads * kAdvU;
   auto ldu = [&](const float* p, int e0, float(&v)[U]) __attribute__((always_inline)) {
 #pragma unroll
@@ -127,15 +156,10 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
     for (int e = tid; e < E; e += blockDim.x) kk(0)[e] = K[e];
     s.phase = 2;
     if (a.auto_dt) {
-      float p0 = 0.f, p1 = 0.f;
-      for (int e = tid; e < E; e += blockDim.x) {
-        const float sc = fmaf(fabsf(y[e]), rtol, atol);
-        const float u = y[e] / sc, v = K[e] / sc;
-        p0 = fmaf(u, u, p0);
-        p1 = fmaf(v, v, p1);
-      }
-      const float d0 = sqrtf(block_sum(p0, red) * inv_cnt);
-      const float d1 = sqrtf(block_sum(p1, red) * inv_cnt);
+      for (int e = tid; e < E; e += blockDim.x) vb[e] = y[e] / fmaf(fabsf(y[e]), rtol, atol);
+      const float d0 = sqrtf(canon_sumsq(vb, rb, a.n, a.d, red) * inv_cnt);
+      for (int e = tid; e < E; e += blockDim.x) vb[e] = K[e] / fmaf(fabsf(y[e]), rtol, atol);
+      const float d1 = sqrtf(canon_sumsq(vb, rb, a.n, a.d, red) * inv_cnt);
       s.d1 = d1;
       s.h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : 0.01f * (d0 / d1);
       for (int e = tid; e < E; e += blockDim.x) yt[e] = fmaf(s.h0, K[e], y[e]);
@@ -145,13 +169,8 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
       start = true;
     }
   } else if (s.phase == 1) {  // f(t0 + h0, y0 + h0 f0)
-    float p2 = 0.f;
-    for (int e = tid; e < E; e += blockDim.x) {
-      const float sc = fmaf(fabsf(y[e]), rtol, atol);
-      const float v = (K[e] - kk(0)[e]) / sc;
-      p2 = fmaf(v, v, p2);
-    }
-    const float d2 = sqrtf(block_sum(p2, red) * inv_cnt) / s.h0;
+    for (int e = tid; e < E; e += blockDim.x) vb[e] = (K[e] - kk(0)[e]) / fmaf(fabsf(y[e]), rtol, atol);
+    const float d2 = sqrtf(canon_sumsq(vb, rb, a.n, a.d, red) * inv_cnt) / s.h0;
     const float md = fmaxf(s.d1, d2);
     const float h1 = md <= 1e-15f ? fmaxf(1e-6f, s.h0 * 1e-3f) : powf(0.01f / md, 0.2f);
     s.dt = fminf(100.0f * s.h0, h1);
@@ -198,7 +217,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
           }
         }
       }
-      s.tst = ns1 >= 5 ? __fadd_rn(s.t, s.h) : stage_time(s.t, cst, s.h);
+      s.tst = ns1 == 6 ? s.tn : ns1 == 5 ? __fadd_rn(s.t, s.h) : stage_time(s.t, cst, s.h);  // FSAL stage at the step end
       s.st = ns1;
       if (slice == 0 && tid == 0) {
         a.state_out[b] = s;
@@ -217,7 +236,6 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
       ldu(K, tid, kv[6]);
       ldu(y, tid, yv);
       ldu(yt, tid, ytv);
-      float pe = 0.f;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = tid + u * kAdvThreads;
@@ -226,10 +244,9 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
         const float err = s.h * (TSIT5_E1 * kv[0][u] + TSIT5_E2 * kv[1][u] + TSIT5_E3 * kv[2][u] + TSIT5_E4 * kv[3][u] +
                                  TSIT5_E5 * kv[4][u] + TSIT5_E6 * kv[5][u] + TSIT5_E7 * kv[6][u]);
         const float sc = fmaf(fmaxf(fabsf(yv[u]), fabsf(ytv[u])), rtol, atol);
-        const float v = err / sc;
-        pe = fmaf(v, v, pe);
+        vb[e] = err / sc;
       }
-      const float err = sqrtf(block_sum(pe, red) * inv_cnt);
+      const float err = sqrtf(canon_sumsq(vb, rb, a.n, a.d, red) * inv_cnt);
       const bool finite = isfinite(err);
       const bool keep = finite && err < 1.0f;
       float factor;
@@ -324,7 +341,6 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
         if (e0 + u * kAdvThreads < E) kst[e0 + u * kAdvThreads] = v[u];
     }
     if (s.st == 6) {  // attempt complete: yt = y1 candidate, kk6 = f(tn, y1) (= K)
-      float pe = 0.f;
       for (int e0 = tid; e0 < E; e0 += P) {
         float k0[U], k1[U], k2[U], k3[U], k4[U], k5[U], k6[U], yv[U], ytv[U];
         ldu(kk(0), e0, k0);
@@ -342,11 +358,10 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
           const float err = s.h * (TSIT5_E1 * k0[u] + TSIT5_E2 * k1[u] + TSIT5_E3 * k2[u] + TSIT5_E4 * k3[u] +
                                    TSIT5_E5 * k4[u] + TSIT5_E6 * k5[u] + TSIT5_E7 * k6[u]);
           const float sc = fmaf(fmaxf(fabsf(yv[u]), fabsf(ytv[u])), rtol, atol);
-          const float v = err / sc;
-          pe = fmaf(v, v, pe);
+          vb[e0 + u * kAdvThreads] = err / sc;
         }
       }
-      const float err = sqrtf(block_sum(pe, red) * inv_cnt);
+      const float err = sqrtf(canon_sumsq(vb, rb, a.n, a.d, red) * inv_cnt);
       const bool finite = isfinite(err);
       const bool keep = finite && err < 1.0f;
       float factor;
@@ -443,7 +458,7 @@ __global__ void __launch_bounds__(kAdvThreads) k_pid_advance(PidArgs a) {
       for (int u = 0; u < U; ++u)
         if (e0 + u * kAdvThreads < E) yt[e0 + u * kAdvThreads] = fmaf(s.h, acc[u], yv[u]);
     }
-    s.tst = ns1 >= 5 ? __fadd_rn(s.t, s.h) : stage_time(s.t, cst, s.h);
+    s.tst = ns1 == 6 ? s.tn : ns1 == 5 ? __fadd_rn(s.t, s.h) : stage_time(s.t, cst, s.h);  // FSAL stage at the step end
     s.st = ns1;
   }
   if (tid == 0) {
@@ -488,7 +503,8 @@ struct PidRun {
 size_t generic_pid_workspace(const GncdeProblem& p) {
   const size_t B = p.B, E = (size_t)p.n * state_dim(p);
   size_t sz = generic_vf_workspace(p);
-  sz += 10 * align_up(B * E * 4, 256);                 // y, yt, K, kk[7]
+  sz += 11 * align_up(B * E * 4, 256);                 // y, yt, K, kk[7], the norms' values
+  sz += align_up(B * (p.n + (p.n + 15) / 16) * 4, 256);  // their row / row-block sums
   sz += 2 * align_up(B * sizeof(PidState), 256) + 2 * align_up(B * 4, 256) + 256;
   return sz;
 }
@@ -527,6 +543,10 @@ int pid_begin(PidRun& r, const GncdeProblem& p, const GncdeSolver& s, const floa
   r.K = reinterpret_cast<float*>(take(B * E * 4));
   a.K = r.K;
   a.kk = reinterpret_cast<float*>(take(7 * B * E * 4));
+  a.vbuf = reinterpret_cast<float*>(take(B * E * 4));
+  a.rbuf = reinterpret_cast<float*>(take(B * (p.n + (p.n + 15) / 16) * 4));
+  a.n = p.n;
+  a.d = (int)(E / p.n);
   a.state = reinterpret_cast<PidState*>(take(B * sizeof(PidState)));
   a.state_out = reinterpret_cast<PidState*>(take(B * sizeof(PidState)));
   r.tst = reinterpret_cast<float*>(take(B * 4));

@@ -790,22 +790,35 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
                                                (int)(((r0 + orow) * H + ocol) * 4), 0, 16);
       arrive();
     };
-    // (sum of v0, sum of v1) over the group's rows: workgroup sums (waves in order), published, and every
-    // workgroup adds the nb partials in row-block order
-    float* sr = reinterpret_cast<float*>(red);  // free between evaluations
+    // (sum of v0, sum of v1) over the group's rows, from each thread's 4-element chunk partials (fma chains from 0)
+    // in the CANONICAL order the host-paced controller uses too (gncde_pid.hip canon_sumsq): a row sums its chunks in
+    // order, the workgroup its rows in order (published as the row block's partial), and every workgroup adds the nb
+    // partials in row-block order — so both controllers take bitwise the same decisions
+    float* sr = reinterpret_cast<float*>(red);  // free between evaluations: [2][4H] chunk partials, [2][16] row sums
     auto group_sum2 = [&](float v0, float v1, float& s0, float& s1) -> bool {
-      for (int o = 32; o > 0; o >>= 1) {
-        v0 += __shfl_xor(v0, o);
-        v1 += __shfl_xor(v1, o);
+      constexpr int CH = H / 4;  // chunks per row
+      float* rsum = sr + 8 * H;
+      if (tid < 4 * H) {
+        sr[tid] = v0;
+        sr[4 * H + tid] = v1;
       }
-      if ((tid & 63) == 0) {
-        sr[2 * (tid >> 6)] = v0;
-        sr[2 * (tid >> 6) + 1] = v1;
+      __syncthreads();
+      if (tid < 32) {
+        const float* c = sr + (tid >> 4) * 4 * H + (tid & 15) * CH;
+        float q = c[0];
+#pragma unroll
+        for (int j = 1; j < CH; ++j) q += c[j];
+        rsum[tid] = q;
       }
       __syncthreads();
       float* part = s.part + (size_t)(2 * b + (pub & 1)) * nb * 2;
       if (tid == 0) {
-        const float p0 = ((sr[0] + sr[2]) + sr[4]) + sr[6], p1 = ((sr[1] + sr[3]) + sr[5]) + sr[7];
+        const int nr = n - r0 < kRB ? n - r0 : kRB;
+        float p0 = rsum[0], p1 = rsum[16];
+        for (int r = 1; r < nr; ++r) {
+          p0 += rsum[r];
+          p1 += rsum[16 + r];
+        }
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, floatx2{p0, p1}),
                                               rsrc(part, (unsigned)(nb * 8)), rb * 8, 0, 16);
       }
@@ -908,7 +921,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       if (ns1 <= 5) record(gk, ns1, u);
       else y1 = u;
       publish(u);
-      tst = ns1 >= 5 ? stage_time(t, 1.0f, h) : stage_time(t, cst, h);
+      tst = ns1 == 6 ? gr[gk + 1] : stage_time(t, cst, h);  // the FSAL stage at the step's end knot
       st = ns1;
       return false;
     };
@@ -982,7 +995,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
         }
         if (ns1 == 6) y1 = u;  // the FSAL stage's input is the step's candidate solution
         publish(u);
-        tst = ns1 >= 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);
+        tst = ns1 == 6 ? tn : ns1 == 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);  // FSAL stage at the step end
         st = ns1;
         return false;
       } else {  // the attempt is complete: K = f(tn, y1); embedded error, accept / reject, next step size
@@ -1365,7 +1378,7 @@ bool rows_pid_supported(const GncdeProblem& p, const GncdeSolver& s) {
   Inst k;
   if (!find_solve_inst(p, s, k)) return false;
   const int nb = (p.n + kRB - 1) / kRB;
-  return resident_blocks(k, rows_smem(p.n, p.dims[0], p.L, false)) >= nb;
+  return resident_blocks(k, rows_smem(p.n, p.dims[0], p.L, false)) >= nb && cu_count() >= nb;
 }
 
 size_t rows_pid_scratch(const GncdeProblem& p) {
@@ -1440,6 +1453,7 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   // r04_config5_solve_stamps*.txt), so B = 64 runs as four B = 16 launches.  A chunk of a multiple of 8 samples takes
   // the XCD-affine layout (G = its sample count); otherwise its workgroups take start-order tickets.
   const int cap = std::min(resident_blocks(k, smem), cu_count()) / nb;
+  if (cap < 1) return GNCDE_ERR_UNSUPPORTED;  // no co-resident group (or the device query failed): never loop
   int bc = p.B < cap ? p.B : cap;
   if (bc >= 8) bc &= ~7;
   unsigned tickets = 0;

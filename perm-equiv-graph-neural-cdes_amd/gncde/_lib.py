@@ -7,7 +7,10 @@ GPU is visible, every entry point raises.
 from __future__ import annotations
 
 import ctypes
+import glob
+import hashlib
 import os
+import sys
 from ctypes import POINTER, c_char_p, c_float, c_int32, c_size_t, c_void_p
 
 MAX_LAYERS = 8
@@ -31,6 +34,7 @@ LIB_PATH = os.environ.get("GNCDE_LIB") or os.path.join(os.path.dirname(os.path.a
 EXPORTED_SYMBOLS = (
     "gncde_abi_version",
     "gncde_strerror",
+    "gncde_source_sha256",
     "gncde_integrate_path",
     "gncde_stage_record_floats",
     "gncde_activation_record_floats",
@@ -101,6 +105,45 @@ class GncdeError(RuntimeError):
     pass
 
 
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # perm-equiv-graph-neural-cdes_amd/
+
+
+def source_files() -> list[str]:
+    """The files whose bytes the library's build-provenance sha covers, in the Makefile's order (SHA_SRC)."""
+    csrc = os.path.join(_PKG_ROOT, "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")),
+                   key=lambda f: os.path.basename(f))
+    return files + [os.path.join(os.path.dirname(_PKG_ROOT), "include", "gncde.h")]
+
+
+def source_sha256() -> str:
+    """sha256 of the kernel sources in this tree (what `make` compiles into gncde_source_sha256())."""
+    files = source_files()
+    missing = [f for f in files if not os.path.exists(f)]
+    if len(files) < 2 or missing:
+        raise GncdeError(f"kernel sources not found ({missing or 'csrc/'}): cannot verify the library's build")
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def verify_provenance(lib) -> str:
+    """Refuse a library that was not compiled from this tree's kernel sources.  An explicit experiment build
+    (GNCDE_LIB with GNCDE_LIB_UNVERIFIED=1, tools/ab_*.sh only) is loaded with a warning instead."""
+    built = lib.gncde_source_sha256().decode()
+    tree = source_sha256()
+    if built != tree:
+        if os.environ.get("GNCDE_LIB") and os.environ.get("GNCDE_LIB_UNVERIFIED") == "1":
+            print(f"gncde: WARNING experiment library {LIB_PATH} built from sources {built[:16]}, tree "
+                  f"{tree[:16]}", file=sys.stderr)
+            return built
+        raise GncdeError(f"{LIB_PATH} was built from kernel sources {built[:16]}..., this tree's are "
+                         f"{tree[:16]}...: rebuild with `make -C perm-equiv-graph-neural-cdes_amd`")
+    return built
+
+
 _lib = None
 
 
@@ -118,6 +161,8 @@ def load(path: str | None = None):
     lib.gncde_abi_version.restype = c_int32
     lib.gncde_strerror.restype = c_char_p
     lib.gncde_strerror.argtypes = [c_int32]
+    lib.gncde_source_sha256.restype = c_char_p
+    lib.gncde_source_sha256.argtypes = []
     lib.gncde_integrate_path.restype = c_int32
     lib.gncde_integrate_path.argtypes = [POINTER(GncdeProblem), POINTER(GncdeSolver), c_char_p, c_size_t]
     lib.gncde_stage_record_floats.restype = c_size_t
@@ -169,6 +214,7 @@ def load(path: str | None = None):
     v = lib.gncde_abi_version()
     if v != ABI_VERSION:
         raise GncdeError(f"ABI mismatch: library {v}, bindings {ABI_VERSION}")
+    verify_provenance(lib)
     _lib = lib
     return lib
 

@@ -162,11 +162,16 @@ class _PidSolve(torch.autograd.Function):
         # The replay's forward keeps every stage's hidden outputs when the reverse sweep can read them (the
         # host-paced replay, not the one-launch persistent one: config 5's shape spends 35 us per stage re-running
         # the forward otherwise, against ~10 us the host-paced replay costs over the persistent one per evaluation)
+        # (only when the activation record is actually allocated: under memory pressure the replay keeps the
+        # one-launch persistent forward, since the reverse recomputes every stage either way)
+        recorded = None
         if engine.integrate_path(ctx.prob, steps).startswith("rows_grid"):
             gen = dataclasses.replace(steps, flags=steps.flags | _lib.FLAG_GENERIC)
             if engine.activation_record_floats(ctx.prob, gen):
-                steps = gen
-        steps = with_stage_record(ctx.prob, steps)
+                gen = with_stage_record(ctx.prob, gen)
+                if gen.act_rec is not None:
+                    recorded = gen
+        steps = recorded if recorded is not None else with_stage_record(ctx.prob, steps)
         ys = engine.integrate(ctx.prob, steps, y0)  # the checkpoints (and stage inputs): the accepted steps replayed
         if dense:
             gys, gst = dense_output_cotangents(grid, nst, spec.save_ts, g)

@@ -167,3 +167,32 @@ def test_stage_record_length_is_checked():
     bf.compute = _lib.COMPUTE_BF16  # no record exists for the bf16 modes
     s.stage_rec_len = 100 * 3 * 64 * 16
     assert lib.gncde_integrate_path(ctypes.byref(bf), ctypes.byref(s), buf, 64) == 1
+
+
+def test_library_sha_matches_tree_sources():
+    lib = _lib.load()
+    assert lib.gncde_source_sha256().decode() == _lib.source_sha256()
+
+
+def test_library_from_other_sources_is_refused(monkeypatch):
+    """A library whose compiled-in source sha differs from this tree's is refused (build provenance)."""
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "source_sha256", lambda: "0" * 64)
+    monkeypatch.delenv("GNCDE_LIB_UNVERIFIED", raising=False)
+    with pytest.raises(_lib.GncdeError, match="built from kernel sources"):
+        _lib.load()
+
+
+def test_tampered_source_changes_the_tree_sha(tmp_path, monkeypatch):
+    """The tree sha covers every kernel source byte: a one-byte edit of a copy of csrc/ gives another sha."""
+    import shutil
+    pkg = tmp_path / "pkg"
+    shutil.copytree(os.path.join(_lib._PKG_ROOT, "csrc"), pkg / "csrc")
+    (tmp_path / "include").mkdir()
+    shutil.copy(HEADER, tmp_path / "include" / "gncde.h")
+    monkeypatch.setattr(_lib, "_PKG_ROOT", str(pkg))
+    base = _lib.source_sha256()
+    assert base == _lib.load().gncde_source_sha256().decode()
+    f = pkg / "csrc" / "gncde_rows.hip"
+    f.write_bytes(f.read_bytes() + b" ")
+    assert _lib.source_sha256() != base
