@@ -637,7 +637,7 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.inv = take(B * n);
   w.q = take((size_t)p.L * B * n);                          // q_l = (I + Abar_l) 1
   w.dx = take(B * n * (size_t)(p.cde_hidden > 0 ? 2 * p.cde_embed : 1));  // data-spline derivative at t
-  w.sync = reinterpret_cast<unsigned*>(take(B + 4));
+  w.sync = reinterpret_cast<unsigned*>(take(rows_sync_words(p.B)));
   w.wbf = reinterpret_cast<uint16_t*>(take(p.compute == GNCDE_COMPUTE_BF16_MFMA ? (wsum + 1) / 2 : 1));
   // the one-launch evaluation reads a node block's column strip [:, R] as rows R of the transposed planes (whole
   // cache lines, like its rows block) instead of 16-column segments of every row
@@ -713,7 +713,7 @@ const float* generic_vf_csum(const GncdeProblem& p, char* ws) {
 const int* generic_vf_fault(const GncdeProblem& p, char* ws) {
   VfWs w;
   carve_vf(p, ws, w);
-  return reinterpret_cast<const int*>(w.sync + p.B);
+  return reinterpret_cast<const int*>(w.sync + rows_fault_word(p.B));
 }
 
 // plane z (= (sample, interval, coefficient)) of [*, n, n] -> its transpose, 32 x 32 tiles through LDS
@@ -749,7 +749,7 @@ void generic_vf_transpose(const GncdeProblem& p, char* ws, hipStream_t st) {
 void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool rows_layout) {
   VfWs w;
   carve_vf(p, ws, w);
-  (void)hipMemsetAsync(w.sync, 0, ((size_t)p.B + 4) * sizeof(unsigned), st);
+  (void)hipMemsetAsync(w.sync, 0, rows_sync_words(p.B) * sizeof(unsigned), st);
   const dim3 gs(4, p.T - 1, p.B);
   if (coef_is_bf16(p))
     hipLaunchKernelGGL(k_coef_sums<uint16_t>, gs, dim3(256), 0, st, p.n, p.T,
@@ -793,7 +793,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     }
     // (the workspace holds no (I + Abar_l) planes for these problems: there is no multi-kernel fallback here)
     return rows_vf_eval(p, t, y, dy, w.csum, w.coefT, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync,
-                        reinterpret_cast<int*>(w.sync + B), *bars, st, keep);
+                        reinterpret_cast<int*>(w.sync + rows_fault_word(B)), *bars, st, keep);
   }
   vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st);
   const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);

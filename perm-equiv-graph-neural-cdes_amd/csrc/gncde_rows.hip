@@ -77,7 +77,7 @@ struct RowsArgs {
   int B, n, T, L, G, rounds, nb, big;  // big: floats of the LDS region shared by the strip, Z_l and the partials
   int np;                  // n rounded up to the K chunk (16 fp32, 32 bf16)
   const float* ts;
-  const void* coef;        // [B, T-1, 4, n, n] fp32, or bfloat16 (GNCDE_COMPUTE_BF16_MFMA)
+  const void* coef;        // [B, T-1, 4, n, n] fp32, or bfloat16 (PREC 1 / 2)
   const void* coefT;       // the same planes transposed (generic_vf_prepare, once per solve)
   const float* csum;       // k_coef_sums: [B, T-1, 12 n + 4]
   const float* tcoef;      // [B, T-1, 3, n]
@@ -92,7 +92,7 @@ struct RowsArgs {
   float* zbuf[2];          // [G, n, H] each: the groups' hidden layer outputs, alternating per step
   float* keep;             // optional [L-1, B, n, H]: every sample's hidden layer outputs kept (reverse mode), used
                            // instead of zbuf
-  unsigned* bar;           // [G] arrivals per group, monotonic within a solve
+  unsigned* bar;           // [G][kBarStride] arrivals per group (one line each), monotonic within a solve
   unsigned bar0;           // barriers every group completed before this launch
   int* fault;              // set when a barrier wait gives up
   unsigned spin_limit;     // polls before a barrier wait gives up
@@ -160,14 +160,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
 
 // MODE 1: ODE output layer.  MODE 2: CDE read-out (de = 8, cde_hidden = H).  Three workgroups per CU (168 VGPRs)
 // for the ODE output, two for the CDE read-out (its weight slice is prefetched into registers).
-// BF (GNCDE_COMPUTE_BF16_MFMA): bfloat16 coefficients, and every product — (I + Abar_l) diag(inv) Z, the Linears, the
-// read-out — on v_mfma_f32_16x16x32_bf16 with single-plane bf16 operands rounded from the fp32 values (fp32
-// accumulation); the spline, the reductions, RMSNorm and all sums outside the MFMAs stay fp32.
+// PREC 0: fp32.  PREC 1 (GNCDE_COMPUTE_BF16_MFMA): bfloat16 coefficients, and every product — (I + Abar_l) diag(inv) Z,
+// the Linears, the read-out — on v_mfma_f32_16x16x32_bf16 with single-plane bf16 operands rounded from the fp32 values
+// (fp32 accumulation); the spline, the reductions, RMSNorm and all sums outside the MFMAs stay fp32.  PREC 2
+// (GNCDE_COMPUTE_BF16_STORAGE, the persistent solve): bfloat16 coefficients (half the form's coefficient stream and
+// its L2 footprint), widened exactly on load, every product fp32: the result is the fp32 computation on the
+// bf16-rounded operator, so the adaptive controller sees no per-stage rounding noise.
 // SOLVE: 0 one evaluation per launch; the persistent solve with 1 the Tsit5 + PIDController controller, 2 a fixed
 // step grid (§ the solve below).
-template <int H, int MODE, bool BF, int SOLVE>
+template <int H, int MODE, int PREC, int SOLVE>
 __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr bool CBF = PREC != 0;  // bfloat16 coefficients
+  constexpr bool BF = PREC == 1;   // bf16 products
   constexpr int ZS = rows_zs(H);
   constexpr int CT = H / 16;           // column tiles of a width-H operand / output
   constexpr int KW = BF ? 32 : 16;     // K chunk of one MFMA step
@@ -227,7 +232,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
   auto arrive = [&]() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores have reached memory
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(a.bar + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(a.bar + (size_t)g * kBarStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ++pub;
   };
   // wait until every workgroup of the group has arrived `epoch` times; a bounded spin: past the limit (or when
@@ -238,7 +243,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       const unsigned target = epoch * (unsigned)nb;
       unsigned spins = 0;
       int gave_up = 0;
-      while (__hip_atomic_load(a.bar + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      while (__hip_atomic_load(a.bar + (size_t)g * kBarStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
         ++spins;
         if (spins > a.spin_limit ||
@@ -282,7 +287,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       idx = interval_index_wave(tsb, T, tb);
       f = tb - tsb[idx];
     }
-    using CT_ = typename std::conditional<BF, uint16_t, float>::type;
+    using CT_ = typename std::conditional<CBF, uint16_t, float>::type;
     const CT_* cb = reinterpret_cast<const CT_*>(a.coef) + ((size_t)b * (T - 1) + idx) * 4 * nn;
 
     // ---- form -------------------------------------------------------------------------------------------------
@@ -298,7 +303,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     const int rr = tid >> 4;
     // fp32: 4 columns per 16-byte load (row rr = tid / 16, columns 4 (tid % 16) + 64 u, u < 4); bf16: 8 per load
     // (columns 8 (tid % 16) + 128 u, u < 2); the strip the same over the transposed planes
-    constexpr int CE = BF ? 8 : 4, NU = BF ? 2 : 4;
+    constexpr int CE = CBF ? 8 : 4, NU = CBF ? 2 : 4;
     const int cq = CE * (tid & 15);
     u32x4 rc[NU][4], sc[NU][4];
 #pragma unroll
@@ -307,7 +312,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       for (int q = 0; q < 4; ++q)
       {
         const int e = (int)(q * nn + (size_t)(r0 + rr) * n + cq + 16 * CE * u);
-        if constexpr (BF) rc[u][q] = load8_bf16(crs, e);
+        if constexpr (CBF) rc[u][q] = load8_bf16(crs, e);
         else rc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, e * 4, 0, 0);
       }
     // the column strip [:, R] = rows R of the transposed planes: the same whole-line pattern as the rows block
@@ -319,7 +324,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       for (int q = 0; q < 4; ++q)
       {
         const int e = (int)(q * nn + (size_t)(r0 + rr) * n + cq + 16 * CE * u);
-        if constexpr (BF) sc[u][q] = load8_bf16(crt, e);
+        if constexpr (CBF) sc[u][q] = load8_bf16(crt, e);
         else sc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crt, e * 4, 0, 0);
       }
     const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
@@ -350,7 +355,8 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
 #pragma unroll
         for (int e = 0; e < CE; ++e) {
           const bool in = r0 + rr < n && c0 + e < n;
-          const float cc[4] = {coef_el<BF>(rc[u][0], e), coef_el<BF>(rc[u][1], e), coef_el<BF>(rc[u][2], e), coef_el<BF>(rc[u][3], e)};
+          const float cc[4] = {coef_el<CBF>(rc[u][0], e), coef_el<CBF>(rc[u][1], e), coef_el<CBF>(rc[u][2], e),
+                               coef_el<CBF>(rc[u][3], e)};
           sAr[rr * RS + c0 + e] = in ? cubic(cc, f) : 0.f;
           sAr[(16 + rr) * RS + c0 + e] = in ? dcubic(cc, f) : 0.f;
         }
@@ -365,8 +371,8 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
           for (int e = 0; e < CE; ++e) {
             const int kk = c0 + e;
             const bool in = r0 + rr < n && kk < n;
-            const float cc[4] = {coef_el<BF>(sc[u][0], e), coef_el<BF>(sc[u][1], e), coef_el<BF>(sc[u][2], e),
-                                 coef_el<BF>(sc[u][3], e)};
+            const float cc[4] = {coef_el<CBF>(sc[u][0], e), coef_el<CBF>(sc[u][1], e), coef_el<CBF>(sc[u][2], e),
+                                 coef_el<CBF>(sc[u][3], e)};
             big[kk * kStrip + rr] = in ? cubic(cc, f) : 0.f;
             big[(NP + kk) * kStrip + rr] = in ? dcubic(cc, f) : 0.f;
           }
@@ -1148,28 +1154,28 @@ struct Inst {
   void (*launch)(const RowsArgs&, int, size_t, hipStream_t);
 };
 
-template <int H, int MODE, bool BF, int SOLVE>
+template <int H, int MODE, int PREC, int SOLVE>
 void launch_rows(const RowsArgs& a, int grid, size_t smem, hipStream_t st) {
-  hipLaunchKernelGGL((k_rows<H, MODE, BF, SOLVE>), dim3(grid), dim3(256), smem, st, a);
+  hipLaunchKernelGGL((k_rows<H, MODE, PREC, SOLVE>), dim3(grid), dim3(256), smem, st, a);
 }
 
-template <int H, int MODE, bool BF, int SOLVE>
+template <int H, int MODE, int PREC, int SOLVE>
 Inst inst() {
-  return Inst{reinterpret_cast<const void*>(&k_rows<H, MODE, BF, SOLVE>), &launch_rows<H, MODE, BF, SOLVE>};
+  return Inst{reinterpret_cast<const void*>(&k_rows<H, MODE, PREC, SOLVE>), &launch_rows<H, MODE, PREC, SOLVE>};
 }
 
-template <bool BF, int SOLVE>
+template <int PREC, int SOLVE>
 bool find_inst_t(int H, int mode, Inst& out) {
   if (mode == 1) {
-    if (H == 16) out = inst<16, 1, BF, SOLVE>();
-    else if (H == 32) out = inst<32, 1, BF, SOLVE>();
-    else if (H == 64) out = inst<64, 1, BF, SOLVE>();
+    if (H == 16) out = inst<16, 1, PREC, SOLVE>();
+    else if (H == 32) out = inst<32, 1, PREC, SOLVE>();
+    else if (H == 64) out = inst<64, 1, PREC, SOLVE>();
     else return false;
   } else {
-    if (H == 16) out = inst<16, 2, BF, SOLVE>();
-    else if (H == 32) out = inst<32, 2, BF, SOLVE>();
-    else if constexpr (BF && SOLVE == 0) {  // (fp32: the H = 64 read-out keeps the multi-kernel path)
-      if (H == 64) out = inst<64, 2, BF, SOLVE>();
+    if (H == 16) out = inst<16, 2, PREC, SOLVE>();
+    else if (H == 32) out = inst<32, 2, PREC, SOLVE>();
+    else if constexpr (PREC == 1 && SOLVE == 0) {  // (fp32: the H = 64 read-out keeps the multi-kernel path)
+      if (H == 64) out = inst<64, 2, PREC, SOLVE>();
       else return false;
     } else {
       return false;
@@ -1178,7 +1184,7 @@ bool find_inst_t(int H, int mode, Inst& out) {
   return true;
 }
 bool find_inst(int H, int mode, bool bf, Inst& out) {
-  return bf ? find_inst_t<true, 0>(H, mode, out) : find_inst_t<false, 0>(H, mode, out);
+  return bf ? find_inst_t<1, 0>(H, mode, out) : find_inst_t<0, 0>(H, mode, out);
 }
 
 // 256-thread workgroups of one instance resident at this LDS size, x CUs (cached per device): min(occupancy query,
@@ -1222,6 +1228,13 @@ int cu_count() {
   if (!cached[dev] && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
     cached[dev] = cus;
   return cached[dev];
+}
+
+// workgroups per CU the persistent solve places (GNCDE_SOLVE_WG_PER_CU, default 1; at most what is resident)
+int solve_wgs_per_cu() {
+  const char* e = getenv("GNCDE_SOLVE_WG_PER_CU");
+  const int v = e ? atoi(e) : 1;
+  return v < 1 ? 1 : (v > 8 ? 8 : v);
 }
 
 // polls before a group barrier wait gives up (each poll is an L2 round trip plus s_sleep 1: seconds in all);
@@ -1294,8 +1307,6 @@ extern "C" int gncde_debug_rows_stamps(unsigned long long* host, int count) {
 }
 #endif
 
-size_t rows_sync_ints(const GncdeProblem& p) { return align_up((size_t)p.B + 4, 4); }
-
 // Launch one evaluation (RowsState: the group layout, fixed per problem, and the barriers done so far).
 int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum, const void* coefT,
                  const float* wperm, const uint16_t* wbf, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
@@ -1356,14 +1367,16 @@ int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* d
 // the host-paced paths instead).
 bool rows_solve_shape(const GncdeProblem& p) {
   Inst k;
-  return p.compute == GNCDE_COMPUTE_FP32 && rows_shape(p, false) &&
-         find_inst_t<false, 1>(p.dims[0], p.cde_hidden > 0 ? 2 : 1, k);
+  return (p.compute == GNCDE_COMPUTE_FP32 || p.compute == GNCDE_COMPUTE_BF16_STORAGE) && rows_shape(p, false) &&
+         find_inst_t<0, 1>(p.dims[0], p.cde_hidden > 0 ? 2 : 1, k);
 }
 
-// the persistent solve's instance for this controller
+// the persistent solve's instance for this controller (fp32, or bfloat16 coefficient storage: PREC 2)
 bool find_solve_inst(const GncdeProblem& p, const GncdeSolver& s, Inst& k) {
   const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
-  return s.controller == GNCDE_CTRL_GRID ? find_inst_t<false, 2>(H, mode, k) : find_inst_t<false, 1>(H, mode, k);
+  if (p.compute == GNCDE_COMPUTE_BF16_STORAGE)
+    return s.controller == GNCDE_CTRL_GRID ? find_inst_t<2, 2>(H, mode, k) : find_inst_t<2, 1>(H, mode, k);
+  return s.controller == GNCDE_CTRL_GRID ? find_inst_t<0, 2>(H, mode, k) : find_inst_t<0, 1>(H, mode, k);
 }
 
 bool rows_pid_supported(const GncdeProblem& p, const GncdeSolver& s) {
@@ -1416,9 +1429,9 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   a.bf = bf;
   a.zbuf[0] = z0;
   a.zbuf[1] = z1;
-  a.bar = sync;                                   // [B] per-sample arrivals (zeroed by generic_vf_prepare)
-  a.fault = reinterpret_cast<int*>(sync + p.B);   // the workspace's fault word
-  a.ticket = sync + p.B + 1;
+  a.bar = sync;  // per-sample arrivals, one line each (zeroed by generic_vf_prepare)
+  a.fault = reinterpret_cast<int*>(sync + rows_fault_word(p.B));  // the workspace's fault word
+  a.ticket = sync + rows_fault_word(p.B) + 1;
   a.ticket0 = 0;
   a.bar0 = 0;
   a.spin_limit = spin_limit();
@@ -1452,7 +1465,7 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   // every group: config 5 at B = 32 took 93 us per iteration against 29.6 us at B = 16 (profiles/
   // r04_config5_solve_stamps*.txt), so B = 64 runs as four B = 16 launches.  A chunk of a multiple of 8 samples takes
   // the XCD-affine layout (G = its sample count); otherwise its workgroups take start-order tickets.
-  const int cap = std::min(resident_blocks(k, smem), cu_count()) / nb;
+  const int cap = std::min(resident_blocks(k, smem), solve_wgs_per_cu() * cu_count()) / nb;
   if (cap < 1) return GNCDE_ERR_UNSUPPORTED;  // no co-resident group (or the device query failed): never loop
   int bc = p.B < cap ? p.B : cap;
   if (bc >= 8) bc &= ~7;

@@ -40,7 +40,7 @@ def executed_flops_per_eval(n, dims, de=0):
     return f + (4 * n * dims[-1] if de else 0)
 
 
-def run(name, prob, spec, y0, reps, ref=None):
+def run(name, prob, spec, y0, reps, ref=None, ref_steps=None):
     import gncde
     path = gncde.integrate_path(prob, spec)
     ys, st = gncde.integrate(prob, spec, y0, stats=True)
@@ -58,11 +58,15 @@ def run(name, prob, spec, y0, reps, ref=None):
            "mfma_frac": round(evals * fpe / dt / 1e12 / FP32_PEAK, 4),
            "executed_frac": round(evals * executed_flops_per_eval(prob.n, prob.dims, prob.cde_embed) / dt / 1e12
                                   / FP32_PEAK, 4),
-           "finite": bool(torch.isfinite(ys).all())}
+           "finite": bool(torch.isfinite(ys).all()),
+           "steps_mean": float(st[:, 0].float().mean()), "rejects_mean": float(st[:, 1].float().mean())}
     if ref is not None:  # deviation of this arithmetic from the fp32 solve of the same problem
         out["rel_dev_vs_fp32"] = float((ys - ref).abs().max() / ref.abs().max())
+    if ref_steps is not None:  # accepted steps per sample against the fp32 solve's
+        d = (st[:, 0].float() - ref_steps.float()).abs() / ref_steps.float()
+        out["steps_max_rel_diff_vs_fp32"] = round(float(d.max()), 4)
     print(json.dumps(out), flush=True)
-    return ys
+    return ys, st[:, 0].clone()
 
 
 def main():
@@ -70,6 +74,7 @@ def main():
     ap.add_argument("--configs", default="3,4,5")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch5", type=int, default=16, help="config 5 windows per launch (the TGB trainer uses 1)")
+    ap.add_argument("--quick", action="store_true", help="config 5: fp32 and bf16_storage only")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     import gncde
@@ -80,7 +85,7 @@ def main():
             prob, y0 = synthetic.cde_batch(64, 129, 4, 64, 8, 3, 3.0)
             grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, 3.0, 0.1)] * prob.B)
             spec = gncde.SolverSpec(method=L.TSIT5, save_mode=L.SAVE_T1, grid=grid, nsteps=ns)
-            ys = run("3_england_n129_h64_de8_L3_tsit5c", prob, spec, y0, args.reps)
+            ys, _ = run("3_england_n129_h64_de8_L3_tsit5c", prob, spec, y0, args.reps)
             run("3_england_n129_h64_de8_L3_tsit5c_bf16_mfma", prob.with_compute("bf16_mfma"), spec, y0, args.reps, ref=ys)
         elif c == "4":  # gene community n=128, h=16, L=2, RK4 100 steps, B=1024 (forward)
             prob, y0, _ = synthetic.heat_batch(1024, num_nodes=128, hidden=16, num_layers=2, T=80, graph="community")
@@ -93,15 +98,21 @@ def main():
             spec = gncde.SolverSpec(method=L.TSIT5, controller=L.CTRL_PID, save_mode=L.SAVE_T1, rtol=1e-3, atol=1e-6,
                                     t0=torch.zeros(B, device="cuda"), t1=torch.ones(B, device="cuda"),
                                     dt0=torch.full((B,), 0.01, device="cuda"))
-            ys = run("5_trade_n255_h32_de8_L4_tsit5pid", prob, spec, y0, args.reps)
-            # BASELINE config 5's bf16 MFMA path: bf16 coefficients and (I + Abar), bf16 n x n products
-            run("5_trade_n255_h32_de8_L4_tsit5pid_bf16", prob.with_compute("bf16"), spec, y0, args.reps, ref=ys)
+            ys, s32 = run("5_trade_n255_h32_de8_L4_tsit5pid", prob, spec, y0, args.reps)
+            # BASELINE config 5's bf16 path: bf16 operator coefficients in the persistent solve, fp32 products
+            run("5_trade_n255_h32_de8_L4_tsit5pid_bf16_storage", prob.with_compute("bf16_storage"), spec, y0,
+                args.reps, ref=ys, ref_steps=s32)
+            if not args.quick:  # the multi-kernel split-product mode
+                run("5_trade_n255_h32_de8_L4_tsit5pid_bf16", prob.with_compute("bf16"), spec, y0, args.reps, ref=ys,
+                    ref_steps=s32)
             # the single-plane mode (bf16 coefficients, every product on bf16 operands) on the reference's own fixed
             # grid (100 Tsit5 steps; the PID controller refuses the mode)
             grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, 1.0, 0.01)] * B)
             fspec = gncde.SolverSpec(method=L.TSIT5, save_mode=L.SAVE_T1, grid=grid, nsteps=ns)
-            yf = run("5_trade_fixed100", prob, fspec, y0, args.reps)
-            run("5_trade_fixed100_bf16_mfma", prob.with_compute("bf16_mfma"), fspec, y0, args.reps, ref=yf)
+            yf, _ = run("5_trade_fixed100", prob, fspec, y0, args.reps)
+            run("5_trade_fixed100_bf16_storage", prob.with_compute("bf16_storage"), fspec, y0, args.reps, ref=yf)
+            if not args.quick:
+                run("5_trade_fixed100_bf16_mfma", prob.with_compute("bf16_mfma"), fspec, y0, args.reps, ref=yf)
 
 
 if __name__ == "__main__":
