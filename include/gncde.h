@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GNCDE_ABI_VERSION 7
+#define GNCDE_ABI_VERSION 8
 #define GNCDE_MAX_LAYERS 8
 #define GNCDE_FC 24
 
@@ -177,9 +177,23 @@ typedef struct GncdeSolver {
    * gncde_integrate_vjp* READ it instead of re-running every stage's forward (288 GB of HBM per GPU: the forward
    * keeps what the reverse would recompute).  Only where gncde_activation_record_floats() is nonzero (an fp32
    * multi-kernel forward whose reverse takes the per-layer kernels: BASELINE config 3's shape); act_rec_len must
-   * equal it (else GNCDE_ERR_ARG).  Batch-major: a caller that shards the batch records per shard. */
+   * equal it (else GNCDE_ERR_ARG).  Batch-major: a caller that shards the batch records per shard.
+   * PID controller (ABI 8, see pid_ckpt below): the same slabs, written by the adaptive solve itself. */
   float* act_rec;
   int64_t act_rec_len;
+  /* PID only, optional (ABI 8): the adaptive solve records its ACCEPTED steps for the reverse mode, so that no
+   * forward has to be re-run over the accepted grid.  Slots k < rec_steps (R) hold, for the k-th accepted step:
+   *   pid_ckpt  [B, R, n, d]                 its starting state y_k (slot ns: the final state),
+   *   stage_rec [B, R, 5, n, d]              its stage inputs U_1 .. U_5 (stage_rec_len = R * 5 * n * d),
+   *   act_rec   [R, 6, L-1, B, n, H]         the hidden outputs Z_1 .. Z_{L-1} of its six stage evaluations, stage 0
+   *                                          being the FSAL evaluation of step k - 1 (act_rec_len = R*6*(L-1)*B*n*H).
+   * A rejected attempt writes the slots of the step it tried and its retry overwrites them.  A sample is recorded
+   * completely iff its accepted steps + 1 <= R; otherwise the caller replays its accepted grid (step_ts).  The
+   * layouts are the GRID records' with G - 1 = R (act_rec's leading dimension only), so the fixed-grid reverse
+   * sweep reads them directly.  Only the persistent solve writes them (gncde_stage_record_floats /
+   * gncde_activation_record_floats return 0 for any other PID path); all three or none. */
+  float* pid_ckpt;
+  int32_t rec_steps;
 } GncdeSolver;
 
 /* Library / error helpers */

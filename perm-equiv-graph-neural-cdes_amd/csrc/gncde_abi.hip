@@ -31,8 +31,24 @@ int validate_problem(const GncdeProblem* p) {
   return GNCDE_OK;
 }
 
-// Floats per sample of the stage record an fp32 GRID solve writes and its reverse sweep reads (gncde.h).
+bool use_fused(const GncdeProblem& p, const GncdeSolver& s, char* name, size_t len);
+bool use_stage_vjp(const GncdeProblem& p, const GncdeSolver& s);
+
+// The persistent adaptive solve records its accepted steps (ABI 8, gncde.h pid_ckpt): Tsit5 on the persistent path
+// (fp32, or bf16 coefficient storage: its products are fp32), at least one hidden layer, and a reverse mode that
+// takes the per-layer kernels (which read the activation slabs)
+bool pid_record_supported(const GncdeProblem& p, const GncdeSolver& s) {
+  if (s.controller != GNCDE_CTRL_PID || s.rec_steps < 1 || p.L < 2 || s.method != GNCDE_TSIT5) return false;
+  if (p.compute != GNCDE_COMPUTE_FP32 && p.compute != GNCDE_COMPUTE_BF16_STORAGE) return false;
+  GncdeProblem q = p;
+  q.compute = GNCDE_COMPUTE_FP32;
+  return !use_fused(p, s, nullptr, 0) && rows_pid_supported(p, s) && rows_vjp_supported(q);
+}
+
+// Floats per sample of the stage record an fp32 GRID solve writes and its reverse sweep reads (gncde.h); under the
+// PID controller, the persistent solve's record of its accepted steps (R slots of 5 stage inputs).
 size_t record_floats(const GncdeProblem& p, const GncdeSolver& s) {
+  if (pid_record_supported(p, s)) return (size_t)s.rec_steps * 5 * (size_t)p.n * (size_t)p.dims[0];
   if (s.controller != GNCDE_CTRL_GRID || p.compute != GNCDE_COMPUTE_FP32 || s.grid_len < 2) return 0;
   const size_t S = s.method == GNCDE_RK4 ? 4 : 6;
   return (size_t)(s.grid_len - 1) * (S - 1) * (size_t)p.n * (size_t)p.dims[0];
@@ -40,9 +56,9 @@ size_t record_floats(const GncdeProblem& p, const GncdeSolver& s) {
 
 // Floats of the activation record (gncde.h): the multi-kernel fixed-grid forward (not the fused kernel, not the
 // persistent solve) whose reverse sweep takes the per-layer kernels
-bool use_fused(const GncdeProblem& p, const GncdeSolver& s, char* name, size_t len);
-bool use_stage_vjp(const GncdeProblem& p, const GncdeSolver& s);
 size_t act_floats(const GncdeProblem& p, const GncdeSolver& s) {
+  if (pid_record_supported(p, s))
+    return (size_t)s.rec_steps * 6 * (size_t)(p.L - 1) * (size_t)p.B * (size_t)p.n * (size_t)p.dims[0];
   if (s.controller != GNCDE_CTRL_GRID || p.compute != GNCDE_COMPUTE_FP32 || s.grid_len < 2 || p.L < 2) return 0;
   if (use_fused(p, s, nullptr, 0) || use_stage_vjp(p, s) || rows_pid_supported(p, s) || !rows_vjp_supported(p))
     return 0;
@@ -59,6 +75,7 @@ int validate_solver(const GncdeProblem* p, const GncdeSolver* s) {
   if (s->controller == GNCDE_CTRL_GRID) {
     if (!s->grid || !s->nsteps || s->grid_len < 1) return GNCDE_ERR_ARG;
     if (s->save_mode == GNCDE_SAVE_TS) return GNCDE_ERR_UNSUPPORTED;
+    if (s->pid_ckpt) return GNCDE_ERR_ARG;
     // a record must be exactly the one this solve writes / its sweep reads (none exists for the bf16 modes)
     if (s->stage_rec && (s->stage_rec_len <= 0 || (size_t)s->stage_rec_len != record_floats(*p, *s)))
       return GNCDE_ERR_ARG;
@@ -68,7 +85,16 @@ int validate_solver(const GncdeProblem* p, const GncdeSolver* s) {
       if (s->act_rec_len <= 0 || (size_t)s->act_rec_len != act_floats(*p, q)) return GNCDE_ERR_ARG;
     }
   } else if (s->controller == GNCDE_CTRL_PID) {
-    if (s->act_rec) return GNCDE_ERR_ARG;
+    if (s->act_rec || s->stage_rec || s->pid_ckpt) {  // the accepted-step record (ABI 8): all three, sized exactly
+      if (!(s->act_rec && s->stage_rec && s->pid_ckpt) || s->rec_steps < 1) return GNCDE_ERR_ARG;
+      GncdeSolver q = *s;
+      q.act_rec = q.stage_rec = q.pid_ckpt = nullptr;
+      const size_t sf = record_floats(*p, q), af = act_floats(*p, q);
+      if (sf == 0 || af == 0) return GNCDE_ERR_UNSUPPORTED;
+      if (s->stage_rec_len <= 0 || (size_t)s->stage_rec_len != sf || s->act_rec_len <= 0 ||
+          (size_t)s->act_rec_len != af)
+        return GNCDE_ERR_ARG;
+    }
     // the single-plane bf16 mode puts ~1e-2 relative noise into every stage, which the embedded error estimate
     // reads as truncation error: at rtol 1e-3 the controller takes 12-21x the evaluations, so
     // the mode is for fixed grids (ConstantStepSize, the reference's own PGT / TGB solves) only
@@ -142,8 +168,10 @@ const char* gncde_strerror(int code) {
 
 size_t gncde_stage_record_floats(const GncdeProblem* prob, const GncdeSolver* solver) {
   if (validate_problem(prob) != GNCDE_OK || !solver) return 0;
-  GncdeSolver s = *solver;  // the record itself is not part of the question
+  GncdeSolver s = *solver;  // the records themselves are not part of the question
   s.stage_rec = nullptr;
+  s.act_rec = nullptr;
+  s.pid_ckpt = nullptr;
   if (validate_solver(prob, &s) != GNCDE_OK) return 0;
   return record_floats(*prob, s);
 }
@@ -153,6 +181,7 @@ size_t gncde_activation_record_floats(const GncdeProblem* prob, const GncdeSolve
   GncdeSolver s = *solver;  // the records themselves are not part of the question
   s.stage_rec = nullptr;
   s.act_rec = nullptr;
+  s.pid_ckpt = nullptr;
   if (validate_solver(prob, &s) != GNCDE_OK) return 0;
   return act_floats(*prob, s);
 }

@@ -59,7 +59,10 @@ struct SolveArgs {
   int method, G, save_steps;
   const float* grid;     // [B, G]
   const int32_t* nsteps; // [B]
-  float* rec;            // [B, G-1, S-1, n, H] stage record or nullptr
+  float* rec;            // GRID: [B, G-1, S-1, n, H] stage record; PID: [B, R, 5, n, H] (the accepted steps); or nullptr
+  float* ckpt;           // PID: [B, R, n, H] accepted steps' starting states (GncdeSolver.pid_ckpt) or nullptr
+  float* arec;           // PID: [R, 6, L-1, B, n, H] their stage evaluations' hidden outputs or nullptr
+  int R;                 // PID: record slots (GncdeSolver.rec_steps)
   int S, max_steps, auto_dt, step_len;
   float rtol, atol;
   const float* t0;       // [B]
@@ -266,7 +269,9 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
   // Layer 0 reads the stage input z0: with plain loads (written before this launch), or, with `handoff`, as a
   // publication of the group (a barrier wait first, sc1 loads).  The output tile dy[R, 0 .. H-1] lands in sOut.
   // Returns false when a barrier wait gave up.
-  auto evaluate = [&](const int b, const float tb, const float* z0, const bool handoff, const bool live)
+  // kslab: nullptr, or this evaluation's [L-1, B, n, H] slab of kept hidden outputs (the reverse mode's activation
+  // record): the hidden hand-offs go through it instead of the group's double buffer
+  auto evaluate = [&](const int b, const float tb, const float* z0, const bool handoff, float* kslab)
       __attribute__((always_inline)) -> bool {
     bool ok = true;
     ROWS_STAMP(0);
@@ -470,7 +475,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
         // publications alternate buffers, so a buffer is rewritten only after a barrier that every reader of its
         // previous contents has passed
         const float* zin = l == 0 ? z0
-                         : a.keep && live ? a.keep + ((size_t)(l - 1) * a.B + b) * zgroup
+                         : kslab ? kslab + ((size_t)(l - 1) * a.B + b) * zgroup
                                           : a.zbuf[(pub - 1) & 1] + (size_t)zslot * zgroup;
         const auto rs = rsrc(zin, (unsigned)(zgroup * sizeof(float)));
         for (int e0 = tid; e0 < tot; e0 += 256 * U) {
@@ -633,7 +638,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       }
       __syncthreads();
       // (an idle round keeps to its group's own buffers: the sample it recomputes is another group's)
-      float* zout = a.keep && live ? a.keep + ((size_t)l * a.B + b) * zgroup : a.zbuf[pub & 1] + (size_t)zslot * zgroup;
+      float* zout = kslab ? kslab + ((size_t)l * a.B + b) * zgroup : a.zbuf[pub & 1] + (size_t)zslot * zgroup;
       const auto rs = rsrc(zout, (unsigned)(zgroup * sizeof(float)));
       constexpr int G4 = H / 4;
       if (tid < 16 * G4) {  // write-through 16-byte stores of this workgroup's rows, then one arrival
@@ -755,7 +760,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       const int bs = g + it * a.G;
       const bool live = bs < a.B;
       const int b = live ? bs : a.B - 1;  // an idle round computes on a valid sample, keeps its barriers, stores no dy
-      evaluate(b, a.t[b], a.y + (size_t)b * zgroup, false, live);
+      evaluate(b, a.t[b], a.y + (size_t)b * zgroup, false, live ? a.keep : nullptr);
       // dy rows R: 16-byte stores of the output tile
       constexpr int G4 = H / 4;
       const int tid = threadIdx.x;
@@ -861,6 +866,22 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     auto save_col = [&](int k) {
       if (s.save_steps && mine) *reinterpret_cast<floatx4*>(s.ys + ((size_t)b * Gl + k) * E + own) = y;
     };
+    // PID (GncdeSolver.pid_ckpt, ABI 8): the accepted-step record — slot k holds step k's starting state, its stage
+    // inputs U_1 .. U_5 and the kept hidden outputs of its six stage evaluations (stage 0 = the FSAL evaluation of
+    // step k - 1); an attempt writes the slot of the step it tries, so a rejected attempt's slot is rewritten by the
+    // retry; slots >= R are not written (the caller then replays the accepted grid)
+    float* kslab = nullptr;  // the next evaluation's kept-output slab
+    const size_t aslab = (size_t)(a.L - 1) * a.B * E;
+    auto pid_slab = [&](int k, int i) -> float* {
+      return !GRIDC && s.arec && k < s.R ? s.arec + ((size_t)k * 6 + i) * aslab : nullptr;
+    };
+    auto pid_record = [&](int k, int i, const floatx4 u) {  // U_i of step k -> slot (k, i - 1)
+      if (!GRIDC && s.rec && mine && k < s.R)
+        *reinterpret_cast<floatx4*>(s.rec + (((size_t)b * s.R + k) * 5 + i - 1) * E + own) = u;
+    };
+    auto pid_ckpt = [&](int k) {
+      if (!GRIDC && s.ckpt && mine && k < s.R) *reinterpret_cast<floatx4*>(s.ckpt + ((size_t)b * s.R + k) * E + own) = y;
+    };
     auto record = [&](int k, int i, const floatx4 u) {  // stage input U_i of step k -> slot (k, i - 1)
       if (s.rec && mine) *reinterpret_cast<floatx4*>(s.rec + (((size_t)b * (Gl - 1) + k) * S1 + i - 1) * E + own) = u;
     };
@@ -958,6 +979,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
           floatx4 u;
 #pragma unroll
           for (int e = 0; e < 4; ++e) u[e] = fmaf(h0, K[e], y[e]);
+          kslab = nullptr;  // (the heuristic's evaluation is not part of the solve)
           publish(u);
           tst = t0 + h0;
           phase = 1;
@@ -999,7 +1021,13 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
           for (int j = 0; j < 6; ++j) acc = j < ns1 ? fmaf(ar[j], kk[j][e], acc) : acc;
           u[e] = fmaf(h, acc, y[e]);
         }
-        if (ns1 == 6) y1 = u;  // the FSAL stage's input is the step's candidate solution
+        if (ns1 == 6) {
+          y1 = u;  // the FSAL stage's input is the step's candidate solution
+          kslab = pid_slab(steps + 1, 0);  // its evaluation is stage 0 of the next step, if this one is accepted
+        } else {
+          pid_record(steps, ns1, u);
+          kslab = pid_slab(steps, ns1);
+        }
         publish(u);
         tst = ns1 == 6 ? tn : ns1 == 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);  // FSAL stage at the step end
         st = ns1;
@@ -1071,6 +1099,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
         }
         if (finish) {
           if (s.step_ts && status == 0 && steps + 1 > s.step_len) status = 3;  // step record truncated
+          pid_ckpt(steps);  // the final state
           if (mine) {
             if (s.S == 0) *reinterpret_cast<floatx4*>(s.ys + oel) = y;
             for (int q = si; q < s.S; ++q)  // SAVE_TS: only on failure
@@ -1084,6 +1113,9 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
         floatx4 u;
 #pragma unroll
         for (int e = 0; e < 4; ++e) u[e] = fmaf(h, fmaf(TSIT5_A21, kk[0][e], 0.f), y[e]);
+        pid_ckpt(steps);
+        pid_record(steps, 1, u);
+        kslab = pid_slab(steps, 1);
         publish(u);
         tst = stage_time(t, TSIT5_C2, h);
         st = 1;
@@ -1106,6 +1138,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     }
     // RK4 on an empty grid evaluates nothing; Tsit5 evaluates its FSAL k0 even then (stats: 1 + 6 ns)
     if (!GRIDC || !rk4 || ns > 0) {
+      kslab = pid_slab(0, 0);  // PID: f(t0, y0) is stage 0 of the first step
       publish(y);  // the first evaluation's input: f(t0, y0) (PID: the FSAL k0 and the initial-step heuristic's f0)
       for (;;) {
 #ifdef GNCDE_ROWS_STAMPS
@@ -1113,7 +1146,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
         if (evals == kStampEval + 1 && threadIdx.x == 0)  // the next evaluation's start: the whole iteration
           g_rows_stamps[stamp_slot * 16 + 15] = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (!evaluate(b, tst, a.zbuf[(pub - 1) & 1] + (size_t)b * zgroup, true, true)) {
+        if (!evaluate(b, tst, a.zbuf[(pub - 1) & 1] + (size_t)b * zgroup, true, kslab)) {
           fault = true;
           break;
         }
@@ -1442,7 +1475,10 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   v.save_steps = s.save_mode == GNCDE_SAVE_STEPS;
   v.grid = s.grid;
   v.nsteps = s.nsteps;
-  v.rec = s.grid_len >= 2 ? s.stage_rec : nullptr;
+  v.rec = s.controller == GNCDE_CTRL_GRID ? (s.grid_len >= 2 ? s.stage_rec : nullptr) : s.stage_rec;
+  v.ckpt = s.controller == GNCDE_CTRL_PID ? s.pid_ckpt : nullptr;
+  v.arec = s.controller == GNCDE_CTRL_PID ? s.act_rec : nullptr;
+  v.R = s.rec_steps;
   v.S = s.save_mode == GNCDE_SAVE_TS ? s.n_save : 0;
   v.max_steps = s.max_steps;
   v.auto_dt = s.dt0 == nullptr;

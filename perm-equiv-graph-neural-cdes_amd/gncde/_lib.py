@@ -15,7 +15,7 @@ from ctypes import POINTER, c_char_p, c_float, c_int32, c_size_t, c_void_p
 
 MAX_LAYERS = 8
 FC = 24
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 RK4, TSIT5 = 0, 1
 CTRL_GRID, CTRL_PID = 0, 1
@@ -98,6 +98,8 @@ class GncdeSolver(ctypes.Structure):
         ("flags", c_int32),
         ("act_rec", c_void_p),
         ("act_rec_len", ctypes.c_int64),
+        ("pid_ckpt", c_void_p),
+        ("rec_steps", c_int32),
     ]
 
 

@@ -22,6 +22,9 @@ import torch
 from . import _lib, engine
 
 
+# Tests / A-B runs set NO_PID_RECORD[0] = True to take the replay backward of adaptive solves instead of their record
+NO_PID_RECORD = [False]
+
 # Share of the free device memory a stage record may take (GncdeSolver.stage_rec: the forward stores every step's
 # stage inputs so the reverse sweep recomputes none; config 4 needs 2.5 GB of the 288 GB).
 STAGE_RECORD_SHARE = 0.25
@@ -132,20 +135,80 @@ def dense_output_cotangents(grid: torch.Tensor, nsteps: torch.Tensor, save_ts: t
     return gys.view((B, G) + shp), gst.view((B, G - 1, 6) + shp)
 
 
+# The accepted-step record's slot count is sized from the largest step count seen so far (records that turn out too
+# short fall back to the replay); at most STAGE_RECORD_SHARE of the free device memory.
+_PID_STEPS_SEEN = [0]
+
+
+def pid_records(prob: engine.Problem, spec: engine.SolverSpec) -> engine.SolverSpec:
+    """``spec`` with the persistent adaptive solve's accepted-step record allocated (GncdeSolver.pid_ckpt, ABI 8:
+    checkpoints, stage inputs and the stage evaluations' hidden outputs, so that the reverse mode need not re-run
+    the forward over the accepted grid), or unchanged when the solve's path keeps none or it does not fit."""
+    if prob.B == 0:
+        return spec
+    R = min(spec.max_steps + 1, max(64, 2 * _PID_STEPS_SEEN[0] + 8))
+    trial = dataclasses.replace(spec, rec_steps=R, stage_rec=None, act_rec=None, pid_ckpt=None)
+    sf, af = engine.stage_record_floats(prob, trial), engine.activation_record_floats(prob, trial)
+    if not sf or not af:
+        return spec
+    E = prob.n * prob.dims[0]
+    per_slot = (prob.B * sf + af) // R + prob.B * E  # floats per record slot (stage inputs, activations, checkpoint)
+    free, _ = torch.cuda.mem_get_info(prob.params.device)
+    fit = int(STAGE_RECORD_SHARE * free) // (4 * per_slot)
+    if fit < R:
+        if fit < 8:
+            return spec
+        R = fit
+        trial = dataclasses.replace(trial, rec_steps=R)
+        sf, af = engine.stage_record_floats(prob, trial), engine.activation_record_floats(prob, trial)
+    dev = prob.params.device
+    return dataclasses.replace(trial, stage_rec=torch.empty(prob.B, sf, dtype=torch.float32, device=dev),
+                               act_rec=torch.empty(af, dtype=torch.float32, device=dev),
+                               pid_ckpt=torch.empty(prob.B, R, prob.n, prob.dims[0], dtype=torch.float32, device=dev))
+
+
+def pid_record_grid_inputs(spec: engine.SolverSpec, ns: torch.Tensor, G: int, L: int):
+    """The fixed-grid reverse sweep's inputs on the replayed accepted grid (G columns) from the adaptive solve's
+    record: checkpoints ys [B, G, n, d], the stage record [B, (G-1) 5 n d] and the activation record's first G-1
+    slots.  Past a sample's ns accepted steps the grid has zero-length padded steps: their checkpoints and stage
+    inputs are the final state, and every stage evaluation is f(t_ns, y_ns) = the recorded FSAL evaluation of the
+    last step (slot (ns, 0)), which is copied into the padded slots."""
+    ck = spec.pid_ckpt
+    B, R = ck.shape[0], ck.shape[1]
+    E = ck[0, 0].numel()
+    cols = torch.arange(G, device=ck.device)
+    nsl = ns.to(torch.long)
+    idx = torch.minimum(cols[None, :], nsl[:, None])  # [B, G]
+    ckf = ck.view(B, R, E)
+    ys = ckf.gather(1, idx[..., None].expand(B, G, E)).view((B, G) + tuple(ck.shape[2:]))
+    final = ckf.gather(1, nsl[:, None, None].expand(B, 1, E))  # [B, 1, E]
+    src = spec.stage_rec.view(B, R, 5, E)[:, :G - 1]
+    pad = (cols[:G - 1][None, :] >= nsl[:, None])[..., None, None]  # [B, G-1, 1, 1]
+    srec = torch.where(pad, final[:, :, None, :], src).reshape(B, -1).contiguous()
+    ar = spec.act_rec.view(R, 6, L - 1, B, E)
+    kk, bb = torch.nonzero(cols[:G - 1][:, None] >= nsl[None, :], as_tuple=True)  # padded (step, sample) pairs
+    if kk.numel():
+        ar[kk, :, :, bb] = ar[nsl[bb], 0, :, bb][:, None].expand(-1, 6, -1, -1).clone()
+    return ys.contiguous(), srec, ar[:G - 1].reshape(-1)
+
+
 class _PidSolve(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y0, params, fusion, data_coef, prob, spec):
+    def forward(ctx, y0, params, fusion, data_coef, prob, spec, record):
         p = dataclasses.replace(prob, params=params.detach().to(torch.float32).contiguous(),
                                 fusion=fusion.detach().to(torch.float32).contiguous())
         if data_coef is not None:
             p = dataclasses.replace(p, data_coef=data_coef.detach().to(torch.float32).contiguous())
         rec = torch.empty(prob.B, spec.max_steps + 1, dtype=torch.float32, device=y0.device)
-        ys, st = engine.integrate(p, dataclasses.replace(spec, step_ts=rec), y0.detach(), stats=True)
+        fwd = dataclasses.replace(spec, step_ts=rec)
+        if record:  # the backward reads the solve's own record of its accepted steps instead of replaying them
+            fwd = pid_records(p, fwd)
+        ys, st = engine.integrate(p, fwd, y0.detach(), stats=True)
         if torch.any(st[:, _lib.STAT_STATUS] != 0):
             raise _lib.GncdeError("adaptive solve failed (max_steps reached or non-finite error estimate)")
         if spec.stats_out is not None:
             spec.stats_out.copy_(st)
-        ctx.prob, ctx.spec = p, spec
+        ctx.prob, ctx.spec, ctx.fwd = p, spec, fwd
         ctx.dtypes = (y0.dtype, params.dtype, fusion.dtype)
         ctx.save_for_backward(y0.detach().to(torch.float32).contiguous(), rec, st[:, _lib.STAT_STEPS].contiguous())
         return ys
@@ -153,12 +216,30 @@ class _PidSolve(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         y0, rec, ns = ctx.saved_tensors
-        spec = ctx.spec
+        spec, fwd = ctx.spec, ctx.fwd
+        ctx.fwd = None
         dense = spec.save_mode == _lib.SAVE_TS
         grid, nst = pid_replay_grid(rec, ns, pad=1 if dense else 0)
         steps = engine.SolverSpec(method=_lib.TSIT5, controller=_lib.CTRL_GRID, save_mode=_lib.SAVE_STEPS, grid=grid,
                                   nsteps=nst, flags=spec.flags)
         want_data = ctx.needs_input_grad[3]
+        max_ns = int(ns.max().item()) if ns.numel() else 0
+        _PID_STEPS_SEEN[0] = max(_PID_STEPS_SEEN[0], max_ns)
+        if fwd.pid_ckpt is not None and max_ns + 1 <= fwd.rec_steps:
+            # the forward's own record: the reverse sweep of the accepted grid on the fp32 view of the problem
+            # (bf16 coefficient storage: its values widened, which is what that forward read)
+            p32 = ctx.prob if ctx.prob.compute == _lib.COMPUTE_FP32 else ctx.prob.with_compute("fp32")
+            ys, srec, arec = pid_record_grid_inputs(fwd, ns, grid.shape[1], p32.L)
+            rsteps = dataclasses.replace(steps, flags=steps.flags | _lib.FLAG_GENERIC, stage_rec=srec, act_rec=arec)
+            if dense:
+                gys, gst = dense_output_cotangents(grid, nst, spec.save_ts, g)
+                res = engine.integrate_vjp(p32, rsteps, ys, gys, data_grad=want_data, gstage=gst)
+            else:
+                res = engine.integrate_vjp(p32, dataclasses.replace(rsteps, save_mode=_lib.SAVE_T1), ys, g,
+                                           data_grad=want_data)
+            gy0, gp, gf = res[:3]
+            d0, dp, df = ctx.dtypes
+            return gy0.to(d0), gp.to(dp), gf.to(df), (res[3] if want_data else None), None, None, None
         # The replay's forward keeps every stage's hidden outputs when the reverse sweep can read them (the
         # host-paced replay, not the one-launch persistent one: config 5's shape spends 35 us per stage re-running
         # the forward otherwise, against ~10 us the host-paced replay costs over the persistent one per evaluation)
@@ -181,7 +262,7 @@ class _PidSolve(torch.autograd.Function):
             res = engine.integrate_vjp(ctx.prob, t1, ys, g, data_grad=want_data)
         gy0, gp, gf = res[:3]
         d0, dp, df = ctx.dtypes
-        return gy0.to(d0), gp.to(dp), gf.to(df), (res[3] if want_data else None), None, None
+        return gy0.to(d0), gp.to(dp), gf.to(df), (res[3] if want_data else None), None, None, None
 
 
 def solve(prob: engine.Problem, spec: engine.SolverSpec, y0: torch.Tensor, params: torch.Tensor | None = None,
@@ -198,7 +279,7 @@ def solve(prob: engine.Problem, spec: engine.SolverSpec, y0: torch.Tensor, param
     if spec.controller == _lib.CTRL_PID:
         if spec.method != _lib.TSIT5 or spec.save_mode not in (_lib.SAVE_T1, _lib.SAVE_TS):
             raise _lib.GncdeError("differentiable adaptive solve: Tsit5 with SAVE_T1 or SAVE_TS")
-        return _PidSolve.apply(y0, params, fusion, data_coef, prob, spec)
+        return _PidSolve.apply(y0, params, fusion, data_coef, prob, spec, record and not NO_PID_RECORD[0])
     if spec.save_mode not in (_lib.SAVE_T1, _lib.SAVE_STEPS):
         raise _lib.GncdeError("differentiable fixed-grid solve: save_mode must be SAVE_T1 or SAVE_STEPS")
     return _FixedGridSolve.apply(y0, params, fusion, data_coef, prob, spec, record)

@@ -192,6 +192,10 @@ class SolverSpec:
     # GRID: activation record [activation_record_floats(prob, solver)] (the whole batch, [G-1, S, L-1, B, n, H]),
     # written by integrate, read by integrate_vjp (ABI 7)
     act_rec: torch.Tensor | None = None
+    # PID (ABI 8): the persistent solve's record of its accepted steps — checkpoints [B, rec_steps, n, d] here,
+    # stage_rec [B, rec_steps * 5 * n * d], act_rec [rec_steps * 6 * (L-1) * B * n * H] (autograd.pid_records)
+    pid_ckpt: torch.Tensor | None = None
+    rec_steps: int = 0
 
     def c_struct(self) -> _lib.GncdeSolver:
         s = _lib.GncdeSolver()
@@ -222,6 +226,11 @@ class SolverSpec:
                 raise _lib.GncdeError("SolverSpec.act_rec must be a contiguous fp32 CUDA tensor")
             s.act_rec = _ptr(self.act_rec).value
             s.act_rec_len = int(self.act_rec.numel())
+        if self.pid_ckpt is not None:
+            if not (self.pid_ckpt.is_cuda and self.pid_ckpt.dtype == torch.float32 and self.pid_ckpt.is_contiguous()):
+                raise _lib.GncdeError("SolverSpec.pid_ckpt must be a contiguous fp32 CUDA tensor [B, rec_steps, n, d]")
+            s.pid_ckpt = _ptr(self.pid_ckpt).value
+        s.rec_steps = int(self.rec_steps)
         s.flags = int(self.flags)
         return s
 

@@ -223,6 +223,40 @@ def test_rows_pid_batch_independent(G):
     assert torch.equal(G.integrate(one, ospec, y0[47:48].contiguous()), ys[47:48])
 
 
+@pytest.mark.parametrize("save", ["t1", "ts"])
+def test_config5_pid_record_backward_equals_replay(G, save):
+    """BASELINE config 5's adaptive solve (n = 255, h = 32, L = 4, de = 8; 4 windows) differentiated through the
+    solve's own accepted-step record (ABI 8: checkpoints, stage inputs and hidden outputs written by the persistent
+    kernel) and through the replay backward (the accepted grid re-run by a fixed-grid forward): bitwise the same
+    outputs and gradients, SaveAt(t1) and SaveAt(ts)."""
+    prob, y0, spec = _config5(G, 4, seed=58)
+    if save == "ts":
+        sts = torch.tensor([[0.25, 0.5, 1.0]] * prob.B, device="cuda")
+        spec = dataclasses.replace(spec, save_mode=G._lib.SAVE_TS, save_ts=sts)
+    shape = (prob.B, 3, prob.n, 32) if save == "ts" else (prob.B, prob.n, 32)
+    gout = torch.randn(shape, generator=torch.Generator().manual_seed(5)).cuda()
+    probe = G.autograd.pid_records(prob, dataclasses.replace(spec, step_ts=torch.empty(prob.B, 4097, device="cuda")))
+    assert probe.pid_ckpt is not None  # the persistent solve keeps the record at this shape
+
+    def run(no_rec):
+        params = prob.params.clone().requires_grad_(True)
+        fus = prob.fusion.clone().requires_grad_(True)
+        y = y0.clone().requires_grad_(True)
+        G.autograd.NO_PID_RECORD[0] = no_rec
+        try:
+            out = G.autograd.solve(prob, spec, y, params, fus)
+            (out * gout).sum().backward()
+        finally:
+            G.autograd.NO_PID_RECORD[0] = False
+        return out.detach(), y.grad, params.grad, fus.grad
+
+    a, b = run(False), run(True)
+    for x, z, what in zip(a, b, ("output", "dL/dy0", "params", "fusion table")):
+        print(f"  {what}: record vs replay max |diff| {float((x - z).abs().max()):.2e}")
+        assert torch.isfinite(x).all()
+        assert torch.equal(x, z), what
+
+
 def test_rows_eval_largest_resident_batch(G):
     """The one-evaluation-per-launch kernel (fixed grids, and the keep forwards of the reverse mode) needs every
     sample's group co-resident; its grid is sized from the occupancy query capped by the SGPR file, with one

@@ -491,7 +491,7 @@ def _pid_recorded_grids(G, prob, spec, y0n):
 
 
 @pytest.mark.parametrize("case,save", [("fused", "ts"), ("fused", "t1"), ("generic", "ts"), ("cde", "ts"),
-                                       ("cde", "t1")])
+                                       ("cde", "t1"), ("rows", "ts"), ("rows", "t1")])
 def test_pid_solve_gradient_matches_oracle(G, case, save):
     """Reverse mode of the adaptive Tsit5 + PIDController(1e-3, 1e-6) solve (graph_neural_cde.py:53-54,94-104,
     differentiated by trainer.py:315) through autograd.solve: the forward records each sample's accepted steps
@@ -499,18 +499,22 @@ def test_pid_solve_gradient_matches_oracle(G, case, save):
     cotangents (gncde_integrate_vjp_ex).  Against the fp64 oracle's adjoint on the SAME step sequence
     (solve_grid_dense_vjp, FD-pinned in tests/test_oracle_grad.py), at RTOL_GRAD for every path.  Paths: the fused
     PID forward + fused reverse sweep (n = 16, h = 16), the generic PID forward + generic reverse (mixed widths),
-    and the CDE wrapper (generic, de = 2).
+    the CDE wrapper (generic, de = 2), and the persistent solve (the de = 8 read-out, n = 40, h = 16: BASELINE config
+    5's path), whose backward reads the solve's own accepted-step record (ABI 8) instead of replaying the accepted
+    grid — and must give the replay-based gradient bit for bit.
 
     ReLU networks have gradients that jump where a pre-activation crosses 0, so (as make_golden.grad_case does for
     the fixtures) a sample whose oracle gradient moves by more than 1e-5 under a 1e-6 relative change of y0 is
     redrawn, and its step sequence re-recorded, until every sample is kink-stable.  The fused case also runs the
     generic reverse sweep (GNCDE_FLAG_GENERIC) on the identical recorded grid: fused and generic sweeps must agree
     with each other as well as with the oracle."""
-    rng = np.random.default_rng({"fused": 31, "generic": 32, "cde": 33}[case])
+    rng = np.random.default_rng({"fused": 31, "generic": 32, "cde": 33, "rows": 34}[case])
     if case == "fused":
         ts, P, prob, fns, y0n = _pid_case(G, rng, 3, 16, "undirected", [16, 16, 16])
     elif case == "generic":
         ts, P, prob, fns, y0n = _pid_case(G, rng, 2, 12, "directed", [8, 12, 8])
+    elif case == "rows":
+        ts, P, prob, fns, y0n = _pid_case(G, rng, 2, 40, "undirected", [16, 16, 16, 0], cde=(16, 8))
     else:
         ts, P, prob, fns, y0n = _pid_case(G, rng, 2, 10, "undirected", [8, 8, 0], cde=(8, 2))
     B = prob.B
@@ -521,6 +525,7 @@ def test_pid_solve_gradient_matches_oracle(G, case, save):
                         save_ts=tsd.contiguous() if save == "ts" else None)
     path = G.integrate_path(prob, spec)
     assert path.startswith("fused<") == (case == "fused"), path
+    assert path.startswith("rows_pid<") == (case == "rows"), path
     names = OG.FUSION_NAMES[P.kind]
     fus_leaves = [[_leaf(lay[nm]) for nm in names] for lay in P.layers]
     fusion = G.layout.fusion_table_torch(P.kind, fus_leaves, prob.n).float()
@@ -589,6 +594,23 @@ def test_pid_solve_gradient_matches_oracle(G, case, save):
           f"{errs[worst]:.2e}")
     for k, e in errs.items():
         assert e <= RTOL_GRAD, (k, e)
+    if case == "rows":
+        # the backward above read the forward's accepted-step record; the replay backward (the accepted grid
+        # re-run by a fixed-grid forward for its checkpoints, stage inputs and activations) gives the same bits
+        probe = G.autograd.pid_records(fprob, dataclasses.replace(spec, step_ts=rec))
+        assert probe.pid_ckpt is not None and probe.rec_steps >= int(st[:, 0].max()) + 1
+        G.autograd.NO_PID_RECORD[0] = True
+        try:
+            out_r, gy0_r, gp_r, gfus_r = run(0)
+        finally:
+            G.autograd.NO_PID_RECORD[0] = False
+        assert torch.equal(out_r, out)
+        print(f"  record vs replay backward: dL/dy0 max |diff| {np.max(np.abs(gy0_r - gy0)):.2e}, params "
+              f"{np.max(np.abs(gp_r - gp)):.2e}")
+        assert np.array_equal(gy0_r, gy0) and np.array_equal(gp_r, gp)
+        for la, lb in zip(gfus_r, gfus):
+            for xa, xb in zip(la, lb):
+                assert np.array_equal(xa, xb)
     if case == "fused":
         # the generic reverse sweep on the SAME recorded grid: the backward replays the forward's step_ts, so only
         # the forward's own step sequence must be the fused one (the generic PID forward could step differently)

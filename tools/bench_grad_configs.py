@@ -41,11 +41,15 @@ def main():
                                     dt0=torch.full((B,), 0.01, device="cuda"))
             name = "5_trade_n255_h32_de8_L4_tsit5pid"
         # config 5 also in BASELINE's bf16 mode (reverse mode: the fp32 adjoint over the coefficients read)
-        runs = [(prob, 0.25, "fp32"), (prob, 0.0, "fp32")]
+        # (problem, record share, mode, replay the accepted grid instead of the PID solve's own record)
+        runs = [(prob, 0.25, "fp32", False), (prob, 0.0, "fp32", False)]
         if c == "5":
-            runs.append((prob.with_compute("bf16"), 0.25, "bf16"))
-        for pr, share, mode in runs:
+            runs = [(prob, 0.25, "fp32", False), (prob, 0.25, "fp32", True), (prob, 0.0, "fp32", True),
+                    (prob.with_compute("bf16_storage"), 0.25, "bf16_storage", False),
+                    (prob.with_compute("bf16"), 0.25, "bf16", False)]
+        for pr, share, mode, replay in runs:
             autograd.STAGE_RECORD_SHARE = share
+            autograd.NO_PID_RECORD[0] = replay
             fw, bw = [], []
             for _ in range(args.reps + 1):
                 params = pr.params.clone().requires_grad_(True)
@@ -59,10 +63,12 @@ def main():
                 torch.cuda.synchronize()
                 fw.append(e[0].elapsed_time(e[1]))
                 bw.append(e[1].elapsed_time(e[2]))
-            print(json.dumps({"config": name, "compute": mode, "stage_record": share > 0 and mode == "fp32",
+            print(json.dumps({"config": name, "compute": mode, "stage_record": share > 0,
+                              "pid_backward": ("replay" if replay else "record") if c == "5" else None,
                               "grad_finite": bool(torch.isfinite(params.grad).all()), "forward_ms": round(min(fw[1:]), 3),
                               "backward_ms": round(min(bw[1:]), 3)}), flush=True)
     autograd.STAGE_RECORD_SHARE = 0.25
+    autograd.NO_PID_RECORD[0] = False
 
 
 if __name__ == "__main__":
