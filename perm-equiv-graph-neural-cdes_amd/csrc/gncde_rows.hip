@@ -1263,10 +1263,10 @@ int cu_count() {
   return cached[dev];
 }
 
-// workgroups per CU the persistent solve places (GNCDE_SOLVE_WG_PER_CU, default 1; at most what is resident)
+// workgroups per CU the persistent solve places (GNCDE_SOLVE_WG_PER_CU, default 2; at most what is resident)
 int solve_wgs_per_cu() {
   const char* e = getenv("GNCDE_SOLVE_WG_PER_CU");
-  const int v = e ? atoi(e) : 1;
+  const int v = e ? atoi(e) : 2;
   return v < 1 ? 1 : (v > 8 ? 8 : v);
 }
 
@@ -1494,13 +1494,14 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   v.step_ts = s.step_ts;
   v.stats = stats;
   v.part = part;
-  // The batch runs in chunks of co-resident groups, one launch each, at most one workgroup per CU.  A launch past
-  // residency starts later groups only as earlier solves finish, its resident groups sharing CUs with a
-  // start-order skew (config 5 at B = 64: 53.5 ms); and two workgroups per CU, though resident, double the
-  // coefficient stream each evaluation's form pulls through HBM / MALL at ~6 TB/s (130 KB per workgroup) and slow
-  // every group: config 5 at B = 32 took 93 us per iteration against 29.6 us at B = 16 (profiles/
-  // r04_config5_solve_stamps*.txt), so B = 64 runs as four B = 16 launches.  A chunk of a multiple of 8 samples takes
-  // the XCD-affine layout (G = its sample count); otherwise its workgroups take start-order tickets.
+  // The batch runs in chunks of co-resident groups, one launch each, at most solve_wgs_per_cu() (2) workgroups per
+  // CU.  A launch past residency starts later groups only as earlier solves finish (config 5 at B = 64: 53.5 ms).
+  // Two workgroups per CU used to make every phase 2-3x longer (93 us per iteration at B = 32 against 29.6 us at
+  // B = 16, profiles/r04_config5_solve_stamps*.txt): the groups' arrival counters shared one cache line, so every
+  // group's atomics and polls queued on it; with one line per counter (kBarStride) config 5 takes 7.7 ms at B = 32
+  // in one launch against 12.4 ms as two B = 16 launches (profiles/r05_config5_batch.txt).  A chunk of a multiple
+  // of 8 samples takes the XCD-affine layout (G = its sample count); otherwise its workgroups take start-order
+  // tickets.
   const int cap = std::min(resident_blocks(k, smem), solve_wgs_per_cu() * cu_count()) / nb;
   if (cap < 1) return GNCDE_ERR_UNSUPPORTED;  // no co-resident group (or the device query failed): never loop
   int bc = p.B < cap ? p.B : cap;

@@ -256,9 +256,11 @@ class TGBGraphNeuralCDE(nn.Module):
     94-104), differentiated on each window's accepted steps; ``last_steps`` then holds every window's accepted
     step count of the latest forward (the data-parallel trainer balances ranks by it).
 
-    ``compute`` (build extension): the solve's arithmetic, engine.COMPUTE_MODES — "bf16_mfma" is config 5's
-    single-plane bf16 MFMA mode (bf16 coefficients, every product on bf16 operands; include/gncde.h), refused with
-    ``solver="pid"``."""
+    ``compute`` (build extension): the solve's arithmetic, "fp32" | "bf16" | "bf16_storage" (include/gncde.h
+    GNCDE_COMPUTE_*).  "bf16_storage" is config 5's bf16 path: bfloat16 operator coefficients (half the form's
+    coefficient stream) read by the persistent adaptive solve with fp32 products, so the PID controller sees no
+    rounding noise.  The single-plane "bf16_mfma" mode is not offered here: it deviates 8-24 % from
+    fp32 at no speed-up (round-4 measurements) and the PID controller refuses it."""
 
     def __init__(self, cfg, vector_field, interpolation="cubic", model_key=None, dt0=0.01, solver=None,
                  compute="fp32", **kwargs):
@@ -279,12 +281,9 @@ class TGBGraphNeuralCDE(nn.Module):
         if solver not in (None, "constant", "pid"):
             raise ValueError(f"solver {solver!r}: None / 'constant' (ConstantStepSize) or 'pid'")
         self.adaptive = solver == "pid"
-        if compute not in engine.COMPUTE_MODES:
-            raise ValueError(f"compute {compute!r}: one of {sorted(engine.COMPUTE_MODES)}")
-        if self.adaptive and compute == "bf16_mfma":
-            raise ValueError("compute 'bf16_mfma' with solver 'pid': the single-plane bf16 rounding noise makes the "
-                             "PID controller take 12-21x the steps (gncde.h GNCDE_COMPUTE_BF16_MFMA); use it with "
-                             "the ConstantStepSize solve, or compute 'bf16' (split products) under PID")
+        if compute not in ("fp32", "bf16", "bf16_storage"):
+            raise ValueError(f"compute {compute!r}: 'fp32', 'bf16' or 'bf16_storage' (the single-plane 'bf16_mfma' "
+                             "mode is retired from the TGB model: 8-24 % from fp32 at no speed-up, DESIGN.md §3.5)")
         self.compute = compute
         self.last_steps = None
 

@@ -269,7 +269,7 @@ class WindowTrainer:
         if self.tgb:
             # build-only model key `solver: pid` (BASELINE config 5's adaptive Tsit5); absent: the reference's
             # ConstantStepSize(0.01)
-            # build-only key `compute` ("fp32" | "bf16" | "bf16_storage" | "bf16_mfma"): the solve's arithmetic
+            # build-only key `compute` ("fp32" | "bf16" | "bf16_storage"): the solve's arithmetic
             model = TGBGraphNeuralCDE({k: v for k, v in m.items() if k not in ("solver", "compute")}, vf,
                                       m.get("interpolation", "cubic"), self.seed, solver=m.get("solver"),
                                       compute=m.get("compute", "fp32"))

@@ -318,7 +318,11 @@ def test_stage_record_matches_recompute(G, method, dims):
     """The reverse sweep reading the forward's stage record equals the one recomputing the stage inputs (to fp32
     rounding: the record holds the forward kernel's values), with ragged step counts (padded steps read the
     checkpoint, never unwritten slots).  dims (16,16,16): fused forward + fused sweep; (16,24,16): generic forward
-    (k_combo writes the record) + generic sweep; (32,32,32): fused forward + generic sweep."""
+    (k_combo writes the record) + generic sweep; (32,32,32): fused forward + generic sweep.
+
+    The two sweeps linearise at stage inputs that differ in the last bits (the forward kernel's vs the sweep's own
+    recomputation), so a ReLU pre-activation within rounding of 0 puts them on different sides of a kink: samples
+    whose gradient moves by more than 1e-5 under a 1e-6 relative change of y0 are redrawn first."""
     rng = np.random.default_rng(7)
     B, n, T = 3, 100, 5
     ts, coeffs = _graph_controls(rng, B, n, T, irregular=False)
@@ -331,8 +335,23 @@ def test_stage_record_matches_recompute(G, method, dims):
     spec = G.SolverSpec(method=G._lib.RK4 if method == "rk4" else G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS,
                         grid=grid, nsteps=ns)
     h = dims[0]
-    y0 = torch.tensor(rng.standard_normal((B, n, h)), dtype=torch.float32, device="cuda")
+    y0n = rng.standard_normal((B, n, h))
     g = torch.tensor(rng.standard_normal((B, grid.shape[1], n, h)), dtype=torch.float32, device="cuda")
+    for _ in range(8):  # GPU-side kink screen: the recompute sweep's gradient at y0 and at y0 (1 + 1e-6)
+        y0 = torch.tensor(y0n, dtype=torch.float32, device="cuda")
+        gp0 = G.integrate_vjp(prob, spec, G.integrate(prob, spec, y0), g)
+        y0p = torch.tensor(y0n * (1 + 1e-6), dtype=torch.float32, device="cuda")
+        gp1 = G.integrate_vjp(prob, spec, G.integrate(prob, spec, y0p), g)
+        mv = [rel_err(gp1[0][b].cpu().numpy(), gp0[0][b].cpu().numpy()) for b in range(B)]
+        mp = max(rel_err(x.cpu().numpy(), y.cpu().numpy()) for x, y in zip(gp1[1:], gp0[1:]))
+        unstable = [b for b in range(B) if mv[b] > 1e-5] or (list(range(B)) if mp > 1e-5 else [])
+        if not unstable:
+            break
+        print(f"  kink-unstable samples {unstable} (dL/dy0 moves {mv}, params {mp:.2e}): redrawn")
+        for b in unstable:
+            y0n[b] = rng.standard_normal((n, h))
+    else:
+        pytest.fail("no kink-stable draw")
     floats = G.engine.stage_record_floats(prob, spec)
     assert floats == (grid.shape[1] - 1) * (3 if method == "rk4" else 5) * n * h
     rec = torch.full((B, floats), float("nan"), device="cuda")
@@ -479,6 +498,26 @@ def _pid_spread(P, gy0, gr, gy0p, grp):
     return max(rel_err(gy0p, gy0), float(np.max(np.abs(vb - va)) / np.max(np.abs(va))))
 
 
+def _gpu_pid_spread(G, prob, spec, y0n, g, b, flags=0):
+    """GPU-side kink screen of sample b (solved alone): the relative movement of its adaptive-solve gradient (dL/dy0,
+    params, fusion table) under a 1e-6 relative change of y0 — how close the fp32 linearisation sits to a ReLU kink
+    (the oracle screen measures the fp64 one; the two trajectories differ in the last bits)."""
+    sub = prob.take([b])
+    sp = dataclasses.replace(spec, t0=spec.t0[b:b + 1].contiguous(), t1=spec.t1[b:b + 1].contiguous(), flags=flags,
+                             save_ts=None if spec.save_ts is None else spec.save_ts[b:b + 1].contiguous())
+
+    def grads(y):
+        params = sub.params.clone().requires_grad_(True)
+        fus = sub.fusion.clone().requires_grad_(True)
+        yl = torch.tensor(y, dtype=torch.float32, device="cuda", requires_grad=True)
+        out = G.autograd.solve(sub, sp, yl, params, fus)
+        (out.double() * torch.tensor(g[b:b + 1], device="cuda")).sum().backward()
+        return [yl.grad.cpu().numpy(), params.grad.cpu().numpy(), fus.grad.cpu().numpy()]
+
+    a, p = grads(y0n[b:b + 1]), grads(y0n[b:b + 1] * (1 + 1e-6))
+    return max(rel_err(x, y) for x, y in zip(p, a))
+
+
 def _pid_recorded_grids(G, prob, spec, y0n):
     """Each sample's accepted step sequence from the GPU forward (the grid the backward differentiates on)."""
     B = prob.B
@@ -549,6 +588,13 @@ def test_pid_solve_gradient_matches_oracle(G, case, save):
                 refs[key] = (gy0, gr, _pid_spread(P, gy0, gr, gy0p, grp))
             if refs[key][2] >= 1e-5:
                 unstable.append(b)
+        if not unstable:  # and the GPU's own linearisation (every path the test compares) away from a kink
+            for b in range(B):
+                spreads = [_gpu_pid_spread(G, fprob, spec, y0n, g, b, fl)
+                           for fl in ((0, G._lib.FLAG_GENERIC) if case == "fused" else (0,))]
+                if max(spreads) >= 1e-5:
+                    print(f"  sample {b}: GPU gradient moves {max(spreads):.2e} under a 1e-6 change of y0: redrawn")
+                    unstable.append(b)
         if not unstable:
             break
         for b in unstable:

@@ -35,21 +35,21 @@ def test_dyn_single_run_small(tmp_path, spi):
     assert losses[-1] < losses[0]
 
 
-# config 5's bf16 MFMA mode needs the one-launch evaluation's shapes (h = 16 = the hidden width, de = 8) and a fixed
-# grid (the reference's own ConstantStepSize TGB solve; the PID controller refuses the mode)
-BF16M_TGB = {"compute": "bf16_mfma", "hidden_dim": 16,
+# config 5's bf16 path: bfloat16 operator coefficients in the persistent adaptive solve (fp32 products), which needs
+# its shapes (h = 16 = the hidden width, de = 8); trained through the solve's accepted-step record
+BF16S_TGB = {"compute": "bf16_storage", "solver": "pid", "hidden_dim": 16,
              "vector_field": {"name": "PermEquivGraphVectorField", "hidden_dim": 16, "num_layers": 2, "data_embed_dim": 8}}
 
 
 @pytest.mark.parametrize("config,metric,model", [("pgt_england_small.yaml", "best_validation_loss", None),
                                                  ("tgb_trade_small.yaml", "best_validation_ndcg@10", None),
                                                  ("tgb_trade_small.yaml", "best_validation_ndcg@10", {"solver": "pid"}),
-                                                 ("tgb_trade_small.yaml", "best_validation_ndcg@10", BF16M_TGB)])
+                                                 ("tgb_trade_small.yaml", "best_validation_ndcg@10", BF16S_TGB)])
 def test_window_single_run_small(tmp_path, config, metric, model):
     """trainer_pgt / trainer_tgb flow: windows -> one optimiser step per window -> validation (MSE / NDCG@10)
     -> checkpoint -> test metrics of the best model.  solver "pid": the TGB model on BASELINE config 5's adaptive
     Tsit5 + PIDController (build-only `model.solver: pid`), trained through the reverse mode on the accepted steps;
-    with `model.compute: bf16_mfma`, the ConstantStepSize forward solves in the single-plane bf16 mode."""
+    with `model.compute: bf16_storage`, the adaptive solve reads bfloat16 operator coefficients."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a HIP device")
     from gncde import data, run

@@ -58,13 +58,14 @@ def test_drivers_construct():
     assert torch.equal(p.encoder.layers[0].weight[:, :8].flatten()[:4], p.encoder.layers[0].weight[:, :8].flatten()[:4])
 
 
-def test_bf16_mfma_refuses_the_pid_controller():
-    """The single-plane bf16 mode is for fixed grids: under the adaptive controller its rounding noise costs 12-21x
-    the steps, so the TGB driver refuses the combination up front (and the C-ABI returns
-    GNCDE_ERR_UNSUPPORTED)."""
+def test_tgb_model_bf16_modes():
+    """The TGB driver offers fp32, the split-product "bf16" and the bf16-coefficient "bf16_storage" path (config 5's
+    bf16 path on the persistent adaptive solve); the single-plane "bf16_mfma" mode is retired from it, with either
+    solver (8-24 % from fp32 at no speed-up; the C-ABI also refuses it under PID)."""
     from gncde.models import TGBGraphNeuralCDE
     vf = V.PermEquivGraphVectorField(16, 16, 16 * 8 * 2, 2, 8, 40, key=0)
-    TGBGraphNeuralCDE({"hidden_dim": 16}, vf, "cubic", 1, solver=None, compute="bf16_mfma")
-    TGBGraphNeuralCDE({"hidden_dim": 16}, vf, "cubic", 1, solver="pid", compute="bf16")
-    with pytest.raises(ValueError, match="bf16_mfma"):
-        TGBGraphNeuralCDE({"hidden_dim": 16}, vf, "cubic", 1, solver="pid", compute="bf16_mfma")
+    for compute in ("fp32", "bf16", "bf16_storage"):
+        TGBGraphNeuralCDE({"hidden_dim": 16}, vf, "cubic", 1, solver="pid", compute=compute)
+    for solver in (None, "pid"):
+        with pytest.raises(ValueError, match="bf16_mfma"):
+            TGBGraphNeuralCDE({"hidden_dim": 16}, vf, "cubic", 1, solver=solver, compute="bf16_mfma")
