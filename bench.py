@@ -267,13 +267,6 @@ def main():
     import gncde
     from gncde import layout, synthetic
 
-    # BASELINE config 4's training line runs first: besides its own measurement it brings the GPU to its steady
-    # clocks before the headline region (launched cold, the first ~15 k_fused launches ramp 3.25 -> 2.65 ms,
-    # profiles/r05_bench_notes.txt); its buffers are freed before the headline problem is built
-    tr = None
-    if args.train_steps > 0:
-        tr = train_line(dist, rank, world, args.train_steps, 1, args.rk4_steps)
-
     n_nodes, hidden, L, T = 64, 16, 3, 120
     B = args.batch
     prob, y0, layers = synthetic.heat_batch(B, num_nodes=n_nodes, hidden=hidden, num_layers=L, T=T,
@@ -283,6 +276,13 @@ def main():
     spec = gncde.SolverSpec(method=gncde._lib.RK4, save_mode=gncde._lib.SAVE_T1, grid=grid, nsteps=ns)
     path = gncde.integrate_path(prob, spec)
     workload = f"heat_n{prob.n}_b{B}_L{L}_h{hidden}_T{T}_rk4x{args.rk4_steps}"
+
+    # BASELINE config 4's training line runs between building the headline problem and its launches: besides its
+    # own measurement it keeps the GPU busy up to the headline region (launched after an idle host-side setup, the
+    # first ~12 k_fused launches ramp 3.26 -> 2.66 ms as the clocks rise, profiles/r05_bench_notes.txt)
+    tr = None
+    if args.train_steps > 0:
+        tr = train_line(dist, rank, world, args.train_steps, 1, args.rk4_steps)
 
     ys, st = gncde.integrate(prob, spec, y0, stats=True)
     evals_per_launch = int(st[:, gncde._lib.STAT_EVALS].sum().item())

@@ -92,20 +92,31 @@ def test_config3_exact_shape_trajectory_and_gradient(G):
     ys, st = G.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda"), stats=True)
     st = st.cpu().numpy()
     assert np.all(st[:, 0] == 30) and np.all(st[:, 2] == 181) and np.all(st[:, 3] == 0)
-    # candidates spread over the batch; the first two whose oracle gradient is kink-stable are checked
+    # candidates spread over the batch; the first two whose gradient is kink-stable at BOTH linearisations — the
+    # GPU's fp32 trajectory and the oracle's own fp64 one (1e-5 apart after 30 x 6 x 3 ReLU layers, so a
+    # pre-activation within that distance of 0 sits on different sides of a kink in the two) — are checked, end to
+    # end: the GPU gradient against the oracle adjoint of the oracle's own forward.
+    # The GPU screen: every sample's dL/dy0 (independent per sample) at y0 and at y0 (1 + 1e-6).
+    gall = rng.standard_normal((B, n, H))
+    spec_t1 = dataclasses.replace(spec, save_mode=G._lib.SAVE_T1)
+    gpu_g = []
+    for scale in (1.0, 1.0 + 1e-6):
+        yd = torch.tensor(y0 * scale, dtype=torch.float32, device="cuda")
+        gpu_g.append(G.integrate_vjp(prob, spec_t1, G.integrate(prob, spec, yd),
+                                     torch.tensor(gall, dtype=torch.float32, device="cuda"))[0].cpu().numpy())
+    gpu_move = [rel_err(gpu_g[1][b], gpu_g[0][b]) for b in range(B)]
     gfin = np.zeros((B, n, H))
     chosen, refs = [], []
     for b in (5, 40, 63, 17, 28, 51, 22, 34, 9, 56):  # windows 5, 0, 3, 7, 8, 1, 2, 4, 9, 6
+        if gpu_move[b] > 1e-5:
+            print(f"  sample {b}: GPU gradient not kink-stable ({gpu_move[b]:.2e}), skipped")
+            continue
         f, fv = oracle_fns(ts, coeffs, dco, P, H, de, b)
-        g = rng.standard_normal((n, H))
-        # the oracle adjoint is linearised at the GPU's own step states: over 30 x 6 x 3 ReLU layers an fp32
-        # trajectory 1e-5 away from fp64 crosses kinks a fp64 forward does not, which moves the gradient by more
-        # than the adjoint's own rounding
-        lin = ys[b].cpu().numpy()
-        g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g, y_lin=lin)
-        g1, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g, y_lin=lin * (1 + 1e-6))
+        g = gall[b]
+        g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g)
+        g1, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b] * (1 + 1e-6), "tsit5", g_final=g)
         if np.max(np.abs(g1 - g0)) > 1e-5 * np.max(np.abs(g0)):
-            print(f"  sample {b}: gradient not kink-stable, skipped")
+            print(f"  sample {b}: oracle gradient not kink-stable, skipped")
             continue
         traj, _ = O.solve_fixed_grid(f, grids[b], y0[b], "tsit5", save_every_step=True, time_dtype=np.float32)
         err = rel_err(ys[b].cpu().numpy(), traj)
@@ -118,8 +129,7 @@ def test_config3_exact_shape_trajectory_and_gradient(G):
         if len(chosen) == 2:
             break
     assert len(chosen) == 2, "fewer than two kink-stable samples among the candidates"
-    spec.save_mode = G._lib.SAVE_T1
-    gy0, gp, gf = G.integrate_vjp(prob, spec, ys, torch.tensor(gfin, dtype=torch.float32, device="cuda"))
+    gy0, gp, gf = G.integrate_vjp(prob, spec_t1, ys, torch.tensor(gfin, dtype=torch.float32, device="cuda"))
     total = OG._acc(OG._acc(None, refs[0][1]), refs[1][1])
     errs = {f"gy0[{b}]": rel_err(gy0[b].cpu().numpy(), r[0]) for b, r in zip(chosen, refs)}
     others = [b for b in range(B) if b not in chosen]
@@ -135,7 +145,7 @@ def test_config3_exact_shape_trajectory_and_gradient(G):
     ref_f = np.stack([np.concatenate([total[l][nm] for nm in names]) for l in range(L)])
     errs["fusion"] = rel_err(gf.double().cpu().numpy() @ M.numpy().T, ref_f)
     worst = max(errs, key=errs.get)
-    print(f"  config 3 gradient of samples {chosen}: worst {worst} {errs[worst]:.2e}")
+    print(f"  config 3 end-to-end gradient of samples {chosen}: worst {worst} {errs[worst]:.2e}")
     for k, e in errs.items():
         assert e <= RTOL_GRAD, (k, e)
 
@@ -342,6 +352,31 @@ def test_fused_configs_exact_shape_vs_oracle(G, config):
         ref, _ = O.solve_fixed_grid(f, grids[b], y0n[b], "rk4", time_dtype=np.float32)
         err = rel_err(ys[b].cpu().numpy(), ref)
         print(f"  config {config} sample {b}: 100 RK4 steps vs fp64 oracle {err:.2e}")
+        assert err <= RTOL_SOLVE
+
+
+def test_config5_reference_tgb_grid_vs_oracle(G):
+    """The reference's own TGB solve (tgb_graph_neural_cde.py:143,152-162: Tsit5, ConstantStepSize dt0 = 0.01, 100
+    steps on [0, 1], SaveAt(t1)) at config 5's shape (n = 255, h = 32, L = 4, de = 8; the persistent fixed-grid
+    solve, 601 evaluations per window): two windows' final states against the fp64 oracle at RTOL_SOLVE."""
+    from gncde import layout
+    B, n, T, H, de, L = 8, 255, 3, 32, 8, 4
+    _, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(59, B, n, T, 1.0, H, de, L, distinct=4)
+    prob = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
+    g100 = O.constant_grid(0.0, 1.0, 0.01)
+    assert len(g100) == 101 and g100[-1] == np.float32(1.0)
+    grid, ns = layout.stack_grids([g100] * B)
+    spec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=grid, nsteps=ns)
+    assert G.integrate_path(prob, spec) == "rows_grid<32,cde,tsit5>"
+    ys, st = G.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda"), stats=True)
+    st = st.cpu().numpy()
+    assert np.all(st[:, 0] == 100) and np.all(st[:, 2] == 601) and np.all(st[:, 3] == 0)
+    for b in (2, 5):
+        f, _ = oracle_fns(ts, coeffs, dco, P, H, de, b)
+        ref, nev = O.solve_fixed_grid(f, g100, y0[b], "tsit5", time_dtype=np.float32)
+        assert nev == 601
+        err = rel_err(ys[b].cpu().numpy(), ref)
+        print(f"  window {b}: 100 Tsit5 steps of dt0 = 0.01 vs the fp64 oracle {err:.2e}")
         assert err <= RTOL_SOLVE
 
 

@@ -498,21 +498,27 @@ def _pid_spread(P, gy0, gr, gy0p, grp):
     return max(rel_err(gy0p, gy0), float(np.max(np.abs(vb - va)) / np.max(np.abs(va))))
 
 
-def _gpu_pid_spread(G, prob, spec, y0n, g, b, flags=0):
-    """GPU-side kink screen of sample b (solved alone): the relative movement of its adaptive-solve gradient (dL/dy0,
-    params, fusion table) under a 1e-6 relative change of y0 — how close the fp32 linearisation sits to a ReLU kink
-    (the oracle screen measures the fp64 one; the two trajectories differ in the last bits)."""
+def _gpu_pid_spread(G, prob, spec, rec, nsteps, y0n, g, b, flags=0):
+    """GPU-side kink screen of sample b (solved alone): the relative movement of the gradient of its solve on its
+    recorded accepted grid (dL/dy0, params, fusion table; the reverse mode the adaptive solve's backward runs) under
+    a 1e-6 relative change of y0, on that same grid (the controller's own step choice is discontinuous) — how close
+    the fp32 linearisation sits to a ReLU kink (the oracle screen measures the fp64 one)."""
+    from gncde import autograd as AG
     sub = prob.take([b])
-    sp = dataclasses.replace(spec, t0=spec.t0[b:b + 1].contiguous(), t1=spec.t1[b:b + 1].contiguous(), flags=flags,
-                             save_ts=None if spec.save_ts is None else spec.save_ts[b:b + 1].contiguous())
+    dense = spec.save_mode == G._lib.SAVE_TS
+    gridt, nst = AG.pid_replay_grid(rec[b:b + 1], torch.tensor([int(nsteps[b])], device="cuda"), pad=1 if dense else 0)
+    steps = G.SolverSpec(method=G._lib.TSIT5, controller=G._lib.CTRL_GRID, save_mode=G._lib.SAVE_STEPS, grid=gridt,
+                         nsteps=nst, flags=flags)
+    gt = torch.tensor(g[b:b + 1], dtype=torch.float32, device="cuda")
 
     def grads(y):
-        params = sub.params.clone().requires_grad_(True)
-        fus = sub.fusion.clone().requires_grad_(True)
-        yl = torch.tensor(y, dtype=torch.float32, device="cuda", requires_grad=True)
-        out = G.autograd.solve(sub, sp, yl, params, fus)
-        (out.double() * torch.tensor(g[b:b + 1], device="cuda")).sum().backward()
-        return [yl.grad.cpu().numpy(), params.grad.cpu().numpy(), fus.grad.cpu().numpy()]
+        ysteps = G.integrate(sub, steps, torch.tensor(y, dtype=torch.float32, device="cuda"))
+        if dense:
+            gys, gst = AG.dense_output_cotangents(gridt, nst, spec.save_ts[b:b + 1].contiguous(), gt)
+            res = G.integrate_vjp(sub, steps, ysteps, gys, gstage=gst)
+        else:
+            res = G.integrate_vjp(sub, dataclasses.replace(steps, save_mode=G._lib.SAVE_T1), ysteps, gt)
+        return [r.cpu().numpy() for r in res[:3]]
 
     a, p = grads(y0n[b:b + 1]), grads(y0n[b:b + 1] * (1 + 1e-6))
     return max(rel_err(x, y) for x, y in zip(p, a))
@@ -590,7 +596,7 @@ def test_pid_solve_gradient_matches_oracle(G, case, save):
                 unstable.append(b)
         if not unstable:  # and the GPU's own linearisation (every path the test compares) away from a kink
             for b in range(B):
-                spreads = [_gpu_pid_spread(G, fprob, spec, y0n, g, b, fl)
+                spreads = [_gpu_pid_spread(G, fprob, spec, rec, st[:, 0], y0n, g, b, fl)
                            for fl in ((0, G._lib.FLAG_GENERIC) if case == "fused" else (0,))]
                 if max(spreads) >= 1e-5:
                     print(f"  sample {b}: GPU gradient moves {max(spreads):.2e} under a 1e-6 change of y0: redrawn")
