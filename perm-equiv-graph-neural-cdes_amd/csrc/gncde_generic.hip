@@ -609,6 +609,7 @@ struct VfWs {
   void* coefT;     // one-launch evaluation: every (sample, interval, plane) transposed, once per solve
   uint16_t* wbf;   // GNCDE_COMPUTE_BF16_MFMA: W' per layer rounded to bfloat16, natural layout
   unsigned* sync;  // one-launch evaluation: per-group arrival counters [B] + the fault word, zeroed per solve
+  unsigned* zgran;  // persistent solve: the tagged hand-off granules [2][B][n H][2], zeroed per solve
 };
 
 size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
@@ -638,6 +639,7 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.q = take((size_t)p.L * B * n);                          // q_l = (I + Abar_l) 1
   w.dx = take(B * n * (size_t)(p.cde_hidden > 0 ? 2 * p.cde_embed : 1));  // data-spline derivative at t
   w.sync = reinterpret_cast<unsigned*>(take(rows_sync_words(p.B)));
+  w.zgran = reinterpret_cast<unsigned*>(take(rows_solve_shape(p) ? 4 * B * n * (size_t)p.dims[0] : 1));
   w.wbf = reinterpret_cast<uint16_t*>(take(p.compute == GNCDE_COMPUTE_BF16_MFMA ? (wsum + 1) / 2 : 1));
   // the one-launch evaluation reads a node block's column strip [:, R] as rows R of the transposed planes (whole
   // cache lines, like its rows block) instead of 16-column segments of every row
@@ -934,7 +936,9 @@ int generic_rows_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y
   carve_vf(p, ws, w);
   generic_vf_prepare(p, ws, st, true);
   float* part = reinterpret_cast<float*>(ws + generic_vf_workspace(p));
-  const int rc = rows_integrate_pid(p, s, y0, ys, stats, ws, part, w.csum, w.coefT, w.wp, w.bf, w.Z0, w.Z1, w.sync, st);
+  (void)hipMemsetAsync(w.zgran, 0, 4 * (size_t)p.B * p.n * p.dims[0] * sizeof(unsigned), st);  // no tag is current
+  const int rc = rows_integrate_pid(p, s, y0, ys, stats, ws, part, w.csum, w.coefT, w.wp, w.bf, w.Z0, w.Z1, w.sync,
+                                    w.zgran, st);
   if (rc) return rc;
   return rows_fault_status(p, ws, st, true);
 }

@@ -95,6 +95,7 @@ struct RowsArgs {
   float* zbuf[2];          // [G, n, H] each: the groups' hidden layer outputs, alternating per step
   float* keep;             // optional [L-1, B, n, H]: every sample's hidden layer outputs kept (reverse mode), used
                            // instead of zbuf
+  unsigned* zgran;         // solve: [2][B][n H] tagged hand-off granules {value, tag} (zeroed before the solve)
   unsigned* bar;           // [G][kBarStride] arrivals per group (one line each), monotonic within a solve
   unsigned bar0;           // barriers every group completed before this launch
   int* fault;              // set when a barrier wait gives up
@@ -226,7 +227,16 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
   const size_t nn = (size_t)n * n;
   const size_t zgroup = (size_t)n * H;
   unsigned epoch = a.bar0;
-  unsigned pub = 0;  // publications of this launch (stage inputs, hidden outputs, partial sums): buffer parity
+  unsigned pub = 0;  // arrivals of this launch (one-evaluation launches: hidden outputs; solve: group sums): parity
+  // The persistent solve hands the stage inputs and hidden outputs over as TAGGED GRANULES: element e of the s-th
+  // publication of sample b is the 8-byte {value, s + 1} at zgran[((s & 1) B + b) n H + e], two per 16-byte sc1
+  // store (MI355X_MICROARCH.md: an 8-byte granule written by one sc1 store, also as half of a 16-byte one, is
+  // observed untorn), so no arrival counter and no store drain sit between a producer and its consumers: a consumer
+  // polls the data itself until every tag is the current one.  (The group sums keep the counter barrier.)  A
+  // publication's buffer is rewritten two publications later, by which time every consumer has read it: a
+  // producer of publication s + 2 has consumed s + 1, which every workgroup published after reading s.
+  constexpr bool GRAN = SOLVE != 0;
+  unsigned hseq = 0;  // solve: granule publications of this group so far
 #ifdef GNCDE_ROWS_STAMPS
   bool stamp_on = true;
   const int stamp_slot = SOLVE != 0 ? g * nb + rb : (int)blockIdx.x;
@@ -260,6 +270,72 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     }
     __syncthreads();
     return sFlag[0] == 0;
+  };
+
+  auto gran_rsrc = [&](unsigned s, int bb) {
+    return rsrc(a.zgran + ((size_t)(s & 1) * a.B + bb) * zgroup * 2, (unsigned)(zgroup * 8));
+  };
+  // elements e .. e + 3 (one float4 of a row) as two 16-byte {value, tag, value, tag} stores
+  auto gran_store4 = [&](__amdgpu_buffer_rsrc_t r, int e, const floatx4 v, unsigned tag) {
+    __builtin_amdgcn_raw_buffer_store_b128(
+        u32x4{__builtin_bit_cast(unsigned, v.x), tag, __builtin_bit_cast(unsigned, v.y), tag}, r, e * 8, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(
+        u32x4{__builtin_bit_cast(unsigned, v.z), tag, __builtin_bit_cast(unsigned, v.w), tag}, r, e * 8 + 16, 0, 16);
+  };
+  // publication s of this sample into Zs [NP][ZS] (rows >= n zero): every granule polled until its tag is s + 1; a
+  // bounded wait (past the limit, or when another workgroup gave up, it sets the fault word and returns false)
+  auto gran_load = [&](float* Zs, unsigned s) -> bool {
+    constexpr int G4 = H / 4, UG = 4;
+    const unsigned tag = s + 1;
+    const auto r = gran_rsrc(s, g);
+    const int tot = a.np * G4, valid = a.n * G4;
+    const int tid = threadIdx.x;
+    bool good = true;
+    for (int e0 = tid; e0 < tot; e0 += 256 * UG) {
+      u32x4 p0[UG], p1[UG];
+#pragma unroll
+      for (int u = 0; u < UG; ++u) {
+        const int e = e0 + 256 * u;
+        const bool in = e < valid;
+        p0[u] = in ? __builtin_amdgcn_raw_buffer_load_b128(r, e * 32, 0, 16) : u32x4{0u, tag, 0u, tag};
+        p1[u] = in ? __builtin_amdgcn_raw_buffer_load_b128(r, e * 32 + 16, 0, 16) : u32x4{0u, tag, 0u, tag};
+      }
+      auto stale = [&]() {
+        unsigned m = 0;
+#pragma unroll
+        for (int u = 0; u < UG; ++u)
+          if (p0[u][1] != tag || p0[u][3] != tag || p1[u][1] != tag || p1[u][3] != tag) m |= 1u << u;
+        return m;
+      };
+      unsigned st = stale(), spins = 0;
+      while (st) {
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int u = 0; u < UG; ++u)
+          if ((st >> u) & 1u) {
+            const int e = e0 + 256 * u;
+            p0[u] = __builtin_amdgcn_raw_buffer_load_b128(r, e * 32, 0, 16);
+            p1[u] = __builtin_amdgcn_raw_buffer_load_b128(r, e * 32 + 16, 0, 16);
+          }
+        st = stale();
+        ++spins;
+        if (st && (spins > a.spin_limit ||
+                   ((spins & 1023u) == 0 && __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))) {
+          __hip_atomic_store(a.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          good = false;
+          break;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UG; ++u) {
+        const int e = e0 + 256 * u;
+        if (e < tot)
+          *reinterpret_cast<floatx4*>(Zs + (e / G4) * ZS + 4 * (e % G4)) =
+              floatx4{__builtin_bit_cast(float, p0[u][0]), __builtin_bit_cast(float, p0[u][2]),
+                      __builtin_bit_cast(float, p1[u][0]), __builtin_bit_cast(float, p1[u][2])};
+      }
+    }
+    return good;
   };
 
   // the solve's knots, one per lane (T <= 64)
@@ -455,6 +531,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       float* Zs = big;
       constexpr int G4 = H / 4, U = 8;
       const int tot = NP * G4, valid = n * G4;
+      bool gave = false;
       if (l == 0 && !handoff) {
         const floatx4* Z4 = reinterpret_cast<const floatx4*>(z0);
         for (int e0 = tid; e0 < tot; e0 += 256 * U) {
@@ -470,6 +547,8 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
             if (e < tot) *reinterpret_cast<floatx4*>(Zs + (e / G4) * ZS + 4 * (e % G4)) = v[u];
           }
         }
+      } else if constexpr (GRAN) {  // the group's latest publication (stage input or hidden output)
+        gave = !gran_load(Zs, hseq - 1);
       } else {
         ok = wait_all() && ok;
         // publications alternate buffers, so a buffer is rewritten only after a barrier that every reader of its
@@ -493,7 +572,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
           }
         }
       }
-      __syncthreads();
+      if (__syncthreads_or(gave ? 1 : 0)) ok = false;
       for (int r = tid; r < NP; r += 256) {
         float ss = 0.f;
 #pragma unroll
@@ -637,18 +716,35 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
         for (int r = 0; r < 4; ++r) sOut[(4 * hi + r) * ZS + 16 * tile + lo] = fmaxf(v[r], 0.f);
       }
       __syncthreads();
-      // (an idle round keeps to its group's own buffers: the sample it recomputes is another group's)
-      float* zout = kslab ? kslab + ((size_t)l * a.B + b) * zgroup : a.zbuf[pub & 1] + (size_t)zslot * zgroup;
-      const auto rs = rsrc(zout, (unsigned)(zgroup * sizeof(float)));
       constexpr int G4 = H / 4;
-      if (tid < 16 * G4) {  // write-through 16-byte stores of this workgroup's rows, then one arrival
-        const int R = tid / G4, q = tid % G4;
-        if (r0 + R < n)
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(u32x4, *reinterpret_cast<const floatx4*>(sOut + R * ZS + 4 * q)), rs,
-              ((r0 + R) * H + 4 * q) * 4, 0, 16);
+      if constexpr (GRAN) {  // the rows as tagged granules (and, recording, as plain floats into the slab)
+        const unsigned tag = hseq + 1;
+        const auto rg = gran_rsrc(hseq, b);
+        const auto rk = rsrc(kslab ? kslab + ((size_t)l * a.B + b) * zgroup : a.zbuf[0], (unsigned)(zgroup * 4));
+        if (tid < 16 * G4) {
+          const int R = tid / G4, q = tid % G4;
+          if (r0 + R < n) {
+            const floatx4 v = *reinterpret_cast<const floatx4*>(sOut + R * ZS + 4 * q);
+            gran_store4(rg, (r0 + R) * H + 4 * q, v, tag);
+            if (kslab)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rk, ((r0 + R) * H + 4 * q) * 4, 0, 0);
+          }
+        }
+        ++hseq;
+        __syncthreads();  // the output tile is read before the next layer's staging rewrites the region
+      } else {
+        // (an idle round keeps to its group's own buffers: the sample it recomputes is another group's)
+        float* zout = kslab ? kslab + ((size_t)l * a.B + b) * zgroup : a.zbuf[pub & 1] + (size_t)zslot * zgroup;
+        const auto rs = rsrc(zout, (unsigned)(zgroup * sizeof(float)));
+        if (tid < 16 * G4) {  // write-through 16-byte stores of this workgroup's rows, then one arrival
+          const int R = tid / G4, q = tid % G4;
+          if (r0 + R < n)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(u32x4, *reinterpret_cast<const floatx4*>(sOut + R * ZS + 4 * q)), rs,
+                ((r0 + R) * H + 4 * q) * 4, 0, 16);
+        }
+        arrive();  // its barrier also orders the partials' reuse by the next layer
       }
-      arrive();  // its barrier also orders the partials' reuse by the next layer
       ROWS_STAMP(5 + 3 * l);
     }
     {  // the output layer
@@ -793,13 +889,11 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     floatx4 y1 = zero, kk[7];
 #pragma unroll
     for (int j = 0; j < 7; ++j) kk[j] = zero;
-    // the stage input of the next evaluation, published to the group (sc1 16-byte stores + one arrival)
+    // the stage input of the next evaluation, published to the group as tagged granules
     auto publish = [&](const floatx4 u) {
-      if (mine)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, u),
-                                               rsrc(a.zbuf[pub & 1] + (size_t)b * zgroup, (unsigned)(E * 4)),
-                                               (int)(((r0 + orow) * H + ocol) * 4), 0, 16);
-      arrive();
+      if (mine) gran_store4(gran_rsrc(hseq, b), (r0 + orow) * H + ocol, u, hseq + 1);
+      ++hseq;
+      __syncthreads();  // every thread has taken its K from the output tile before the next form rewrites it
     };
     // (sum of v0, sum of v1) over the group's rows, from each thread's 4-element chunk partials (fma chains from 0)
     // in the CANONICAL order the host-paced controller uses too (gncde_pid.hip canon_sumsq): a row sums its chunks in
@@ -1434,7 +1528,7 @@ size_t rows_pid_scratch(const GncdeProblem& p) {
 
 int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
                        char* vf_ws, float* part, const float* csum, const void* coefT, const float* wperm,
-                       const float* bf, float* z0, float* z1, unsigned* sync, hipStream_t st) {
+                       const float* bf, float* z0, float* z1, unsigned* sync, unsigned* zgran, hipStream_t st) {
   Inst k;
   const int H = p.dims[0];
   if (!find_solve_inst(p, s, k)) return GNCDE_ERR_UNSUPPORTED;
@@ -1462,6 +1556,7 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   a.bf = bf;
   a.zbuf[0] = z0;
   a.zbuf[1] = z1;
+  a.zgran = zgran;
   a.bar = sync;  // per-sample arrivals, one line each (zeroed by generic_vf_prepare)
   a.fault = reinterpret_cast<int*>(sync + rows_fault_word(p.B));  // the workspace's fault word
   a.ticket = sync + rows_fault_word(p.B) + 1;

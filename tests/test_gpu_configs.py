@@ -92,11 +92,16 @@ def test_config3_exact_shape_trajectory_and_gradient(G):
     ys, st = G.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda"), stats=True)
     st = st.cpu().numpy()
     assert np.all(st[:, 0] == 30) and np.all(st[:, 2] == 181) and np.all(st[:, 3] == 0)
-    # candidates spread over the batch; the first two whose gradient is kink-stable at BOTH linearisations — the
-    # GPU's fp32 trajectory and the oracle's own fp64 one (1e-5 apart after 30 x 6 x 3 ReLU layers, so a
-    # pre-activation within that distance of 0 sits on different sides of a kink in the two) — are checked, end to
-    # end: the GPU gradient against the oracle adjoint of the oracle's own forward.
-    # The GPU screen: every sample's dL/dy0 (independent per sample) at y0 and at y0 (1 + 1e-6).
+    # ReLU kinks: over 30 steps x 6 stages x 2 ReLU layers of 129 x 64 pre-activations the fp32 trajectory (1e-5
+    # from fp64) sits on the other side of some kink than the fp64 one, so the END-TO-END gradients of the two
+    # differ by a kink flip, not by adjoint error.  Measured on the GPU: every candidate's fp32 dL/dy0 moves by
+    # 2e-4 .. 4e-2 under a 1e-6 relative change of y0 (printed below), i.e. at this shape the fp32 gradient itself
+    # is only defined to that scale.  So the check is in two parts, on the first two candidates whose fp64 oracle
+    # gradient is kink-stable (moves < 1e-5 under the same change):
+    #   1. the adjoint: the oracle adjoint linearised at the GPU's own step states, at RTOL_GRAD;
+    #   2. end to end: the oracle adjoint of the oracle's own fp64 forward, within max(RTOL_GRAD, 3 x the GPU
+    #      gradient's own movement) — the gradient's fp32 discontinuity scale.
+    # The GPU's movement: every sample's dL/dy0 (independent per sample) at y0 and at y0 (1 + 1e-6).
     gall = rng.standard_normal((B, n, H))
     spec_t1 = dataclasses.replace(spec, save_mode=G._lib.SAVE_T1)
     gpu_g = []
@@ -105,17 +110,18 @@ def test_config3_exact_shape_trajectory_and_gradient(G):
         gpu_g.append(G.integrate_vjp(prob, spec_t1, G.integrate(prob, spec, yd),
                                      torch.tensor(gall, dtype=torch.float32, device="cuda"))[0].cpu().numpy())
     gpu_move = [rel_err(gpu_g[1][b], gpu_g[0][b]) for b in range(B)]
+    print("  GPU dL/dy0 movement under a 1e-6 change of y0: " +
+          ", ".join(f"{b}: {gpu_move[b]:.1e}" for b in (5, 40, 63, 17, 28, 51, 22, 34, 9, 56)))
     gfin = np.zeros((B, n, H))
-    chosen, refs = [], []
+    chosen, refs, e2e = [], [], []
     for b in (5, 40, 63, 17, 28, 51, 22, 34, 9, 56):  # windows 5, 0, 3, 7, 8, 1, 2, 4, 9, 6
-        if gpu_move[b] > 1e-5:
-            print(f"  sample {b}: GPU gradient not kink-stable ({gpu_move[b]:.2e}), skipped")
-            continue
         f, fv = oracle_fns(ts, coeffs, dco, P, H, de, b)
         g = gall[b]
-        g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g)
-        g1, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b] * (1 + 1e-6), "tsit5", g_final=g)
-        if np.max(np.abs(g1 - g0)) > 1e-5 * np.max(np.abs(g0)):
+        lin = ys[b].cpu().numpy()
+        g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g, y_lin=lin)
+        e0, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g)
+        e1, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b] * (1 + 1e-6), "tsit5", g_final=g)
+        if np.max(np.abs(e1 - e0)) > 1e-5 * np.max(np.abs(e0)):
             print(f"  sample {b}: oracle gradient not kink-stable, skipped")
             continue
         traj, _ = O.solve_fixed_grid(f, grids[b], y0[b], "tsit5", save_every_step=True, time_dtype=np.float32)
@@ -126,10 +132,16 @@ def test_config3_exact_shape_trajectory_and_gradient(G):
         gfin[b] = g
         chosen.append(b)
         refs.append((g0, gr))
+        e2e.append(e0)
         if len(chosen) == 2:
             break
     assert len(chosen) == 2, "fewer than two kink-stable samples among the candidates"
     gy0, gp, gf = G.integrate_vjp(prob, spec_t1, ys, torch.tensor(gfin, dtype=torch.float32, device="cuda"))
+    for b, ref in zip(chosen, e2e):  # 2. end to end, at the gradient's own fp32 discontinuity scale
+        e, bound = rel_err(gy0[b].cpu().numpy(), ref), max(RTOL_GRAD, 3.0 * gpu_move[b])
+        print(f"  sample {b}: end-to-end dL/dy0 vs the oracle's own forward {e:.2e} (bound {bound:.2e}: the GPU "
+              f"gradient moves {gpu_move[b]:.2e} under a 1e-6 change of y0)")
+        assert e <= bound
     total = OG._acc(OG._acc(None, refs[0][1]), refs[1][1])
     errs = {f"gy0[{b}]": rel_err(gy0[b].cpu().numpy(), r[0]) for b, r in zip(chosen, refs)}
     others = [b for b in range(B) if b not in chosen]
@@ -145,7 +157,7 @@ def test_config3_exact_shape_trajectory_and_gradient(G):
     ref_f = np.stack([np.concatenate([total[l][nm] for nm in names]) for l in range(L)])
     errs["fusion"] = rel_err(gf.double().cpu().numpy() @ M.numpy().T, ref_f)
     worst = max(errs, key=errs.get)
-    print(f"  config 3 end-to-end gradient of samples {chosen}: worst {worst} {errs[worst]:.2e}")
+    print(f"  config 3 adjoint at the GPU's step states, samples {chosen}: worst {worst} {errs[worst]:.2e}")
     for k, e in errs.items():
         assert e <= RTOL_GRAD, (k, e)
 

@@ -598,7 +598,7 @@ def test_pid_solve_gradient_matches_oracle(G, case, save):
             for b in range(B):
                 spreads = [_gpu_pid_spread(G, fprob, spec, rec, st[:, 0], y0n, g, b, fl)
                            for fl in ((0, G._lib.FLAG_GENERIC) if case == "fused" else (0,))]
-                if max(spreads) >= 1e-5:
+                if max(spreads) >= RTOL_GRAD / 5:  # (a flip that moves it less stays below RTOL_GRAD)
                     print(f"  sample {b}: GPU gradient moves {max(spreads):.2e} under a 1e-6 change of y0: redrawn")
                     unstable.append(b)
         if not unstable:
