@@ -275,12 +275,14 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
   auto gran_rsrc = [&](unsigned s, int bb) {
     return rsrc(a.zgran + ((size_t)(s & 1) * a.B + bb) * zgroup * 2, (unsigned)(zgroup * 8));
   };
-  // elements e .. e + 3 (one float4 of a row) as two 16-byte {value, tag, value, tag} stores
+  // elements e .. e + 3 (one float4 of a row) as two 16-byte {value, tag, value, tag} stores (every vector element
+  // copied to a scalar before its bit cast: a bit cast of an ext-vector element reads element 0, see coef_el)
   auto gran_store4 = [&](__amdgpu_buffer_rsrc_t r, int e, const floatx4 v, unsigned tag) {
+    const float x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3];
     __builtin_amdgcn_raw_buffer_store_b128(
-        u32x4{__builtin_bit_cast(unsigned, v.x), tag, __builtin_bit_cast(unsigned, v.y), tag}, r, e * 8, 0, 16);
+        u32x4{__builtin_bit_cast(unsigned, x0), tag, __builtin_bit_cast(unsigned, x1), tag}, r, e * 8, 0, 16);
     __builtin_amdgcn_raw_buffer_store_b128(
-        u32x4{__builtin_bit_cast(unsigned, v.z), tag, __builtin_bit_cast(unsigned, v.w), tag}, r, e * 8 + 16, 0, 16);
+        u32x4{__builtin_bit_cast(unsigned, x2), tag, __builtin_bit_cast(unsigned, x3), tag}, r, e * 8 + 16, 0, 16);
   };
   // publication s of this sample into Zs [NP][ZS] (rows >= n zero): every granule polled until its tag is s + 1; a
   // bounded wait (past the limit, or when another workgroup gave up, it sets the fault word and returns false)
@@ -329,10 +331,11 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
 #pragma unroll
       for (int u = 0; u < UG; ++u) {
         const int e = e0 + 256 * u;
+        const unsigned w0 = p0[u][0], w1 = p0[u][2], w2 = p1[u][0], w3 = p1[u][2];
         if (e < tot)
           *reinterpret_cast<floatx4*>(Zs + (e / G4) * ZS + 4 * (e % G4)) =
-              floatx4{__builtin_bit_cast(float, p0[u][0]), __builtin_bit_cast(float, p0[u][2]),
-                      __builtin_bit_cast(float, p1[u][0]), __builtin_bit_cast(float, p1[u][2])};
+              floatx4{__builtin_bit_cast(float, w0), __builtin_bit_cast(float, w1), __builtin_bit_cast(float, w2),
+                      __builtin_bit_cast(float, w3)};
       }
     }
     return good;
