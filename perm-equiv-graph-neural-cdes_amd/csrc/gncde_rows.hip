@@ -310,7 +310,13 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
         return m;
       };
       unsigned st = stale(), spins = 0;
-      while (st) {
+      while (st) {  // (like wait_all: a wait that has to poll more than spin_limit times gives up)
+        if (spins >= a.spin_limit ||
+            ((spins & 1023u) == 1023u && __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          __hip_atomic_store(a.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          good = false;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
         for (int u = 0; u < UG; ++u)
@@ -321,12 +327,6 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
           }
         st = stale();
         ++spins;
-        if (st && (spins > a.spin_limit ||
-                   ((spins & 1023u) == 0 && __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))) {
-          __hip_atomic_store(a.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          good = false;
-          break;
-        }
       }
 #pragma unroll
       for (int u = 0; u < UG; ++u) {
