@@ -96,6 +96,7 @@ struct RowsArgs {
   float* keep;             // optional [L-1, B, n, H]: every sample's hidden layer outputs kept (reverse mode), used
                            // instead of zbuf
   unsigned* zgran;         // solve: [2][B][n H] tagged hand-off granules {value, tag} (zeroed before the solve)
+  int poll1;               // solve: a granule wait re-polls only its first stale pair per spin (GNCDE_GRAN_POLL1)
   unsigned* bar;           // [G][kBarStride] arrivals per group (one line each), monotonic within a solve
   unsigned bar0;           // barriers every group completed before this launch
   int* fault;              // set when a barrier wait gives up
@@ -318,9 +319,10 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
           break;
         }
         __builtin_amdgcn_s_sleep(1);
+        const unsigned want = a.poll1 ? st & (0u - st) : st;  // poll1: the first stale pair only
 #pragma unroll
         for (int u = 0; u < UG; ++u)
-          if ((st >> u) & 1u) {
+          if ((want >> u) & 1u) {
             const int e = e0 + 256 * u;
             p0[u] = __builtin_amdgcn_raw_buffer_load_b128(r, e * 32, 0, 16);
             p1[u] = __builtin_amdgcn_raw_buffer_load_b128(r, e * 32 + 16, 0, 16);
@@ -1560,6 +1562,10 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   a.zbuf[0] = z0;
   a.zbuf[1] = z1;
   a.zgran = zgran;
+  {
+    const char* e = getenv("GNCDE_GRAN_POLL1");
+    a.poll1 = e && atoi(e) != 0;
+  }
   a.bar = sync;  // per-sample arrivals, one line each (zeroed by generic_vf_prepare)
   a.fault = reinterpret_cast<int*>(sync + rows_fault_word(p.B));  // the workspace's fault word
   a.ticket = sync + rows_fault_word(p.B) + 1;
