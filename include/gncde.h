@@ -200,7 +200,7 @@ typedef struct GncdeSolver {
 int gncde_abi_version(void);
 const char* gncde_strerror(int code);
 /* Build provenance: lowercase hex sha256 of the kernel sources this library was compiled from (the bytes of the
- * sorted csrc/*.hip and csrc/*.h, then this header, concatenated).  The Python binding refuses a library whose
+ * sorted .hip and .h files of csrc, then this header, concatenated).  The Python binding refuses a library whose
  * sha differs from the source tree's, so a stale prebuilt binary cannot stand in for the tree's kernels. */
 const char* gncde_source_sha256(void);
 /* Name of the kernel path gncde_integrate would take for this problem ("fused<64,16,3,rk4>" or
