@@ -936,7 +936,8 @@ int generic_rows_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y
   carve_vf(p, ws, w);
   generic_vf_prepare(p, ws, st, true);
   float* part = reinterpret_cast<float*>(ws + generic_vf_workspace(p));
-  (void)hipMemsetAsync(w.zgran, 0, 4 * (size_t)p.B * p.n * p.dims[0] * sizeof(unsigned), st);  // no tag is current
+  if (rows_solve_granules())  // no tag is current
+    (void)hipMemsetAsync(w.zgran, 0, 4 * (size_t)p.B * p.n * p.dims[0] * sizeof(unsigned), st);
   const int rc = rows_integrate_pid(p, s, y0, ys, stats, ws, part, w.csum, w.coefT, w.wp, w.bf, w.Z0, w.Z1, w.sync,
                                     w.zgran, st);
   if (rc) return rc;

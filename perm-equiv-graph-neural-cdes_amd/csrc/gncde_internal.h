@@ -307,6 +307,10 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
 void rows_pid_name(const GncdeProblem& p, const GncdeSolver& s, char* buf, size_t len);
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device, kernel, size) for launches above 64 KB of LDS
 bool ensure_dyn_lds(const void* fn, size_t smem);
+// compute units of the current device (cached per device; 0 when the query fails)
+int device_cu_count();
+// the persistent solve hands off through tagged granules (GNCDE_SOLVE_GRANULES=1) instead of counter barriers
+bool rows_solve_granules();
 // a one-launch evaluation's group barrier gave up in this call: GNCDE_ERR_BARRIER (reads the workspace's fault word
 // back, one stream synchronisation; GNCDE_OK without one-launch evaluations)
 int rows_fault_status(const GncdeProblem& p, char* vf_ws, hipStream_t st, bool ran_rows);

@@ -34,7 +34,7 @@ typedef float floatx4u __attribute__((ext_vector_type(4), aligned(4)));  // dwor
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x8u __attribute__((ext_vector_type(8), aligned(2)));  // 8 bf16 of an (I + Abar) plane row
 
-constexpr int kRows = 32;  // node rows per workgroup: two 16-row MFMA tiles
+constexpr int kTiles = 2;  // 16-row MFMA tiles per workgroup (hidden / ODE output layers; the CDE read-out picks 2 or 5)
 constexpr int kSplit = 2;  // CDE read-out: workgroups per row block (channel groups)
 
 struct LayerArgs {
@@ -61,6 +61,10 @@ __host__ __device__ constexpr int zs_stride() {
 }
 
 // MODE 0: hidden layer, ReLU.  MODE 1: ODE output layer, out = tg * Z_next.  MODE 2: CDE output layer (DOUT = h).
+// NT: 16-row tiles per workgroup.  The CDE read-out's MFMA chain (K = 16 h per output) dominates its launch, and with
+// NT = 2 config 3's 640 workgroups were 2.5 per CU: the CUs holding three ran 3 x (P product + read-out) MFMA chains,
+// every workgroup staged its sample's whole Z first, and no staging overlapped an MFMA chain.  With NT = 5 (when the
+// batch still gives every CU a workgroup) config 3 is 256 workgroups, one per CU, each staging Z once for 5 tiles.
 // BF: the n x n product on v_mfma_f32_16x16x32_bf16 (GNCDE_COMPUTE_BF16*): (I + Abar) from its bf16 (hi, lo) planes,
 // diag(inv) Z split into (hi, lo) on the fly, three products (hi hi, hi lo, lo hi) with fp32 accumulation.
 // Phase stamps of the fp32 CDE read-out launch (diagnostic build -DGNCDE_LAYER_STAMPS only: tools/diag_layer_stamps.py):
@@ -76,18 +80,21 @@ __device__ unsigned long long g_layer_stamps[1024 * 8];
 #define LAYER_STAMP(k) do {} while (0)
 #endif
 
-template <int DIN, int DOUT, int MODE, bool BF>
-__global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
+template <int DIN, int DOUT, int MODE, bool BF, int NT>
+__global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
+  static_assert(MODE == 2 || NT == 2, "the Linear epilogue's tile split assumes two row tiles");
+  static_assert(!BF || NT == 2, "bf16 modes: two row tiles");
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int kRows = 16 * NT;
   constexpr int ZS = zs_stride<DIN>();
   constexpr int CTP = DIN / 16;  // product column tiles
   constexpr int KPP = 4;         // product K parts (one per wave)
   constexpr int NCC = DIN / 16;  // 16-deep K chunks of the Linear
   const int n = a.n;
   const int nk = BF ? (n + 31) & ~31 : (n + 15) & ~15;  // K rows of Zs: whole MFMA K chunks
-  floatx4* red = reinterpret_cast<floatx4*>(smem);  // [4][2][64] K-part partials (MODE 2)
-  float* sDx = smem + 4 * 2 * 64 * 4;               // [32][17] (MODE 2)
-  float* Zs = sDx + kRows * 17 + 12;                // [nk][ZS] (16-byte aligned: 2048 + 556 is a multiple of 4)
+  floatx4* red = reinterpret_cast<floatx4*>(smem);  // [4][NT][64] K-part partials (MODE 2)
+  float* sDx = smem + 4 * NT * 64 * 4;              // [kRows][17] (MODE 2)
+  float* Zs = sDx + kRows * 17 + 12;                // [nk][ZS] (16-byte aligned: 1024 NT + 272 NT + 12 = 0 mod 4)
   float* Ps = Zs;                                   // [KPP][32][ZS] after the product (max(nk, 128) rows reserved)
   float* sInv = Zs + (nk > 4 * kRows ? nk : 4 * kRows) * ZS;  // [nk] RMSNorm factors of the Z rows
   // MODE 2 splits the read-out's channels over kSplit workgroups per row block (each recomputes P: the product is
@@ -102,11 +109,22 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
   LAYER_STAMP(0);
 
   const bool two = r0 + 16 < n;  // the second row tile holds a valid row (else its MFMAs are skipped)
+  const int ntl = (n - r0 + 15) >> 4 < NT ? (n - r0 + 15) >> 4 : NT;  // tiles holding a valid row
+  // f(integral_constant<int, ntl>) (uniform; counts 1..NT, NT <= 5)
+  auto with_count = [&](int cnt, auto&& f) __attribute__((always_inline)) {
+    if (cnt >= NT) f(std::integral_constant<int, NT>{});
+    else if (NT > 4 && cnt == 4) f(std::integral_constant<int, (NT > 4 ? 4 : 1)>{});
+    else if (NT > 3 && cnt == 3) f(std::integral_constant<int, (NT > 3 ? 3 : 1)>{});
+    else if (NT > 2 && cnt == 2) f(std::integral_constant<int, (NT > 2 ? 2 : 1)>{});
+    else f(std::integral_constant<int, 1>{});
+  };
   // The fp32 product's first round of (I + Abar) operand loads is issued before Z is staged: the two HBM / L2 round
   // trips overlap instead of following each other (the operand does not depend on Z; diag(inv) is applied later).
   const int nch16 = nk >> 4;
-  const int ra0 = r0 + lo < n ? r0 + lo : n - 1, ra1 = r0 + 16 + lo < n ? r0 + 16 + lo : n - 1;
-  floatx4 av[4][2];
+  int ra[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) ra[t] = r0 + 16 * t + lo < n ? r0 + 16 * t + lo : n - 1;
+  floatx4 av[4][NT];
   auto load_round = [&](int kr) __attribute__((always_inline)) {
     const float* Ab = a.abar + nb * n;
 #pragma unroll
@@ -114,10 +132,10 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
       const int kc = kr + 4 * c;
       const int k = 16 * kc + 4 * hi;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const float* pa = Ab + (size_t)(t ? ra1 : ra0) * n + k;
+      for (int t = 0; t < NT; ++t) {
+        const float* pa = Ab + (size_t)ra[t] * n + k;
         floatx4 v = {0.f, 0.f, 0.f, 0.f};
-        if (kc < nch16) {
+        if (kc < nch16 && (NT == 2 || t < ntl)) {
           if (k + 4 <= n) {
             const floatx4u u = *reinterpret_cast<const floatx4u*>(pa);
             v = floatx4{u.x, u.y, u.z, u.w};
@@ -136,7 +154,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
   constexpr int CTO = MODE != 2 ? DOUT / 16 : 1;
   constexpr int NCCE = MODE != 2 ? DIN / 16 : 1;
   floatx4 wpre[2][NCCE];
-  float bpre[2], qpre[2][4], gpre[2][4];
+  float bpre[2], qpre[NT][4], gpre[NT][4];
   if constexpr (MODE != 2) {
     const floatx4* W4p = reinterpret_cast<const floatx4*>(a.wperm);
 #pragma unroll
@@ -155,7 +173,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
     }
   } else {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int R = r0 + 16 * t + 4 * hi + r;
@@ -231,7 +249,7 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
       bf16x8 ah[2], al[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const uint16_t* pa = Ab + (size_t)(t ? ra1 : ra0) * n + k;
+        const uint16_t* pa = Ab + (size_t)ra[t] * n + k;
         ah[t] = ld8(pa, k);
         al[t] = ld8(pa + a.a_lo, k);
       }
@@ -265,9 +283,9 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         for (int r = 0; r < 4; ++r) Ps[(w * kRows + 16 * t + 4 * hi + r) * ZS + 16 * ct + lo] = acc[t][ct][r];
   } else {
     const int nch = nch16;
-    floatx4 acc[2][CTP];
+    floatx4 acc[NT][CTP];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int ct = 0; ct < CTP; ++ct) acc[t][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
     for (int kr = w; kr < nch; kr += 16) {  // rounds of up to 4 chunks: kr, kr + 4, kr + 8, kr + 12
@@ -277,16 +295,20 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         const int kc = kr + 4 * c;
         if (kc < nch) {
           const floatx4 iv = *reinterpret_cast<const floatx4*>(sInv + 16 * kc + 4 * hi);
-          av[c][0] *= iv;
-          av[c][1] *= iv;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) av[c][t] *= iv;
         }
       }
-      auto mm = [&](auto two_c) __attribute__((always_inline)) {
-        constexpr bool TWO = decltype(two_c)::value;
+      // the first CNT tiles (NT = 2: both, or the first when the second holds no row; NT > 2: the ntl tiles holding a
+      // row, one copy of the loop per count: a runtime test per MFMA compiled to a branch around each of them)
+      auto mm = [&](auto cnt_c) __attribute__((always_inline)) {
+        constexpr int CNT = decltype(cnt_c)::value;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const int kc = kr + 4 * c;
           if (kc >= nch) break;
+          // NT > 2: MFMA steps s whose K rows 16 kc + 4 hi + s all lie past n add exact zeros and are skipped
+          const int ks = NT > 2 && n - 16 * kc < 4 ? n - 16 * kc : 4;
           const float* zb = Zs + (16 * kc + 4 * hi) * ZS + lo;
           float bv[4][CTP];  // the chunk's B operands: every LDS read issued before the first MFMA
 #pragma unroll
@@ -294,23 +316,22 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
 #pragma unroll
             for (int ct = 0; ct < CTP; ++ct) bv[s][ct] = zb[s * ZS + 16 * ct];
 #pragma unroll
-          for (int s = 0; s < 4; ++s)
+          for (int s = 0; s < 4; ++s) {
+            if (NT > 2 && s >= ks) break;
 #pragma unroll
-            for (int ct = 0; ct < CTP; ++ct) {
-              acc[0][ct] = mfma4(av[c][0][s], bv[s][ct], acc[0][ct]);
-              if constexpr (TWO) acc[1][ct] = mfma4(av[c][1][s], bv[s][ct], acc[1][ct]);
-            }
+            for (int ct = 0; ct < CTP; ++ct)
+#pragma unroll
+              for (int t = 0; t < NT; ++t)
+                if (t < CNT) acc[t][ct] = mfma4(av[c][t][s], bv[s][ct], acc[t][ct]);
+          }
         }
       };
-      if (two)
-        mm(std::true_type{});
-      else
-        mm(std::false_type{});
+      with_count(ntl, mm);
     }
     __syncthreads();  // Zs reads done: the partials alias it
     LAYER_STAMP(3);
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int ct = 0; ct < CTP; ++ct)
 #pragma unroll
@@ -365,17 +386,19 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
     constexpr int KP = 4 / CT;             // waves per column tile, splitting j
     constexpr int JP = 16 / KP;
     const int ct = ch * CT + w % CT, kp = w / CT, j0 = kp * JP;
-    float dxr[2][JP];
+    float dxr[NT][JP];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int j = 0; j < JP; ++j) dxr[t][j] = sDx[(16 * t + lo) * 17 + j0 + j];
-    floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    // one copy of the K loop per row-tile count (a per-MFMA branch on `two` costs a branch per MFMA)
+    floatx4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // one copy of the K loop per row-tile count (a per-MFMA test of the count compiles to a branch per MFMA)
     // Per 16-deep c chunk: all JP W' operand loads are issued first (one L2 round trip per chunk), the next chunk's
     // while this one's MFMAs run; the j loop is fully unrolled so dX stays in statically indexed registers.
-    auto kloop = [&](auto two_c) __attribute__((always_inline)) {
-      constexpr bool TWO = decltype(two_c)::value;
+    auto kloop = [&](auto cnt_c) __attribute__((always_inline)) {
+      constexpr int CNT = decltype(cnt_c)::value;
       floatx4 wv[2][JP];
 #pragma unroll
       for (int j = 0; j < JP; ++j) wv[0][j] = W4[((ct * 16 + j0 + j) * NCC + 0) * 64 + lane];
@@ -384,27 +407,28 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         if (cc + 1 < NCC)
 #pragma unroll
           for (int j = 0; j < JP; ++j) wv[(cc + 1) & 1][j] = W4[((ct * 16 + j0 + j) * NCC + cc + 1) * 64 + lane];
-        const floatx4 p0 = prow(0, cc), p1 = TWO ? prow(1, cc) : floatx4{0.f, 0.f, 0.f, 0.f};
+        floatx4 pv[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) pv[t] = t < CNT ? prow(t, cc) : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < JP; ++j) {
-          const floatx4 a0 = p0 * dxr[0][j], a1 = p1 * dxr[1][j];
+          floatx4 av4[NT];
 #pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            acc[0] = mfma4(a0[s], wv[cc & 1][j][s], acc[0]);
-            if constexpr (TWO) acc[1] = mfma4(a1[s], wv[cc & 1][j][s], acc[1]);
-          }
+          for (int t = 0; t < NT; ++t) av4[t] = pv[t] * dxr[t][j];
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+              if (t < CNT) acc[t] = mfma4(av4[t][s], wv[cc & 1][j][s], acc[t]);
         }
       }
     };
-    if (two)
-      kloop(std::true_type{});
-    else
-      kloop(std::false_type{});
+    with_count(ntl, kloop);
     LAYER_STAMP(5);
     // bias term of this wave's j range; rows 16 t + 4 hi + r, channel m = 16 ct + lo
     const int m = 16 * ct + lo;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rl = 16 * t + 4 * hi + r, R = r0 + rl;
@@ -414,20 +438,19 @@ __global__ void __launch_bounds__(256, 2) k_layer(LayerArgs a) {
         acc[t][r] = fmaf(R < n ? qpre[t][r] : 0.f, sb, acc[t][r]);
       }
     if constexpr (KP > 1) {
-      red[(w * 2 + 0) * 64 + lane] = acc[0];
-      red[(w * 2 + 1) * 64 + lane] = acc[1];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) red[(w * NT + t) * 64 + lane] = acc[t];
       __syncthreads();
       if (kp == 0) {
 #pragma unroll
-        for (int p = 1; p < KP; ++p) {
-          acc[0] += red[((w + p * CT) * 2 + 0) * 64 + lane];
-          acc[1] += red[((w + p * CT) * 2 + 1) * 64 + lane];
-        }
+        for (int p = 1; p < KP; ++p)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t] += red[((w + p * CT) * NT + t) * 64 + lane];
       }
     }
     if (kp == 0) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int R = r0 + 16 * t + 4 * hi + r;
@@ -463,20 +486,47 @@ __global__ void k_permute_linear(int rows, int din, int cde, const float* __rest
 }
 
 template <int DIN>
-size_t layer_smem(int n, bool bf) {
+size_t layer_smem(int n, bool bf, int nt = kTiles) {
   constexpr int ZS = zs_stride<DIN>();
-  const int nk = bf ? (n + 31) & ~31 : (n + 15) & ~15;
-  return sizeof(float) * (4 * 2 * 64 * 4 + kRows * 17 + 12 + (size_t)(nk > 4 * kRows ? nk : 4 * kRows) * ZS + nk);
+  const int nk = bf ? (n + 31) & ~31 : (n + 15) & ~15, rows = 16 * nt;
+  return sizeof(float) * (4 * nt * 64 * 4 + rows * 17 + 12 + (size_t)(nk > 4 * rows ? nk : 4 * rows) * ZS + nk);
 }
 
-constexpr size_t kMaxSmem = 64 * 1024;  // the default dynamic-LDS limit of a launch
+constexpr size_t kMaxSmem = 64 * 1024;  // the default dynamic-LDS limit of a launch (NT = 2)
+constexpr int kWideTiles = 5;           // the CDE read-out's wide workgroups (one per CU)
+constexpr size_t kMaxWideSmem = 150 * 1024;
+
+// The fp32 CDE read-out takes kWideTiles tiles per workgroup when the batch still puts a workgroup on every CU (config
+// 3: 64 samples x 2 row groups x 2 channel groups = 256); GNCDE_READOUT_TILES=2 forces the two-tile launch (A/B).
+template <int DIN, int DOUT>
+bool readout_wide(int n, int B) {
+  const char* e = getenv("GNCDE_READOUT_TILES");  // read per launch: the parity test flips it in one process
+  const int forced = e ? atoi(e) : 0;
+  if (forced == kTiles) return false;
+  const int split = DOUT / 16 >= kSplit ? kSplit : 1;
+  const long wgs = (long)B * ((n + 16 * kWideTiles - 1) / (16 * kWideTiles)) * split;
+  if (layer_smem<DIN>(n, false, kWideTiles) > kMaxWideSmem) return false;
+  return forced == kWideTiles || wgs >= device_cu_count();
+}
 
 template <int DIN, int DOUT, int MODE, bool BF>
 void launch(const LayerArgs& a, int B, hipStream_t st) {
-  const size_t sm = layer_smem<DIN>(a.n, BF);
   const int split = (MODE == 2 && DOUT / 16 >= kSplit) ? kSplit : 1;
-  hipLaunchKernelGGL((k_layer<DIN, DOUT, MODE, BF>), dim3((a.n + kRows - 1) / kRows * split, B), dim3(256), sm, st,
-                     a);
+  if constexpr (MODE == 2 && !BF) {
+    if (readout_wide<DIN, DOUT>(a.n, B)) {
+      const size_t sm = layer_smem<DIN>(a.n, false, kWideTiles);
+      auto k = k_layer<DIN, DOUT, MODE, BF, kWideTiles>;
+      if (ensure_dyn_lds(reinterpret_cast<const void*>(k), sm)) {
+        const int rows = 16 * kWideTiles;
+        hipLaunchKernelGGL(k, dim3((a.n + rows - 1) / rows * split, B), dim3(256), sm, st, a);
+        return;
+      }
+    }
+  }
+  const size_t sm = layer_smem<DIN>(a.n, BF);
+  const int rows = 16 * kTiles;
+  hipLaunchKernelGGL((k_layer<DIN, DOUT, MODE, BF, kTiles>), dim3((a.n + rows - 1) / rows * split, B), dim3(256), sm,
+                     st, a);
 }
 
 template <int DIN, bool BF>

@@ -44,10 +44,10 @@ def G():
     return gncde
 
 
-def cde_inputs(seed, B, n, T, t1, H, de, L, kind="undirected", scale=1.0, distinct=None):
+def cde_inputs(seed, B, n, T, t1, H, de, L, kind="undirected", scale=1.0, distinct=None, dims=None):
     """numpy inputs of a CDE-wrapper problem (operator spline, data spline, parameters, y0).  ``distinct``: draw
     that many windows and cycle them over the batch (config 3's 49 England windows cycled to B = 64); every sample
-    keeps its own y0."""
+    keeps its own y0.  ``dims``: the layer widths (default [H] * L + [2 H de])."""
     rng = np.random.default_rng(seed)
     ts_all, co_all, dco = [], [], []
     for _ in range(distinct or B):
@@ -57,7 +57,7 @@ def cde_inputs(seed, B, n, T, t1, H, de, L, kind="undirected", scale=1.0, distin
         x = rng.standard_normal((T, n, de))
         Xd = np.stack([np.broadcast_to(ts[:, None, None], x.shape), x], axis=-1)
         dco.append(O.backward_hermite_coefficients(ts, Xd))
-    P = O.init_vf_params(rng, kind, [H] * L + [2 * H * de])
+    P = O.init_vf_params(rng, kind, dims or [H] * L + [2 * H * de])
     for lay in P.layers:
         for nm in OG.FUSION_NAMES[kind]:
             lay[nm] = lay[nm] * scale
@@ -243,6 +243,26 @@ def test_rows_pid_batch_independent(G):
     ospec = dataclasses.replace(spec, t0=spec.t0[47:48].contiguous(), t1=spec.t1[47:48].contiguous(),
                                 dt0=spec.dt0[47:48].contiguous())
     assert torch.equal(G.integrate(one, ospec, y0[47:48].contiguous()), ys[47:48])
+
+
+def test_rows_solve_granule_handoffs_bitwise(G, monkeypatch):
+    """The persistent solve's two hand-off variants — counter barriers (the default) and tagged granules
+    (GNCDE_SOLVE_GRANULES=1) — move the same values between the same arithmetic: bitwise the same outputs, stats and
+    accepted-step records at config 5's shape (B = 32, two workgroups per CU) under PID and on the reference's fixed
+    grid (100 x 0.01)."""
+    prob, y0, spec = _config5(G, 32, seed=57)
+    grid, ns = G.layout.stack_grids([O.constant_grid(0.0, 1.0, 0.01)] * prob.B)
+    fspec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=grid, nsteps=ns)
+    outs = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("GNCDE_SOLVE_GRANULES", v)
+        rec = torch.zeros(prob.B, 256, device="cuda")
+        ys, st = G.integrate(prob, dataclasses.replace(spec, step_ts=rec), y0, stats=True)
+        yf = G.integrate(prob, fspec, y0)
+        outs[v] = (ys, st, rec, yf)
+    assert torch.all(outs["0"][1][:, 3] == 0) and bool(torch.isfinite(outs["0"][0]).all())
+    for a, b in zip(outs["0"], outs["1"]):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("save", ["t1", "ts"])
@@ -447,6 +467,34 @@ def test_rows_grid_against_host_paced_and_oracle(G, method, save):
         e = rel_err(got, ref)
         print(f"  sample {b} ({len(grids[b]) - 1} steps) vs fp64 oracle {e:.2e}")
         assert e <= RTOL_SOLVE
+
+
+@pytest.mark.parametrize("B,n,dims", [(8, 129, [64, 64, 64, 1024]), (6, 77, [32, 16, 32, 512]),
+                                      (5, 40, [16, 32, 16, 256]), (3, 150, [32, 32, 64, 512])])
+def test_readout_tiles_bitwise(G, monkeypatch, B, n, dims):
+    """The CDE read-out k_layer with two and with five 16-row tiles per workgroup (GNCDE_READOUT_TILES; the default
+    takes five when the batch still gives every CU a workgroup, config 3) gives bitwise the same trajectory: every
+    row's P product and read-out accumulate in the same order, the tiles only share the workgroup's Z staging.
+    Ragged last groups (n = 129: five + four tiles, the last holding one row), mixed hidden widths (the generic
+    path), h = 16 / 32 / 64."""
+    H, de, L, T = dims[0], 8, len(dims) - 1, 4
+    rng, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(41, B, n, T, 1.0, H, de, L, distinct=3, dims=dims)
+    prob = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
+    grid, ns = G.layout.stack_grids([O.constant_grid(0.0, 0.3, 0.1)] * B)
+    spec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS, grid=grid, nsteps=ns)
+    assert G.integrate_path(prob, spec) == "generic"
+    yd = torch.tensor(y0, dtype=torch.float32, device="cuda")
+    outs = {}
+    for tiles in ("2", "5"):
+        monkeypatch.setenv("GNCDE_READOUT_TILES", tiles)
+        outs[tiles] = G.integrate(prob, spec, yd).clone()
+    assert bool(torch.isfinite(outs["2"]).all())
+    assert torch.equal(outs["5"], outs["2"])
+    if n <= 129:  # and both against the fp64 oracle on one sample
+        f, _ = oracle_fns(ts, coeffs, dco, P, H, de, B - 1)
+        traj, _ = O.solve_fixed_grid(f, O.constant_grid(0.0, 0.3, 0.1), y0[B - 1], "tsit5", save_every_step=True,
+                                     time_dtype=np.float32)
+        assert rel_err(outs["5"][B - 1].cpu().numpy(), traj) <= RTOL_SOLVE
 
 
 def test_bwd_row_blocks_per_workgroup_bitwise(G, monkeypatch):

@@ -645,6 +645,15 @@ def test_pid_solve_gradient_matches_oracle(G, case, save):
     worst = max(errs, key=errs.get)
     print(f"pid {case} save={save} [{path}]: steps {st[:, 0].tolist()} rejects {st[:, 1].tolist()}; worst {worst} "
           f"{errs[worst]:.2e}")
+    if errs[worst] > RTOL_GRAD:  # diagnostics: every error, and each fusion gradient's size against its layer's
+        print("   all:", {k: f"{e:.1e}" for k, e in errs.items()})
+        for l, lay in enumerate(P.layers):
+            scale = max(float(np.max(np.abs(total[l][nm]))) for nm in names)
+            for j, nm in enumerate(names):
+                ref = np.asarray(total[l][nm], np.float64)
+                print(f"   l{l}.{nm}: ref {np.array2string(ref, precision=3)} gpu "
+                      f"{np.array2string(np.asarray(gfus[l][j], np.float64), precision=3)} "
+                      f"|diff|/layer-scale {float(np.max(np.abs(gfus[l][j] - ref))) / scale:.1e}")
     for k, e in errs.items():
         assert e <= RTOL_GRAD, (k, e)
     if case == "rows":

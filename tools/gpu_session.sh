@@ -6,6 +6,8 @@
 #   bench  : python bench.py (default args)
 #   prof   : rocprofv3 --kernel-trace --stats on bench.py (summary into gpurun_out/prof)
 #   pmc    : rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes (separate runs)
+#   profdrv: rocprofv3 --kernel-trace --stats on the driver's exact bench command (--gpus 1 --steps 20 --warmup 5)
+#   pmccfg : SQ / TCC counter passes over tools/bench_configs.py for each config in $CFGS (tools/pmc_configs.sh)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
 ROOTDIR=$(pwd)
@@ -34,6 +36,12 @@ for step in "$@"; do
              python3 "$ROOTDIR/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --train-steps 0 > "$ROOTDIR/gpurun_out/prof.log" 2>&1; \
            rc=$?; echo "prof rc=$rc"; tail -n 5 "$ROOTDIR/gpurun_out/prof.log"; \
            case $rc in 124|134|137|139) exit $rc;; esac) || exit $? ;;
+    profdrv) (cd /tmp && run_dir="$ROOTDIR/gpurun_out/prof_driver" && rm -rf "$run_dir" && \
+           timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$run_dir" -o run -- \
+             python3 "$ROOTDIR/bench.py" --gpus 1 --steps 20 --warmup 5 > "$ROOTDIR/gpurun_out/prof_driver.log" 2>&1; \
+           rc=$?; echo "profdrv rc=$rc"; tail -n 3 "$ROOTDIR/gpurun_out/prof_driver.log"; \
+           case $rc in 124|134|137|139) exit $rc;; esac) || exit $? ;;
+    pmccfg) for c in ${CFGS:-3 5}; do CFGS=$c bash tools/pmc_configs.sh || exit $?; echo "pmccfg $c done"; done ;;
     pmc) for ctr in FETCH_SIZE WRITE_SIZE; do
            (cd /tmp && run_dir="$ROOTDIR/gpurun_out/pmc_$ctr" && rm -rf "$run_dir" && \
             timeout -k 10 900 rocprofv3 --pmc $ctr --output-format csv -d "$run_dir" -o run -- \
