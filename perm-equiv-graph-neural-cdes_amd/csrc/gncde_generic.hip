@@ -286,7 +286,44 @@ __global__ void __launch_bounds__(256) k_coef_sums(int n, int T, const CT* __res
   if (tid == 0) o[12 * n + q] = (wt[0] + wt[1]) + (wt[2] + wt[3]);
 }
 
-// grid (tile pairs I <= K of 32 x 32 tiles, B).  A block reads the coefficients of tile (I, K) and of its mirror
+// kComboU elements per thread (strided by the block), each element's stage-buffer loads issued together before the
+// summation: the load latency is paid once per thread, not once per term.  Same summation order per element.
+constexpr int kComboU = 4;
+constexpr int kComboThreads = 256;
+// block bx of sample b's combination (k_combo, or the combination blocks of a merged k_abar_direct launch)
+__device__ __forceinline__ void combo_block(size_t E, const float* __restrict__ y, const Combo& cb,
+                                            const float* __restrict__ hcur, float* __restrict__ out, int bx, int b) {
+  const size_t e0 = (size_t)bx * (kComboThreads * kComboU) + threadIdx.x;
+  if (cb.tst && e0 == 0) cb.tst[b] = cb.tend ? cb.tend[b] : stage_time(cb.tcur[b], cb.c, hcur[b]);
+  const float hb = hcur[b];
+  float kv[7][kComboU], yv[kComboU];
+#pragma unroll
+  for (int u = 0; u < kComboU; ++u) {
+    const size_t e = e0 + (size_t)u * kComboThreads, o = (size_t)b * E + e;
+    const bool in = e < E;
+    yv[u] = in ? y[o] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) kv[j][u] = (in && j < cb.nk) ? cb.K[j][o] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < kComboU; ++u) {
+    const size_t e = e0 + (size_t)u * kComboThreads;
+    if (e >= E) break;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+      if (j < cb.nk) s = fmaf(cb.a[j], kv[j][u], s);
+    const float v = fmaf(hb, s, yv[u]);
+    out[(size_t)b * E + e] = v;
+    if (cb.rec) cb.rec[(size_t)b * cb.rec_stride + e] = v;
+  }
+}
+__global__ void __launch_bounds__(kComboThreads) k_combo(int B, size_t E, const float* __restrict__ y, Combo cb,
+                                                         const float* __restrict__ hcur, float* __restrict__ out) {
+  combo_block(E, y, cb, hcur, out, blockIdx.x, blockIdx.y);
+}
+
+// grid (tile pairs I <= K of 32 x 32 tiles [+ a pending combination's blocks], B).  A block reads the coefficients of tile (I, K) and of its mirror
 // (K, I) once (the two tiles each need the other's transposed elements), evaluates A and dA/dt there, and writes
 // both tiles of every layer's (I + Abar_l); the node vectors of its two ranges are cubics of k_coef_sums' planes.
 // Diagonal blocks (I == K) also write q_l = (I + Abar_l) 1 for their rows, tg and the CDE data-spline derivative.
@@ -297,8 +334,12 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
                                                      const float* __restrict__ fus, OT* __restrict__ out,
                                                      size_t layer_stride, float* __restrict__ qrow,
                                                      float* __restrict__ tg, const float* __restrict__ data_coef,
-                                                     int de2, float* __restrict__ dx, int B) {
+                                                     int de2, float* __restrict__ dx, int B, PendingCombo pc) {
   const int b = blockIdx.y, nt = (n + 31) >> 5;
+  if ((int)blockIdx.x >= nt * (nt + 1) / 2) {  // the pending stage combination's blocks
+    combo_block(pc.E, pc.y, pc.cb, pc.hcur, pc.out, (int)blockIdx.x - nt * (nt + 1) / 2, b);
+    return;
+  }
   int I = 0, rem = blockIdx.x;
   while (rem >= nt - I) {
     rem -= nt - I;
@@ -308,7 +349,8 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
   const bool dg = I == K;
   const int i0 = I * 32, k0 = K * 32;
   const size_t nn = (size_t)n * n;
-  const float tb = t[b];
+  // merged launch: the stage time as the combination computes it (it writes tst in this same launch)
+  const float tb = pc.blocks ? (pc.cb.tend ? pc.cb.tend[b] : stage_time(pc.cb.tcur[b], pc.cb.c, pc.hcur[b])) : t[b];
   const float* tsb = ts + (size_t)b * T;
   const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;  // 32 x 8
   const int idx = interval_index_wave(tsb, T, tb);
@@ -525,51 +567,6 @@ __global__ void k_grid_step(int B, int G, int k, const float* __restrict__ grid,
   tst[b] = tcur[b];
 }
 
-// out = y + h_b * sum_j a_j K_j   (up to 7 terms; K_j == nullptr terms skipped), and (tst != nullptr) the next
-// stage's time t_b + c h_b (the stage-time launch folded in)
-struct Combo {
-  const float* K[7];
-  float a[7];
-  int nk;
-  float c;
-  const float* tcur;
-  const float* tend;  // non-null: the next stage is Tsit5's FSAL stage, evaluated at the step's end knot tend[b]
-  float* tst;
-  float* rec;         // stage record slot of this stage input ([B, G-1, S-1, E] at (k, i-1)) or nullptr
-  size_t rec_stride;  // floats between consecutive samples' slots: (G-1)*(S-1)*E
-};
-// kComboU elements per thread (strided by the block), each element's stage-buffer loads issued together before the
-// summation: the load latency is paid once per thread, not once per term.  Same summation order per element.
-constexpr int kComboU = 4;
-__global__ void __launch_bounds__(256) k_combo(int B, size_t E, const float* __restrict__ y, Combo cb,
-                                               const float* __restrict__ hcur, float* __restrict__ out) {
-  const int b = blockIdx.y;
-  const size_t e0 = (size_t)blockIdx.x * (blockDim.x * kComboU) + threadIdx.x;
-  if (cb.tst && e0 == 0) cb.tst[b] = cb.tend ? cb.tend[b] : stage_time(cb.tcur[b], cb.c, hcur[b]);
-  const float hb = hcur[b];
-  float kv[7][kComboU], yv[kComboU];
-#pragma unroll
-  for (int u = 0; u < kComboU; ++u) {
-    const size_t e = e0 + (size_t)u * blockDim.x, o = (size_t)b * E + e;
-    const bool in = e < E;
-    yv[u] = in ? y[o] : 0.f;
-#pragma unroll
-    for (int j = 0; j < 7; ++j) kv[j][u] = (in && j < cb.nk) ? cb.K[j][o] : 0.f;
-  }
-#pragma unroll
-  for (int u = 0; u < kComboU; ++u) {
-    const size_t e = e0 + (size_t)u * blockDim.x;
-    if (e >= E) break;
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < 7; ++j)
-      if (j < cb.nk) s = fmaf(cb.a[j], kv[j][u], s);
-    const float v = fmaf(hb, s, yv[u]);
-    out[(size_t)b * E + e] = v;
-    if (cb.rec) cb.rec[(size_t)b * cb.rec_stride + e] = v;
-  }
-}
-
 __global__ void k_save_step(int B, size_t E, int G, int k, const float* __restrict__ y,
                             float* __restrict__ ys) {
   const int b = blockIdx.y;
@@ -686,24 +683,26 @@ void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float*
 // The forward evaluation's forms: one k_abar_direct launch (every layer's (I + Abar_l), q_l, tg, dX) from the
 // coefficients and k_coef_sums' reductions.
 void vf_forms_direct(const GncdeProblem& p, const float* t, const float* csum, float* abar, float* qrow, float* tg,
-                     float* dx, hipStream_t st) {
+                     float* dx, hipStream_t st, const PendingCombo* pending) {
   const int B = p.B, n = p.n;
   const unsigned nt = cdiv(n, 32);
-  const dim3 grid(nt * (nt + 1) / 2, B);
+  PendingCombo pc{};
+  if (pending) pc = *pending;
+  const dim3 grid(nt * (nt + 1) / 2 + pc.blocks, B);
   float* dxo = p.cde_hidden > 0 ? dx : nullptr;
   const size_t ls = (size_t)B * n * n;
   const bool bf16 = p.compute != GNCDE_COMPUTE_FP32;
   if (coef_is_bf16(p))
     hipLaunchKernelGGL((k_abar_direct<uint16_t, uint16_t>), grid, dim3(256), 0, st, n, p.T, p.L, p.ts,
                        reinterpret_cast<const uint16_t*>(p.coef), csum, p.tcoef, t, p.fusion,
-                       reinterpret_cast<uint16_t*>(abar), ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B);
+                       reinterpret_cast<uint16_t*>(abar), ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B, pc);
   else if (bf16)
     hipLaunchKernelGGL((k_abar_direct<float, uint16_t>), grid, dim3(256), 0, st, n, p.T, p.L, p.ts, p.coef, csum,
                        p.tcoef, t, p.fusion, reinterpret_cast<uint16_t*>(abar), ls, qrow, tg, p.data_coef,
-                       2 * p.cde_embed, dxo, B);
+                       2 * p.cde_embed, dxo, B, pc);
   else
     hipLaunchKernelGGL((k_abar_direct<float, float>), grid, dim3(256), 0, st, n, p.T, p.L, p.ts, p.coef, csum,
-                       p.tcoef, t, p.fusion, abar, ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B);
+                       p.tcoef, t, p.fusion, abar, ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B, pc);
 }
 
 const float* generic_vf_csum(const GncdeProblem& p, char* ws) {
@@ -781,7 +780,8 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool ro
 }
 
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
-                    hipStream_t st, bool prepared, unsigned* bars, float* keep, bool need_dy) {
+                    hipStream_t st, bool prepared, unsigned* bars, float* keep, bool need_dy,
+                    const PendingCombo* pending) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
   VfWs w;
@@ -789,6 +789,9 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   unsigned local = 0;
   if (!prepared) generic_vf_prepare(p, ws, st);
   if (rows_eval_used(p)) {  // one launch: spline, fusion, every layer (and the read-out) (gncde_rows.hip)
+    if (pending)  // (no forms launch to fold the combination into)
+      hipLaunchKernelGGL(k_combo, dim3(pending->blocks, B), dim3(kComboThreads), 0, st, B, pending->E, pending->y,
+                         pending->cb, pending->hcur, pending->out);
     if (!bars) {
       if (prepared) return GNCDE_ERR_ARG;
       bars = &local;
@@ -797,7 +800,7 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     return rows_vf_eval(p, t, y, dy, w.csum, w.coefT, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync,
                         reinterpret_cast<int*>(w.sync + rows_fault_word(B)), *bars, st, keep);
   }
-  vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st);
+  vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st, pending);
   const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
   const float* Zin = y;
   float* bufs[2] = {w.Z0, w.Z1};
@@ -997,8 +1000,21 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     return s.act_rec && k < G - 1 ? s.act_rec + ((size_t)k * S + i) * slab : nullptr;
   };
   float* keep_next = nullptr;  // the keep slab of the next evaluation
+  // A combination whose output the next evaluation reads right away rides in that evaluation's forms launch
+  // (PendingCombo): one launch per stage fewer.  Anything else in between flushes it as its own k_combo.
+  PendingCombo pend{};
+  bool has_pend = false;
+  const char* nm = getenv("GNCDE_COMBO_SEPARATE");  // A/B: every combination as its own k_combo launch
+  const bool merge = !(nm && atoi(nm) != 0);
+  auto flush = [&]() {
+    if (has_pend)
+      hipLaunchKernelGGL(k_combo, gc, dim3(kComboThreads), 0, st, B, E, pend.y, pend.cb, pend.hcur, pend.out);
+    has_pend = false;
+  };
   auto eval = [&](const float* yin, float* out) {
-    return generic_vf_eval(p, tst, yin, out, ws, st, true, &bars, keep_next);
+    const PendingCombo* pc = has_pend ? &pend : nullptr;
+    has_pend = false;
+    return generic_vf_eval(p, tst, yin, out, ws, st, true, &bars, keep_next, true, pc);
   };
   // stage record (GncdeSolver.stage_rec): the stage input U_i of step k goes to slot (k, i-1) as it is formed
   float* rec = G >= 2 ? s.stage_rec : nullptr;
@@ -1020,7 +1036,13 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     cb.tcur = tcur;
     cb.tend = fsal_next ? tnx : nullptr;
     cb.tst = has_next ? tst : nullptr;
-    hipLaunchKernelGGL(k_combo, gc, dim3(256), 0, st, B, E, y, cb, hcur, out);
+    flush();
+    if (has_next && merge) {  // the next evaluation reads `out` (and its stage time) first: fold it into that launch
+      pend = PendingCombo{cb, y, hcur, out, E, gc.x};
+      has_pend = true;
+    } else {
+      hipLaunchKernelGGL(k_combo, gc, dim3(kComboThreads), 0, st, B, E, y, cb, hcur, out);
+    }
   };
 
   // Stage j's evaluation into K[j] followed by the next stage's input out = y + h sum_i a_i K_i (terms end with
@@ -1038,6 +1060,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   const int steps = G - 1;
   if (s.method == GNCDE_RK4) {
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
+      flush();
       hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst, tnx);
       rec_k = k;
       rec_i = 1;
@@ -1050,6 +1073,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
       rec_i = 0;
       // y + h/6 (k1 + 2k2 + 2k3 + k4)
       eval_combo(yt, 3, {{0, 1.0f / 6.0f}, {1, 2.0f / 6.0f}, {2, 2.0f / 6.0f}, {3, 1.0f / 6.0f}}, yt, 0.f, false);
+      flush();
       std::swap(y, yt);
       if (s.save_mode == GNCDE_SAVE_STEPS)
         hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, k + 1, y, ys);
@@ -1059,6 +1083,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     keep_next = act(0, 0);
     rc |= eval(y, K[0]);
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
+      flush();
       hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst, tnx);
       cur_k = k;
       rec_k = k;
@@ -1080,12 +1105,14 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
       fsal_next = false;
       keep_next = act(k + 1, 0);  // the FSAL evaluation is the next step's stage 0
       rc |= eval(yt, K[6]);
+      flush();
       std::swap(y, yt);
       std::swap(K[0], K[6]);
       if (s.save_mode == GNCDE_SAVE_STEPS)
         hipLaunchKernelGGL(k_save_step, ge, dim3(256), 0, st, B, E, G, k + 1, y, ys);
     }
   }
+  flush();
   if (s.save_mode == GNCDE_SAVE_T1)
     (void)hipMemcpyAsync(ys, y, B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
   if (stats)

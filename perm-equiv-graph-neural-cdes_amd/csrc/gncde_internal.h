@@ -245,9 +245,36 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool ro
 // only together with prepared = false (a standalone evaluation)
 // keep (optional, [L-1, B, n, d]): every hidden layer's output Z_{l+1} kept for the reverse mode (uniform width d);
 // need_dy = false (a reverse sweep's keep forward): dy is not wanted and the multi-kernel path skips the read-out
+// A Tsit5 / RK4 stage combination (k_combo, gncde_generic.hip):
+// out = y + h_b * sum_j a_j K_j   (up to 7 terms; K_j == nullptr terms skipped), and (tst != nullptr) the next
+// stage's time t_b + c h_b (the stage-time launch folded in)
+struct Combo {
+  const float* K[7];
+  float a[7];
+  int nk;
+  float c;
+  const float* tcur;
+  const float* tend;  // non-null: the next stage is Tsit5's FSAL stage, evaluated at the step's end knot tend[b]
+  float* tst;
+  float* rec;         // stage record slot of this stage input ([B, G-1, S-1, E] at (k, i-1)) or nullptr
+  size_t rec_stride;  // floats between consecutive samples' slots: (G-1)*(S-1)*E
+};
+// A stage combination folded into the next evaluation's k_abar_direct launch: its blocks follow the form tiles in
+// the grid (the two are independent: the forms read the coefficients at the stage's time, which they compute from
+// tcur / hcur / c / tend exactly as the combination does; the combination reads K and y), so the combination costs
+// no launch of its own and runs under the forms' memory round trips.
+struct PendingCombo {
+  Combo cb;
+  const float* y;
+  const float* hcur;
+  float* out;
+  size_t E;
+  unsigned blocks;  // combination blocks per sample (0: none)
+};
+// pending (optional): a stage combination folded into this evaluation's forms launch
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared = false, unsigned* bars = nullptr, float* keep = nullptr,
-                    bool need_dy = true);
+                    bool need_dy = true, const PendingCombo* pending = nullptr);
 // the workspace's fault word (a one-launch evaluation's barrier gave up): solver status 4 when set
 const int* generic_vf_fault(const GncdeProblem& p, char* ws);
 
