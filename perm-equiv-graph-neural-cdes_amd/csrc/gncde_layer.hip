@@ -36,6 +36,7 @@ typedef uint16_t u16x8u __attribute__((ext_vector_type(8), aligned(2)));  // 8 b
 
 constexpr int kTiles = 2;  // 16-row MFMA tiles per workgroup (hidden / ODE output layers; the CDE read-out picks 2 or 5)
 constexpr int kSplit = 2;  // CDE read-out: workgroups per row block (channel groups)
+constexpr int kDxS = 20;   // row stride of the read-out's dX rows in LDS: 16-byte rows, 16 rows on 16 distinct banks
 
 struct LayerArgs {
   int n;
@@ -93,8 +94,8 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
   const int n = a.n;
   const int nk = BF ? (n + 31) & ~31 : (n + 15) & ~15;  // K rows of Zs: whole MFMA K chunks
   floatx4* red = reinterpret_cast<floatx4*>(smem);  // [4][NT][64] K-part partials (MODE 2)
-  float* sDx = smem + 4 * NT * 64 * 4;              // [kRows][17] (MODE 2)
-  float* Zs = sDx + kRows * 17 + 12;                // [nk][ZS] (16-byte aligned: 1024 NT + 272 NT + 12 = 0 mod 4)
+  float* sDx = smem + 4 * NT * 64 * 4;              // [kRows][kDxS] (MODE 2)
+  float* Zs = sDx + kRows * kDxS;                   // [nk][ZS] (16-byte aligned)
   float* Ps = Zs;                                   // [KPP][32][ZS] after the product (max(nk, 128) rows reserved)
   float* sInv = Zs + (nk > 4 * kRows ? nk : 4 * kRows) * ZS;  // [nk] RMSNorm factors of the Z rows
   // MODE 2 splits the read-out's channels over kSplit workgroups per row block (each recomputes P: the product is
@@ -148,6 +149,28 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
       }
     }
   };
+  // NT > 2 (one workgroup per CU): the Z rows and the tiles' dX rows are loaded into registers FIRST and the
+  // (I + Abar) rows after them, so the wait for Z (loads complete in issue order) does not include the 5-tile
+  // (I + Abar) round, which lands while Z is stored, normed and the barriers pass
+  constexpr int G4Z = DIN / 4, UZ = 12, UD = (kRows * 16 + 255) / 256;
+  const bool zfirst = NT > 2 && nk * G4Z <= 256 * UZ;
+  floatx4 zpre[NT > 2 ? UZ : 1];
+  float dxpre[NT > 2 ? UD : 1];
+  if constexpr (NT > 2) {
+    if (zfirst) {
+      const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.Z + nb * DIN);
+#pragma unroll
+      for (int u = 0; u < UZ; ++u) {
+        const int e = tid + 256 * u;
+        zpre[u] = e < n * G4Z ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < UD; ++u) {
+        const int e = tid + 256 * u, row = e >> 4, R = r0 + row;
+        dxpre[u] = e < kRows * 16 && R < n ? a.dx[(nb + R) * 16 + (e & 15)] : 0.f;
+      }
+    }
+  }
   if constexpr (!BF) load_round(w);
   // The epilogue's operands (W' B operands of the wave's output tiles, b', q, tg of its rows) do not depend on the
   // product either: issued here, so the tail after the last barrier is MFMA + stores, not two more L2 round trips.
@@ -189,7 +212,19 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
     constexpr int U = 8;
     const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.Z + nb * DIN);
     const int tot = nk * G, valid = n * G;
-    for (int e0 = tid; e0 < tot; e0 += 256 * U) {
+    if (zfirst) {  // (NT > 2) stores of the registers loaded first
+#pragma unroll
+      for (int u = 0; u < (NT > 2 ? UZ : 1); ++u) {
+        const int e = tid + 256 * u;
+        if (e < tot) *reinterpret_cast<floatx4*>(Zs + (e / G) * ZS + 4 * (e % G)) = zpre[u];
+      }
+#pragma unroll
+      for (int u = 0; u < (NT > 2 ? UD : 1); ++u) {
+        const int e = tid + 256 * u;
+        if (e < kRows * 16) sDx[(e >> 4) * kDxS + (e & 15)] = dxpre[u];
+      }
+    }
+    for (int e0 = zfirst ? tot : tid; e0 < tot; e0 += 256 * U) {
       floatx4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -202,10 +237,10 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
         if (e < tot) *reinterpret_cast<floatx4*>(Zs + (e / G) * ZS + 4 * (e % G)) = v[u];
       }
     }
-    if (MODE == 2)
+    if (MODE == 2 && !zfirst)
       for (int e = tid; e < kRows * 16; e += 256) {
         const int row = e >> 4, j = e & 15, R = r0 + row;
-        sDx[row * 17 + j] = R < n ? a.dx[(nb + R) * 16 + j] : 0.f;
+        sDx[row * kDxS + j] = R < n ? a.dx[(nb + R) * 16 + j] : 0.f;
       }
     __syncthreads();
     LAYER_STAMP(1);
@@ -390,13 +425,15 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int j = 0; j < JP; ++j) dxr[t][j] = sDx[(16 * t + lo) * 17 + j0 + j];
+      for (int j = 0; j < JP; ++j) dxr[t][j] = sDx[(16 * t + lo) * kDxS + j0 + j];
     floatx4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
     // one copy of the K loop per row-tile count (a per-MFMA test of the count compiles to a branch per MFMA)
     // Per 16-deep c chunk: all JP W' operand loads are issued first (one L2 round trip per chunk), the next chunk's
     // while this one's MFMAs run; the j loop is fully unrolled so dX stays in statically indexed registers.
+    const int m = 16 * ct + lo;  // this lane's output channel
+    float bfr[JP];                 // b'[16 m + j0 + j]: loaded under the last c chunk's MFMAs (its W' slot is free)
     auto kloop = [&](auto cnt_c) __attribute__((always_inline)) {
       constexpr int CNT = decltype(cnt_c)::value;
       floatx4 wv[2][JP];
@@ -404,37 +441,61 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
       for (int j = 0; j < JP; ++j) wv[0][j] = W4[((ct * 16 + j0 + j) * NCC + 0) * 64 + lane];
 #pragma unroll
       for (int cc = 0; cc < NCC; ++cc) {
-        if (cc + 1 < NCC)
+        if (cc + 1 < NCC) {
 #pragma unroll
           for (int j = 0; j < JP; ++j) wv[(cc + 1) & 1][j] = W4[((ct * 16 + j0 + j) * NCC + cc + 1) * 64 + lane];
+        } else {
+#pragma unroll
+          for (int j = 0; j < JP; ++j) bfr[j] = a.bf[16 * m + j0 + j];
+        }
         floatx4 pv[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) pv[t] = t < CNT ? prow(t, cc) : floatx4{0.f, 0.f, 0.f, 0.f};
+        // A operands P[., c] dX[., j]: CNT > 2 (one wave per SIMD, no other wave to cover a VALU -> MFMA operand
+        // wait) forms those of step j + 1 between the MFMA groups of step j, a whole step ahead of their use
+        floatx4 av4[NT], nx4[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) av4[t] = pv[t] * dxr[t][0];
 #pragma unroll
         for (int j = 0; j < JP; ++j) {
-          floatx4 av4[NT];
 #pragma unroll
-          for (int t = 0; t < NT; ++t) av4[t] = pv[t] * dxr[t][j];
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
+          for (int s = 0; s < 4; ++s) {
 #pragma unroll
             for (int t = 0; t < NT; ++t)
               if (t < CNT) acc[t] = mfma4(av4[t][s], wv[cc & 1][j][s], acc[t]);
+            if constexpr (CNT > 2) {
+              if (j + 1 < JP)
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+                  if (t % 4 == s) nx4[t] = pv[t] * dxr[t][j + 1];
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+          if (j + 1 < JP) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) av4[t] = CNT > 2 ? nx4[t] : pv[t] * dxr[t][j + 1];
+          }
         }
       }
     };
     with_count(ntl, kloop);
     LAYER_STAMP(5);
-    // bias term of this wave's j range; rows 16 t + 4 hi + r, channel m = 16 ct + lo
-    const int m = 16 * ct + lo;
+    // bias term of this wave's j range; rows 16 t + 4 hi + r, channel m
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rl = 16 * t + 4 * hi + r, R = r0 + rl;
+        float dxv[JP];  // dX[row, j0 .. j0 + JP): JP / 4 aligned 16-byte reads (broadcast over the 16 lanes of a row)
+#pragma unroll
+        for (int q = 0; q < JP / 4; ++q) {
+          const floatx4 v = *reinterpret_cast<const floatx4*>(sDx + rl * kDxS + j0 + 4 * q);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dxv[4 * q + e] = v[e];
+        }
         float sb = 0.f;
 #pragma unroll
-        for (int j = 0; j < JP; ++j) sb = fmaf(a.bf[16 * m + j0 + j], sDx[rl * 17 + j0 + j], sb);
+        for (int j = 0; j < JP; ++j) sb = fmaf(bfr[j], dxv[j], sb);
         acc[t][r] = fmaf(R < n ? qpre[t][r] : 0.f, sb, acc[t][r]);
       }
     if constexpr (KP > 1) {
@@ -489,7 +550,7 @@ template <int DIN>
 size_t layer_smem(int n, bool bf, int nt = kTiles) {
   constexpr int ZS = zs_stride<DIN>();
   const int nk = bf ? (n + 31) & ~31 : (n + 15) & ~15, rows = 16 * nt;
-  return sizeof(float) * (4 * nt * 64 * 4 + rows * 17 + 12 + (size_t)(nk > 4 * rows ? nk : 4 * rows) * ZS + nk);
+  return sizeof(float) * (4 * nt * 64 * 4 + rows * kDxS + (size_t)(nk > 4 * rows ? nk : 4 * rows) * ZS + nk);
 }
 
 constexpr size_t kMaxSmem = 64 * 1024;  // the default dynamic-LDS limit of a launch (NT = 2)

@@ -1,9 +1,14 @@
 #!/bin/bash
 # Round 5 final evidence, part 2 (GPU box): SQ / TCC counter passes over configs 3 and 5 (tools/pmc_configs.sh), the
-# kernel statistics of both, their timings (B = 16 and 64 for config 5) and the training-step gradients.
+# kernel statistics of both, their timings (B = 16 and 64 for config 5), the training-step gradients, and the
+# persistent solve's phase stamps at B = 16 and 32 (stamps build in build_alt/).
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+for B in 16 32; do
+  DIAG_SOLVE=1 DIAG_B=$B GNCDE_LIB=$PWD/build_alt/libgncde_hip.so timeout -k 10 200 python tools/diag_rows_stamps.py > gpurun_out/k_solve_stamps_b$B.txt 2>&1 || exit $?
+  echo "== solve stamps B=$B"; grep -v Warning gpurun_out/k_solve_stamps_b$B.txt | tail -22
+done
 CFGS="3 5" bash tools/gpu_session.sh pmccfg || exit $?
 CFGS=3,5 bash tools/gpu_session.sh profcfg || exit $?
 timeout -k 10 300 python tools/bench_configs.py --configs 3,5 > gpurun_out/k_configs.jsonl 2>&1 || exit $?
