@@ -287,8 +287,10 @@ inline bool coef_is_bf16(const GncdeProblem& p) {
 // The one-launch evaluation's synchronisation words: one 128-byte line per group's arrival counter (the groups'
 // atomics and polls never share a line), then the fault word and the start-order ticket.
 constexpr int kBarStride = 32;
-inline size_t rows_sync_words(int B) { return (size_t)B * kBarStride + 64; }
-inline size_t rows_fault_word(int B) { return (size_t)B * kBarStride; }
+// [B] arrival counter lines, [B] group mailbox lines (the persistent solve's sample queue), then the fault word, the
+// ticket counter and the sample queue counter
+inline size_t rows_sync_words(int B) { return (size_t)2 * B * kBarStride + 64; }
+inline size_t rows_fault_word(int B) { return (size_t)2 * B * kBarStride; }
 int rows_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, const float* csum, const void* coefT,
                  const float* wperm, const uint16_t* wbf, const float* bf, float* z0, float* z1, unsigned* bar, int* fault,
                  unsigned& bars_done, hipStream_t st, float* keep = nullptr);

@@ -104,6 +104,9 @@ struct RowsArgs {
   unsigned* ticket;        // solve: start-order tickets -> (sample, row block)
   unsigned ticket0;        // tickets taken before this launch
   int b0;                  // solve: the first sample of this launch (the batch runs in resident chunks)
+  unsigned* queue;         // solve: samples handed out past the resident groups' first ones (zeroed per solve)
+  unsigned* mail;          // solve: [G][kBarStride] each group's latest sample assignment (zeroed per solve)
+  int G_all;               // solve: groups of this launch (each starts on sample b0 + its slot)
   SolveArgs s;             // solve only
 };
 
@@ -223,7 +226,8 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     g = blockIdx.x / nb;
     rb = blockIdx.x % nb;
   }
-  if constexpr (SOLVE != 0) g += a.b0;  // the solve's groups are samples b0 .. b0 + G - 1 of the batch
+  const int gslot = g;  // the group's slot in this launch
+  if constexpr (SOLVE != 0) g += a.b0;  // the solve's groups start on samples b0 .. b0 + G - 1 of the batch
   const int r0 = rb * kRB;
   const size_t nn = (size_t)n * n;
   const size_t zgroup = (size_t)n * H;
@@ -347,7 +351,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
   };
 
   // the solve's knots, one per lane (T <= 64)
-  const float ts_lane = SOLVE != 0 && (int)(threadIdx.x & 63) < T ? a.ts[(size_t)g * T + (threadIdx.x & 63)] : 0.f;
+  float ts_lane = SOLVE != 0 && (int)(threadIdx.x & 63) < T ? a.ts[(size_t)g * T + (threadIdx.x & 63)] : 0.f;
 
   // ---- one vector-field evaluation of sample b at time tb ----------------------------------------------------
   // Layer 0 reads the stage input z0: with plain loads (written before this launch), or, with `handoff`, as a
@@ -879,7 +883,11 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
   } else {
     // ---- the persistent Tsit5 + PIDController solve of sample g (gncde_pid.hip's k_pid_advance state machine,
     // graph_neural_cde.py:94-104 semantics): every workgroup of the group runs the controller redundantly on
-    // identical inputs (the group sums are added in row-block order by everyone), so all take the same decisions
+    // identical inputs (the group sums are added in row-block order by everyone), so all take the same decisions.
+    // A batch larger than the resident groups runs as ONE launch: a group that finishes its sample takes the next
+    // one from a queue (its first workgroup draws it, the others read the group's mailbox), so the batch's cost is
+    // its total work over the groups, not the sum of per-chunk maxima (the slowest sample of every chunk).
+    for (unsigned asg = 1;; ++asg) {
     const SolveArgs& s = a.s;
     const int b = g;
     const int tid = threadIdx.x;
@@ -1289,6 +1297,43 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       o[GNCDE_STAT_EVALS] = evals;
       o[GNCDE_STAT_STATUS] = bad ? 4 : status;
     }
+    if (!a.queue || a.B <= a.b0 + a.G_all) break;  // no queue: every sample started on a group of its own
+    // the next sample: workgroup 0 of the group draws it and posts (assignment << 20 | sample) to the group's
+    // mailbox; every workgroup polls the mailbox until it holds this assignment (a bounded wait, like wait_all)
+    if (threadIdx.x == 0) {
+      unsigned* mb = a.mail + (size_t)gslot * kBarStride;
+      if (rb == 0) {
+        const unsigned q = __hip_atomic_fetch_add(a.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned nx = (unsigned)(a.b0 + a.G_all) + q;
+        const bool stop = fault || __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        __hip_atomic_store(mb, (asg << 20) | (!stop && nx < (unsigned)a.B ? nx : (unsigned)a.B), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      unsigned v, spins = 0;
+      int next = a.B;
+      while (((v = __hip_atomic_load(mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 20) != (asg & 0xFFFu)) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > a.spin_limit ||
+            ((spins & 1023u) == 0 && __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          __hip_atomic_store(a.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v = (asg << 20) | (unsigned)a.B;  // give up: no further sample
+          break;
+        }
+      }
+      next = (int)(v & 0xFFFFFu);
+      sFlag[1] = fault ? a.B : next;
+    }
+    __syncthreads();
+    const int nx = sFlag[1];
+    __syncthreads();  // sFlag is reused by the next sample's barriers
+    if (nx >= a.B) break;
+    // the group's state for sample nx: its counter line and hand-off buffers start from zero, its knots in registers
+    g = nx;
+    epoch = a.bar0;
+    pub = 0;
+    hseq = 0;
+    ts_lane = (int)(threadIdx.x & 63) < T ? a.ts[(size_t)g * T + (threadIdx.x & 63)] : 0.f;
+    }
   }
 }
 
@@ -1594,6 +1639,8 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   a.bar = sync;  // per-sample arrivals, one line each (zeroed by generic_vf_prepare)
   a.fault = reinterpret_cast<int*>(sync + rows_fault_word(p.B));  // the workspace's fault word
   a.ticket = sync + rows_fault_word(p.B) + 1;
+  a.queue = sync + rows_fault_word(p.B) + 2;
+  a.mail = sync + (size_t)p.B * kBarStride;
   a.ticket0 = 0;
   a.bar0 = 0;
   a.spin_limit = spin_limit();
@@ -1623,26 +1670,44 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   v.step_ts = s.step_ts;
   v.stats = stats;
   v.part = part;
-  // The batch runs in chunks of co-resident groups, one launch each, at most solve_wgs_per_cu() (2) workgroups per
-  // CU.  A launch past residency starts later groups only as earlier solves finish (config 5 at B = 64: 53.5 ms).
-  // Two workgroups per CU used to make every phase 2-3x longer (93 us per iteration at B = 32 against 29.6 us at
-  // B = 16, profiles/r04_config5_solve_stamps*.txt): the groups' arrival counters shared one cache line, so every
-  // group's atomics and polls queued on it; with one line per counter (kBarStride) config 5 takes 7.7 ms at B = 32
-  // in one launch against 12.4 ms as two B = 16 launches (profiles/r05_config5_batch.txt).  A chunk of a multiple
-  // of 8 samples takes the XCD-affine layout (G = its sample count); otherwise its workgroups take start-order
-  // tickets.
+  // The solve places at most solve_wgs_per_cu() (2) workgroups per CU: cap co-resident groups.  (Round 4: two per CU
+  // made every phase 2-3x longer, 93 us per iteration at B = 32 against 29.6 us at B = 16,
+  // profiles/r04_config5_solve_stamps*.txt: the groups' arrival counters shared one cache line, so every group's
+  // atomics and polls queued on it; with one line per counter (kBarStride) B = 32 takes 7.7 ms in one launch against
+  // 12.4 ms as two B = 16 launches, profiles/r05_config5_batch.jsonl, and an iteration 35 us,
+  // profiles/r05_config5_solve_stamps_b32.txt.)  A batch past cap runs in the same single launch: each group takes
+  // its next sample from the queue when it finishes one (round 5; before, one launch per chunk of cap samples, whose
+  // time is the slowest sample of each chunk).  A launch of a multiple of 8 groups takes the XCD-affine layout;
+  // otherwise its workgroups take start-order tickets.
   const int cap = std::min(resident_blocks(k, smem), solve_wgs_per_cu() * cu_count()) / nb;
   if (cap < 1) return GNCDE_ERR_UNSUPPORTED;  // no co-resident group (or the device query failed): never loop
   int bc = p.B < cap ? p.B : cap;
   if (bc >= 8) bc &= ~7;
-  unsigned tickets = 0;
-  for (int c0 = 0; c0 < p.B; c0 += bc) {
-    const int nbc = p.B - c0 < bc ? p.B - c0 : bc;
-    a.b0 = c0;
-    a.G = nbc % 8 == 0 ? nbc : 0;
-    a.ticket0 = tickets;
-    if (a.G == 0) tickets += (unsigned)(nbc * nb);
-    k.launch(a, nbc * nb, smem, st);
+  // The queue pays where samples differ in cost — the adaptive controller's step counts (config 5 B = 64: 17.76 ->
+  // 16.37 ms, B = 48: 14.07 -> 13.66 ms, alternating on one box).  A fixed grid gives every sample the same work,
+  // and there the chunked launches win when the last chunk is small (B = 48, 100 Tsit5 steps: 40.1 vs 43.2 ms —
+  // its 16 samples run one workgroup per CU, while the queue leaves them on CUs still shared two ways): fixed
+  // grids keep the chunks.  GNCDE_SOLVE_CHUNKED=1 / 0 forces either (A/B, tests).
+  const char* ce = getenv("GNCDE_SOLVE_CHUNKED");
+  const bool chunked = ce ? atoi(ce) != 0 : s.controller != GNCDE_CTRL_PID;
+  if (chunked) {
+    a.queue = nullptr;
+    unsigned tickets = 0;
+    for (int c0 = 0; c0 < p.B; c0 += bc) {
+      const int nbc = p.B - c0 < bc ? p.B - c0 : bc;
+      a.b0 = c0;
+      a.G = nbc % 8 == 0 ? nbc : 0;
+      a.G_all = nbc;
+      a.ticket0 = tickets;
+      if (a.G == 0) tickets += (unsigned)(nbc * nb);
+      k.launch(a, nbc * nb, smem, st);
+    }
+  } else {  // one launch: bc resident groups, the rest of the batch from the sample queue
+    a.b0 = 0;
+    a.G = bc % 8 == 0 ? bc : 0;
+    a.G_all = bc;
+    a.ticket0 = 0;
+    k.launch(a, bc * nb, smem, st);
   }
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }

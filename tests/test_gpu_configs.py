@@ -245,6 +245,25 @@ def test_rows_pid_batch_independent(G):
     assert torch.equal(G.integrate(one, ospec, y0[47:48].contiguous()), ys[47:48])
 
 
+def test_rows_solve_sample_queue_bitwise(G, monkeypatch):
+    """A batch past the resident groups (config 5's shape, B = 40: 32 groups at two workgroups per CU) runs as one
+    launch whose groups take their next sample from a queue: outputs, stats and accepted-step records bitwise equal
+    to the chunked launches (GNCDE_SOLVE_CHUNKED=1: 32 + 8 samples), PID and the fixed grid."""
+    prob, y0, spec = _config5(G, 40, seed=59)
+    grid, ns = G.layout.stack_grids([O.constant_grid(0.0, 1.0, 0.05)] * prob.B)
+    fspec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS, grid=grid, nsteps=ns)
+    outs = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("GNCDE_SOLVE_CHUNKED", v)
+        rec = torch.zeros(prob.B, 256, device="cuda")
+        ys, st = G.integrate(prob, dataclasses.replace(spec, step_ts=rec), y0, stats=True)
+        yf, sf = G.integrate(prob, fspec, y0, stats=True)
+        outs[v] = (ys, st, rec, yf, sf)
+    assert torch.all(outs["0"][1][:, 3] == 0) and torch.all(outs["0"][4][:, 3] == 0)
+    for a, b in zip(outs["0"], outs["1"]):
+        assert torch.equal(a, b)
+
+
 def test_rows_solve_granule_handoffs_bitwise(G, monkeypatch):
     """The persistent solve's two hand-off variants — counter barriers (the default) and tagged granules
     (GNCDE_SOLVE_GRANULES=1) — move the same values between the same arithmetic: bitwise the same outputs, stats and
