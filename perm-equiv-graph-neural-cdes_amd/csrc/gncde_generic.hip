@@ -9,6 +9,8 @@
 // (perm_equiv_graph_vector_field.py:122-128), CDE wrapper (cde_wrapper_vector_field.py:19-26).
 #include "gncde_internal.h"
 
+#include <vector>
+
 #include <utility>
 
 namespace gncde {
@@ -334,7 +336,8 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
                                                      const float* __restrict__ fus, OT* __restrict__ out,
                                                      size_t layer_stride, float* __restrict__ qrow,
                                                      float* __restrict__ tg, const float* __restrict__ data_coef,
-                                                     int de2, float* __restrict__ dx, int B, PendingCombo pc) {
+                                                     int de2, float* __restrict__ dx, int B, PendingCombo pc,
+                                                     GridTime gt) {
   const int b = blockIdx.y, nt = (n + 31) >> 5;
   if ((int)blockIdx.x >= nt * (nt + 1) / 2) {  // the pending stage combination's blocks
     combo_block(pc.E, pc.y, pc.cb, pc.hcur, pc.out, (int)blockIdx.x - nt * (nt + 1) / 2, b);
@@ -350,7 +353,17 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
   const int i0 = I * 32, k0 = K * 32;
   const size_t nn = (size_t)n * n;
   // merged launch: the stage time as the combination computes it (it writes tst in this same launch)
-  const float tb = pc.blocks ? (pc.cb.tend ? pc.cb.tend[b] : stage_time(pc.cb.tcur[b], pc.cb.c, pc.hcur[b])) : t[b];
+  float tb;
+  if (gt.grid) {  // the stage time from the grid (overlapped forms: no combination has written tst yet)
+    const float* g = gt.grid + (size_t)b * gt.G;
+    int ns = gt.nsteps[b];
+    ns = ns < 0 ? 0 : (ns > gt.G - 1 ? gt.G - 1 : ns);
+    const float tc = gt.k < ns ? g[gt.k] : g[ns];
+    const float hc = gt.k < ns ? g[gt.k + 1] - g[gt.k] : 0.f;
+    tb = gt.fsal ? (gt.k < ns ? g[gt.k + 1] : g[ns]) : stage_time(tc, gt.c, hc);
+  } else {
+    tb = pc.blocks ? (pc.cb.tend ? pc.cb.tend[b] : stage_time(pc.cb.tcur[b], pc.cb.c, pc.hcur[b])) : t[b];
+  }
   const float* tsb = ts + (size_t)b * T;
   const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;  // 32 x 8
   const int idx = interval_index_wave(tsb, T, tb);
@@ -683,11 +696,13 @@ void vf_forms(const GncdeProblem& p, const float* t, float* A, float* dA, float*
 // The forward evaluation's forms: one k_abar_direct launch (every layer's (I + Abar_l), q_l, tg, dX) from the
 // coefficients and k_coef_sums' reductions.
 void vf_forms_direct(const GncdeProblem& p, const float* t, const float* csum, float* abar, float* qrow, float* tg,
-                     float* dx, hipStream_t st, const PendingCombo* pending) {
+                     float* dx, hipStream_t st, const PendingCombo* pending, const GridTime* gtime = nullptr) {
   const int B = p.B, n = p.n;
   const unsigned nt = cdiv(n, 32);
   PendingCombo pc{};
   if (pending) pc = *pending;
+  GridTime gt{};
+  if (gtime) gt = *gtime;
   const dim3 grid(nt * (nt + 1) / 2 + pc.blocks, B);
   float* dxo = p.cde_hidden > 0 ? dx : nullptr;
   const size_t ls = (size_t)B * n * n;
@@ -695,14 +710,14 @@ void vf_forms_direct(const GncdeProblem& p, const float* t, const float* csum, f
   if (coef_is_bf16(p))
     hipLaunchKernelGGL((k_abar_direct<uint16_t, uint16_t>), grid, dim3(256), 0, st, n, p.T, p.L, p.ts,
                        reinterpret_cast<const uint16_t*>(p.coef), csum, p.tcoef, t, p.fusion,
-                       reinterpret_cast<uint16_t*>(abar), ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B, pc);
+                       reinterpret_cast<uint16_t*>(abar), ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B, pc, gt);
   else if (bf16)
     hipLaunchKernelGGL((k_abar_direct<float, uint16_t>), grid, dim3(256), 0, st, n, p.T, p.L, p.ts, p.coef, csum,
                        p.tcoef, t, p.fusion, reinterpret_cast<uint16_t*>(abar), ls, qrow, tg, p.data_coef,
-                       2 * p.cde_embed, dxo, B, pc);
+                       2 * p.cde_embed, dxo, B, pc, gt);
   else
     hipLaunchKernelGGL((k_abar_direct<float, float>), grid, dim3(256), 0, st, n, p.T, p.L, p.ts, p.coef, csum,
-                       p.tcoef, t, p.fusion, abar, ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B, pc);
+                       p.tcoef, t, p.fusion, abar, ls, qrow, tg, p.data_coef, 2 * p.cde_embed, dxo, B, pc, gt);
 }
 
 const float* generic_vf_csum(const GncdeProblem& p, char* ws) {
@@ -781,7 +796,7 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool ro
 
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared, unsigned* bars, float* keep, bool need_dy,
-                    const PendingCombo* pending) {
+                    const PendingCombo* pending, const FormBufs* forms) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
   VfWs w;
@@ -800,7 +815,14 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     return rows_vf_eval(p, t, y, dy, w.csum, w.coefT, w.wp, w.wbf, w.bf, w.Z0, w.Z1, w.sync,
                         reinterpret_cast<int*>(w.sync + rows_fault_word(B)), *bars, st, keep);
   }
-  vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st, pending);
+  if (forms) {  // the caller launched this evaluation's forms into its own buffers
+    w.abar = forms->abar;
+    w.q = forms->q;
+    w.tg = forms->tg;
+    w.dx = forms->dx;
+  } else {
+    vf_forms_direct(p, t, w.csum, w.abar, w.q, w.tg, w.dx, st, pending);
+  }
   const bool fused_out = p.cde_hidden == 0 || (p.cde_embed == 8 && p.dims[p.L] == 16 * p.cde_hidden);
   const float* Zin = y;
   float* bufs[2] = {w.Z0, w.Z1};
@@ -947,12 +969,56 @@ int generic_rows_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y
   return rows_fault_status(p, ws, st, true);
 }
 
+// The fixed-grid solve's forms (k_abar_direct) do not depend on the stage input, only on the stage time, which the
+// grid fixes: with GNCDE_FORMS_OVERLAP=1 they run one evaluation ahead on a side stream, into a second set of form
+// buffers, while the caller's stream runs the previous evaluation's layers and the stage combination.  Measured at
+// config 3 (alternating, one box): 13.2 ms per solve against 11.94 ms in line — the two cross-stream event waits
+// per evaluation cost more than the 14.7 us forms launch they hide — so it is off by default (bitwise the same
+// results either way: tests/test_gpu_configs.py::test_forms_overlap_bitwise).
+bool forms_overlap(const GncdeProblem& p) {
+  if (rows_eval_used(p)) return false;  // (the one-launch evaluation forms inside its own launch)
+  const char* e = getenv("GNCDE_FORMS_OVERLAP");
+  return e && atoi(e) != 0;
+}
+
+size_t form_set_floats(const GncdeProblem& p, int part) {  // abar, q, tg, dx of one form buffer set
+  const size_t B = p.B, n = p.n;
+  switch (part) {
+    case 0: return (size_t)p.L * B * n * n;
+    case 1: return (size_t)p.L * B * n;
+    case 2: return B * n;
+    default: return B * n * (size_t)(p.cde_hidden > 0 ? 2 * p.cde_embed : 1);
+  }
+}
+
+// per (host thread, device): the side stream of the overlapped forms and its events (created once)
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t ev[6] = {};
+  bool ok = false;
+};
+SideStream* side_stream() {
+  static thread_local SideStream cache[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  SideStream& c = cache[dev];
+  if (!c.ok) {
+    if (hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    for (auto& e : c.ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    c.ok = true;
+  }
+  return &c;
+}
+
 size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s) {
   if (s.controller == GNCDE_CTRL_PID) return generic_pid_workspace(p);
   const size_t B = p.B, E = (size_t)p.n * state_dim(p);
   size_t sz = generic_vf_workspace(p);
   sz += 9 * align_up(B * E * 4, 256);  // y, ytmp, K[7]
   sz += 4 * align_up(B * 4, 256);      // tcur, hcur, tstage, tnx
+  if (forms_overlap(p))
+    for (int q = 0; q < 4; ++q) sz += align_up(form_set_floats(p, q) * 4, 256);  // the second form buffer set
   return sz;
 }
 
@@ -982,6 +1048,40 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   float* tst = take(B);
   float* tnx = take(B);
   const int G = s.grid_len;
+  // overlapped forms: buffer set e % 2 holds evaluation e's forms; the plan lists every evaluation's stage time
+  const bool ovl = forms_overlap(p);
+  SideStream* side = ovl ? side_stream() : nullptr;
+  if (ovl && !side) return GNCDE_ERR_HIP;
+  FormBufs fbs[2];
+  std::vector<GridTime> plan;
+  if (ovl) {
+    VfWs w0;
+    carve_vf(p, ws, w0);
+    fbs[0] = FormBufs{w0.abar, w0.q, w0.tg, w0.dx};
+    fbs[1].abar = take(form_set_floats(p, 0));
+    fbs[1].q = take(form_set_floats(p, 1));
+    fbs[1].tg = take(form_set_floats(p, 2));
+    fbs[1].dx = take(form_set_floats(p, 3));
+    auto add = [&](int k, float c, int fsal) { plan.push_back(GridTime{s.grid, s.nsteps, G, k, c, fsal}); };
+    if (s.method == GNCDE_RK4) {
+      for (int k = 0; k < G - 1; ++k) {
+        add(k, 0.f, 0);
+        add(k, 0.5f, 0);
+        add(k, 0.5f, 0);
+        add(k, 1.0f, 0);
+      }
+    } else {  // the FSAL k0, then per step the stages at c2 .. c5, 1 and the FSAL stage at the step's end knot
+      add(0, 0.f, 0);
+      for (int k = 0; k < G - 1; ++k) {
+        add(k, TSIT5_C2, 0);
+        add(k, TSIT5_C3, 0);
+        add(k, TSIT5_C4, 0);
+        add(k, TSIT5_C5, 0);
+        add(k, 1.0f, 0);
+        add(k, 0.f, 1);
+      }
+    }
+  }
   const unsigned gb = cdiv(B, 256);
   const dim3 ge(cdiv(E, 256), B);
   const dim3 gc(cdiv(E, 256 * kComboU), B);
@@ -1005,13 +1105,36 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   PendingCombo pend{};
   bool has_pend = false;
   const char* nm = getenv("GNCDE_COMBO_SEPARATE");  // A/B: every combination as its own k_combo launch
-  const bool merge = !(nm && atoi(nm) != 0);
+  const bool merge = !ovl && !(nm && atoi(nm) != 0);
+  int ecur = 0, issued = 0;  // overlapped forms: the next evaluation, the forms launched so far
+  const float* csum = generic_vf_csum(p, ws);
+  auto issue_forms = [&](int e) {  // side stream: forms of evaluation e into set e % 2, once layers e - 2 are done
+    if (e >= (int)plan.size()) return;
+    if (e >= 2) (void)hipStreamWaitEvent(side->s, side->ev[2 + (e & 1)], 0);
+    const FormBufs& f = fbs[e & 1];
+    vf_forms_direct(p, tst, csum, f.abar, f.q, f.tg, f.dx, side->s, nullptr, &plan[e]);
+    (void)hipEventRecord(side->ev[e & 1], side->s);
+    issued = e + 1;
+  };
+  if (ovl) {  // the side stream starts after everything queued on st so far (the prepared workspace)
+    (void)hipEventRecord(side->ev[4], st);
+    (void)hipStreamWaitEvent(side->s, side->ev[4], 0);
+    issue_forms(0);
+  }
   auto flush = [&]() {
     if (has_pend)
       hipLaunchKernelGGL(k_combo, gc, dim3(kComboThreads), 0, st, B, E, pend.y, pend.cb, pend.hcur, pend.out);
     has_pend = false;
   };
   auto eval = [&](const float* yin, float* out) {
+    if (ovl) {  // the next evaluation's forms go out first, then this one's layers once its forms are done
+      if (issued <= ecur + 1) issue_forms(ecur + 1);
+      (void)hipStreamWaitEvent(st, side->ev[ecur & 1], 0);
+      const int r = generic_vf_eval(p, tst, yin, out, ws, st, true, &bars, keep_next, true, nullptr, &fbs[ecur & 1]);
+      (void)hipEventRecord(side->ev[2 + (ecur & 1)], st);
+      ++ecur;
+      return r;
+    }
     const PendingCombo* pc = has_pend ? &pend : nullptr;
     has_pend = false;
     return generic_vf_eval(p, tst, yin, out, ws, st, true, &bars, keep_next, true, pc);
@@ -1113,6 +1236,10 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     }
   }
   flush();
+  if (ovl) {  // st resumes after the side stream's last launch (forms issued past a failed evaluation included)
+    (void)hipEventRecord(side->ev[5], side->s);
+    (void)hipStreamWaitEvent(st, side->ev[5], 0);
+  }
   if (s.save_mode == GNCDE_SAVE_T1)
     (void)hipMemcpyAsync(ys, y, B * E * sizeof(float), hipMemcpyDeviceToDevice, st);
   if (stats)

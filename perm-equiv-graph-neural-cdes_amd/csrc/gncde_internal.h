@@ -271,10 +271,26 @@ struct PendingCombo {
   size_t E;
   unsigned blocks;  // combination blocks per sample (0: none)
 };
-// pending (optional): a stage combination folded into this evaluation's forms launch
+// A fixed-grid evaluation's stage time computed by the forms launch itself from the grid (the overlapped forms of
+// generic_integrate: launched on a side stream ahead of the stage combination that writes tst), with exactly the
+// arithmetic of k_grid_step + the combination: tcur = g[min(k, ns)], h = k < ns ? g[k+1] - g[k] : 0,
+// t = fsal ? g[min(k + 1, ns)] : tcur + c h (stage_time).
+struct GridTime {
+  const float* grid;  // [B, G] (nullptr: not used)
+  const int32_t* nsteps;
+  int G, k;
+  float c;
+  int fsal;
+};
+// The outputs of one evaluation's forms launch (every layer's (I + Abar_l), q_l, tg, dX), when the caller owns them
+struct FormBufs {
+  float *abar, *q, *tg, *dx;
+};
+// pending (optional): a stage combination folded into this evaluation's forms launch; forms (optional): the forms
+// were launched by the caller into these buffers (no forms launch here)
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared = false, unsigned* bars = nullptr, float* keep = nullptr,
-                    bool need_dy = true, const PendingCombo* pending = nullptr);
+                    bool need_dy = true, const PendingCombo* pending = nullptr, const FormBufs* forms = nullptr);
 // the workspace's fault word (a one-launch evaluation's barrier gave up): solver status 4 when set
 const int* generic_vf_fault(const GncdeProblem& p, char* ws);
 

@@ -516,6 +516,35 @@ def test_readout_tiles_bitwise(G, monkeypatch, B, n, dims):
         assert rel_err(outs["5"][B - 1].cpu().numpy(), traj) <= RTOL_SOLVE
 
 
+@pytest.mark.parametrize("method", ["rk4", "tsit5"])
+def test_forms_overlap_bitwise(G, monkeypatch, method):
+    """With GNCDE_FORMS_OVERLAP=1 the fixed-grid generic solve launches each evaluation's forms one evaluation ahead
+    on a side stream, timed from the grid (GridTime), into alternating buffer sets; by default (0) the forms follow
+    the stage combination on the caller's stream.  Same stage times, same kernels: bitwise the same trajectory, stats and
+    stage record — ragged per-sample grids (padded steps) included, at config 3's shape and a mixed-width one."""
+    for B, n, dims, distinct in ((64, 129, [64, 64, 64, 1024], 4), (5, 70, [32, 16, 32, 512], 3)):
+        H, de, L = dims[0], 8, len(dims) - 1
+        rng, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(43, B, n, 4, 1.0, H, de, L, distinct=distinct, dims=dims)
+        prob = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
+        grids = [O.constant_grid(0.0, 0.3, 0.1) if b % 2 else O.constant_grid(0.0, 0.2, 0.05) for b in range(B)]
+        grid, ns = G.layout.stack_grids(grids)
+        m = G._lib.RK4 if method == "rk4" else G._lib.TSIT5
+        spec = G.SolverSpec(method=m, save_mode=G._lib.SAVE_STEPS, grid=grid, nsteps=ns)
+        assert G.integrate_path(prob, spec) == "generic"
+        floats = G.engine.stage_record_floats(prob, spec)
+        yd = torch.tensor(y0, dtype=torch.float32, device="cuda")
+        outs = {}
+        for v in ("0", "1"):
+            monkeypatch.setenv("GNCDE_FORMS_OVERLAP", v)
+            rec = torch.zeros(B, max(floats, 1), device="cuda")
+            sp = dataclasses.replace(spec, stage_rec=rec) if floats else spec
+            ys, st = G.integrate(prob, sp, yd, stats=True)
+            outs[v] = (ys.clone(), st.clone(), rec)
+        assert bool(torch.isfinite(outs["1"][0]).all())
+        for a, b in zip(outs["0"], outs["1"]):
+            assert torch.equal(a, b)
+
+
 def test_bwd_row_blocks_per_workgroup_bitwise(G, monkeypatch):
     """k_bwd_layer at config 3's shape (B = 64, n = 129: nine 16-row blocks per sample) with one, two and three row
     blocks per workgroup (GNCDE_BWD_RBW; the default picks three there, one round on 256 CUs): every sample's
