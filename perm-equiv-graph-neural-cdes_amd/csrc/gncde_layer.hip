@@ -81,20 +81,31 @@ __device__ unsigned long long g_layer_stamps[1024 * 8];
 #define LAYER_STAMP(k) do {} while (0)
 #endif
 
+// Wave count: 4, or 8 for the five-tile CDE read-out with two channel tiles per workgroup (config 3's h = 64): one
+// workgroup per CU then has two waves per SIMD, so one wave's operand formation and waits run under the other's
+// MFMAs.  The product's K parts and the read-out's j quarters keep one summation order for every wave count.
+template <int DOUT, int MODE, bool BF, int NT>
+constexpr int layer_waves() {
+  return (MODE == 2 && !BF && NT > 2 && DOUT / 16 / ((DOUT / 16 >= kSplit) ? kSplit : 1) == 2) ? 8 : 4;
+}
+
 template <int DIN, int DOUT, int MODE, bool BF, int NT>
-__global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
+__global__ void __launch_bounds__((64 * layer_waves<DOUT, MODE, BF, NT>()), (NT > 2 ? 1 : 2)) k_layer(LayerArgs a) {
   static_assert(MODE == 2 || NT == 2, "the Linear epilogue's tile split assumes two row tiles");
   static_assert(!BF || NT == 2, "bf16 modes: two row tiles");
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int WV = layer_waves<DOUT, MODE, BF, NT>();
+  constexpr int NTH = 64 * WV;   // threads
   constexpr int kRows = 16 * NT;
   constexpr int ZS = zs_stride<DIN>();
   constexpr int CTP = DIN / 16;  // product column tiles
-  constexpr int KPP = 4;         // product K parts (one per wave)
+  constexpr int KPP = 4;         // product K parts (waves w and w + 4 share one: each takes half the column tiles)
+  constexpr int CTW = CTP * 4 / WV;  // product column tiles per wave
   constexpr int NCC = DIN / 16;  // 16-deep K chunks of the Linear
   const int n = a.n;
   const int nk = BF ? (n + 31) & ~31 : (n + 15) & ~15;  // K rows of Zs: whole MFMA K chunks
-  floatx4* red = reinterpret_cast<floatx4*>(smem);  // [4][NT][64] K-part partials (MODE 2)
-  float* sDx = smem + 4 * NT * 64 * 4;              // [kRows][kDxS] (MODE 2)
+  floatx4* red = reinterpret_cast<floatx4*>(smem);  // [WV][NT][64] read-out partials (MODE 2)
+  float* sDx = smem + WV * NT * 64 * 4;             // [kRows][kDxS] (MODE 2)
   float* Zs = sDx + kRows * kDxS;                   // [nk][ZS] (16-byte aligned)
   float* Ps = Zs;                                   // [KPP][32][ZS] after the product (max(nk, 128) rows reserved)
   float* sInv = Zs + (nk > 4 * kRows ? nk : 4 * kRows) * ZS;  // [nk] RMSNorm factors of the Z rows
@@ -106,6 +117,7 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
   const int bx = wx % (int)gridDim.x;
   const int b = wx / (int)gridDim.x, r0 = (bx / SPLIT) * kRows, ch = bx % SPLIT;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
+  const int kpp = w & 3, ct0 = (w >> 2) * CTW;  // this wave's product K part and first column tile
   const size_t nb = (size_t)b * n;
   LAYER_STAMP(0);
 
@@ -152,8 +164,8 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
   // NT > 2 (one workgroup per CU): the Z rows and the tiles' dX rows are loaded into registers FIRST and the
   // (I + Abar) rows after them, so the wait for Z (loads complete in issue order) does not include the 5-tile
   // (I + Abar) round, which lands while Z is stored, normed and the barriers pass
-  constexpr int G4Z = DIN / 4, UZ = 12, UD = (kRows * 16 + 255) / 256;
-  const bool zfirst = NT > 2 && nk * G4Z <= 256 * UZ;
+  constexpr int G4Z = DIN / 4, UZ = 3072 / NTH, UD = (kRows * 16 + NTH - 1) / NTH;
+  const bool zfirst = NT > 2 && nk * G4Z <= NTH * UZ;
   floatx4 zpre[NT > 2 ? UZ : 1];
   float dxpre[NT > 2 ? UD : 1];
   if constexpr (NT > 2) {
@@ -161,17 +173,17 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
       const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.Z + nb * DIN);
 #pragma unroll
       for (int u = 0; u < UZ; ++u) {
-        const int e = tid + 256 * u;
+        const int e = tid + NTH * u;
         zpre[u] = e < n * G4Z ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
       for (int u = 0; u < UD; ++u) {
-        const int e = tid + 256 * u, row = e >> 4, R = r0 + row;
+        const int e = tid + NTH * u, row = e >> 4, R = r0 + row;
         dxpre[u] = e < kRows * 16 && R < n ? a.dx[(nb + R) * 16 + (e & 15)] : 0.f;
       }
     }
   }
-  if constexpr (!BF) load_round(w);
+  if constexpr (!BF) load_round(kpp);
   // The epilogue's operands (W' B operands of the wave's output tiles, b', q, tg of its rows) do not depend on the
   // product either: issued here, so the tail after the last barrier is MFMA + stores, not two more L2 round trips.
   constexpr int CTO = MODE != 2 ? DOUT / 16 : 1;
@@ -215,36 +227,36 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
     if (zfirst) {  // (NT > 2) stores of the registers loaded first
 #pragma unroll
       for (int u = 0; u < (NT > 2 ? UZ : 1); ++u) {
-        const int e = tid + 256 * u;
+        const int e = tid + NTH * u;
         if (e < tot) *reinterpret_cast<floatx4*>(Zs + (e / G) * ZS + 4 * (e % G)) = zpre[u];
       }
 #pragma unroll
       for (int u = 0; u < (NT > 2 ? UD : 1); ++u) {
-        const int e = tid + 256 * u;
+        const int e = tid + NTH * u;
         if (e < kRows * 16) sDx[(e >> 4) * kDxS + (e & 15)] = dxpre[u];
       }
     }
-    for (int e0 = zfirst ? tot : tid; e0 < tot; e0 += 256 * U) {
+    for (int e0 = zfirst ? tot : tid; e0 < tot; e0 += NTH * U) {
       floatx4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int e = e0 + 256 * u;
+        const int e = e0 + NTH * u;
         v[u] = e < valid ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int e = e0 + 256 * u;
+        const int e = e0 + NTH * u;
         if (e < tot) *reinterpret_cast<floatx4*>(Zs + (e / G) * ZS + 4 * (e % G)) = v[u];
       }
     }
     if (MODE == 2 && !zfirst)
-      for (int e = tid; e < kRows * 16; e += 256) {
+      for (int e = tid; e < kRows * 16; e += NTH) {
         const int row = e >> 4, j = e & 15, R = r0 + row;
         sDx[row * kDxS + j] = R < n ? a.dx[(nb + R) * 16 + j] : 0.f;
       }
     __syncthreads();
     LAYER_STAMP(1);
-    for (int r = tid; r < nk; r += 256) {
+    for (int r = tid; r < nk; r += NTH) {
       float ss = 0.f;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
@@ -318,13 +330,13 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
         for (int r = 0; r < 4; ++r) Ps[(w * kRows + 16 * t + 4 * hi + r) * ZS + 16 * ct + lo] = acc[t][ct][r];
   } else {
     const int nch = nch16;
-    floatx4 acc[NT][CTP];
+    floatx4 acc[NT][CTW];  // this wave's K part of P[., 16 (ct0 + ct) ...] (the same MFMA order for any CTW)
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int ct = 0; ct < CTP; ++ct) acc[t][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
-    for (int kr = w; kr < nch; kr += 16) {  // rounds of up to 4 chunks: kr, kr + 4, kr + 8, kr + 12
-      if (kr != w) load_round(kr);  // the first round was issued before the Z staging
+      for (int ct = 0; ct < CTW; ++ct) acc[t][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int kr = kpp; kr < nch; kr += 16) {  // rounds of up to 4 chunks: kr, kr + 4, kr + 8, kr + 12
+      if (kr != kpp) load_round(kr);  // the first round was issued before the Z staging
 #pragma unroll
       for (int c = 0; c < 4; ++c) {  // (I + Abar) diag(inv): column k of the operand scaled by inv[k]
         const int kc = kr + 4 * c;
@@ -345,16 +357,16 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
           // NT > 2: MFMA steps s whose K rows 16 kc + 4 hi + s all lie past n add exact zeros and are skipped
           const int ks = NT > 2 && n - 16 * kc < 4 ? n - 16 * kc : 4;
           const float* zb = Zs + (16 * kc + 4 * hi) * ZS + lo;
-          float bv[4][CTP];  // the chunk's B operands: every LDS read issued before the first MFMA
+          float bv[4][CTW];  // the chunk's B operands: every LDS read issued before the first MFMA
 #pragma unroll
           for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int ct = 0; ct < CTP; ++ct) bv[s][ct] = zb[s * ZS + 16 * ct];
+            for (int ct = 0; ct < CTW; ++ct) bv[s][ct] = zb[s * ZS + 16 * (ct0 + ct)];
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
             if (NT > 2 && s >= ks) break;
 #pragma unroll
-            for (int ct = 0; ct < CTP; ++ct)
+            for (int ct = 0; ct < CTW; ++ct)
 #pragma unroll
               for (int t = 0; t < NT; ++t)
                 if (t < CNT) acc[t][ct] = mfma4(av[c][t][s], bv[s][ct], acc[t][ct]);
@@ -368,9 +380,10 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int ct = 0; ct < CTP; ++ct)
+      for (int ct = 0; ct < CTW; ++ct)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Ps[(w * kRows + 16 * t + 4 * hi + r) * ZS + 16 * ct + lo] = acc[t][ct][r];
+        for (int r = 0; r < 4; ++r)
+          Ps[(kpp * kRows + 16 * t + 4 * hi + r) * ZS + 16 * (ct0 + ct) + lo] = acc[t][ct][r];
   }
   __syncthreads();
   LAYER_STAMP(4);
@@ -418,17 +431,23 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
   } else {
     // ---- 3'. CDE output layer: dZ = tg * (sum_{c,j} P[., c] dX[., j] W'[16 m + j, c] + q sum_j b'[16 m + j] dX) --
     constexpr int CT = DOUT / 16 / SPLIT;  // this workgroup's output column tiles (channels m)
-    constexpr int KP = 4 / CT;             // waves per column tile, splitting j
+    constexpr int KP = WV / CT;            // waves per column tile, splitting j (2 or 4)
     constexpr int JP = 16 / KP;
+    // The canonical order for every wave count: one partial per QUARTER of the 16 j (sequential over c chunks, its
+    // 4 j and the MFMA steps, then its share of the bias term), combined as (q0 + q1) + (q2 + q3)
+    constexpr int QW = JP / 4;             // quarters per wave
+    static_assert(KP == 2 || KP == 4, "read-out j split");
     const int ct = ch * CT + w % CT, kp = w / CT, j0 = kp * JP;
     float dxr[NT][JP];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int j = 0; j < JP; ++j) dxr[t][j] = sDx[(16 * t + lo) * kDxS + j0 + j];
-    floatx4 acc[NT];
+    floatx4 acc[QW][NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < QW; ++q)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[q][t] = floatx4{0.f, 0.f, 0.f, 0.f};
     // one copy of the K loop per row-tile count (a per-MFMA test of the count compiles to a branch per MFMA)
     // Per 16-deep c chunk: all JP W' operand loads are issued first (one L2 round trip per chunk), the next chunk's
     // while this one's MFMAs run; the j loop is fully unrolled so dX stays in statically indexed registers.
@@ -462,7 +481,7 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
           for (int s = 0; s < 4; ++s) {
 #pragma unroll
             for (int t = 0; t < NT; ++t)
-              if (t < CNT) acc[t] = mfma4(av4[t][s], wv[cc & 1][j][s], acc[t]);
+              if (t < CNT) acc[j >> 2][t] = mfma4(av4[t][s], wv[cc & 1][j][s], acc[j >> 2][t]);
             if constexpr (CNT > 2) {
               if (j + 1 < JP)
 #pragma unroll
@@ -480,33 +499,36 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
     };
     with_count(ntl, kloop);
     LAYER_STAMP(5);
-    // bias term of this wave's j range; rows 16 t + 4 hi + r, channel m
+    // bias term of each j quarter; rows 16 t + 4 hi + r, channel m
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rl = 16 * t + 4 * hi + r, R = r0 + rl;
-        float dxv[JP];  // dX[row, j0 .. j0 + JP): JP / 4 aligned 16-byte reads (broadcast over the 16 lanes of a row)
 #pragma unroll
-        for (int q = 0; q < JP / 4; ++q) {
+        for (int q = 0; q < QW; ++q) {  // dX[row, j0 + 4 q .. + 3]: one aligned 16-byte read (a row's 16 lanes share it)
           const floatx4 v = *reinterpret_cast<const floatx4*>(sDx + rl * kDxS + j0 + 4 * q);
+          float sb = 0.f;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) dxv[4 * q + e] = v[e];
+          for (int e = 0; e < 4; ++e) sb = fmaf(bfr[4 * q + e], v[e], sb);
+          acc[q][t][r] = fmaf(R < n ? qpre[t][r] : 0.f, sb, acc[q][t][r]);
         }
-        float sb = 0.f;
-#pragma unroll
-        for (int j = 0; j < JP; ++j) sb = fmaf(bfr[j], dxv[j], sb);
-        acc[t][r] = fmaf(R < n ? qpre[t][r] : 0.f, sb, acc[t][r]);
       }
-    if constexpr (KP > 1) {
+    floatx4 fin[NT];  // (q0 + q1) + (q2 + q3)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) red[(w * NT + t) * 64 + lane] = acc[t];
-      __syncthreads();
-      if (kp == 0) {
+    for (int t = 0; t < NT; ++t) fin[t] = QW == 2 ? acc[0][t] + acc[QW - 1][t] : acc[0][t];
 #pragma unroll
-        for (int p = 1; p < KP; ++p)
+    for (int t = 0; t < NT; ++t) red[(w * NT + t) * 64 + lane] = fin[t];
+    __syncthreads();
+    if (kp == 0) {
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[t] += red[((w + p * CT) * NT + t) * 64 + lane];
+      for (int t = 0; t < NT; ++t) {
+        if constexpr (KP == 2) {
+          fin[t] += red[((w + CT) * NT + t) * 64 + lane];
+        } else {
+          fin[t] = (fin[t] + red[((w + CT) * NT + t) * 64 + lane]) +
+                   (red[((w + 2 * CT) * NT + t) * 64 + lane] + red[((w + 3 * CT) * NT + t) * 64 + lane]);
+        }
       }
     }
     if (kp == 0) {
@@ -517,7 +539,7 @@ __global__ void __launch_bounds__(256, NT > 2 ? 1 : 2) k_layer(LayerArgs a) {
           const int R = r0 + 16 * t + 4 * hi + r;
           if (R < n) {
             const size_t o = (nb + R) * DOUT + m;
-            a.out[o] = gpre[t][r] * acc[t][r];
+            a.out[o] = gpre[t][r] * fin[t][r];
           }
         }
     }
@@ -547,10 +569,10 @@ __global__ void k_permute_linear(int rows, int din, int cde, const float* __rest
 }
 
 template <int DIN>
-size_t layer_smem(int n, bool bf, int nt = kTiles) {
+size_t layer_smem(int n, bool bf, int nt = kTiles, int waves = 4) {
   constexpr int ZS = zs_stride<DIN>();
   const int nk = bf ? (n + 31) & ~31 : (n + 15) & ~15, rows = 16 * nt;
-  return sizeof(float) * (4 * nt * 64 * 4 + rows * kDxS + (size_t)(nk > 4 * rows ? nk : 4 * rows) * ZS + nk);
+  return sizeof(float) * ((size_t)waves * nt * 64 * 4 + rows * kDxS + (size_t)(nk > 4 * rows ? nk : 4 * rows) * ZS + nk);
 }
 
 constexpr size_t kMaxSmem = 64 * 1024;  // the default dynamic-LDS limit of a launch (NT = 2)
@@ -566,7 +588,7 @@ bool readout_wide(int n, int B) {
   if (forced == kTiles) return false;
   const int split = DOUT / 16 >= kSplit ? kSplit : 1;
   const long wgs = (long)B * ((n + 16 * kWideTiles - 1) / (16 * kWideTiles)) * split;
-  if (layer_smem<DIN>(n, false, kWideTiles) > kMaxWideSmem) return false;
+  if (layer_smem<DIN>(n, false, kWideTiles, layer_waves<DOUT, 2, false, kWideTiles>()) > kMaxWideSmem) return false;
   return forced == kWideTiles || wgs >= device_cu_count();
 }
 
@@ -575,11 +597,12 @@ void launch(const LayerArgs& a, int B, hipStream_t st) {
   const int split = (MODE == 2 && DOUT / 16 >= kSplit) ? kSplit : 1;
   if constexpr (MODE == 2 && !BF) {
     if (readout_wide<DIN, DOUT>(a.n, B)) {
-      const size_t sm = layer_smem<DIN>(a.n, false, kWideTiles);
+      constexpr int wv = layer_waves<DOUT, MODE, BF, kWideTiles>();
+      const size_t sm = layer_smem<DIN>(a.n, false, kWideTiles, wv);
       auto k = k_layer<DIN, DOUT, MODE, BF, kWideTiles>;
       if (ensure_dyn_lds(reinterpret_cast<const void*>(k), sm)) {
         const int rows = 16 * kWideTiles;
-        hipLaunchKernelGGL(k, dim3((a.n + rows - 1) / rows * split, B), dim3(256), sm, st, a);
+        hipLaunchKernelGGL(k, dim3((a.n + rows - 1) / rows * split, B), dim3(64 * wv), sm, st, a);
         return;
       }
     }
