@@ -154,12 +154,15 @@ __host__ __device__ inline int rows_big(int n, int H, bool bf) {
   const int np = rows_np(n, bf), z = (np > 80 ? np : 80) * rows_zs(H), s = 2 * np * kStrip + 32 * (np + 4);
   return ((z > s ? z : s) + 3) & ~3;
 }
-inline size_t rows_smem(int n, int H, int L, bool bf) {
+// the bf16-storage solve's per-thread coefficient cache (SOLVE & 8): every thread's raw rows-block and strip loads of
+// the current interval, [2][NU = 2][4 planes][256 threads] x 16 bytes
+constexpr size_t kCoefCacheBytes = (size_t)2 * 2 * 4 * 256 * 16;
+inline size_t rows_smem(int n, int H, int L, bool bf, bool cache = false) {
   const int np = rows_np(n, bf);
-  // big | inv [NP] | v_l [L][NP] | w, u, q [3][L][16] | tg [16] | dX [16][17] | red [4][64] x4
-  // (config 5, n = 255 h = 32 L = 4: 77.4 KiB, two workgroups per CU)
+  // big | inv [NP] | v_l [L][NP] | w, u, q [3][L][16] | tg [16] | dX [16][17] | red [4][64] x4 | flags [4] | cache
+  // (config 5, n = 255 h = 32 L = 4: 77.4 KiB, two workgroups per CU; with the cache 141.4 KiB, one)
   return sizeof(float) * ((size_t)rows_big(n, H, bf) + np + (size_t)L * np + 48 * L + 16 + 16 * kStrip +
-                          4 * 64 * 4 + 4);
+                          4 * 64 * 4 + 4) + (cache ? kCoefCacheBytes : 0);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
@@ -175,7 +178,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
 // its L2 footprint), widened exactly on load, every product fp32: the result is the fp32 computation on the
 // bf16-rounded operator, so the adaptive controller sees no per-stage rounding noise.
 // SOLVE: 0 one evaluation per launch; the persistent solve with 1 the Tsit5 + PIDController controller, 2 a fixed
-// step grid (§ the solve below); + 4: the solve's hand-offs as tagged granules instead of counter barriers.
+// step grid (§ the solve below); + 4: the solve's hand-offs as tagged granules instead of counter barriers; + 8
+// (bf16 coefficient storage only): each thread keeps its raw coefficient loads of the current interval in LDS.
 template <int H, int MODE, int PREC, int SOLVE>
 __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -198,6 +202,10 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
   float* sOut = big + 64 * ZS;  // the output tile [16][ZS] (rows_big)
   floatx4* red = reinterpret_cast<floatx4*>(sDx + 16 * kStrip);
   int* sFlag = reinterpret_cast<int*>(red + 4 * 64);  // [0] barrier gave up, [1] ticket
+  // SOLVE & 8: the coefficient cache (thread-private slots: a thread reads back only what it wrote)
+  constexpr bool CCACHE = (SOLVE & 8) != 0 && PREC == 2;
+  u32x4* ccache = reinterpret_cast<u32x4*>(sFlag + 4);
+  int cidx = -1;  // the interval the cache holds (uniform; -1: none, reset for every new sample)
 
   // ---- which rows of which sample ------------------------------------------------------------------------------
   // One evaluation (k_rows): the grid holds G co-resident groups that loop over the samples in rounds.  Solve: one
@@ -399,27 +407,40 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     constexpr int CE = CBF ? 8 : 4, NU = CBF ? 2 : 4;
     const int cq = CE * (tid & 15);
     u32x4 rc[NU][4], sc[NU][4];
+    // SOLVE & 8: an evaluation on the interval the cache holds reads the raw loads back from LDS (no memory round
+    // trip: the adaptive solve stays on one interval for most of its evaluations)
+    const bool fresh = !CCACHE || idx != cidx;
+    if (fresh) {
 #pragma unroll
-    for (int u = 0; u < NU; ++u)
+      for (int u = 0; u < NU; ++u)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-      {
-        const int e = (int)(q * nn + (size_t)(r0 + rr) * n + cq + 16 * CE * u);
-        if constexpr (CBF) rc[u][q] = load8_bf16(crs, e);
-        else rc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, e * 4, 0, 0);
-      }
-    // the column strip [:, R] = rows R of the transposed planes: the same whole-line pattern as the rows block
-    const CT_* cbt = reinterpret_cast<const CT_*>(a.coefT) + ((size_t)b * (T - 1) + idx) * 4 * nn;
-    const auto crt = rsrc(cbt, (unsigned)(4 * nn * sizeof(CT_)));
+        for (int q = 0; q < 4; ++q)
+        {
+          const int e = (int)(q * nn + (size_t)(r0 + rr) * n + cq + 16 * CE * u);
+          if constexpr (CBF) rc[u][q] = load8_bf16(crs, e);
+          else rc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crs, e * 4, 0, 0);
+        }
+      // the column strip [:, R] = rows R of the transposed planes: the same whole-line pattern as the rows block
+      const CT_* cbt = reinterpret_cast<const CT_*>(a.coefT) + ((size_t)b * (T - 1) + idx) * 4 * nn;
+      const auto crt = rsrc(cbt, (unsigned)(4 * nn * sizeof(CT_)));
 #pragma unroll
-    for (int u = 0; u < NU; ++u)
+      for (int u = 0; u < NU; ++u)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-      {
-        const int e = (int)(q * nn + (size_t)(r0 + rr) * n + cq + 16 * CE * u);
-        if constexpr (CBF) sc[u][q] = load8_bf16(crt, e);
-        else sc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crt, e * 4, 0, 0);
-      }
+        for (int q = 0; q < 4; ++q)
+        {
+          const int e = (int)(q * nn + (size_t)(r0 + rr) * n + cq + 16 * CE * u);
+          if constexpr (CBF) sc[u][q] = load8_bf16(crt, e);
+          else sc[u][q] = __builtin_amdgcn_raw_buffer_load_b128(crt, e * 4, 0, 0);
+        }
+    } else if constexpr (CCACHE) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          rc[u][q] = ccache[((0 * NU + u) * 4 + q) * 256 + tid];
+          sc[u][q] = ccache[((1 * NU + u) * 4 + q) * 256 + tid];
+        }
+    }
     const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
     const int nd = tid < n ? tid : n - 1;  // clamped indices + selects: no load inside a divergent branch
     float pv[3][4], pt[4];
@@ -455,6 +476,18 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
         }
     }
     ROWS_STAMP(15);
+    if constexpr (CCACHE) {
+      if (fresh) {  // keep this interval's raw loads (thread-private slots)
+#pragma unroll
+        for (int u = 0; u < NU; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            ccache[((0 * NU + u) * 4 + q) * 256 + tid] = rc[u][q];
+            ccache[((1 * NU + u) * 4 + q) * 256 + tid] = sc[u][q];
+          }
+        cidx = idx;
+      }
+    }
     {  // 2. the column strip: Horner of transposed row rr (= column r0 + rr), element kk = node; LDS [node][column]
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
@@ -1332,6 +1365,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     epoch = a.bar0;
     pub = 0;
     hseq = 0;
+    cidx = -1;
     ts_lane = (int)(threadIdx.x & 63) < T ? a.ts[(size_t)g * T + (threadIdx.x & 63)] : 0.f;
     }
   }
@@ -1568,9 +1602,21 @@ bool rows_solve_shape(const GncdeProblem& p) {
 
 // the persistent solve's instance for this controller (fp32, or bfloat16 coefficient storage: PREC 2), with the
 // counter hand-offs or (GNCDE_SOLVE_GRANULES=1) the tagged-granule ones
+// The bf16-storage solve keeps its coefficient loads in LDS (SOLVE & 8) when one workgroup per CU holds the whole
+// batch (the cache takes 64 KB more LDS per workgroup: one workgroup per CU instead of two); GNCDE_SOLVE_COEF_CACHE=0
+// turns it off.
+bool solve_coef_cache(const GncdeProblem& p) {
+  if (p.compute != GNCDE_COMPUTE_BF16_STORAGE || rows_solve_granules()) return false;
+  const char* e = getenv("GNCDE_SOLVE_COEF_CACHE");
+  if (e && atoi(e) == 0) return false;
+  const int nb = (p.n + kRB - 1) / kRB;
+  return (long)p.B * nb <= cu_count();
+}
+
 bool find_solve_inst(const GncdeProblem& p, const GncdeSolver& s, Inst& k) {
   const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
   const bool grid = s.controller == GNCDE_CTRL_GRID;
+  if (solve_coef_cache(p)) return grid ? find_inst_t<2, 10>(H, mode, k) : find_inst_t<2, 9>(H, mode, k);
   if (rows_solve_granules()) {
     if (p.compute == GNCDE_COMPUTE_BF16_STORAGE)
       return grid ? find_inst_t<2, 6>(H, mode, k) : find_inst_t<2, 5>(H, mode, k);
@@ -1593,7 +1639,7 @@ bool rows_pid_supported(const GncdeProblem& p, const GncdeSolver& s) {
   Inst k;
   if (!find_solve_inst(p, s, k)) return false;
   const int nb = (p.n + kRB - 1) / kRB;
-  return resident_blocks(k, rows_smem(p.n, p.dims[0], p.L, false)) >= nb && cu_count() >= nb;
+  return resident_blocks(k, rows_smem(p.n, p.dims[0], p.L, false, solve_coef_cache(p))) >= nb && cu_count() >= nb;
 }
 
 size_t rows_pid_scratch(const GncdeProblem& p) {
@@ -1608,7 +1654,7 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   const int H = p.dims[0];
   if (!find_solve_inst(p, s, k)) return GNCDE_ERR_UNSUPPORTED;
   (void)vf_ws;
-  const size_t smem = rows_smem(p.n, H, p.L, false);
+  const size_t smem = rows_smem(p.n, H, p.L, false, solve_coef_cache(p));
   if (!ensure_dyn_lds(k.fn, smem)) return GNCDE_ERR_HIP;
   const int nb = (p.n + kRB - 1) / kRB;
   RowsArgs a{};

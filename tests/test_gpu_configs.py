@@ -264,6 +264,27 @@ def test_rows_solve_sample_queue_bitwise(G, monkeypatch):
         assert torch.equal(a, b)
 
 
+def test_rows_solve_coef_cache_bitwise(G, monkeypatch):
+    """bf16 coefficient storage at config 5's shape (B = 16: one workgroup per CU holds the batch): the persistent
+    solve keeps each thread's raw coefficient loads of the current interval in LDS and reads them back while the
+    interval holds (SOLVE & 8); with GNCDE_SOLVE_COEF_CACHE=0 it reloads them every evaluation.  Same values into the
+    same arithmetic: bitwise the same outputs, stats and step records, PID and the reference's fixed grid."""
+    prob, y0, spec = _config5(G, 16, seed=61)
+    prob = prob.with_compute("bf16_storage")
+    grid, ns = G.layout.stack_grids([O.constant_grid(0.0, 1.0, 0.01)] * prob.B)
+    fspec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_T1, grid=grid, nsteps=ns)
+    outs = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("GNCDE_SOLVE_COEF_CACHE", v)
+        rec = torch.zeros(prob.B, 256, device="cuda")
+        ys, st = G.integrate(prob, dataclasses.replace(spec, step_ts=rec), y0, stats=True)
+        yf = G.integrate(prob, fspec, y0)
+        outs[v] = (ys, st, rec, yf)
+    assert torch.all(outs["1"][1][:, 3] == 0) and bool(torch.isfinite(outs["1"][0]).all())
+    for a, b in zip(outs["0"], outs["1"]):
+        assert torch.equal(a, b)
+
+
 def test_rows_solve_granule_handoffs_bitwise(G, monkeypatch):
     """The persistent solve's two hand-off variants — counter barriers (the default) and tagged granules
     (GNCDE_SOLVE_GRANULES=1) — move the same values between the same arithmetic: bitwise the same outputs, stats and
