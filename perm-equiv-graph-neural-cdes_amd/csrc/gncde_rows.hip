@@ -1610,6 +1610,9 @@ bool solve_coef_cache(const GncdeProblem& p) {
   const char* e = getenv("GNCDE_SOLVE_COEF_CACHE");
   if (e && atoi(e) == 0) return false;
   const int nb = (p.n + kRB - 1) / kRB;
+  if (rows_smem(p.n, p.dims[0], p.L, false, true) > 160 * 1024) return false;  // (the LDS a workgroup may take)
+  // (caching the form's small loads too — plane sums, totals, time channel, data spline — measured no faster:
+  // 5.63 vs 5.62 ms at config 5, B = 16)
   return (long)p.B * nb <= cu_count();
 }
 
