@@ -1738,7 +1738,8 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   // its 16 samples run one workgroup per CU, while the queue leaves them on CUs still shared two ways): fixed
   // grids keep the chunks.  GNCDE_SOLVE_CHUNKED=1 / 0 forces either (A/B, tests).
   const char* ce = getenv("GNCDE_SOLVE_CHUNKED");
-  const bool chunked = ce ? atoi(ce) != 0 : s.controller != GNCDE_CTRL_PID;
+  // (the mailbox packs a sample index into 20 bits: larger batches keep the chunks)
+  const bool chunked = (ce ? atoi(ce) != 0 : s.controller != GNCDE_CTRL_PID) || p.B >= (1 << 20);
   if (chunked) {
     a.queue = nullptr;
     unsigned tickets = 0;
