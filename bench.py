@@ -232,8 +232,8 @@ def train_line(dist, rank, world, steps, warmup, rk4_steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1024, help="samples per GPU")
     ap.add_argument("--rk4-steps", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
