@@ -161,14 +161,15 @@ __global__ void __launch_bounds__((64 * layer_waves<DOUT, MODE, BF, NT>()), (NT 
       }
     }
   };
-  // NT > 2 (one workgroup per CU): the Z rows and the tiles' dX rows are loaded into registers FIRST and the
-  // (I + Abar) rows after them, so the wait for Z (loads complete in issue order) does not include the 5-tile
-  // (I + Abar) round, which lands while Z is stored, normed and the barriers pass
+  // The Z rows (and the read-out tiles' dX rows) are loaded into registers FIRST and the (I + Abar) rows after them,
+  // so the wait for Z (loads complete in issue order) does not include the (I + Abar) round, which lands while Z is
+  // stored, normed and the barriers pass (five-tile read-out: staging 5.36 -> 3.90 us)
   constexpr int G4Z = DIN / 4, UZ = 3072 / NTH, UD = (kRows * 16 + NTH - 1) / NTH;
-  const bool zfirst = NT > 2 && nk * G4Z <= NTH * UZ;
-  floatx4 zpre[NT > 2 ? UZ : 1];
-  float dxpre[NT > 2 ? UD : 1];
-  if constexpr (NT > 2) {
+  constexpr bool ZF = !BF;  // (every fp32 launch; the bf16 product splits Z on the fly and keeps the old order)
+  const bool zfirst = ZF && nk * G4Z <= NTH * UZ;
+  floatx4 zpre[ZF ? UZ : 1];
+  float dxpre[ZF && MODE == 2 ? UD : 1];
+  if constexpr (ZF) {
     if (zfirst) {
       const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.Z + nb * DIN);
 #pragma unroll
@@ -176,11 +177,12 @@ __global__ void __launch_bounds__((64 * layer_waves<DOUT, MODE, BF, NT>()), (NT 
         const int e = tid + NTH * u;
         zpre[u] = e < n * G4Z ? Z4[e] : floatx4{0.f, 0.f, 0.f, 0.f};
       }
+      if constexpr (MODE == 2)
 #pragma unroll
-      for (int u = 0; u < UD; ++u) {
-        const int e = tid + NTH * u, row = e >> 4, R = r0 + row;
-        dxpre[u] = e < kRows * 16 && R < n ? a.dx[(nb + R) * 16 + (e & 15)] : 0.f;
-      }
+        for (int u = 0; u < UD; ++u) {
+          const int e = tid + NTH * u, row = e >> 4, R = r0 + row;
+          dxpre[u] = e < kRows * 16 && R < n ? a.dx[(nb + R) * 16 + (e & 15)] : 0.f;
+        }
     }
   }
   if constexpr (!BF) load_round(kpp);
@@ -224,17 +226,18 @@ __global__ void __launch_bounds__((64 * layer_waves<DOUT, MODE, BF, NT>()), (NT 
     constexpr int U = 8;
     const floatx4* Z4 = reinterpret_cast<const floatx4*>(a.Z + nb * DIN);
     const int tot = nk * G, valid = n * G;
-    if (zfirst) {  // (NT > 2) stores of the registers loaded first
+    if (zfirst) {  // stores of the registers loaded first
 #pragma unroll
-      for (int u = 0; u < (NT > 2 ? UZ : 1); ++u) {
+      for (int u = 0; u < (ZF ? UZ : 1); ++u) {
         const int e = tid + NTH * u;
         if (e < tot) *reinterpret_cast<floatx4*>(Zs + (e / G) * ZS + 4 * (e % G)) = zpre[u];
       }
+      if constexpr (MODE == 2)
 #pragma unroll
-      for (int u = 0; u < (NT > 2 ? UD : 1); ++u) {
-        const int e = tid + NTH * u;
-        if (e < kRows * 16) sDx[(e >> 4) * kDxS + (e & 15)] = dxpre[u];
-      }
+        for (int u = 0; u < (ZF ? UD : 1); ++u) {
+          const int e = tid + NTH * u;
+          if (e < kRows * 16) sDx[(e >> 4) * kDxS + (e & 15)] = dxpre[u];
+        }
     }
     for (int e0 = zfirst ? tot : tid; e0 < tot; e0 += NTH * U) {
       floatx4 v[U];

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5 (GPU box): eight-wave five-tile read-out (two waves per SIMD): parity, then config 3 A/B against the
+# Round 5 (GPU box): config 3 layer changes: parity, then config 3 A/B against the previous build (abtest/libgncde_old.so), alternating.
 # previous build (abtest/libgncde_old.so), alternating.
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
 export TMPDIR=/tmp
