@@ -7,6 +7,7 @@
 // Reference semantics: spline (perm_equiv_graph_vector_field.py:98-102), fusion (layers.py:102-160,
 // :256-337 via the factored table of gncde.h), ConvLayer (layers.py:36-48), VF epilogue
 // (perm_equiv_graph_vector_field.py:122-128), CDE wrapper (cde_wrapper_vector_field.py:19-26).
+#include "gncde_forms.h"
 #include "gncde_internal.h"
 
 #include <vector>
@@ -24,12 +25,6 @@ constexpr int kRedStride = 8;  // red[b][q][n]: r, rd, c, cd, diagA, diagdA, {s}
 // partials that one block reduction turns into complete row sums (a slab holds whole rows).  Column partials
 // go to part[b][slab][2][n]; k_abar_all sums them over slabs (fixed order) and forms the totals.
 constexpr int kSlab = 16;
-
-// Coefficient storage: fp32, or bf16 (GNCDE_COMPUTE_BF16_STORAGE / _BF16_MFMA) widened on load.
-__device__ __forceinline__ float coef_at(const float* c, size_t e) { return c[e]; }
-__device__ __forceinline__ float coef_at(const uint16_t* c, size_t e) {
-  return __builtin_bit_cast(float, (uint32_t)c[e] << 16);
-}
 
 template <typename CT>
 __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* __restrict__ ts,
@@ -121,15 +116,6 @@ __global__ void __launch_bounds__(256) k_spline_slab(int n, int T, const float* 
 // LDS so both A[i][k] and A[k][i] are read coalesced).  The block also finishes the reductions it needs: column sums
 // of its i and k ranges from k_spline_slab's slab partials (fixed order) and the totals; blocks on the first tile
 // row / the first tile publish the column sums / totals into red (the reverse sweep reads them later).
-__device__ __forceinline__ void abar_store(float* o, size_t e, size_t, float v) { o[e] = v; }
-// bf16 pair: hi = rne(v) in the first plane, lo = rne(v - hi) in the second (planes `plane` elements apart);
-// hi + lo carries 16 significand bits, so the split products lose ~2^-16, far below the PID tolerances.
-__device__ __forceinline__ void abar_store(uint16_t* o, size_t e, size_t plane, float v) {
-  const __bf16 h = (__bf16)v;
-  o[e] = __builtin_bit_cast(uint16_t, h);
-  o[plane + e] = __builtin_bit_cast(uint16_t, (__bf16)(v - (float)h));
-}
-
 template <typename OT>
 __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const float* __restrict__ fus,
                                                   const float* __restrict__ A, const float* __restrict__ dA,
@@ -255,9 +241,6 @@ __global__ void __launch_bounds__(256) k_abar_all(int n, int L, int slabs, const
 // never sums n^2 values, so one launch (k_abar_direct) goes from the coefficients to every layer's (I + Abar_l)
 // with no A / dA round trip through HBM and no reduction pass in front of it.
 //
-// csum per (sample, interval): [plane q = d, c, b, a][kind = row sum, column sum, diagonal][n], then the 4 totals.
-__host__ __device__ inline size_t csum_stride(int n) { return (size_t)12 * n + 4; }
-
 // grid (4 planes, T-1 intervals, B).  Fixed summation orders (deterministic, no atomics).
 template <typename CT>
 __global__ void __launch_bounds__(256) k_coef_sums(int n, int T, const CT* __restrict__ coef, float* __restrict__ csum) {
@@ -343,185 +326,14 @@ __global__ void __launch_bounds__(256) k_abar_direct(int n, int T, int L, const 
     combo_block(pc.E, pc.y, pc.cb, pc.hcur, pc.out, (int)blockIdx.x - nt * (nt + 1) / 2, b);
     return;
   }
-  int I = 0, rem = blockIdx.x;
-  while (rem >= nt - I) {
-    rem -= nt - I;
-    ++I;
-  }
-  const int K = I + rem;
-  const bool dg = I == K;
-  const int i0 = I * 32, k0 = K * 32;
-  const size_t nn = (size_t)n * n;
   // merged launch: the stage time as the combination computes it (it writes tst in this same launch)
-  float tb;
-  if (gt.grid) {  // the stage time from the grid (overlapped forms: no combination has written tst yet)
-    const float* g = gt.grid + (size_t)b * gt.G;
-    int ns = gt.nsteps[b];
-    ns = ns < 0 ? 0 : (ns > gt.G - 1 ? gt.G - 1 : ns);
-    const float tc = gt.k < ns ? g[gt.k] : g[ns];
-    const float hc = gt.k < ns ? g[gt.k + 1] - g[gt.k] : 0.f;
-    tb = gt.fsal ? (gt.k < ns ? g[gt.k + 1] : g[ns]) : stage_time(tc, gt.c, hc);
-  } else {
-    tb = pc.blocks ? (pc.cb.tend ? pc.cb.tend[b] : stage_time(pc.cb.tcur[b], pc.cb.c, pc.hcur[b])) : t[b];
-  }
-  const float* tsb = ts + (size_t)b * T;
-  const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;  // 32 x 8
-  const int idx = interval_index_wave(tsb, T, tb);
-  const float f = tb - tsb[idx], f3 = 3.0f * f;
-  const CT* cb = coef + ((size_t)b * (T - 1) + idx) * 4 * nn;
-  const float* cs = csum + ((size_t)b * (T - 1) + idx) * csum_stride(n);
-
-  // Every load of the block is issued before the first use (one memory round trip): the thread's elements of
-  // tile (I, K) and of the mirror (K, I), rows ty + 8 u; the node-vector planes; the totals.
-  float cx[4][4], cy[4][4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int y = ty + 8 * u;
-    const bool okx = i0 + y < n && k0 + tx < n, oky = !dg && k0 + y < n && i0 + tx < n;
-    const size_t ex = (size_t)(i0 + y) * n + k0 + tx, ey = (size_t)(k0 + y) * n + i0 + tx;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      cx[u][c] = okx ? coef_at(cb, c * nn + ex) : 0.f;
-      cy[u][c] = oky ? coef_at(cb, c * nn + ey) : 0.f;
-    }
-  }
-  // node vectors: thread (range r, kind k, node x) for tid < 192 evaluates value and derivative of one reduction
-  float pv[4] = {0.f, 0.f, 0.f, 0.f};
-  const int vr = tid / 96, vk = (tid / 32) % 3, vx = tid & 31, vnode = (vr ? k0 : i0) + vx;
-  if (tid < 192 && vnode < n)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) pv[c] = cs[(c * 3 + vk) * n + vnode];
-  float pt[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) pt[c] = cs[12 * n + c];
-  // the fusion table (to LDS) and, in diagonal blocks, the time-channel and data-spline coefficients of the
-  // block's rows: the same round trip, not one more after the first barrier
-  __shared__ float sF[GNCDE_MAX_LAYERS * GNCDE_FC];
-  const float fv = tid < L * GNCDE_FC ? fus[tid] : 0.f;
-  float tcv[3] = {0.f, 0.f, 0.f};
-  const size_t blk = (size_t)n * de2;
-  const int drows = n - i0 < 32 ? n - i0 : 32, dn = dx ? drows * de2 : 0;
-  const float* dc = dx ? data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)i0 * de2 : nullptr;
-  float dcv[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
-  if (dg) {
-    if (tid < 32 && i0 + tid < n) {
-      const float* tc = tcoef + ((size_t)b * (T - 1) + idx) * 3 * n + i0 + tid;
-      tcv[0] = tc[0];
-      tcv[1] = tc[n];
-      tcv[2] = tc[2 * n];
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int e = tid + 256 * h;
-      if (e < dn) {
-        dcv[h][0] = dc[e];
-        dcv[h][1] = dc[blk + e];
-        dcv[h][2] = dc[2 * blk + e];
-      }
-    }
-  }
-
-  __shared__ float tX[32][33], tXd[32][33], tY[32][33], tYd[32][33];
-  __shared__ float sv[2][6][32];  // [range][r, rd, c, cd, diag, diag_d][node]
-  float ax[4], adx[4], ay[4], ady[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int y = ty + 8 * u;
-    ax[u] = fmaf(f, fmaf(f, fmaf(f, cx[u][0], cx[u][1]), cx[u][2]), cx[u][3]);
-    adx[u] = fmaf(f, fmaf(f3, cx[u][0], 2.0f * cx[u][1]), cx[u][2]);
-    ay[u] = fmaf(f, fmaf(f, fmaf(f, cy[u][0], cy[u][1]), cy[u][2]), cy[u][3]);
-    ady[u] = fmaf(f, fmaf(f3, cy[u][0], 2.0f * cy[u][1]), cy[u][2]);
-    tX[y][tx] = ax[u];
-    tXd[y][tx] = adx[u];
-    tY[y][tx] = ay[u];
-    tYd[y][tx] = ady[u];
-  }
-  if (tid < 192) {
-    sv[vr][2 * vk][vx] = fmaf(f, fmaf(f, fmaf(f, pv[0], pv[1]), pv[2]), pv[3]);
-    sv[vr][2 * vk + 1][vx] = fmaf(f, fmaf(f3, pv[0], 2.0f * pv[1]), pv[2]);
-  }
-  const float s = fmaf(f, fmaf(f, fmaf(f, pt[0], pt[1]), pt[2]), pt[3]);
-  const float sd = fmaf(f, fmaf(f3, pt[0], 2.0f * pt[1]), pt[2]);
-  if (tid < L * GNCDE_FC) sF[tid] = fv;
-  if (dg) {
-    if (tid < 32 && i0 + tid < n) tg[(size_t)b * n + i0 + tid] = fmaf(f, fmaf(f3, tcv[0], 2.0f * tcv[1]), tcv[2]);
-    float* dxo = dx + (size_t)b * blk + (size_t)i0 * de2;  // CDE wrapper: dX[i][q] at t for the block's rows
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int e = tid + 256 * h;
-      if (e < dn) dxo[e] = fmaf(f, fmaf(f3, dcv[h][0], 2.0f * dcv[h][1]), dcv[h][2]);
-    }
-    for (int e = tid + 512; e < dn; e += 256) dxo[e] = fmaf(f, fmaf(f3, dc[e], 2.0f * dc[blk + e]), dc[2 * blk + e]);
-  }
-  __syncthreads();
-
-  // the rank-1 and diagonal families per layer: w_l over the rows, v_l over the columns of each range, u_l on
-  // the diagonal (diagonal blocks only)
-  __shared__ float sW[GNCDE_MAX_LAYERS][2][32], sV[GNCDE_MAX_LAYERS][2][32], sU[GNCDE_MAX_LAYERS][32];
-  for (int e = tid; e < L * 64; e += 256) {
-    const int l = e >> 6, r = (e >> 5) & 1, x = e & 31;
-    const float* fc = sF + l * GNCDE_FC;
-    const float ri = sv[r][0][x], rdi = sv[r][1][x], ci = sv[r][2][x], cdi = sv[r][3][x];
-    sW[l][r][x] = fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci +
-                  fc[GNCDE_FC_WC_DA] * cdi + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
-    sV[l][r][x] = fc[GNCDE_FC_VR_A] * ri + fc[GNCDE_FC_VR_DA] * rdi + fc[GNCDE_FC_VC_A] * ci + fc[GNCDE_FC_VC_DA] * cdi;
-    if (r == 0)
-      sU[l][x] = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * sv[0][4][x] + fc[GNCDE_FC_UD_DA] * sv[0][5][x] +
-                 fc[GNCDE_FC_UR_A] * ri + fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci +
-                 fc[GNCDE_FC_UC_DA] * cdi + fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
-  }
-  if (dg) {
-    const int i = i0 + tid;
-    if (tid < 32 && i < n) {
-      // q_l[i] = sum_k (I + Abar_l)[i][k]: the dense terms give their row / column sums, the w (row) family n
-      // copies, the v (column) family sum_k v_k (sum_k r_k = sum_k c_k = s), the diagonal once.
-      const float ri = sv[0][0][tid], rdi = sv[0][1][tid], ci = sv[0][2][tid], cdi = sv[0][3][tid];
-      const float dgi = sv[0][4][tid], dgdi = sv[0][5][tid], fn = (float)n;
-      if (qrow)
-        for (int l = 0; l < L; ++l) {
-          const float* fc = sF + l * GNCDE_FC;
-          float q = fc[GNCDE_FC_E_A] * ri + fc[GNCDE_FC_E_DA] * rdi + fc[GNCDE_FC_ET_A] * ci + fc[GNCDE_FC_ET_DA] * cdi;
-          q += fn * (fc[GNCDE_FC_WR_A] * ri + fc[GNCDE_FC_WR_DA] * rdi + fc[GNCDE_FC_WC_A] * ci +
-                     fc[GNCDE_FC_WC_DA] * cdi + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd);
-          q += (fc[GNCDE_FC_VR_A] + fc[GNCDE_FC_VC_A]) * s + (fc[GNCDE_FC_VR_DA] + fc[GNCDE_FC_VC_DA]) * sd;
-          q += fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dgi + fc[GNCDE_FC_UD_DA] * dgdi + fc[GNCDE_FC_UR_A] * ri +
-               fc[GNCDE_FC_UR_DA] * rdi + fc[GNCDE_FC_UC_A] * ci + fc[GNCDE_FC_UC_DA] * cdi +
-               fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
-          qrow[((size_t)l * B + b) * n + i] = q;
-        }
-    }
-  }
-  __syncthreads();
-  const float(*sX)[33] = dg ? tX : tY;  // transposed source of tile (I, K)
-  const float(*sXd)[33] = dg ? tXd : tYd;
-  const size_t plane = (size_t)L * layer_stride;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int y = ty + 8 * u;
-    if (i0 + y < n && k0 + tx < n) {  // tile (I, K): element (i0 + y, k0 + tx)
-      const float aki = sX[tx][y], dki = sXd[tx][y];
-      const size_t e = (size_t)b * nn + (size_t)(i0 + y) * n + k0 + tx;
-      for (int l = 0; l < L; ++l) {
-        const float* fc = sF + l * GNCDE_FC;
-        float v = fc[GNCDE_FC_E_A] * ax[u] + fc[GNCDE_FC_E_DA] * adx[u] + fc[GNCDE_FC_ET_A] * aki +
-                  fc[GNCDE_FC_ET_DA] * dki;
-        v += sW[l][0][y] + sV[l][1][tx];
-        if (dg && y == tx) v += sU[l][y];
-        abar_store(out, l * layer_stride + e, plane, v);
-      }
-    }
-    if (!dg && k0 + y < n && i0 + tx < n) {  // mirror tile (K, I): element (k0 + y, i0 + tx)
-      const float aik = tX[tx][y], dik = tXd[tx][y];
-      const size_t e = (size_t)b * nn + (size_t)(k0 + y) * n + i0 + tx;
-      for (int l = 0; l < L; ++l) {
-        const float* fc = sF + l * GNCDE_FC;
-        float v = fc[GNCDE_FC_E_A] * ay[u] + fc[GNCDE_FC_E_DA] * ady[u] + fc[GNCDE_FC_ET_A] * aik +
-                  fc[GNCDE_FC_ET_DA] * dik;
-        v += sW[l][1][y] + sV[l][0][tx];
-        abar_store(out, l * layer_stride + e, plane, v);
-      }
-    }
-  }
+  const float tb = gt.grid ? grid_stage_time(gt, b)  // overlapped forms: no combination has written tst yet
+                           : (pc.blocks ? (pc.cb.tend ? pc.cb.tend[b] : stage_time(pc.cb.tcur[b], pc.cb.c, pc.hcur[b]))
+                                        : t[b]);
+  __shared__ float lds[kFormsLdsFloats];
+  const FormsArgs fa{n, T, L, de2, B, ts, reinterpret_cast<const float*>(coef), csum, tcoef, fus, data_coef,
+                     reinterpret_cast<float*>(out), layer_stride, qrow, tg, dx};
+  forms_tile<CT, OT>(fa, (int)blockIdx.x, b, tb, lds);
 }
 
 // ---- epilogue: ODE dy = tg * Z; CDE dy[i,m] = tg[i] * sum_{l,k} Z[i,(m*de+l)*2+k] dX[i,l,k] --------
@@ -796,7 +608,7 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool ro
 
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared, unsigned* bars, float* keep, bool need_dy,
-                    const PendingCombo* pending, const FormBufs* forms) {
+                    const PendingCombo* pending, const FormBufs* forms, const FormsRide* ride) {
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
   VfWs w;
@@ -827,6 +639,9 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   const float* Zin = y;
   float* bufs[2] = {w.Z0, w.Z1};
   size_t wo = 0, bo = 0;
+  // the riding forms: samples split evenly over the hidden launches (the caller checked forms_ride: all fused)
+  const int nh = ride ? p.L - 1 : 0;
+  int hidx = 0;
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
     float* Zout = keep && l + 1 < p.L ? keep + (size_t)l * B * n * p.dims[l + 1] : bufs[l & 1];
@@ -840,8 +655,17 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     const int mode = layer_mode(p, l);
     if (mode >= 0 && (mode != 2 || fused_out)) {  // one fused launch (gncde_layer.hip)
       float* out = mode == 0 ? Zout : dy;
+      FormsRide r{};
+      if (mode == 0 && hidx < nh) {
+        r = *ride;
+        const unsigned per = ride->blocks / ride->nb;  // tile pairs
+        r.b0 = ride->b0 + ride->nb * hidx / nh;
+        r.nb = ride->b0 + ride->nb * (hidx + 1) / nh - r.b0;
+        r.blocks = per * r.nb;
+        ++hidx;
+      }
       layer_fused(p, l, mode, abar_layer(p, w.abar, l), Zin, w.wp + wo, w.bf + bo, w.q + (size_t)l * B * n, out, w.tg,
-                  w.dx, st);
+                  w.dx, st, r.blocks ? &r : nullptr);
       wo += (size_t)din * dout;
       bo += dout;
       Zin = Zout;
@@ -981,6 +805,18 @@ bool forms_overlap(const GncdeProblem& p) {
   return e && atoi(e) != 0;
 }
 
+// The fixed-grid solve's forms of evaluation e + 1 ride as extra workgroups in evaluation e's hidden-layer launches
+// (FormsRide, split by samples over them), into the second form buffer set: those launches leave most of every
+// CU's registers and LDS idle, and the forms do not depend on the stage input.  Needs every hidden layer on the
+// fused fp32 k_layer launch.  GNCDE_FORMS_RIDE=0 keeps one forms launch per evaluation (A/B, bitwise the same).
+bool forms_ride(const GncdeProblem& p) {
+  if (rows_eval_used(p) || p.compute != GNCDE_COMPUTE_FP32 || p.L < 2) return false;
+  for (int l = 0; l + 1 < p.L; ++l)
+    if (layer_mode(p, l) != 0) return false;
+  const char* e = getenv("GNCDE_FORMS_RIDE");
+  return !(e && atoi(e) == 0);
+}
+
 size_t form_set_floats(const GncdeProblem& p, int part) {  // abar, q, tg, dx of one form buffer set
   const size_t B = p.B, n = p.n;
   switch (part) {
@@ -1017,7 +853,7 @@ size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s) 
   size_t sz = generic_vf_workspace(p);
   sz += 9 * align_up(B * E * 4, 256);  // y, ytmp, K[7]
   sz += 4 * align_up(B * 4, 256);      // tcur, hcur, tstage, tnx
-  if (forms_overlap(p))
+  if (forms_overlap(p) || forms_ride(p))
     for (int q = 0; q < 4; ++q) sz += align_up(form_set_floats(p, q) * 4, 256);  // the second form buffer set
   return sz;
 }
@@ -1052,9 +888,10 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   const bool ovl = forms_overlap(p);
   SideStream* side = ovl ? side_stream() : nullptr;
   if (ovl && !side) return GNCDE_ERR_HIP;
+  const bool ride = !ovl && forms_ride(p);
   FormBufs fbs[2];
   std::vector<GridTime> plan;
-  if (ovl) {
+  if (ovl || ride) {
     VfWs w0;
     carve_vf(p, ws, w0);
     fbs[0] = FormBufs{w0.abar, w0.q, w0.tg, w0.dx};
@@ -1105,7 +942,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   PendingCombo pend{};
   bool has_pend = false;
   const char* nm = getenv("GNCDE_COMBO_SEPARATE");  // A/B: every combination as its own k_combo launch
-  const bool merge = !ovl && !(nm && atoi(nm) != 0);
+  const bool merge = !ovl && !ride && !(nm && atoi(nm) != 0);
   int ecur = 0, issued = 0;  // overlapped forms: the next evaluation, the forms launched so far
   const float* csum = generic_vf_csum(p, ws);
   auto issue_forms = [&](int e) {  // side stream: forms of evaluation e into set e % 2, once layers e - 2 are done
@@ -1116,6 +953,19 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     (void)hipEventRecord(side->ev[e & 1], side->s);
     issued = e + 1;
   };
+  const unsigned tpairs = cdiv(p.n, 32) * (cdiv(p.n, 32) + 1) / 2;
+  auto ride_of = [&](int e) {  // evaluation e's forms into set e % 2, all samples (generic_vf_eval splits them)
+    const FormBufs& f = fbs[e & 1];
+    FormsRide r{};
+    r.f = FormsArgs{p.n, p.T, p.L, 2 * p.cde_embed, B, p.ts, p.coef, csum, p.tcoef, p.fusion, p.data_coef,
+                    f.abar, (size_t)B * p.n * p.n, f.q, f.tg, p.cde_hidden > 0 ? f.dx : nullptr};
+    r.gt = plan[e];
+    r.b0 = 0;
+    r.nb = B;
+    r.blocks = tpairs * B;
+    return r;
+  };
+  if (ride) vf_forms_direct(p, tst, csum, fbs[0].abar, fbs[0].q, fbs[0].tg, fbs[0].dx, st, nullptr, &plan[0]);
   if (ovl) {  // the side stream starts after everything queued on st so far (the prepared workspace)
     (void)hipEventRecord(side->ev[4], st);
     (void)hipStreamWaitEvent(side->s, side->ev[4], 0);
@@ -1134,6 +984,14 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
       (void)hipEventRecord(side->ev[2 + (ecur & 1)], st);
       ++ecur;
       return r;
+    }
+    if (ride) {  // this evaluation's forms are in set ecur % 2; the next one's ride in its hidden layers
+      FormsRide r{};
+      if (ecur + 1 < (int)plan.size()) r = ride_of(ecur + 1);
+      const int res = generic_vf_eval(p, tst, yin, out, ws, st, true, &bars, keep_next, true, nullptr,
+                                      &fbs[ecur & 1], r.blocks ? &r : nullptr);
+      ++ecur;
+      return res;
     }
     const PendingCombo* pc = has_pend ? &pend : nullptr;
     has_pend = false;

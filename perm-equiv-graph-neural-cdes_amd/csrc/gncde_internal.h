@@ -224,8 +224,11 @@ void row_inv(int rows, int d, const float* Z, float* inv, hipStream_t st);
 int layer_mode(const GncdeProblem& p, int l);
 void permute_linear(int rows, int din, bool cde, const float* W, float* out, hipStream_t st);
 
+struct FormsRide;
+// ride (optional, fp32 hidden layers only): forms blocks launched after the layer's workgroups in the same grid
 void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, const float* Z, const float* wperm,
-                 const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st);
+                 const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st,
+                 const FormsRide* ride = nullptr);
 
 // generic (any-shape, multi-kernel) path: gncde_generic.hip
 size_t generic_vf_workspace(const GncdeProblem& p);
@@ -286,11 +289,29 @@ struct GridTime {
 struct FormBufs {
   float *abar, *q, *tg, *dx;
 };
+// What one forms tile block reads and writes (fp32 coefficients and planes; gncde_forms.h)
+struct FormsArgs {
+  int n, T, L, de2, B;  // de2 = 2 de (CDE wrapper), B = the batch (q_l rows are [L, B, n])
+  const float *ts, *coef, *csum, *tcoef, *fus, *data_coef;
+  float* abar;          // (I + Abar_l) planes [L, B, n, n]
+  size_t layer_stride;  // B n n
+  float *qrow, *tg, *dx;  // dx: nullptr unless the CDE wrapper
+};
+// A fixed-grid evaluation's forms riding as extra workgroups in the previous evaluation's hidden-layer launches
+// (gncde_layer.hip): samples [b0, b0 + nb) of the next evaluation's forms, its stage time from the grid (gt)
+struct FormsRide {
+  FormsArgs f;
+  GridTime gt;
+  int b0, nb;
+  unsigned blocks;  // tile pairs x nb (0: no ride)
+};
 // pending (optional): a stage combination folded into this evaluation's forms launch; forms (optional): the forms
-// were launched by the caller into these buffers (no forms launch here)
+// were launched by the caller into these buffers (no forms launch here); ride (optional, with forms): the next
+// evaluation's forms, split over this evaluation's hidden-layer launches
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared = false, unsigned* bars = nullptr, float* keep = nullptr,
-                    bool need_dy = true, const PendingCombo* pending = nullptr, const FormBufs* forms = nullptr);
+                    bool need_dy = true, const PendingCombo* pending = nullptr, const FormBufs* forms = nullptr,
+                    const FormsRide* ride = nullptr);
 // the workspace's fault word (a one-launch evaluation's barrier gave up): solver status 4 when set
 const int* generic_vf_fault(const GncdeProblem& p, char* ws);
 

@@ -21,6 +21,7 @@
 //      step), so the 16-column contraction happens inside the MFMA accumulation.
 //
 // This replaces, per layer, two GEMM launches, the row-norm kernel and the read-out's 16-lane shuffle epilogue.
+#include "gncde_forms.h"
 #include "gncde_internal.h"
 
 #include <type_traits>
@@ -50,6 +51,7 @@ struct LayerArgs {
   float* out;          // [B, n, DOUT] (CDE: dy [B, n, H])
   const float* tg;     // [B n] time-channel derivative (MODE 1, 2)
   const float* dx;     // [B n, 16] data-spline derivative (MODE 2)
+  FormsRide ride;      // fp32 hidden layers: the next evaluation's forms as the grid's z >= 1 workgroups
 };
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
@@ -94,6 +96,16 @@ __global__ void __launch_bounds__((64 * layer_waves<DOUT, MODE, BF, NT>()), (NT 
   static_assert(MODE == 2 || NT == 2, "the Linear epilogue's tile split assumes two row tiles");
   static_assert(!BF || NT == 2, "bf16 modes: two row tiles");
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  if (blockIdx.z) {  // a forms block of the next evaluation riding in this launch (FormsRide; 256 threads)
+    if constexpr (MODE == 0 && !BF && NT == 2) {
+      const unsigned fb = (blockIdx.z - 1) * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x;
+      if (fb < a.ride.blocks) {
+        const int nt = (a.n + 31) >> 5, np = nt * (nt + 1) / 2, b = a.ride.b0 + (int)fb / np;
+        forms_tile<float, float>(a.ride.f, (int)fb % np, b, grid_stage_time(a.ride.gt, b), smem);
+      }
+    }
+    return;
+  }
   constexpr int WV = layer_waves<DOUT, MODE, BF, NT>();
   constexpr int NTH = 64 * WV;   // threads
   constexpr int kRows = 16 * NT;
@@ -610,10 +622,15 @@ void launch(const LayerArgs& a, int B, hipStream_t st) {
       }
     }
   }
-  const size_t sm = layer_smem<DIN>(a.n, BF);
+  size_t sm = layer_smem<DIN>(a.n, BF);
   const int rows = 16 * kTiles;
-  hipLaunchKernelGGL((k_layer<DIN, DOUT, MODE, BF, kTiles>), dim3((a.n + rows - 1) / rows * split, B), dim3(256), sm,
-                     st, a);
+  const unsigned gx = (a.n + rows - 1) / rows * split;
+  unsigned gz = 1;
+  if (MODE == 0 && !BF && a.ride.blocks) {  // the riding forms blocks: whole z planes after the layer's plane
+    gz += (a.ride.blocks + gx * B - 1) / (gx * B);
+    sm = sm > sizeof(float) * kFormsLdsFloats ? sm : sizeof(float) * kFormsLdsFloats;
+  }
+  hipLaunchKernelGGL((k_layer<DIN, DOUT, MODE, BF, kTiles>), dim3(gx, B, gz), dim3(256), sm, st, a);
 }
 
 template <int DIN, bool BF>
@@ -659,8 +676,10 @@ void permute_linear(int rows, int din, bool cde, const float* W, float* out, hip
 }
 
 void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, const float* Z, const float* wperm,
-                 const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st) {
+                 const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st,
+                 const FormsRide* ride) {
   LayerArgs a{};
+  if (ride && mode == 0 && p.compute == GNCDE_COMPUTE_FP32) a.ride = *ride;
   a.n = p.n;
   a.abar = abar;
   a.Z = Z;

@@ -539,11 +539,15 @@ def test_readout_tiles_bitwise(G, monkeypatch, B, n, dims):
 
 @pytest.mark.parametrize("method", ["rk4", "tsit5"])
 def test_forms_overlap_bitwise(G, monkeypatch, method):
-    """With GNCDE_FORMS_OVERLAP=1 the fixed-grid generic solve launches each evaluation's forms one evaluation ahead
-    on a side stream, timed from the grid (GridTime), into alternating buffer sets; by default (0) the forms follow
-    the stage combination on the caller's stream.  Same stage times, same kernels: bitwise the same trajectory, stats and
-    stage record — ragged per-sample grids (padded steps) included, at config 3's shape and a mixed-width one."""
-    for B, n, dims, distinct in ((64, 129, [64, 64, 64, 1024], 4), (5, 70, [32, 16, 32, 512], 3)):
+    """The fixed-grid generic solve places each evaluation's forms three ways: by default they ride as extra workgroups
+    in the previous evaluation's hidden-layer launches (FormsRide, the samples split over those launches), with
+    GNCDE_FORMS_RIDE=0 they get their own launch behind the stage combination (the combination's blocks folded in),
+    and with GNCDE_FORMS_OVERLAP=1 they run one evaluation ahead on a side stream.  All three time the stage from the
+    grid or the combination with the same arithmetic and run the same forms code into alternating buffer sets:
+    bitwise the same trajectory, stats and stage record — ragged per-sample grids (padded steps) included, at config
+    3's shape, a mixed-width one (5 samples over two hidden launches) and one hidden layer (L = 2)."""
+    for B, n, dims, distinct in ((64, 129, [64, 64, 64, 1024], 4), (5, 70, [32, 16, 32, 512], 3),
+                                 (3, 40, [32, 16, 512], 2)):
         H, de, L = dims[0], 8, len(dims) - 1
         rng, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(43, B, n, 4, 1.0, H, de, L, distinct=distinct, dims=dims)
         prob = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
@@ -555,15 +559,17 @@ def test_forms_overlap_bitwise(G, monkeypatch, method):
         floats = G.engine.stage_record_floats(prob, spec)
         yd = torch.tensor(y0, dtype=torch.float32, device="cuda")
         outs = {}
-        for v in ("0", "1"):
-            monkeypatch.setenv("GNCDE_FORMS_OVERLAP", v)
+        for v, (ovl, ride) in {"ride": ("0", "1"), "inline": ("0", "0"), "overlap": ("1", "0")}.items():
+            monkeypatch.setenv("GNCDE_FORMS_OVERLAP", ovl)
+            monkeypatch.setenv("GNCDE_FORMS_RIDE", ride)
             rec = torch.zeros(B, max(floats, 1), device="cuda")
             sp = dataclasses.replace(spec, stage_rec=rec) if floats else spec
             ys, st = G.integrate(prob, sp, yd, stats=True)
             outs[v] = (ys.clone(), st.clone(), rec)
-        assert bool(torch.isfinite(outs["1"][0]).all())
-        for a, b in zip(outs["0"], outs["1"]):
-            assert torch.equal(a, b)
+        assert bool(torch.isfinite(outs["ride"][0]).all())
+        for v in ("inline", "overlap"):
+            for a, b in zip(outs["ride"], outs[v]):
+                assert torch.equal(a, b), (B, n, v)
 
 
 def test_bwd_row_blocks_per_workgroup_bitwise(G, monkeypatch):
