@@ -279,8 +279,23 @@ constexpr int kComboThreads = 256;
 __device__ __forceinline__ void combo_block(size_t E, const float* __restrict__ y, const Combo& cb,
                                             const float* __restrict__ hcur, float* __restrict__ out, int bx, int b) {
   const size_t e0 = (size_t)bx * (kComboThreads * kComboU) + threadIdx.x;
-  if (cb.tst && e0 == 0) cb.tst[b] = cb.tend ? cb.tend[b] : stage_time(cb.tcur[b], cb.c, hcur[b]);
-  const float hb = hcur[b];
+  float hb, tc = 0.f;
+  if (cb.grid) {  // the step's geometry, as k_grid_step forms it
+    const float* g = cb.grid + (size_t)b * cb.G;
+    int ns = cb.nsteps[b];
+    ns = ns < 0 ? 0 : (ns > cb.G - 1 ? cb.G - 1 : ns);
+    const bool on = cb.gk < ns;
+    tc = on ? g[cb.gk] : g[ns];
+    hb = on ? g[cb.gk + 1] - g[cb.gk] : 0.f;
+    if (e0 == 0) {
+      cb.tcur_out[b] = tc;
+      cb.hcur_out[b] = hb;
+      cb.tnx_out[b] = on ? g[cb.gk + 1] : g[ns];
+    }
+  } else {
+    hb = hcur[b];
+  }
+  if (cb.tst && e0 == 0) cb.tst[b] = cb.tend ? cb.tend[b] : stage_time(cb.grid ? tc : cb.tcur[b], cb.c, hb);
   float kv[7][kComboU], yv[kComboU];
 #pragma unroll
   for (int u = 0; u < kComboU; ++u) {
@@ -639,9 +654,17 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
   const float* Zin = y;
   float* bufs[2] = {w.Z0, w.Z1};
   size_t wo = 0, bo = 0;
-  // the riding forms: samples split evenly over the hidden launches (the caller checked forms_ride: all fused)
-  const int nh = ride ? p.L - 1 : 0;
-  int hidx = 0;
+  // the riding forms: samples split evenly over the hidden launches [hf, hf + nh) (the caller checked forms_ride:
+  // every hidden layer is a fused launch).  A/B: GNCDE_FORMS_RIDE=2 puts them all in the first one, 3 in the last.
+  int nh = ride ? p.L - 1 : 0, hf = 0, hidx = 0;
+  if (ride) {
+    const char* e = getenv("GNCDE_FORMS_RIDE");
+    const int v = e ? atoi(e) : 1;
+    if (v == 2 || v == 3) {
+      hf = v == 3 ? p.L - 2 : 0;
+      nh = 1;
+    }
+  }
   for (int l = 0; l < p.L; ++l) {
     const int din = p.dims[l], dout = p.dims[l + 1];
     float* Zout = keep && l + 1 < p.L ? keep + (size_t)l * B * n * p.dims[l + 1] : bufs[l & 1];
@@ -656,14 +679,15 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
     if (mode >= 0 && (mode != 2 || fused_out)) {  // one fused launch (gncde_layer.hip)
       float* out = mode == 0 ? Zout : dy;
       FormsRide r{};
-      if (mode == 0 && hidx < nh) {
+      if (mode == 0 && ride && hidx >= hf && hidx < hf + nh) {
+        const int q = hidx - hf;
         r = *ride;
         const unsigned per = ride->blocks / ride->nb;  // tile pairs
-        r.b0 = ride->b0 + ride->nb * hidx / nh;
-        r.nb = ride->b0 + ride->nb * (hidx + 1) / nh - r.b0;
+        r.b0 = ride->b0 + ride->nb * q / nh;
+        r.nb = ride->b0 + ride->nb * (q + 1) / nh - r.b0;
         r.blocks = per * r.nb;
-        ++hidx;
       }
+      if (mode == 0) ++hidx;
       layer_fused(p, l, mode, abar_layer(p, w.abar, l), Zin, w.wp + wo, w.bf + bo, w.q + (size_t)l * B * n, out, w.tg,
                   w.dx, st, r.blocks ? &r : nullptr);
       wo += (size_t)din * dout;
@@ -1001,8 +1025,18 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   float* rec = G >= 2 ? s.stage_rec : nullptr;
   int rec_k = 0, rec_i = 0;  // slot of the next combination's output (rec_i == 0: not recorded)
   bool fsal_next = false;     // the combination forms Tsit5's FSAL stage input (its time: the step's end knot)
-  auto combo = [&](std::initializer_list<std::pair<int, float>> terms, float* out, float c_next, bool has_next) {
+  auto combo = [&](std::initializer_list<std::pair<int, float>> terms, float* out, float c_next, bool has_next,
+                   int gk = -1) {
     Combo cb{};
+    if (gk >= 0) {  // step gk's k_grid_step folded in (nothing before this combination reads its outputs)
+      cb.grid = s.grid;
+      cb.nsteps = s.nsteps;
+      cb.G = G;
+      cb.gk = gk;
+      cb.tcur_out = tcur;
+      cb.hcur_out = hcur;
+      cb.tnx_out = tnx;
+    }
     if (rec && rec_i > 0) {
       cb.rec = rec + ((size_t)rec_k * (S - 1) + rec_i - 1) * E;
       cb.rec_stride = (size_t)(G - 1) * (S - 1) * E;
@@ -1065,11 +1099,14 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     rc |= eval(y, K[0]);
     for (int k = 0; k < steps && rc == GNCDE_OK; ++k) {
       flush();
-      hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst, tnx);
+      // With the forms riding (timed from the grid) nothing reads the step geometry before the step's first
+      // combination, which then forms it itself: one launch per step fewer.
+      if (!ride)
+        hipLaunchKernelGGL(k_grid_step, dim3(gb), dim3(256), 0, st, B, G, k, s.grid, s.nsteps, tcur, hcur, tst, tnx);
       cur_k = k;
       rec_k = k;
       rec_i = 1;
-      combo({{0, TSIT5_A21}}, yt, TSIT5_C2, true);  // K[0] is the FSAL value; k_grid_step set this step's h
+      combo({{0, TSIT5_A21}}, yt, TSIT5_C2, true, ride ? k : -1);  // K[0] is the FSAL value
       rec_i = 2;
       eval_combo(yt, 1, {{0, TSIT5_A31}, {1, TSIT5_A32}}, yt, TSIT5_C3, true);
       rec_i = 3;

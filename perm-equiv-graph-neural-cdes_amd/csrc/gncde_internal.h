@@ -261,6 +261,12 @@ struct Combo {
   float* tst;
   float* rec;         // stage record slot of this stage input ([B, G-1, S-1, E] at (k, i-1)) or nullptr
   size_t rec_stride;  // floats between consecutive samples' slots: (G-1)*(S-1)*E
+  // grid != nullptr: step gk's geometry from the grid folded in (k_grid_step's work and arithmetic): h and the
+  // stage time come from grid / nsteps, and block 0 of each sample writes tcur, hcur_out and tnx
+  const float* grid;
+  const int32_t* nsteps;
+  int G, gk;
+  float *tcur_out, *hcur_out, *tnx_out;
 };
 // A stage combination folded into the next evaluation's k_abar_direct launch: its blocks follow the form tiles in
 // the grid (the two are independent: the forms read the coefficients at the stage's time, which they compute from
