@@ -623,7 +623,9 @@ void generic_vf_prepare(const GncdeProblem& p, char* ws, hipStream_t st, bool ro
 
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared, unsigned* bars, float* keep, bool need_dy,
-                    const PendingCombo* pending, const FormBufs* forms, const FormsRide* ride) {
+                    const PendingCombo* pending, const FormBufs* forms, const FormsRide* ride,
+                    const PendingCombo* post, bool* post_done) {
+  if (post_done) *post_done = false;
   const int B = p.B, n = p.n;
   const size_t nn = (size_t)n * n;
   VfWs w;
@@ -688,8 +690,10 @@ int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float
         r.blocks = per * r.nb;
       }
       if (mode == 0) ++hidx;
-      layer_fused(p, l, mode, abar_layer(p, w.abar, l), Zin, w.wp + wo, w.bf + bo, w.q + (size_t)l * B * n, out, w.tg,
-                  w.dx, st, r.blocks ? &r : nullptr);
+      const bool folded = layer_fused(p, l, mode, abar_layer(p, w.abar, l), Zin, w.wp + wo, w.bf + bo,
+                                      w.q + (size_t)l * B * n, out, w.tg, w.dx, st, r.blocks ? &r : nullptr,
+                                      mode == 2 ? post : nullptr);
+      if (folded && post_done) *post_done = true;
       wo += (size_t)din * dout;
       bo += dout;
       Zin = Zout;
@@ -995,6 +999,12 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     (void)hipStreamWaitEvent(side->s, side->ev[4], 0);
     issue_forms(0);
   }
+  // With the forms riding, a combination that follows a read-out runs in that launch's epilogue (PendingCombo as
+  // `post`); GNCDE_COMBO_FOLD=0 keeps it a k_combo launch (A/B, bitwise the same)
+  const char* nf = getenv("GNCDE_COMBO_FOLD");
+  const bool fold = ride && !(nf && atoi(nf) == 0);
+  PendingCombo post_pc{};
+  bool post_on = false, post_done = false;
   auto flush = [&]() {
     if (has_pend)
       hipLaunchKernelGGL(k_combo, gc, dim3(kComboThreads), 0, st, B, E, pend.y, pend.cb, pend.hcur, pend.out);
@@ -1012,8 +1022,10 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     if (ride) {  // this evaluation's forms are in set ecur % 2; the next one's ride in its hidden layers
       FormsRide r{};
       if (ecur + 1 < (int)plan.size()) r = ride_of(ecur + 1);
+      post_done = false;
       const int res = generic_vf_eval(p, tst, yin, out, ws, st, true, &bars, keep_next, true, nullptr,
-                                      &fbs[ecur & 1], r.blocks ? &r : nullptr);
+                                      &fbs[ecur & 1], r.blocks ? &r : nullptr, post_on ? &post_pc : nullptr,
+                                      &post_done);
       ++ecur;
       return res;
     }
@@ -1025,8 +1037,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   float* rec = G >= 2 ? s.stage_rec : nullptr;
   int rec_k = 0, rec_i = 0;  // slot of the next combination's output (rec_i == 0: not recorded)
   bool fsal_next = false;     // the combination forms Tsit5's FSAL stage input (its time: the step's end knot)
-  auto combo = [&](std::initializer_list<std::pair<int, float>> terms, float* out, float c_next, bool has_next,
-                   int gk = -1) {
+  auto make_combo = [&](std::initializer_list<std::pair<int, float>> terms, float c_next, bool has_next, int gk) {
     Combo cb{};
     if (gk >= 0) {  // step gk's k_grid_step folded in (nothing before this combination reads its outputs)
       cb.grid = s.grid;
@@ -1051,6 +1062,11 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     cb.tcur = tcur;
     cb.tend = fsal_next ? tnx : nullptr;
     cb.tst = has_next ? tst : nullptr;
+    return cb;
+  };
+  auto combo = [&](std::initializer_list<std::pair<int, float>> terms, float* out, float c_next, bool has_next,
+                   int gk = -1) {
+    const Combo cb = make_combo(terms, c_next, has_next, gk);
     flush();
     if (has_next && merge) {  // the next evaluation reads `out` (and its stage time) first: fold it into that launch
       pend = PendingCombo{cb, y, hcur, out, E, gc.x};
@@ -1061,13 +1077,25 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   };
 
   // Stage j's evaluation into K[j] followed by the next stage's input out = y + h sum_i a_i K_i (terms end with
-  // K[j]).  (Folding the combination into the read-out k_layer's epilogue measured slower at config 3, 15.8 vs
-  // 15.15 ms per solve: the epilogue's dependent K loads lengthen the critical launch by more than k_combo costs.)
+  // K[j]).  (Round 2 folded the combination into the read-out k_layer's epilogue and measured it slower at config 3,
+  // 15.8 vs 15.15 ms per solve: the epilogue's dependent K loads lengthened the critical launch by more than k_combo
+  // cost.  Round 5's fold issues those loads right after each wave's K loop, under the partials' barrier.)
   int rc = GNCDE_OK;
   int cur_k = 0;  // the step eval_combo's evaluations belong to (activation slab (cur_k, j))
   auto eval_combo = [&](const float* yin, int j, std::initializer_list<std::pair<int, float>> terms, float* out,
                         float c_next, bool has_next) {
     keep_next = act(cur_k, j);
+    if (fold) {  // the combination rides in the evaluation's read-out epilogue when that launch can take it
+      flush();
+      post_pc = PendingCombo{make_combo(terms, c_next, has_next, -1), y, hcur, out, E, gc.x};
+      post_on = true;
+      rc |= eval(yin, K[j]);
+      post_on = false;
+      if (!post_done)
+        hipLaunchKernelGGL(k_combo, gc, dim3(kComboThreads), 0, st, B, E, post_pc.y, post_pc.cb, post_pc.hcur,
+                           post_pc.out);
+      return;
+    }
     rc |= eval(yin, K[j]);
     combo(terms, out, c_next, has_next);
   };

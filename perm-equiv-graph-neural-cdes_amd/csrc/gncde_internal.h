@@ -225,10 +225,13 @@ int layer_mode(const GncdeProblem& p, int l);
 void permute_linear(int rows, int din, bool cde, const float* W, float* out, hipStream_t st);
 
 struct FormsRide;
-// ride (optional, fp32 hidden layers only): forms blocks launched after the layer's workgroups in the same grid
-void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, const float* Z, const float* wperm,
+struct PendingCombo;
+// ride (optional, fp32 hidden layers only): forms blocks launched after the layer's workgroups in the same grid;
+// post (optional, the fp32 CDE read-out): the stage combination whose last term is this launch's output, folded into
+// its epilogue.  Returns whether post was folded (else the caller launches it).
+bool layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, const float* Z, const float* wperm,
                  const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st,
-                 const FormsRide* ride = nullptr);
+                 const FormsRide* ride = nullptr, const PendingCombo* post = nullptr);
 
 // generic (any-shape, multi-kernel) path: gncde_generic.hip
 size_t generic_vf_workspace(const GncdeProblem& p);
@@ -314,10 +317,12 @@ struct FormsRide {
 // pending (optional): a stage combination folded into this evaluation's forms launch; forms (optional): the forms
 // were launched by the caller into these buffers (no forms launch here); ride (optional, with forms): the next
 // evaluation's forms, split over this evaluation's hidden-layer launches
+// post (optional): the stage combination that follows this evaluation; *post_done tells whether the read-out launch
+// took it (else the caller launches it)
 int generic_vf_eval(const GncdeProblem& p, const float* t, const float* y, float* dy, char* ws,
                     hipStream_t st, bool prepared = false, unsigned* bars = nullptr, float* keep = nullptr,
                     bool need_dy = true, const PendingCombo* pending = nullptr, const FormBufs* forms = nullptr,
-                    const FormsRide* ride = nullptr);
+                    const FormsRide* ride = nullptr, const PendingCombo* post = nullptr, bool* post_done = nullptr);
 // the workspace's fault word (a one-launch evaluation's barrier gave up): solver status 4 when set
 const int* generic_vf_fault(const GncdeProblem& p, char* ws);
 

@@ -52,6 +52,10 @@ struct LayerArgs {
   const float* tg;     // [B n] time-channel derivative (MODE 1, 2)
   const float* dx;     // [B n, 16] data-spline derivative (MODE 2)
   FormsRide ride;      // fp32 hidden layers: the next evaluation's forms as the grid's z >= 1 workgroups
+  // fp32 CDE read-out (post.blocks != 0): the stage combination that follows this evaluation, folded into the
+  // epilogue.  Its last term is this launch's own output; every thread sums its elements' earlier terms (the same
+  // fmaf order as k_combo) from loads issued right after its K loop, then adds the output read back from LDS.
+  PendingCombo post;
 };
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
@@ -514,6 +518,43 @@ __global__ void __launch_bounds__((64 * layer_waves<DOUT, MODE, BF, NT>()), (NT 
     };
     with_count(ntl, kloop);
     LAYER_STAMP(5);
+    // The folded stage combination: element k = tid + NTH u of the workgroup's (row, channel) block, row-major over
+    // its CW channels; y and the earlier stage outputs are loaded here, under the bias term and the partials' barrier.
+    constexpr int CW = 16 * CT;
+    constexpr int CE = 16 * NT * CW / NTH;  // elements per thread (5 / 4 / 2 for the launches here)
+    static_assert(CE * NTH == 16 * NT * CW, "combination elements per thread");
+    const bool post = !BF && a.post.blocks != 0;
+    const Combo& cb = a.post.cb;
+    const size_t pE = (size_t)n * DOUT;
+    float ppre[CE], pyv[CE], phb = 0.f, ptc = 0.f;
+    if (post) {
+      float kv[6][CE];
+#pragma unroll
+      for (int u = 0; u < CE; ++u) {
+        const int k = tid + NTH * u, R = r0 + k / CW;
+        const size_t o = (size_t)b * pE + (size_t)R * DOUT + 16 * ch * CT + k % CW;
+        pyv[u] = R < n ? a.post.y[o] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) kv[j][u] = (R < n && j < cb.nk - 1) ? cb.K[j][o] : 0.f;
+      }
+      if (cb.grid) {  // the step's geometry, as k_grid_step forms it
+        const float* g = cb.grid + (size_t)b * cb.G;
+        int ns = cb.nsteps[b];
+        ns = ns < 0 ? 0 : (ns > cb.G - 1 ? cb.G - 1 : ns);
+        ptc = cb.gk < ns ? g[cb.gk] : g[ns];
+        phb = cb.gk < ns ? g[cb.gk + 1] - g[cb.gk] : 0.f;
+      } else {
+        phb = a.post.hcur[b];
+      }
+#pragma unroll
+      for (int u = 0; u < CE; ++u) {
+        float sp = 0.f;
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (j < cb.nk - 1) sp = fmaf(cb.a[j], kv[j][u], sp);
+        ppre[u] = sp;
+      }
+    }
     // bias term of each j quarter; rows 16 t + 4 hi + r, channel m
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -554,11 +595,38 @@ __global__ void __launch_bounds__((64 * layer_waves<DOUT, MODE, BF, NT>()), (NT 
           const int R = r0 + 16 * t + 4 * hi + r;
           if (R < n) {
             const size_t o = (nb + R) * DOUT + m;
-            a.out[o] = gpre[t][r] * fin[t][r];
+            const float v = gpre[t][r] * fin[t][r];
+            a.out[o] = v;
+            if (post) Zs[(16 * t + 4 * hi + r) * CW + 16 * w + lo] = v;  // (Ps is dead: every K loop is done)
           }
         }
     }
     LAYER_STAMP(6);
+    if (post) {  // out = y + h (sum of the earlier terms + a_last K_last), K_last this launch's output
+      __syncthreads();
+      const float al = cb.a[cb.nk - 1];
+#pragma unroll
+      for (int u = 0; u < CE; ++u) {
+        const int k = tid + NTH * u, R = r0 + k / CW;
+        if (R < n) {
+          const size_t e = (size_t)R * DOUT + 16 * ch * CT + k % CW;
+          const float v = fmaf(phb, fmaf(al, Zs[k], ppre[u]), pyv[u]);
+          a.post.out[(size_t)b * pE + e] = v;
+          if (cb.rec) cb.rec[(size_t)b * cb.rec_stride + e] = v;
+        }
+      }
+      if (r0 == 0 && ch == 0 && tid == 0) {  // (the sample's first workgroup, like k_combo's block 0)
+        if (cb.grid) {
+          const float* g = cb.grid + (size_t)b * cb.G;
+          int ns = cb.nsteps[b];
+          ns = ns < 0 ? 0 : (ns > cb.G - 1 ? cb.G - 1 : ns);
+          cb.tcur_out[b] = ptc;
+          cb.hcur_out[b] = phb;
+          cb.tnx_out[b] = cb.gk < ns ? g[cb.gk + 1] : g[ns];
+        }
+        if (cb.tst) cb.tst[b] = cb.tend ? cb.tend[b] : stage_time(cb.grid ? ptc : cb.tcur[b], cb.c, phb);
+      }
+    }
   }
 }
 
@@ -675,11 +743,14 @@ void permute_linear(int rows, int din, bool cde, const float* W, float* out, hip
   hipLaunchKernelGGL(k_permute_linear, dim3((tot + 255) / 256), dim3(256), 0, st, rows, din, cde ? 1 : 0, W, out);
 }
 
-void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, const float* Z, const float* wperm,
+bool layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, const float* Z, const float* wperm,
                  const float* bf, const float* q, float* out, const float* tg, const float* dx, hipStream_t st,
-                 const FormsRide* ride) {
+                 const FormsRide* ride, const PendingCombo* post) {
   LayerArgs a{};
   if (ride && mode == 0 && p.compute == GNCDE_COMPUTE_FP32) a.ride = *ride;
+  const bool folded = post && mode == 2 && p.compute == GNCDE_COMPUTE_FP32 && p.cde_hidden > 0 && post->cb.nk >= 1 &&
+                      post->cb.nk <= 7 && post->cb.K[post->cb.nk - 1] == out;
+  if (folded) a.post = *post;
   a.n = p.n;
   a.abar = abar;
   a.Z = Z;
@@ -697,11 +768,12 @@ void layer_fused(const GncdeProblem& p, int l, int mode, const float* abar, cons
     if (din == 16) dispatch_dout<16, true>(a, p.B, dout, mode, st);
     else if (din == 32) dispatch_dout<32, true>(a, p.B, dout, mode, st);
     else dispatch_dout<64, true>(a, p.B, dout, mode, st);
-    return;
+    return false;
   }
   if (din == 16) dispatch_dout<16, false>(a, p.B, dout, mode, st);
   else if (din == 32) dispatch_dout<32, false>(a, p.B, dout, mode, st);
   else dispatch_dout<64, false>(a, p.B, dout, mode, st);
+  return folded;
 }
 
 }  // namespace gncde
