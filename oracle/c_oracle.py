@@ -11,12 +11,14 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "libgncde_oracle.so")
+# GNCDE_ORACLE_LIB selects another build of the same source (the ASan/UBSan one: `make -C oracle asan`).
+LIB = os.environ.get("GNCDE_ORACLE_LIB") or os.path.join(HERE, "build", "libgncde_oracle.so")
 _lib = None
 
 
 def build():
-    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+    target = os.path.relpath(LIB, HERE) if os.path.dirname(os.path.abspath(LIB)).startswith(HERE) else "all"
+    subprocess.run(["make", "-C", HERE, "-s", target], check=True)
 
 
 def load():

@@ -135,12 +135,18 @@ def verify_provenance(lib) -> str:
     """Refuse a library that was not compiled from this tree's kernel sources.  An explicit experiment build
     (GNCDE_LIB with GNCDE_LIB_UNVERIFIED=1, tools/ab_*.sh only) is loaded with a warning instead."""
     built = lib.gncde_source_sha256().decode()
-    tree = source_sha256()
-    if built != tree:
-        if os.environ.get("GNCDE_LIB") and os.environ.get("GNCDE_LIB_UNVERIFIED") == "1":
+    if os.environ.get("GNCDE_LIB") and os.environ.get("GNCDE_LIB_UNVERIFIED") == "1":
+        # The opt-out is checked first, so it also works where no csrc/ tree lies next to the package.
+        try:
+            tree = source_sha256()
+        except GncdeError:
+            tree = "no-sources"
+        if built != tree:
             print(f"gncde: WARNING experiment library {LIB_PATH} built from sources {built[:16]}, tree "
                   f"{tree[:16]}", file=sys.stderr)
-            return built
+        return built
+    tree = source_sha256()
+    if built != tree:
         raise GncdeError(f"{LIB_PATH} was built from kernel sources {built[:16]}..., this tree's are "
                          f"{tree[:16]}...: rebuild with `make -C perm-equiv-graph-neural-cdes_amd`")
     return built
