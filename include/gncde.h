@@ -93,16 +93,15 @@ enum { GNCDE_RK4 = 0, GNCDE_TSIT5 = 1 };
  *   BF16:         the n x n products (I + Abar_l) Z run on v_mfma_f32_16x16x32_bf16 with both operands split into
  *                 bf16 (hi, lo) pairs (three products, fp32 accumulation, ~2^-16 relative: fp32-class results and
  *                 no rounding noise for the adaptive controller).  Inputs stay fp32.
- *   BF16_STORAGE: as BF16, and `coef` holds bfloat16 values (same shape, uint16 storage): the operator spline's
- *                 input is quantised to bf16, halving the dominant HBM stream.  Results equal the fp32 reference
- *                 evaluated on the bf16-rounded coefficients.
- *   BF16_MFMA:    `coef` in bfloat16 as for BF16_STORAGE, and EVERY matrix product — (I + Abar_l) diag(inv) Z, the
- *                 Linears, the CDE read-out — on v_mfma_f32_16x16x32_bf16 with single-plane bf16 operands rounded
- *                 from the fp32 values and fp32 accumulation (~2^-8 relative per operand: a genuinely bf16 solve, the
- *                 throughput mode of config 5).  Only the one-launch evaluation runs it (gncde_rows.hip: n <= 256,
- *                 one hidden width H in {16, 32, 64}, ODE output or the de = 8 read-out); other shapes return
- *                 GNCDE_ERR_UNSUPPORTED, and so does the PID controller (its error estimate reads the mode's
- *                 ~1e-2 per-stage rounding noise as truncation error and takes 12-21x the steps): fixed grids only.
+ *   BF16_STORAGE: `coef` holds bfloat16 values (same shape, uint16 storage): the operator spline's input is
+ *                 quantised to bf16, halving the dominant HBM stream.  On the persistent solve (gncde_rows.hip, PREC
+ *                 2: configs 5's shapes) every product stays fp32 on the exactly widened values, so its results are
+ *                 BITWISE the fp32 solve of the bf16-rounded coefficients; on the multi-kernel path the products
+ *                 are BF16's split pairs.
+ *   BF16_MFMA:    (retired, round 6) single-plane bf16 operands for every product.  It lives only in an experiment
+ *                 build (`make experiment`, GNCDE_EXPERIMENT_BF16_MFMA): 8-15 % from fp32 on a fixed grid, 12-21x
+ *                 the steps under the PID controller, and no BASELINE config uses it.  The product library returns
+ *                 GNCDE_ERR_UNSUPPORTED for it.
  * Splines, reductions, RMSNorm, solver and epilogues stay fp32.  The bf16 modes always take the generic path.
  * Their reverse mode (gncde_integrate_vjp*) is the fp32 discrete adjoint over the coefficients the forward read
  * (BF16_STORAGE: the bf16 planes widened exactly into the workspace head, which gncde_vjp_workspace_bytes

@@ -26,8 +26,13 @@ int validate_problem(const GncdeProblem* p) {
   } else if (p->cde_hidden < 0) {
     return GNCDE_ERR_SHAPE;
   }
-  // the single-plane bf16 mode exists only in the one-launch evaluation
+  // the single-plane bf16 mode exists only in the one-launch evaluation, and only in an experiment build
+  // (GNCDE_EXPERIMENT_BF16_MFMA, `make experiment`): the product library refuses it
+#ifdef GNCDE_EXPERIMENT_BF16_MFMA
   if (p->compute == GNCDE_COMPUTE_BF16_MFMA && !rows_supported(*p)) return GNCDE_ERR_UNSUPPORTED;
+#else
+  if (p->compute == GNCDE_COMPUTE_BF16_MFMA) return GNCDE_ERR_UNSUPPORTED;
+#endif
   return GNCDE_OK;
 }
 

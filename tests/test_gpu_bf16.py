@@ -1,4 +1,5 @@
-"""GPU: the bf16 MFMA paths (GNCDE_COMPUTE_BF16 / _BF16_STORAGE / _BF16_MFMA, BASELINE config 5).
+"""GPU: the bf16 paths (GNCDE_COMPUTE_BF16 / _BF16_STORAGE, BASELINE config 5; the retired _BF16_MFMA against an
+experiment build only).
 
 COMPUTE_BF16 runs the n x n products on v_mfma_f32_16x16x32_bf16 with both operands split into bf16 (hi, lo) pairs:
 three products, fp32 accumulation, ~2^-16 relative per product, so it is held to fp32-class tolerances (5x the fp32
@@ -206,6 +207,32 @@ def test_bf16_reverse_mode_is_fp32_adjoint_of_read_coefficients(gncde, golden_di
 #     the mode gives up for its throughput (~2^-8 per operand, grown by the cancellation in (I + Abar) Z).
 AGREE_BF16M = 1e-4
 RTOL_BF16M_EXACT = 5e-2
+# The mode is retired from the product library (round 6, include/gncde.h): these checks run only against the
+# experiment build (`make -C perm-equiv-graph-neural-cdes_amd experiment`, then GNCDE_LIB=build_exp/libgncde_hip.so
+# GNCDE_LIB_UNVERIFIED=1 GNCDE_EXPERIMENT_BF16_MFMA=1); the product suite checks the refusal.
+experiment_bf16m = pytest.mark.skipif(os.environ.get("GNCDE_EXPERIMENT_BF16_MFMA") != "1",
+                                      reason="single-plane bf16 mode: experiment build only")
+
+
+def test_bf16_mfma_refused_by_product_library(gncde, golden_dir):
+    """The product library refuses the retired single-plane mode loudly (GNCDE_ERR_UNSUPPORTED), for an evaluation,
+    a fixed-grid solve and path selection alike: never a silent fallback to another arithmetic."""
+    if os.environ.get("GNCDE_EXPERIMENT_BF16_MFMA") == "1":
+        pytest.skip("experiment build loaded")
+    z = np.load(os.path.join(golden_dir, "cde_n33_h32_de8.npz"))
+    params = MG.load_layers(z)
+    prob = problem_from(gncde, z, params, data=True).with_compute("bf16_mfma")
+    t = torch.tensor(z["t"], dtype=torch.float32, device="cuda")
+    y = torch.tensor(z["y"], dtype=torch.float32, device="cuda")
+    with pytest.raises(gncde._lib.GncdeError, match="not supported"):
+        gncde.vf_eval(prob, t, y)
+    B = prob.B
+    spec = gncde.SolverSpec(method=gncde._lib.TSIT5, save_mode=gncde._lib.SAVE_T1,
+                            grid=prob.ts[:, [0, -1]].contiguous(), nsteps=torch.ones(B, dtype=torch.int32, device="cuda"))
+    with pytest.raises(gncde._lib.GncdeError):
+        gncde.integrate_path(prob, spec)
+    with pytest.raises(gncde._lib.GncdeError):
+        gncde.integrate(prob, spec, y)
 
 
 def rows_envelope(z, data):
@@ -264,6 +291,7 @@ def check_vs_model(label, dy, args, kwargs):
 BF16M_CASES = VF_CASES + [("vf_undirected_n4_L2.npz", False), ("cde_n20_h64_de8.npz", True)]
 
 
+@experiment_bf16m
 @pytest.mark.parametrize("name,data", BF16M_CASES)
 def test_bf16_mfma_vf_eval_vs_rounding_model(gncde, golden_dir, name, data):
     z = np.load(os.path.join(golden_dir, name))
@@ -280,6 +308,7 @@ def test_bf16_mfma_vf_eval_vs_rounding_model(gncde, golden_dir, name, data):
     check_vs_model(name, dy, (z, params, data, z["t"], z["y"]), {})
 
 
+@experiment_bf16m
 @pytest.mark.parametrize("n,H,cde", [(200, 32, False), (255, 32, True), (129, 64, True), (256, 16, False)])
 def test_bf16_mfma_large_n_vs_rounding_model(gncde, n, H, cde):
     """n in (128, 256]: both 32-wide K chunks of every wave, odd n (funnel-shifted coefficient loads), the padded
@@ -315,6 +344,7 @@ RTOL_BF16_CFG5_VF = 5 * 2.0 ** -7
 BF16M_SOLVE_CAP = {255: 0.15, 64: 0.04}
 
 
+@experiment_bf16m
 @pytest.mark.parametrize("n", [255, 64])
 def test_bf16_mfma_config5_shape_vs_fp32(gncde, n):
     """TGB-trade-shaped CDE (n = 255 / 64, h = 32, L = 4, de = 8): one evaluation and a 20-step Tsit5 solve in the

@@ -9,10 +9,10 @@
   accepted steps (GncdeSolver.step_ts); two samples' steps are replayed in the oracle (RTOL_SOLVE).
 
 Inputs are drawn with numpy (oracle.make_graph_control: a dynamic graph's normalised-Laplacian path, node data from
-a standard normal) so the oracle sees exactly what the GPU reads.  The config-3 oracle adjoint is linearised at the
-GPU's step states (OG.solve_fixed_grid_vjp y_lin); samples whose gradient still moves under a 1e-6 relative change
-of those states (a ReLU pre-activation within fp32 reach of its kink) are skipped for the gradient check (the test
-fails if fewer than two stable samples exist among the candidates).
+a standard normal) so the oracle sees exactly what the GPU reads.  The config-3 gradient is checked on two samples
+whose gradient is stable (moves < RTOL_GRAD / 5 under a 1e-6 relative change of y0) under both the GPU's fp32 and
+the oracle's fp64 linearisation: end to end against the oracle's own forward and adjoint, and against the oracle
+adjoint linearised at the GPU's step states, both at RTOL_GRAD.
 """
 import dataclasses
 import os
@@ -93,15 +93,16 @@ def test_config3_exact_shape_trajectory_and_gradient(G):
     st = st.cpu().numpy()
     assert np.all(st[:, 0] == 30) and np.all(st[:, 2] == 181) and np.all(st[:, 3] == 0)
     # ReLU kinks: over 30 steps x 6 stages x 2 ReLU layers of 129 x 64 pre-activations the fp32 trajectory (1e-5
-    # from fp64) sits on the other side of some kink than the fp64 one, so the END-TO-END gradients of the two
-    # differ by a kink flip, not by adjoint error.  Measured on the GPU: every candidate's fp32 dL/dy0 moves by
-    # 2e-4 .. 4e-2 under a 1e-6 relative change of y0 (printed below), i.e. at this shape the fp32 gradient itself
-    # is only defined to that scale.  So the check is in two parts, on the first two candidates whose fp64 oracle
-    # gradient is kink-stable (moves < 1e-5 under the same change):
-    #   1. the adjoint: the oracle adjoint linearised at the GPU's own step states, at RTOL_GRAD;
-    #   2. end to end: the oracle adjoint of the oracle's own fp64 forward, within max(RTOL_GRAD, 3 x the GPU
-    #      gradient's own movement) — the gradient's fp32 discontinuity scale.
-    # The GPU's movement: every sample's dL/dy0 (independent per sample) at y0 and at y0 (1 + 1e-6).
+    # from fp64) can sit on the other side of some kink than the fp64 one; the END-TO-END gradients of the two then
+    # differ by a kink flip, not by adjoint error.  A sample whose gradient is smooth at both trajectories shows no
+    # such flip, so the end-to-end check runs on samples that are stable under BOTH linearisations:
+    #   * the GPU's fp32 dL/dy0 moves < RTOL_GRAD / 5 under a 1e-6 relative change of y0 (measured for all 64
+    #     samples: each sample's adjoint is independent of the others', so one batched pair of solves gives all);
+    #   * the fp64 oracle's dL/dy0 moves < RTOL_GRAD / 5 under the same change.
+    # On the first two such samples (candidates tried from the least-moving GPU gradient up):
+    #   1. end to end: the GPU gradient against the oracle adjoint of the oracle's own fp64 forward, at RTOL_GRAD;
+    #   2. the adjoint: the oracle adjoint linearised at the GPU's own step states, at RTOL_GRAD (every parameter).
+    stable = RTOL_GRAD / 5
     gall = rng.standard_normal((B, n, H))
     spec_t1 = dataclasses.replace(spec, save_mode=G._lib.SAVE_T1)
     gpu_g = []
@@ -109,39 +110,43 @@ def test_config3_exact_shape_trajectory_and_gradient(G):
         yd = torch.tensor(y0 * scale, dtype=torch.float32, device="cuda")
         gpu_g.append(G.integrate_vjp(prob, spec_t1, G.integrate(prob, spec, yd),
                                      torch.tensor(gall, dtype=torch.float32, device="cuda"))[0].cpu().numpy())
-    gpu_move = [rel_err(gpu_g[1][b], gpu_g[0][b]) for b in range(B)]
-    print("  GPU dL/dy0 movement under a 1e-6 change of y0: " +
-          ", ".join(f"{b}: {gpu_move[b]:.1e}" for b in (5, 40, 63, 17, 28, 51, 22, 34, 9, 56)))
+    gpu_move = np.array([rel_err(gpu_g[1][b], gpu_g[0][b]) for b in range(B)])
+    order = [int(b) for b in np.argsort(gpu_move, kind="stable")]
+    print(f"  GPU dL/dy0 movement under a 1e-6 change of y0, all {B} samples: "
+          f"{int(np.sum(gpu_move < stable))} below {stable:.0e}; " +
+          ", ".join(f"{b}: {gpu_move[b]:.1e}" for b in order))
     gfin = np.zeros((B, n, H))
     chosen, refs, e2e = [], [], []
-    for b in (5, 40, 63, 17, 28, 51, 22, 34, 9, 56):  # windows 5, 0, 3, 7, 8, 1, 2, 4, 9, 6
+    for b in order:
+        if gpu_move[b] >= stable:
+            break
         f, fv = oracle_fns(ts, coeffs, dco, P, H, de, b)
         g = gall[b]
-        lin = ys[b].cpu().numpy()
-        g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g, y_lin=lin)
         e0, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g)
         e1, _ = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b] * (1 + 1e-6), "tsit5", g_final=g)
-        if np.max(np.abs(e1 - e0)) > 1e-5 * np.max(np.abs(e0)):
-            print(f"  sample {b}: oracle gradient not kink-stable, skipped")
+        omove = rel_err(e1, e0)
+        if omove >= stable:
+            print(f"  sample {b}: GPU gradient moves {gpu_move[b]:.1e}, oracle gradient {omove:.1e}: skipped")
             continue
         traj, _ = O.solve_fixed_grid(f, grids[b], y0[b], "tsit5", save_every_step=True, time_dtype=np.float32)
         err = rel_err(ys[b].cpu().numpy(), traj)
         per_step = max(rel_err(ys[b, k].cpu().numpy(), traj[k]) for k in range(1, 31))
-        print(f"  config 3 sample {b}: trajectory vs oracle {err:.2e} (worst step-relative {per_step:.2e})")
+        print(f"  config 3 sample {b}: trajectory vs oracle {err:.2e} (worst step-relative {per_step:.2e}); "
+              f"gradient moves GPU {gpu_move[b]:.1e}, oracle {omove:.1e}")
         assert err <= RTOL_SOLVE
+        g0, gr = OG.solve_fixed_grid_vjp(f, fv, grids[b], y0[b], "tsit5", g_final=g, y_lin=ys[b].cpu().numpy())
         gfin[b] = g
         chosen.append(b)
         refs.append((g0, gr))
         e2e.append(e0)
         if len(chosen) == 2:
             break
-    assert len(chosen) == 2, "fewer than two kink-stable samples among the candidates"
+    assert len(chosen) == 2, "fewer than two samples whose gradient is stable under both linearisations"
     gy0, gp, gf = G.integrate_vjp(prob, spec_t1, ys, torch.tensor(gfin, dtype=torch.float32, device="cuda"))
-    for b, ref in zip(chosen, e2e):  # 2. end to end, at the gradient's own fp32 discontinuity scale
-        e, bound = rel_err(gy0[b].cpu().numpy(), ref), max(RTOL_GRAD, 3.0 * gpu_move[b])
-        print(f"  sample {b}: end-to-end dL/dy0 vs the oracle's own forward {e:.2e} (bound {bound:.2e}: the GPU "
-              f"gradient moves {gpu_move[b]:.2e} under a 1e-6 change of y0)")
-        assert e <= bound
+    for b, ref in zip(chosen, e2e):  # 1. end to end against the oracle's own fp64 forward, at RTOL_GRAD
+        e = rel_err(gy0[b].cpu().numpy(), ref)
+        print(f"  sample {b}: end-to-end dL/dy0 vs the oracle's own forward {e:.2e} (bound RTOL_GRAD {RTOL_GRAD:.0e})")
+        assert e <= RTOL_GRAD
     total = OG._acc(OG._acc(None, refs[0][1]), refs[1][1])
     errs = {f"gy0[{b}]": rel_err(gy0[b].cpu().numpy(), r[0]) for b, r in zip(chosen, refs)}
     others = [b for b in range(B) if b not in chosen]
@@ -185,6 +190,62 @@ def test_config5_exact_shape_pid_replay(G):
         ref = OG.solve_grid_dense(f, grid, y0[b], ts[b, -1:], time_dtype=np.float32)
         err = rel_err(ys[b].cpu().numpy()[None], ref)
         print(f"  config 5 sample {b}: replay of {st[b, 0]} accepted steps in the oracle {err:.2e}")
+        assert err <= RTOL_SOLVE
+
+
+def _bf16_round(x):
+    """x (float64) rounded as Problem.with_compute("bf16_storage") rounds the operator planes: to fp32 (pack_control),
+    then to bfloat16 (round to nearest even), widened back exactly."""
+    return torch.from_numpy(np.asarray(x, np.float32)).to(torch.bfloat16).to(torch.float64).numpy()
+
+
+def test_config5_bf16_storage_equals_fp32_on_rounded_coefficients(G):
+    """BASELINE config 5's bf16 path (GNCDE_COMPUTE_BF16_STORAGE, the TGB driver's compute="bf16_storage") at config
+    5's exact shape (B = 16, n = 255, h = 32, L = 4, de = 8, Tsit5 + PID(1e-3, 1e-6)): its persistent solve
+    (k_rows<32, 2, PREC 2, SOLVE>) is the fp32 persistent solve of the bf16-rounded operator.  The mode widens every
+    bfloat16 coefficient exactly on load and runs the fp32 arithmetic of the fp32 instance (same Horner, same plane
+    sums from k_coef_sums on the widened values, same products and controller), so outputs, stats and accepted-step
+    records are asserted BITWISE equal to the fp32 solve on Problem.coef.to(bf16).float().  Two samples' accepted
+    steps are then replayed in the fp64 oracle on those rounded coefficients at RTOL_SOLVE.  The printed deviation
+    from the fp32 solve on the UNROUNDED operator is the model's response to bf16 inputs, not solver error."""
+    B, n, T, H, de, L = 16, 255, 3, 32, 8, 4
+    _, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(55, B, n, T, 1.0, H, de, L)
+    prob32 = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
+    probq = prob32.with_compute("bf16_storage")
+    probr = dataclasses.replace(probq, coef=probq.coef.float().contiguous(), compute=G._lib.COMPUTE_FP32)
+    tsd = torch.tensor(ts, dtype=torch.float32, device="cuda")
+    yd = torch.tensor(y0, dtype=torch.float32, device="cuda")
+
+    def solve(prob):
+        rec = torch.zeros(B, 4097, device="cuda")
+        spec = G.SolverSpec(method=G._lib.TSIT5, controller=G._lib.CTRL_PID, save_mode=G._lib.SAVE_T1, rtol=1e-3,
+                            atol=1e-6, t0=tsd[:, 0].contiguous(), t1=tsd[:, -1].contiguous(),
+                            dt0=torch.full((B,), 0.01, device="cuda"), step_ts=rec)
+        path = G.integrate_path(prob, spec)
+        ys, st = G.integrate(prob, spec, yd, stats=True)
+        return path, ys, st, rec
+
+    pq, yq, sq, rq = solve(probq)
+    pr, yr, sr, rr = solve(probr)
+    p32, y32, s32, _ = solve(prob32)
+    assert pq == pr == "rows_pid<32,cde>", (pq, pr)
+    assert torch.all(sq[:, 3] == 0) and bool(torch.isfinite(yq).all())
+    dsteps = (sq[:, 0] - s32[:, 0]).abs().float() / s32[:, 0].float()
+    print(f"  bf16_storage vs fp32 on the bf16-rounded operator: outputs bitwise {torch.equal(yq, yr)} "
+          f"(max |diff| {float((yq - yr).abs().max()):.1e}), stats bitwise {torch.equal(sq, sr)}, step records "
+          f"bitwise {torch.equal(rq, rr)}; vs fp32 on the unrounded operator: output "
+          f"{rel_err(yq.cpu().numpy(), y32.cpu().numpy()):.2e}, accepted steps within {float(dsteps.max()):.1%}")
+    assert torch.equal(sq, sr) and torch.equal(rq, rr) and torch.equal(yq, yr)
+    sq = sq.cpu().numpy()
+    rounded = tuple(np.stack([c[..., 0], _bf16_round(c[..., 1])], -1) for c in coeffs)
+    for b in (3, 12):
+        f, _ = oracle_fns(ts, rounded, dco, P, H, de, b)
+        grid = rq[b, :sq[b, 0] + 1].cpu().numpy().astype(np.float64)
+        assert grid[0] == 0.0 and grid[-1] == 1.0 and np.all(np.diff(grid) > 0)
+        ref = OG.solve_grid_dense(f, grid, y0[b], ts[b, -1:], time_dtype=np.float32)
+        err = rel_err(yq[b].cpu().numpy()[None], ref)
+        print(f"  bf16_storage sample {b}: replay of {sq[b, 0]} accepted steps in the oracle on the rounded "
+              f"coefficients {err:.2e}")
         assert err <= RTOL_SOLVE
 
 

@@ -69,6 +69,9 @@ def run(name, prob, spec, y0, reps, ref=None, ref_steps=None):
     return ys, st[:, 0].clone()
 
 
+EXPERIMENT_BF16M = os.environ.get("GNCDE_EXPERIMENT_BF16_MFMA") == "1"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="3,4,5")
@@ -86,7 +89,9 @@ def main():
             grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, 3.0, 0.1)] * prob.B)
             spec = gncde.SolverSpec(method=L.TSIT5, save_mode=L.SAVE_T1, grid=grid, nsteps=ns)
             ys, _ = run("3_england_n129_h64_de8_L3_tsit5c", prob, spec, y0, args.reps)
-            run("3_england_n129_h64_de8_L3_tsit5c_bf16_mfma", prob.with_compute("bf16_mfma"), spec, y0, args.reps, ref=ys)
+            if EXPERIMENT_BF16M:  # (the retired single-plane mode: experiment build only)
+                run("3_england_n129_h64_de8_L3_tsit5c_bf16_mfma", prob.with_compute("bf16_mfma"), spec, y0, args.reps,
+                    ref=ys)
         elif c == "4":  # gene community n=128, h=16, L=2, RK4 100 steps, B=1024 (forward)
             prob, y0, _ = synthetic.heat_batch(1024, num_nodes=128, hidden=16, num_layers=2, T=80, graph="community")
             grid, ns = layout.stack_grids([layout.rk4_grid(0.0, 5.0, 100)] * prob.B)
@@ -105,13 +110,13 @@ def main():
             if not args.quick:  # the multi-kernel split-product mode
                 run("5_trade_n255_h32_de8_L4_tsit5pid_bf16", prob.with_compute("bf16"), spec, y0, args.reps, ref=ys,
                     ref_steps=s32)
-            # the single-plane mode (bf16 coefficients, every product on bf16 operands) on the reference's own fixed
-            # grid (100 Tsit5 steps; the PID controller refuses the mode)
+            # the reference's own fixed grid (100 Tsit5 steps), fp32 and bf16 storage (the retired single-plane mode
+            # too, against an experiment build)
             grid, ns = layout.stack_grids([layout.constant_step_grid(0.0, 1.0, 0.01)] * B)
             fspec = gncde.SolverSpec(method=L.TSIT5, save_mode=L.SAVE_T1, grid=grid, nsteps=ns)
             yf, _ = run("5_trade_fixed100", prob, fspec, y0, args.reps)
             run("5_trade_fixed100_bf16_storage", prob.with_compute("bf16_storage"), fspec, y0, args.reps, ref=yf)
-            if not args.quick:
+            if not args.quick and EXPERIMENT_BF16M:
                 run("5_trade_fixed100_bf16_mfma", prob.with_compute("bf16_mfma"), fspec, y0, args.reps, ref=yf)
 
 
