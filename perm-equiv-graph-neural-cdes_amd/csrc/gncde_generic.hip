@@ -447,8 +447,6 @@ struct VfWs {
   uint16_t* wbf;   // GNCDE_COMPUTE_BF16_MFMA: W' per layer rounded to bfloat16, natural layout
   unsigned* sync;  // one-launch evaluation: per-group arrival counters [B] + the fault word, zeroed per solve
   unsigned* zgran;  // persistent solve: the tagged hand-off granules [2][B][n H][2], zeroed per solve
-  float* fslot;     // persistent solve with forms workgroups: [B][nb][2] form slots
-  unsigned* fsync;  // and their request / time / ready / consumed lines, zeroed per solve
 };
 
 size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
@@ -480,9 +478,6 @@ size_t carve_vf(const GncdeProblem& p, char* ws, VfWs& w) {
   w.sync = reinterpret_cast<unsigned*>(take(rows_sync_words(p.B)));
   w.zgran = reinterpret_cast<unsigned*>(take(rows_solve_shape(p) ? 4 * B * n * (size_t)p.dims[0] : 1));
   w.wbf = reinterpret_cast<uint16_t*>(take(p.compute == GNCDE_COMPUTE_BF16_MFMA ? (wsum + 1) / 2 : 1));
-  const size_t fs = rows_solve_shape(p) ? rows_fwg_slot_floats(p) : 0;
-  w.fslot = fs ? take(fs) : nullptr;
-  w.fsync = fs ? reinterpret_cast<unsigned*>(take(rows_fwg_sync_words(p))) : nullptr;
   // the one-launch evaluation reads a node block's column strip [:, R] as rows R of the transposed planes (whole
   // cache lines, like its rows block) instead of 16-column segments of every row
   const size_t planes = B * (size_t)(p.T - 1) * 4 * nn;
@@ -820,10 +815,8 @@ int generic_rows_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y
   float* part = reinterpret_cast<float*>(ws + generic_vf_workspace(p));
   if (rows_solve_granules())  // no tag is current
     (void)hipMemsetAsync(w.zgran, 0, 4 * (size_t)p.B * p.n * p.dims[0] * sizeof(unsigned), st);
-  if (w.fsync && rows_solve_uses_fwg(p))  // no request, form or consumption yet
-    (void)hipMemsetAsync(w.fsync, 0, rows_fwg_sync_words(p) * sizeof(unsigned), st);
   const int rc = rows_integrate_pid(p, s, y0, ys, stats, ws, part, w.csum, w.coefT, w.wp, w.bf, w.Z0, w.Z1, w.sync,
-                                    w.zgran, w.fslot, w.fsync, st);
+                                    w.zgran, st);
   if (rc) return rc;
   return rows_fault_status(p, ws, st, true);
 }

@@ -378,13 +378,9 @@ bool rows_pid_supported(const GncdeProblem& p, const GncdeSolver& s);
 bool rows_solve_shape(const GncdeProblem& p);  // the shape part of rows_pid_supported
 size_t rows_pid_scratch(const GncdeProblem& p);
 // sync: the evaluation workspace's [B] arrival counters, fault word and ticket counter (zeroed by generic_vf_prepare)
-size_t rows_fwg_slot_floats(const GncdeProblem& p);  // the persistent solve's forms workgroups: slots, sync lines
-size_t rows_fwg_sync_words(const GncdeProblem& p);
-bool rows_solve_uses_fwg(const GncdeProblem& p);
 int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
                        char* vf_ws, float* part, const float* csum, const void* coefT, const float* wperm,
-                       const float* bf, float* z0, float* z1, unsigned* sync, unsigned* zgran, float* fslot,
-                       unsigned* fsync, hipStream_t st);
+                       const float* bf, float* z0, float* z1, unsigned* sync, unsigned* zgran, hipStream_t st);
 void rows_pid_name(const GncdeProblem& p, const GncdeSolver& s, char* buf, size_t len);
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device, kernel, size) for launches above 64 KB of LDS
 bool ensure_dyn_lds(const void* fn, size_t smem);

@@ -107,12 +107,6 @@ struct RowsArgs {
   unsigned* queue;         // solve: samples handed out past the resident groups' first ones (zeroed per solve)
   unsigned* mail;          // solve: [G][kBarStride] each group's latest sample assignment (zeroed per solve)
   int G_all;               // solve: groups of this launch (each starts on sample b0 + its slot)
-  // solve with forms workgroups (SOLVE & 16): per (sample, row block) pair two form slots of fslot_stride floats
-  // ([2][B][nb] order: slot-major within a pair) and four sync lines (request count | the requested times [2] |
-  // forms published | forms consumed), zeroed per solve
-  float* fslot;
-  unsigned* fsync;
-  int fslot_stride;
   SolveArgs s;             // solve only
 };
 
@@ -131,8 +125,8 @@ __device__ __forceinline__ float dcubic(const float (&c)[4], float f) {
 }
 
 // The fusion families of layer fc at a node from its row / column / diagonal sums and the totals (r, rd: row sums of
-// A, dA; c, cd: column sums; dg, dgd: diagonals; s, sd: totals), as explicit fma chains: the in-line form and the
-// forms workgroups (SOLVE & 16) must give the same bits, and a contraction the compiler chooses per kernel would not
+// A, dA; c, cd: column sums; dg, dgd: diagonals; s, sd: totals), as explicit fma chains: every instance of the
+// evaluation gives the same bits (a contraction the compiler chooses per kernel need not)
 struct NodeSums {
   float r, rd, c, cd, dg, dgd, s, sd;
 };
@@ -193,31 +187,22 @@ __device__ __forceinline__ float coef_el(u32x4 v, int e) {
 
 __host__ __device__ constexpr int rows_zs(int H) { return H + 4; }
 __host__ __device__ inline int rows_np(int n, bool bf) { return bf ? (n + 31) & ~31 : (n + 15) & ~15; }
-// A form slot (SOLVE & 16): [0] the stage time it was formed at (bits), the product's operand elements of every lane
-// at kFsOps ([NJ = 4][Ar, dAr, At, dAt][256 lanes] float4), and at kFsVec the LDS vector block of the evaluation
-// (v_l [L][NP], w_l / u_l / q_l [3 L][16], tg [16], dX [16][kStrip]) in its LDS order
-constexpr int kFsOps = 64;
-constexpr int kFsVec = kFsOps + 4 * 4 * 256 * 4;
-__host__ __device__ inline int rows_fs_vec(int n, int L) { return L * rows_np(n, false) + 48 * L + 16 + 16 * 17; }
-inline int rows_fslot_stride(int n, int L) { return (kFsVec + rows_fs_vec(n, L) + 63) & ~63; }
 // floats of the shared region: the strip [2][NP][17] and the rows block [2][16][NP+4] during the form, then Z_l
 // [NP][H+4]; after a layer's product the partials [4][16][H+4] (rows 0 .. 63) and the output tile [16][H+4] (rows
 // 64 .. 79: Z_l is consumed by then, and the tile is read before the next form writes the region)
-// (fw: the solve with forms workgroups, whose layer workgroups never form: Z_l and the partials only)
-__host__ __device__ inline int rows_big(int n, int H, bool bf, bool fw = false) {
-  const int np = rows_np(n, bf), z = (np > 80 ? np : 80) * rows_zs(H), s = fw ? 0 : 2 * np * kStrip + 32 * (np + 4);
+__host__ __device__ inline int rows_big(int n, int H, bool bf) {
+  const int np = rows_np(n, bf), z = (np > 80 ? np : 80) * rows_zs(H), s = 2 * np * kStrip + 32 * (np + 4);
   return ((z > s ? z : s) + 3) & ~3;
 }
 // the bf16-storage solve's per-thread coefficient cache (SOLVE & 8): every thread's raw rows-block and strip loads of
 // the current interval, [2][NU = 2][4 planes][256 threads] x 16 bytes
 constexpr size_t kCoefCacheBytes = (size_t)2 * 2 * 4 * 256 * 16;
-inline size_t rows_smem(int n, int H, int L, bool bf, bool cache = false, bool fw = false) {
+inline size_t rows_smem(int n, int H, int L, bool bf, bool cache = false) {
   const int np = rows_np(n, bf);
   // big | inv [NP] | v_l [L][NP] | w, u, q [3][L][16] | tg [16] | dX [16][17] | red [4][64] x4 | flags [4] | cache
-  // (config 5, n = 255 h = 32 L = 4: 77.4 KiB, two workgroups per CU; with the cache 141.4 KiB, one; with forms
-  // workgroups 46 KiB)  (+ 4 floats: the forms workgroups' slot copy rounds the vector block up to float4)
-  return sizeof(float) * ((size_t)rows_big(n, H, bf, fw) + np + (size_t)L * np + 48 * L + 16 + 16 * kStrip +
-                          4 * 64 * 4 + 4 + 4) + (cache ? kCoefCacheBytes : 0);
+  // (config 5, n = 255 h = 32 L = 4: 77.4 KiB, two workgroups per CU; with the cache 141.4 KiB, one)
+  return sizeof(float) * ((size_t)rows_big(n, H, bf) + np + (size_t)L * np + 48 * L + 16 + 16 * kStrip +
+                          4 * 64 * 4 + 4) + (cache ? kCoefCacheBytes : 0);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
@@ -271,28 +256,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
   // that are already running, and groups of later samples start as earlier solves finish (no co-residency
   // assumption).
   int g, rb;
-  // SOLVE & 16: the launch is the layer workgroups (one group per sample, all resident) followed by as many FORMS
-  // workgroups, one per (sample, row block): a forms workgroup computes its layer workgroup's form — the interval
-  // lookup, Horner of the rows block and column strip straight into the product's operand layout, the node
-  // vectors and families — for every evaluation the controller has requested, one evaluation AHEAD whenever the
-  // controller already fixes the next stage time (every stage of a Tsit5 attempt but the first; every stage of a
-  // fixed grid), and hands it over through L2 (two slots per pair).  The layer workgroup then starts an evaluation
-  // with the operand loads instead of the form: the form leaves the stage-input hand-off's critical path.
-  constexpr bool FW = (SOLVE & 16) != 0;
-  bool former = false;
-  if constexpr (FW) {
-    const int pairs = a.G_all * nb;
-    int x = blockIdx.x;
-    former = x >= pairs;
-    if (former) x -= pairs;  // a forms workgroup takes the layout of its layer workgroup (same XCD: one L2)
-    if (a.G_all % 8 == 0) {
-      g = (x & 7) + 8 * (x / (8 * nb));
-      rb = (x >> 3) % nb;
-    } else {
-      g = x / nb;
-      rb = x % nb;
-    }
-  } else if (SOLVE != 0 && a.G > 0 && a.G % 8 == 0) {  // every group resident at once (rows_integrate_pid checked): the XCD-affine layout
+  if (SOLVE != 0 && a.G > 0 && a.G % 8 == 0) {  // every group resident at once (rows_integrate_pid checked): the XCD-affine layout
     const int x = blockIdx.x;
     g = (x & 7) + 8 * (x / (8 * nb));
     rb = (x >> 3) % nb;
@@ -437,173 +401,14 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
   // the solve's knots, one per lane (T <= 64)
   float ts_lane = SOLVE != 0 && (int)(threadIdx.x & 63) < T ? a.ts[(size_t)g * T + (threadIdx.x & 63)] : 0.f;
 
-  if constexpr (FW) {
-    if (former) {  // ---- a forms workgroup: the forms of (sample g, row block rb), in request order -------------
-      using CT_ = typename std::conditional<CBF, uint16_t, float>::type;
-      const int b = g, tid = threadIdx.x;
-      const int w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
-      const int ri = r0 + lo, rr = tid >> 4;
-      unsigned* ln = a.fsync + (size_t)(b * nb + rb) * 4 * kBarStride;
-      unsigned* req = ln;                        // requests posted (| 0x80000000: the sample is done)
-      const unsigned* reqt = ln + kBarStride;     // the requested times, by request parity
-      unsigned* rdy = ln + 2 * kBarStride;       // forms published
-      const unsigned* cons = ln + 3 * kBarStride;  // forms the layer workgroup has loaded
-      int* sF = reinterpret_cast<int*>(sm);
-      for (unsigned e = 0;; ++e) {
-        // request e, and (e >= 2) slot e & 1 free: form e - 2 loaded by the layer workgroup.  A bounded wait.
-        if (tid == 0) {
-          unsigned spins = 0;
-          int stop = 0;
-          for (;;) {
-            const unsigned v = __hip_atomic_load(req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (v & 0x80000000u) {
-              stop = 1;
-              break;
-            }
-            if (v >= e + 1 && (e < 2 || __hip_atomic_load(cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= e - 1))
-              break;
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > a.spin_limit ||
-                ((spins & 1023u) == 0 && __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-              __hip_atomic_store(a.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              stop = 1;
-              break;
-            }
-          }
-          sF[0] = stop;
-          sF[1] = stop ? 0 : (int)__hip_atomic_load(reqt + (e & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        const int stop = sF[0];
-        const float tb = __builtin_bit_cast(float, sF[1]);
-        __syncthreads();  // sF is rewritten by the next request's wait
-        if (stop) break;
-        // the interval and the offset into it (the layer workgroup's evaluate: the same arithmetic)
-        int idx;
-        float f;
-        if (T <= 64) {
-          idx = __popcll(__ballot(lane < T && ts_lane < tb)) - 1;
-          idx = idx < 0 ? 0 : (idx > T - 2 ? T - 2 : idx);
-          f = tb - __shfl(ts_lane, idx);
-        } else {
-          const float* tsb = a.ts + (size_t)b * T;
-          idx = interval_index_wave(tsb, T, tb);
-          f = tb - tsb[idx];
-        }
-        const size_t ib = ((size_t)b * (T - 1) + idx) * 4 * nn;
-        const auto crs = rsrc(reinterpret_cast<const CT_*>(a.coef) + ib, (unsigned)(4 * nn * sizeof(CT_)));
-        const auto crt = rsrc(reinterpret_cast<const CT_*>(a.coefT) + ib, (unsigned)(4 * nn * sizeof(CT_)));
-        float* slot = a.fslot + ((size_t)(b * nb + rb) * 2 + (e & 1)) * a.fslot_stride;
-        const auto ws = rsrc(slot, (unsigned)(a.fslot_stride * sizeof(float)));
-        // the small loads of the vector block (as in evaluate)
-        const float* cs = a.csum + ((size_t)b * (T - 1) + idx) * ((size_t)12 * n + 4);
-        const int nd = tid < n ? tid : n - 1;
-        float pv[3][4], pt[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-#pragma unroll
-          for (int kd = 0; kd < 3; ++kd) pv[kd][q] = cs[(q * 3 + kd) * n + nd];
-          pt[q] = cs[12 * n + q];
-        }
-        const int tr = r0 + (tid & 15) < n ? r0 + (tid & 15) : n - 1;
-        const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n + tr;
-        const float tcv[3] = {tc[0], tc[n], tc[2 * n]};
-        float dcv[3] = {0.f, 0.f, 0.f};
-        if constexpr (MODE >= 2) {
-          const size_t blk = (size_t)n * 16;
-          const int dr = r0 + rr < n ? r0 + rr : n - 1;
-          const float* dc = a.data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)dr * 16 + (tid & 15);
-          dcv[0] = dc[0];
-          dcv[1] = dc[blk];
-          dcv[2] = dc[2 * blk];
-        }
-        // the operand elements of lane (w, lane): A, dA at (ri, k) and at (k, ri), k = 16 kc + 4 hi + e,
-        // kc = w + 4 j — rows of the planes and of the transposed planes, Horner as in evaluate's form
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int kc = w + 4 * j;
-          if (kc < nch) {
-            const int k0 = KW * kc + EL * hi;
-            u32x4 rv[4], tv[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int el = (int)(q * nn + (size_t)ri * n + k0);
-              if constexpr (CBF) {
-                rv[q] = load8_bf16(crs, el);
-                tv[q] = load8_bf16(crt, el);
-              } else {
-                rv[q] = __builtin_amdgcn_raw_buffer_load_b128(crs, el * 4, 0, 0);
-                tv[q] = __builtin_amdgcn_raw_buffer_load_b128(crt, el * 4, 0, 0);
-              }
-            }
-            floatx4 ar, dr, at, dt;
-#pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4) {
-              const bool in = ri < n && k0 + e4 < n;
-              const float cc[4] = {coef_el<CBF>(rv[0], e4), coef_el<CBF>(rv[1], e4), coef_el<CBF>(rv[2], e4),
-                                   coef_el<CBF>(rv[3], e4)};
-              const float ct[4] = {coef_el<CBF>(tv[0], e4), coef_el<CBF>(tv[1], e4), coef_el<CBF>(tv[2], e4),
-                                   coef_el<CBF>(tv[3], e4)};
-              ar[e4] = in ? cubic(cc, f) : 0.f;
-              dr[e4] = in ? dcubic(cc, f) : 0.f;
-              at[e4] = in ? cubic(ct, f) : 0.f;
-              dt[e4] = in ? dcubic(ct, f) : 0.f;
-            }
-            const int o = kFsOps + ((j * 4) * 256 + tid) * 4;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ar), ws, o * 4, 0, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dr), ws, (o + 1024) * 4, 0, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, at), ws, (o + 2048) * 4, 0, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dt), ws, (o + 3072) * 4, 0, 16);
-          }
-        }
-        // the vector block: v_l of every node, the rows' w_l / u_l / q_l, tg and dX (evaluate's step 3)
-        {
-          auto put = [&](int i, float v) { __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ws, (kFsVec + i) * 4, 0, 16); };
-          const bool nin = tid < n;
-          NodeSums x;
-          x.r = nin ? cubic(pv[0], f) : 0.f;
-          x.rd = nin ? dcubic(pv[0], f) : 0.f;
-          x.c = nin ? cubic(pv[1], f) : 0.f;
-          x.cd = nin ? dcubic(pv[1], f) : 0.f;
-          x.dg = cubic(pv[2], f);
-          x.dgd = dcubic(pv[2], f);
-          x.s = cubic(pt, f);
-          x.sd = dcubic(pt, f);
-          const bool row = tid >= r0 && tid < r0 + kRB;
-          for (int l = 0; l < L; ++l) {
-            const float* fc = a.fusion + l * GNCDE_FC;
-            if (tid < NP) put(l * NP + tid, fam_v(fc, x));
-            if (row) {
-              const int t = tid - r0;
-              const float wv = fam_w(fc, x), uv = fam_u(fc, x), qv = fam_q(fc, x, wv, uv, n);
-              put(L * NP + l * 16 + t, nin ? wv : 0.f);
-              put(L * NP + (L + l) * 16 + t, nin ? uv : 0.f);
-              put(L * NP + (2 * L + l) * 16 + t, nin ? qv : 0.f);
-            }
-          }
-          if (tid < 16) put(L * NP + 48 * L + tid, r0 + tid < n ? fmaf(f, fmaf(3.0f * f, tcv[0], 2.0f * tcv[1]), tcv[2]) : 0.f);
-          if (MODE >= 2)
-            put(L * NP + 48 * L + 16 + rr * kStrip + (tid & 15),
-                r0 + rr < n ? fmaf(f, fmaf(3.0f * f, dcv[0], 2.0f * dcv[1]), dcv[2]) : 0.f);
-          if (tid == 0) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, tb), ws, 0, 0, 16);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of the slot has reached memory
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(rdy, e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return;
-    }
-  }
-
   // ---- one vector-field evaluation of sample b at time tb ----------------------------------------------------
   // Layer 0 reads the stage input z0: with plain loads (written before this launch), or, with `handoff`, as a
   // publication of the group (a barrier wait first, sc1 loads).  The output tile dy[R, 0 .. H-1] lands in sOut.
   // Returns false when a barrier wait gave up.
   // kslab: nullptr, or this evaluation's [L-1, B, n, H] slab of kept hidden outputs (the reverse mode's activation
   // record): the hidden hand-offs go through it instead of the group's double buffer
-  // (eidx: the solve's evaluation count — with forms workgroups, the form slot / request this evaluation reads)
-  auto evaluate = [&](const int b, const float tb, const float* z0, const bool handoff, float* kslab,
-                      const unsigned eidx) __attribute__((always_inline)) -> bool {
+  auto evaluate = [&](const int b, const float tb, const float* z0, const bool handoff, float* kslab)
+      __attribute__((always_inline)) -> bool {
     bool ok = true;
     ROWS_STAMP(0);
     // the lane's indices through an opaque move per evaluation: otherwise every per-lane address and bounds mask
@@ -612,65 +417,6 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
     const int w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
     const int ri = r0 + lo;  // this lane's operand row
-    // the product's A-operand elements of this lane: (I + Abar)[ri][k] needs A, dA at (ri, k) and at (k, ri), for
-    // k = KW kc + EL hi + e, kc = w + 4 j (chunks past the matrix read zeros)
-    float Ar[NJ][EL], dAr[NJ][EL], At[NJ][EL], dAt[NJ][EL];
-    if constexpr (FW) {
-      // form eidx from the pair's forms workgroup: wait until it is published (a bounded wait), then the operand
-      // elements straight into registers and the vector block into LDS, with sc1 loads (L2, not this CU's L1)
-      unsigned* ln = a.fsync + (size_t)(b * nb + rb) * 4 * kBarStride;
-      if (tid == 0) {
-        unsigned spins = 0;
-        int gave_up = 0;
-        while (__hip_atomic_load(ln + 2 * kBarStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < eidx + 1) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > a.spin_limit ||
-              ((spins & 1023u) == 0 && __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-            __hip_atomic_store(a.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            gave_up = 1;
-            break;
-          }
-        }
-        sFlag[0] = gave_up;
-      }
-      __syncthreads();
-      if (sFlag[0]) ok = false;
-      const float* slot = a.fslot + ((size_t)(b * nb + rb) * 2 + (eidx & 1)) * a.fslot_stride;
-      const auto rs = rsrc(slot, (unsigned)(a.fslot_stride * sizeof(float)));
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const bool in = w + 4 * j < nch;
-        const int o = (kFsOps + ((j * 4) * 256 + tid) * 4) * 4;
-        const floatx4 z4 = {0.f, 0.f, 0.f, 0.f};
-        const floatx4 ar = in ? __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 16)) : z4;
-        const floatx4 dr = in ? __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 4096, 0, 16)) : z4;
-        const floatx4 at = in ? __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 8192, 0, 16)) : z4;
-        const floatx4 dt = in ? __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 12288, 0, 16)) : z4;
-#pragma unroll
-        for (int e = 0; e < EL; ++e) {
-          Ar[j][e] = ar[e];
-          dAr[j][e] = dr[e];
-          At[j][e] = at[e];
-          dAt[j][e] = dt[e];
-        }
-      }
-      const int nv4 = (rows_fs_vec(n, L) + 3) / 4;
-      for (int i = tid; i < nv4; i += 256)
-        reinterpret_cast<floatx4*>(sV)[i] =
-            __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (kFsVec + 4 * i) * 4, 0, 16));
-      if (tid == 0 && __builtin_amdgcn_raw_buffer_load_b32(rs, 0, 0, 16) != __builtin_bit_cast(unsigned, tb)) {
-        // the form was made for another stage time: the controller's lookahead disagrees with its step (a bug)
-        __hip_atomic_store(a.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sFlag[2] = 1;
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every load of the slot has landed: it may be rewritten
-      __syncthreads();
-      if (sFlag[2]) ok = false;
-      if (tid == 0) __hip_atomic_store(ln + 3 * kBarStride, eidx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ROWS_STAMP(1);
-      ROWS_STAMP(15);
-      ROWS_STAMP(2);
-    } else {
     const float* tsb = a.ts + (size_t)b * T;
     int idx;
     float f;
@@ -828,6 +574,9 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     }
     __syncthreads();
     ROWS_STAMP(1);
+    // the product's A-operand elements of this lane: (I + Abar)[ri][k] needs A, dA at (ri, k) and at (k, ri), for
+    // k = KW kc + EL hi + e, kc = w + 4 j (chunks past the matrix read zeros)
+    float Ar[NJ][EL], dAr[NJ][EL], At[NJ][EL], dAt[NJ][EL];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int kc = w + 4 * j, k0 = KW * kc + EL * hi;
@@ -851,7 +600,6 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     }
     __syncthreads();  // the strip's region becomes Z_l
     ROWS_STAMP(2);
-    }
 
     // ---- layers --------------------------------------------------------------------------------------------
     // Z_l -> LDS (a stage input written before this launch with plain loads; a publication of the group with sc1
@@ -1186,7 +934,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       const int bs = g + it * a.G;
       const bool live = bs < a.B;
       const int b = live ? bs : a.B - 1;  // an idle round computes on a valid sample, keeps its barriers, stores no dy
-      evaluate(b, a.t[b], a.y + (size_t)b * zgroup, false, live ? a.keep : nullptr, 0u);
+      evaluate(b, a.t[b], a.y + (size_t)b * zgroup, false, live ? a.keep : nullptr);
       // dy rows R: 16-byte stores of the output tile
       constexpr int G4 = H / 4;
       const int tid = threadIdx.x;
@@ -1205,9 +953,6 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     // A batch larger than the resident groups runs as ONE launch: a group that finishes its sample takes the next
     // one from a queue (its first workgroup draws it, the others read the group's mailbox), so the batch's cost is
     // its total work over the groups, not the sum of per-chunk maxima (the slowest sample of every chunk).
-    if constexpr (FW) {
-      if (threadIdx.x == 0) sFlag[2] = 0;  // (set when a form slot holds another stage time)
-    }
     for (unsigned asg = 1;; ++asg) {
     const SolveArgs& s = a.s;
     const int b = g;
@@ -1576,86 +1321,16 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       if (rb == 0 && tid == 0 && s.step_ts) s.step_ts[(size_t)b * s.step_len] = t0;
     }
     // RK4 on an empty grid evaluates nothing; Tsit5 evaluates its FSAL k0 even then (stats: 1 + 6 ns)
-    // SOLVE & 16: the forms workgroup's requests.  Evaluation e's stage time is requested once the controller fixes it
-    // (at the latest when its input is published), and so is evaluation e + 1's when it is already fixed then (the
-    // lookahead below): the forms workgroup forms e + 1 while this group runs e.
-    unsigned posted = 0;
-    unsigned* fln = FW ? a.fsync + (size_t)(b * nb + rb) * 4 * kBarStride : nullptr;
-    auto post_req = [&](float tq) {
-      if constexpr (FW) {
-        if (tid == 0) {
-          __hip_atomic_store(fln + kBarStride + (posted & 1), __builtin_bit_cast(unsigned, tq), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the time is in memory before the count
-          __hip_atomic_store(fln, posted + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        ++posted;
-      }
-    };
-    // the stage time of the evaluation AFTER the one whose input was just published, where the controller state
-    // already fixes it (the same arithmetic as grid_step / pid_step; a disagreement is caught by the slot's time)
-    auto lookahead = [&](float& tl) -> bool {
-      if constexpr (GRIDC) {
-        if (rk4) {
-          if (st < 3) {
-            tl = stage_time(t, st < 2 ? 0.5f : 1.0f, h);
-            return true;
-          }
-          if (gk + 1 < ns) {
-            tl = gr[gk + 1];
-            return true;
-          }
-          return false;
-        }
-        float ar[6], cst;
-        if (st < 6) {
-          tsit5_row(st + 1, ar, cst);
-          tl = st + 1 == 6 ? gr[gk + 1] : stage_time(t, cst, h);
-          return true;
-        }
-        if (gk + 1 < ns) {
-          const float t2 = gr[gk + 1], h2 = gr[gk + 2] - t2;
-          tsit5_row(1, ar, cst);
-          tl = stage_time(t2, cst, h2);
-          return true;
-        }
-        return false;
-      } else {
-        if (phase == 0) {  // f(t0, y0) published: the first attempt's stage 1 (dt0 given; Hairer's h0 is not fixed yet)
-          if (s.auto_dt || !(t < t1) || s.max_steps < 1) return false;
-          float tn2 = t + dt;
-          if (tn2 > t1 - 1e-6f) tn2 = t1;
-          tl = stage_time(t, TSIT5_C2, tn2 - t);
-          return true;
-        }
-        if (phase == 2 && st >= 1 && st <= 5) {  // inside an attempt: the next stage
-          float ar[6], cst;
-          const int nx = st + 1;
-          tsit5_row(nx, ar, cst);
-          tl = nx == 6 ? tn : nx == 5 ? __fadd_rn(t, h) : stage_time(t, cst, h);
-          return true;
-        }
-        return false;  // the attempt's last stage: the next step size waits for the error norm
-      }
-    };
-    auto post_next = [&]() {  // after a publication: request the evaluation about to run, and the one after it
-      if constexpr (FW) {
-        if (posted == (unsigned)evals) post_req(tst);
-        float tl;
-        if (posted == (unsigned)evals + 1 && lookahead(tl)) post_req(tl);
-      }
-    };
     if (!GRIDC || !rk4 || ns > 0) {
       kslab = pid_slab(0, 0);  // PID: f(t0, y0) is stage 0 of the first step
       publish(y);  // the first evaluation's input: f(t0, y0) (PID: the FSAL k0 and the initial-step heuristic's f0)
-      post_next();
       for (;;) {
 #ifdef GNCDE_ROWS_STAMPS
         stamp_on = evals == kStampEval;
         if (evals == kStampEval + 1 && threadIdx.x == 0)  // the next evaluation's start: the whole iteration
           g_rows_stamps[stamp_slot * 16 + 15] = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (!evaluate(b, tst, a.zbuf[(pub - 1) & 1] + (size_t)b * zgroup, true, kslab, (unsigned)evals)) {
+        if (!evaluate(b, tst, a.zbuf[(pub - 1) & 1] + (size_t)b * zgroup, true, kslab)) {
           fault = true;
           break;
         }
@@ -1669,7 +1344,6 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
         } else {
           if (pid_step()) break;
         }
-        post_next();
       }
     }
     if constexpr (GRIDC) {
@@ -1680,9 +1354,6 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       }
       if (!s.save_steps && mine) *reinterpret_cast<floatx4*>(s.ys + oel) = y;
       steps = ns;
-    }
-    if constexpr (FW) {  // the sample is done: the forms workgroup stops (after any form it is still making)
-      if (tid == 0) __hip_atomic_fetch_or(fln, 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (rb == 0 && tid == 0 && s.stats) {
       const bool bad = fault || __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1973,27 +1644,8 @@ bool rows_solve_shape(const GncdeProblem& p) {
 // The bf16-storage solve keeps its coefficient loads in LDS (SOLVE & 8) when one workgroup per CU holds the whole
 // batch (the cache takes 64 KB more LDS per workgroup: one workgroup per CU instead of two); GNCDE_SOLVE_COEF_CACHE=0
 // turns it off.
-// Forms workgroups (SOLVE & 16) need a forms workgroup beside every layer workgroup, all resident at once: one
-// launch of 2 B nb workgroups (two per CU at n = 255: B <= 16 on MI355X).  GNCDE_SOLVE_FWG=0 turns them off.
-constexpr long kFwgMaxPairs = 256;
-bool fwg_env() {
-  const char* e = getenv("GNCDE_SOLVE_FWG");  // read per call: a test flips it in one process
-  return !(e && atoi(e) == 0);
-}
-bool solve_fwg(const GncdeProblem& p) {
-  if (rows_solve_granules() || !fwg_env()) return false;
-  if (p.compute != GNCDE_COMPUTE_FP32 && p.compute != GNCDE_COMPUTE_BF16_STORAGE) return false;
-  if (!rows_shape(p, false)) return false;
-  const int nb = (p.n + kRB - 1) / kRB;
-  if ((long)p.B * nb > kFwgMaxPairs || p.B < 1) return false;
-  Inst k;
-  const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
-  const bool found = p.compute == GNCDE_COMPUTE_BF16_STORAGE ? find_inst_t<2, 17>(H, mode, k) : find_inst_t<0, 17>(H, mode, k);
-  return found && resident_blocks(k, rows_smem(p.n, H, p.L, false, false, true)) >= 2L * p.B * nb;
-}
-
 bool solve_coef_cache(const GncdeProblem& p) {
-  if (p.compute != GNCDE_COMPUTE_BF16_STORAGE || rows_solve_granules() || solve_fwg(p)) return false;
+  if (p.compute != GNCDE_COMPUTE_BF16_STORAGE || rows_solve_granules()) return false;
   const char* e = getenv("GNCDE_SOLVE_COEF_CACHE");
   if (e && atoi(e) == 0) return false;
   const int nb = (p.n + kRB - 1) / kRB;
@@ -2006,11 +1658,6 @@ bool solve_coef_cache(const GncdeProblem& p) {
 bool find_solve_inst(const GncdeProblem& p, const GncdeSolver& s, Inst& k) {
   const int H = p.dims[0], mode = p.cde_hidden > 0 ? 2 : 1;
   const bool grid = s.controller == GNCDE_CTRL_GRID;
-  if (solve_fwg(p)) {
-    if (p.compute == GNCDE_COMPUTE_BF16_STORAGE)
-      return grid ? find_inst_t<2, 18>(H, mode, k) : find_inst_t<2, 17>(H, mode, k);
-    return grid ? find_inst_t<0, 18>(H, mode, k) : find_inst_t<0, 17>(H, mode, k);
-  }
   if (solve_coef_cache(p)) return grid ? find_inst_t<2, 10>(H, mode, k) : find_inst_t<2, 9>(H, mode, k);
   if (rows_solve_granules()) {
     if (p.compute == GNCDE_COMPUTE_BF16_STORAGE)
@@ -2034,22 +1681,8 @@ bool rows_pid_supported(const GncdeProblem& p, const GncdeSolver& s) {
   Inst k;
   if (!find_solve_inst(p, s, k)) return false;
   const int nb = (p.n + kRB - 1) / kRB;
-  return resident_blocks(k, rows_smem(p.n, p.dims[0], p.L, false, solve_coef_cache(p), solve_fwg(p))) >= nb &&
-         cu_count() >= nb;
+  return resident_blocks(k, rows_smem(p.n, p.dims[0], p.L, false, solve_coef_cache(p))) >= nb && cu_count() >= nb;
 }
-
-// the forms workgroups' slots and sync lines (workspace; sized where the batch could take them)
-size_t rows_fwg_slot_floats(const GncdeProblem& p) {
-  const int nb = (p.n + kRB - 1) / kRB;
-  if (!rows_shape(p, false) || (long)p.B * nb > kFwgMaxPairs) return 0;
-  return (size_t)2 * p.B * nb * rows_fslot_stride(p.n, p.L);
-}
-size_t rows_fwg_sync_words(const GncdeProblem& p) {
-  const int nb = (p.n + kRB - 1) / kRB;
-  if (!rows_shape(p, false) || (long)p.B * nb > kFwgMaxPairs) return 0;
-  return (size_t)4 * p.B * nb * kBarStride;
-}
-bool rows_solve_uses_fwg(const GncdeProblem& p) { return solve_fwg(p); }
 
 size_t rows_pid_scratch(const GncdeProblem& p) {
   const int nb = (p.n + kRB - 1) / kRB;
@@ -2058,15 +1691,12 @@ size_t rows_pid_scratch(const GncdeProblem& p) {
 
 int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float* y0, float* ys, int32_t* stats,
                        char* vf_ws, float* part, const float* csum, const void* coefT, const float* wperm,
-                       const float* bf, float* z0, float* z1, unsigned* sync, unsigned* zgran, float* fslot,
-                       unsigned* fsync, hipStream_t st) {
+                       const float* bf, float* z0, float* z1, unsigned* sync, unsigned* zgran, hipStream_t st) {
   Inst k;
   const int H = p.dims[0];
   if (!find_solve_inst(p, s, k)) return GNCDE_ERR_UNSUPPORTED;
   (void)vf_ws;
-  const bool fw = solve_fwg(p);
-  if (fw && (!fslot || !fsync)) return GNCDE_ERR_WORKSPACE;
-  const size_t smem = rows_smem(p.n, H, p.L, false, solve_coef_cache(p), fw);
+  const size_t smem = rows_smem(p.n, H, p.L, false, solve_coef_cache(p));
   if (!ensure_dyn_lds(k.fn, smem)) return GNCDE_ERR_HIP;
   const int nb = (p.n + kRB - 1) / kRB;
   RowsArgs a{};
@@ -2076,7 +1706,7 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   a.L = p.L;
   a.rounds = 1;
   a.nb = nb;
-  a.big = rows_big(p.n, H, false, fw);
+  a.big = rows_big(p.n, H, false);
   a.np = rows_np(p.n, false);
   a.ts = p.ts;
   a.coef = p.coef;
@@ -2090,9 +1720,6 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   a.zbuf[0] = z0;
   a.zbuf[1] = z1;
   a.zgran = zgran;
-  a.fslot = fslot;
-  a.fsync = fsync;
-  a.fslot_stride = rows_fslot_stride(p.n, p.L);
   {
     const char* e = getenv("GNCDE_GRAN_POLL1");
     a.poll1 = e && atoi(e) != 0;
@@ -2140,15 +1767,6 @@ int rows_integrate_pid(const GncdeProblem& p, const GncdeSolver& s, const float*
   // its next sample from the queue when it finishes one (round 5; before, one launch per chunk of cap samples, whose
   // time is the slowest sample of each chunk).  A launch of a multiple of 8 groups takes the XCD-affine layout;
   // otherwise its workgroups take start-order tickets.
-  if (fw) {  // every group and its forms workgroups in one launch (solve_fwg checked the residency)
-    a.queue = nullptr;
-    a.b0 = 0;
-    a.G = p.B;
-    a.G_all = p.B;
-    a.ticket0 = 0;
-    k.launch(a, 2 * p.B * nb, smem, st);
-    return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
-  }
   const int cap = std::min(resident_blocks(k, smem), solve_wgs_per_cu() * cu_count()) / nb;
   if (cap < 1) return GNCDE_ERR_UNSUPPORTED;  // no co-resident group (or the device query failed): never loop
   int bc = p.B < cap ? p.B : cap;

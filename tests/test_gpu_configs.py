@@ -346,48 +346,6 @@ def test_rows_solve_coef_cache_bitwise(G, monkeypatch):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("compute", ["fp32", "bf16_storage"])
-def test_rows_solve_forms_workgroups_bitwise(G, monkeypatch, compute):
-    """The persistent solve with forms workgroups (SOLVE & 16, the default where a forms workgroup fits beside every
-    layer workgroup: config 5's B = 16) computes every form — interval, Horner, node vectors — in a workgroup of its
-    own, one evaluation ahead where the controller already fixes the next stage time, and hands it over through L2;
-    the layer workgroups load it instead of forming.  Same values into the same arithmetic: outputs, stats,
-    accepted-step records and the PID record (checkpoints, stage inputs, hidden outputs) bitwise equal to the solve
-    that forms in line (GNCDE_SOLVE_FWG=0), under PID (dt0 given and Hairer's dt0 = None, SaveAt(t1) and SaveAt(ts))
-    and on fixed grids (RK4 and Tsit5, SaveAt(t1) and every step)."""
-    prob, y0, spec = _config5(G, 16, seed=63)
-    prob = prob.with_compute(compute)
-    B = prob.B
-    sts = torch.tensor([[0.3, 0.6, 1.0]] * B, device="cuda")
-    grid, ns = G.layout.stack_grids([O.constant_grid(0.0, 1.0, 0.05)] * B)
-    rgrid, rns = G.layout.stack_grids([O.constant_grid(0.0, 1.0, 0.1)] * B)
-    cases = {"pid": spec, "pid_hairer_ts": dataclasses.replace(spec, dt0=None, save_mode=G._lib.SAVE_TS, save_ts=sts),
-             "tsit5_steps": G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS, grid=grid, nsteps=ns),
-             "rk4_t1": G.SolverSpec(method=G._lib.RK4, save_mode=G._lib.SAVE_T1, grid=rgrid, nsteps=rns)}
-    for name, sp in cases.items():
-        outs = {}
-        for v in ("0", "1"):
-            monkeypatch.setenv("GNCDE_SOLVE_FWG", v)
-            assert G.integrate_path(prob, sp).startswith(("rows_pid<", "rows_grid<"))
-            pid = sp.controller == G._lib.CTRL_PID
-            rec = torch.zeros(B, 256, device="cuda") if pid else None
-            sp2 = dataclasses.replace(sp, step_ts=rec) if pid else sp
-            if pid and name == "pid":  # the accepted-step record the backward reads (ABI 8)
-                sp2 = G.autograd.pid_records(prob, dataclasses.replace(sp2, step_ts=torch.zeros(B, 4097, device="cuda")))
-                assert sp2.pid_ckpt is not None
-                for x in (sp2.stage_rec, sp2.act_rec, sp2.pid_ckpt):
-                    x.zero_()  # (slots past the accepted steps are never written)
-            ys, st = G.integrate(prob, sp2, y0, stats=True)
-            outs[v] = [ys, st] + ([sp2.step_ts] if pid else []) + \
-                [x for x in (getattr(sp2, "pid_ckpt", None), getattr(sp2, "stage_rec", None),
-                             getattr(sp2, "act_rec", None)) if x is not None]
-        assert torch.all(outs["1"][1][:, 3] == 0), (name, outs["1"][1])
-        for a, b in zip(outs["0"], outs["1"]):
-            assert torch.equal(a, b), name
-        print(f"  {compute} {name}: forms workgroups bitwise equal to in-line forms "
-              f"(evaluations {int(outs['1'][1][:, 2].sum())})")
-
-
 def test_rows_solve_granule_handoffs_bitwise(G, monkeypatch):
     """The persistent solve's two hand-off variants — counter barriers (the default) and tagged granules
     (GNCDE_SOLVE_GRANULES=1) — move the same values between the same arithmetic: bitwise the same outputs, stats and
