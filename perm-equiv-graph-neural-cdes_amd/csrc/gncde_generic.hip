@@ -271,10 +271,6 @@ __global__ void __launch_bounds__(256) k_coef_sums(int n, int T, const CT* __res
   if (tid == 0) o[12 * n + q] = (wt[0] + wt[1]) + (wt[2] + wt[3]);
 }
 
-// kComboU elements per thread (strided by the block), each element's stage-buffer loads issued together before the
-// summation: the load latency is paid once per thread, not once per term.  Same summation order per element.
-constexpr int kComboU = 4;
-constexpr int kComboThreads = 256;
 // block bx of sample b's combination (k_combo, or the combination blocks of a merged k_abar_direct launch)
 __device__ __forceinline__ void combo_block(size_t E, const float* __restrict__ y, const Combo& cb,
                                             const float* __restrict__ hcur, float* __restrict__ out, int bx, int b) {
@@ -881,8 +877,10 @@ size_t generic_integrate_workspace(const GncdeProblem& p, const GncdeSolver& s) 
   size_t sz = generic_vf_workspace(p);
   sz += 9 * align_up(B * E * 4, 256);  // y, ytmp, K[7]
   sz += 4 * align_up(B * 4, 256);      // tcur, hcur, tstage, tnx
-  if (forms_overlap(p) || forms_ride(p))
+  if (forms_overlap(p) || forms_ride(p)) {
     for (int q = 0; q < 4; ++q) sz += align_up(form_set_floats(p, q) * 4, 256);  // the second form buffer set
+    sz += align_up(B * E * 4, 256);  // the riding partial sums of the read-out's combination
+  }
   return sz;
 }
 
@@ -918,6 +916,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   if (ovl && !side) return GNCDE_ERR_HIP;
   const bool ride = !ovl && forms_ride(p);
   FormBufs fbs[2];
+  float* cpart = nullptr;  // (ride) the read-out combination's earlier terms, summed by blocks riding in the hidden launches
   std::vector<GridTime> plan;
   if (ovl || ride) {
     VfWs w0;
@@ -927,6 +926,7 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
     fbs[1].q = take(form_set_floats(p, 1));
     fbs[1].tg = take(form_set_floats(p, 2));
     fbs[1].dx = take(form_set_floats(p, 3));
+    cpart = take(B * E);
     auto add = [&](int k, float c, int fsal) { plan.push_back(GridTime{s.grid, s.nsteps, G, k, c, fsal}); };
     if (s.method == GNCDE_RK4) {
       for (int k = 0; k < G - 1; ++k) {
@@ -1003,6 +1003,8 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
   // `post`); GNCDE_COMBO_FOLD=0 keeps it a k_combo launch (A/B, bitwise the same)
   const char* nf = getenv("GNCDE_COMBO_FOLD");
   const bool fold = ride && !(nf && atoi(nf) == 0);
+  const char* npart = getenv("GNCDE_COMBO_PARTIAL");
+  const bool partial_ride = fold && !(npart && atoi(npart) == 0);
   PendingCombo post_pc{};
   bool post_on = false, post_done = false;
   auto flush = [&]() {
@@ -1023,9 +1025,24 @@ int generic_integrate(const GncdeProblem& p, const GncdeSolver& s, const float* 
       FormsRide r{};
       if (ecur + 1 < (int)plan.size()) r = ride_of(ecur + 1);
       post_done = false;
+      // the folded combination's earlier terms ride too (every sample's, split with the forms over the hidden
+      // launches), so the read-out epilogue loads one partial per element; GNCDE_COMBO_PARTIAL=0 keeps them there
+      post_pc.part = nullptr;
+      if (post_on && r.blocks && post_pc.cb.nk >= 2 && post_pc.cb.nk <= 7 && partial_ride && p.L >= 2) {
+        r.pnk = post_pc.cb.nk - 1;
+        for (int j = 0; j < r.pnk; ++j) {
+          r.pK[j] = post_pc.cb.K[j];
+          r.pa[j] = post_pc.cb.a[j];
+        }
+        r.part = cpart;
+        r.pE = E;
+        r.pbs = gc.x;
+        post_pc.part = cpart;
+      }
       const int res = generic_vf_eval(p, tst, yin, out, ws, st, true, &bars, keep_next, true, nullptr,
                                       &fbs[ecur & 1], r.blocks ? &r : nullptr, post_on ? &post_pc : nullptr,
                                       &post_done);
+      post_pc.part = nullptr;
       ++ecur;
       return res;
     }

@@ -282,6 +282,7 @@ struct PendingCombo {
   float* out;
   size_t E;
   unsigned blocks;  // combination blocks per sample (0: none)
+  const float* part;  // folded read-out epilogue: the earlier terms' sum, formed by riding blocks (FormsRide), or null
 };
 // A fixed-grid evaluation's stage time computed by the forms launch itself from the grid (the overlapped forms of
 // generic_integrate: launched on a side stream ahead of the stage combination that writes tst), with exactly the
@@ -308,11 +309,24 @@ struct FormsArgs {
 };
 // A fixed-grid evaluation's forms riding as extra workgroups in the previous evaluation's hidden-layer launches
 // (gncde_layer.hip): samples [b0, b0 + nb) of the next evaluation's forms, its stage time from the grid (gt)
+// kComboU elements per thread (strided by the block), each element's stage-buffer loads issued together before the
+// summation: the load latency is paid once per thread, not once per term.  Same summation order per element.
+constexpr int kComboU = 4;
+constexpr int kComboThreads = 256;
 struct FormsRide {
   FormsArgs f;
   GridTime gt;
   int b0, nb;
   unsigned blocks;  // tile pairs x nb (0: no ride)
+  // the following read-out's stage combination, all terms but its last (that evaluation's own output), summed by
+  // further riding blocks into part [B, pE] (pbs blocks of kComboThreads x kComboU elements per sample; 0: none), in
+  // k_combo's fmaf order: the read-out epilogue then loads one partial per element instead of every earlier term
+  const float* pK[6];
+  float pa[6];
+  int pnk;
+  float* part;
+  size_t pE;
+  unsigned pbs;
 };
 // pending (optional): a stage combination folded into this evaluation's forms launch; forms (optional): the forms
 // were launched by the caller into these buffers (no forms launch here); ride (optional, with forms): the next

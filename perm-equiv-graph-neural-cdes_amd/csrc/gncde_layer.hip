@@ -100,12 +100,34 @@ __global__ void __launch_bounds__((64 * layer_waves<DOUT, MODE, BF, NT>()), (NT 
   static_assert(MODE == 2 || NT == 2, "the Linear epilogue's tile split assumes two row tiles");
   static_assert(!BF || NT == 2, "bf16 modes: two row tiles");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  if (blockIdx.z) {  // a forms block of the next evaluation riding in this launch (FormsRide; 256 threads)
+  if (blockIdx.z) {  // a block riding in this launch (FormsRide; 256 threads): the next evaluation's forms, then
+                     // the partial sums of the following read-out's stage combination
     if constexpr (MODE == 0 && !BF && NT == 2) {
       const unsigned fb = (blockIdx.z - 1) * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x;
       if (fb < a.ride.blocks) {
         const int nt = (a.n + 31) >> 5, np = nt * (nt + 1) / 2, b = a.ride.b0 + (int)fb / np;
         forms_tile<float, float>(a.ride.f, (int)fb % np, b, grid_stage_time(a.ride.gt, b), smem);
+      } else if (fb - a.ride.blocks < a.ride.pbs * (unsigned)a.ride.nb) {
+        const unsigned pb = fb - a.ride.blocks;
+        const int b = a.ride.b0 + (int)(pb / a.ride.pbs);
+        const size_t e0 = (size_t)(pb % a.ride.pbs) * (kComboThreads * kComboU) + threadIdx.x;
+        float kv[6][kComboU];
+#pragma unroll
+        for (int u = 0; u < kComboU; ++u) {  // every load first (one round trip), then k_combo's summation order
+          const size_t e = e0 + (size_t)u * kComboThreads, o = (size_t)b * a.ride.pE + e;
+#pragma unroll
+          for (int j = 0; j < 6; ++j) kv[j][u] = (e < a.ride.pE && j < a.ride.pnk) ? a.ride.pK[j][o] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kComboU; ++u) {
+          const size_t e = e0 + (size_t)u * kComboThreads;
+          if (e >= a.ride.pE) break;
+          float sp = 0.f;
+#pragma unroll
+          for (int j = 0; j < 6; ++j)
+            if (j < a.ride.pnk) sp = fmaf(a.ride.pa[j], kv[j][u], sp);
+          a.ride.part[(size_t)b * a.ride.pE + e] = sp;
+        }
       }
     }
     return;
@@ -527,7 +549,24 @@ __global__ void __launch_bounds__((64 * layer_waves<DOUT, MODE, BF, NT>()), (NT 
     const Combo& cb = a.post.cb;
     const size_t pE = (size_t)n * DOUT;
     float ppre[CE], pyv[CE], phb = 0.f, ptc = 0.f;
-    if (post) {
+    if (post && a.post.part) {  // the earlier terms were summed by blocks riding in the hidden launches: two loads
+#pragma unroll
+      for (int u = 0; u < CE; ++u) {
+        const int k = tid + NTH * u, R = r0 + k / CW;
+        const size_t o = (size_t)b * pE + (size_t)R * DOUT + 16 * ch * CT + k % CW;
+        pyv[u] = R < n ? a.post.y[o] : 0.f;
+        ppre[u] = R < n ? a.post.part[o] : 0.f;
+      }
+      if (cb.grid) {
+        const float* g = cb.grid + (size_t)b * cb.G;
+        int ns = cb.nsteps[b];
+        ns = ns < 0 ? 0 : (ns > cb.G - 1 ? cb.G - 1 : ns);
+        ptc = cb.gk < ns ? g[cb.gk] : g[ns];
+        phb = cb.gk < ns ? g[cb.gk + 1] - g[cb.gk] : 0.f;
+      } else {
+        phb = a.post.hcur[b];
+      }
+    } else if (post) {
       float kv[6][CE];
 #pragma unroll
       for (int u = 0; u < CE; ++u) {
@@ -694,8 +733,8 @@ void launch(const LayerArgs& a, int B, hipStream_t st) {
   const int rows = 16 * kTiles;
   const unsigned gx = (a.n + rows - 1) / rows * split;
   unsigned gz = 1;
-  if (MODE == 0 && !BF && a.ride.blocks) {  // the riding forms blocks: whole z planes after the layer's plane
-    gz += (a.ride.blocks + gx * B - 1) / (gx * B);
+  if (MODE == 0 && !BF && a.ride.blocks) {  // the riding blocks: whole z planes after the layer's plane
+    gz += (a.ride.blocks + a.ride.pbs * (unsigned)a.ride.nb + gx * B - 1) / (gx * B);
     sm = sm > sizeof(float) * kFormsLdsFloats ? sm : sizeof(float) * kFormsLdsFloats;
   }
   hipLaunchKernelGGL((k_layer<DIN, DOUT, MODE, BF, kTiles>), dim3(gx, B, gz), dim3(256), sm, st, a);

@@ -604,7 +604,8 @@ def test_forms_overlap_bitwise(G, monkeypatch, method):
     in the previous evaluation's hidden-layer launches (FormsRide, the samples split over those launches), with
     GNCDE_FORMS_RIDE=0 they get their own launch behind the stage combination (the combination's blocks folded in),
     and with GNCDE_FORMS_OVERLAP=1 they run one evaluation ahead on a side stream.  With the forms riding, a stage
-    combination that follows a read-out runs in that launch's epilogue (GNCDE_COMBO_FOLD=0: its own launch).  All three time the stage from the
+    combination that follows a read-out runs in that launch's epilogue (GNCDE_COMBO_FOLD=0: its own launch), its earlier
+    terms summed by blocks riding in the hidden launches (GNCDE_COMBO_PARTIAL=0: in the epilogue).  All three time the stage from the
     grid or the combination with the same arithmetic and run the same forms code into alternating buffer sets:
     bitwise the same trajectory, stats and stage record — ragged per-sample grids (padded steps) included, at config
     3's shape, a mixed-width one (5 samples over two hidden launches) and one hidden layer (L = 2)."""
@@ -621,18 +622,19 @@ def test_forms_overlap_bitwise(G, monkeypatch, method):
         floats = G.engine.stage_record_floats(prob, spec)
         yd = torch.tensor(y0, dtype=torch.float32, device="cuda")
         outs = {}
-        variants = {"ride": ("0", "1", "1"), "ride_no_fold": ("0", "1", "0"), "inline": ("0", "0", "1"),
-                    "overlap": ("1", "0", "1")}
-        for v, (ovl, ride, fold) in variants.items():
+        variants = {"ride": ("0", "1", "1", "1"), "ride_no_partial": ("0", "1", "1", "0"),
+                    "ride_no_fold": ("0", "1", "0", "1"), "inline": ("0", "0", "1", "1"), "overlap": ("1", "0", "1", "1")}
+        for v, (ovl, ride, fold, part) in variants.items():
             monkeypatch.setenv("GNCDE_FORMS_OVERLAP", ovl)
             monkeypatch.setenv("GNCDE_FORMS_RIDE", ride)
             monkeypatch.setenv("GNCDE_COMBO_FOLD", fold)
+            monkeypatch.setenv("GNCDE_COMBO_PARTIAL", part)
             rec = torch.zeros(B, max(floats, 1), device="cuda")
             sp = dataclasses.replace(spec, stage_rec=rec) if floats else spec
             ys, st = G.integrate(prob, sp, yd, stats=True)
             outs[v] = (ys.clone(), st.clone(), rec)
         assert bool(torch.isfinite(outs["ride"][0]).all())
-        for v in ("ride_no_fold", "inline", "overlap"):
+        for v in ("ride_no_partial", "ride_no_fold", "inline", "overlap"):
             for a, b in zip(outs["ride"], outs[v]):
                 assert torch.equal(a, b), (B, n, v)
 
