@@ -124,46 +124,6 @@ __device__ __forceinline__ float dcubic(const float (&c)[4], float f) {
   return fmaf(f, fmaf(3.0f * f, c[0], 2.0f * c[1]), c[2]);
 }
 
-// The fusion families of layer fc at a node from its row / column / diagonal sums and the totals (r, rd: row sums of
-// A, dA; c, cd: column sums; dg, dgd: diagonals; s, sd: totals), as explicit fma chains: every instance of the
-// evaluation gives the same bits (a contraction the compiler chooses per kernel need not)
-struct NodeSums {
-  float r, rd, c, cd, dg, dgd, s, sd;
-};
-__device__ __forceinline__ float fam_v(const float* fc, const NodeSums& x) {  // v_l[k]: the column family
-  return fmaf(fc[GNCDE_FC_VC_DA], x.cd, fmaf(fc[GNCDE_FC_VC_A], x.c, fmaf(fc[GNCDE_FC_VR_DA], x.rd, fc[GNCDE_FC_VR_A] * x.r)));
-}
-__device__ __forceinline__ float fam_w(const float* fc, const NodeSums& x) {  // w_l[i]: the row family
-  float v = fc[GNCDE_FC_WR_A] * x.r;
-  v = fmaf(fc[GNCDE_FC_WR_DA], x.rd, v);
-  v = fmaf(fc[GNCDE_FC_WC_A], x.c, v);
-  v = fmaf(fc[GNCDE_FC_WC_DA], x.cd, v);
-  v = fmaf(fc[GNCDE_FC_WS_A], x.s, v);
-  return fmaf(fc[GNCDE_FC_WS_DA], x.sd, v);
-}
-__device__ __forceinline__ float fam_u(const float* fc, const NodeSums& x) {  // u_l[i]: the diagonal (incl. the identity)
-  float v = fmaf(fc[GNCDE_FC_UD_A], x.dg, fc[GNCDE_FC_IDC]);
-  v = fmaf(fc[GNCDE_FC_UD_DA], x.dgd, v);
-  v = fmaf(fc[GNCDE_FC_UR_A], x.r, v);
-  v = fmaf(fc[GNCDE_FC_UR_DA], x.rd, v);
-  v = fmaf(fc[GNCDE_FC_UC_A], x.c, v);
-  v = fmaf(fc[GNCDE_FC_UC_DA], x.cd, v);
-  v = fmaf(fc[GNCDE_FC_US_A], x.s, v);
-  return fmaf(fc[GNCDE_FC_US_DA], x.sd, v);
-}
-// q_l[i] = sum_k (I + Abar_l)[i][k]: dense terms -> row / column sums, the w family n copies, the v family
-// sum_k v_k (sum r = sum c = s), the diagonal once
-__device__ __forceinline__ float fam_q(const float* fc, const NodeSums& x, float wv, float uv, int n) {
-  float q = fc[GNCDE_FC_E_A] * x.r;
-  q = fmaf(fc[GNCDE_FC_E_DA], x.rd, q);
-  q = fmaf(fc[GNCDE_FC_ET_A], x.c, q);
-  q = fmaf(fc[GNCDE_FC_ET_DA], x.cd, q);
-  q = fmaf((float)n, wv, q);
-  q = fmaf(fc[GNCDE_FC_VR_A] + fc[GNCDE_FC_VC_A], x.s, q);
-  q = fmaf(fc[GNCDE_FC_VR_DA] + fc[GNCDE_FC_VC_DA], x.sd, q);
-  return q + uv;
-}
-
 // 8 bf16 at element `e` of a buffer: the 16-byte load at the dword boundary at or below e and the next dword,
 // funnel-shifted by one element when e is odd (odd n puts rows at 2-byte boundaries; every load stays dword-aligned)
 __device__ __forceinline__ u32x4 load8_bf16(__amdgpu_buffer_rsrc_t r, int e) {
@@ -547,22 +507,29 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     // 3. node vectors at t from the per-plane sums (thread = node), the layers' families; tg and dX of the rows
     {
       const bool nin = tid < n;
-      NodeSums x;
-      x.r = nin ? cubic(pv[0], f) : 0.f;
-      x.rd = nin ? dcubic(pv[0], f) : 0.f;
-      x.c = nin ? cubic(pv[1], f) : 0.f;
-      x.cd = nin ? dcubic(pv[1], f) : 0.f;
-      x.dg = cubic(pv[2], f);
-      x.dgd = dcubic(pv[2], f);
-      x.s = cubic(pt, f);
-      x.sd = dcubic(pt, f);
+      const float r = nin ? cubic(pv[0], f) : 0.f, rd = nin ? dcubic(pv[0], f) : 0.f;
+      const float c = nin ? cubic(pv[1], f) : 0.f, cd = nin ? dcubic(pv[1], f) : 0.f;
+      const float dg = cubic(pv[2], f), dgd = dcubic(pv[2], f);
+      const float s = cubic(pt, f), sd = dcubic(pt, f);
       const bool row = tid >= r0 && tid < r0 + kRB && nin;
       for (int l = 0; l < L; ++l) {
         const float* fc = a.fusion + l * GNCDE_FC;
-        if (tid < NP) sV[l * NP + tid] = fam_v(fc, x);
+        if (tid < NP)
+          sV[l * NP + tid] = fc[GNCDE_FC_VR_A] * r + fc[GNCDE_FC_VR_DA] * rd + fc[GNCDE_FC_VC_A] * c +
+                             fc[GNCDE_FC_VC_DA] * cd;
         if (row) {
           const int t = tid - r0;
-          const float wv = fam_w(fc, x), uv = fam_u(fc, x), qv = fam_q(fc, x, wv, uv, n);
+          const float wv = fc[GNCDE_FC_WR_A] * r + fc[GNCDE_FC_WR_DA] * rd + fc[GNCDE_FC_WC_A] * c +
+                           fc[GNCDE_FC_WC_DA] * cd + fc[GNCDE_FC_WS_A] * s + fc[GNCDE_FC_WS_DA] * sd;
+          const float uv = fc[GNCDE_FC_IDC] + fc[GNCDE_FC_UD_A] * dg + fc[GNCDE_FC_UD_DA] * dgd + fc[GNCDE_FC_UR_A] * r +
+                           fc[GNCDE_FC_UR_DA] * rd + fc[GNCDE_FC_UC_A] * c + fc[GNCDE_FC_UC_DA] * cd +
+                           fc[GNCDE_FC_US_A] * s + fc[GNCDE_FC_US_DA] * sd;
+          // q_l[i] = sum_k (I + Abar_l)[i][k]: dense terms -> row / column sums, w family n copies, v family
+          // sum_k v_k (sum r = sum c = s), the diagonal once
+          float qv = fc[GNCDE_FC_E_A] * r + fc[GNCDE_FC_E_DA] * rd + fc[GNCDE_FC_ET_A] * c + fc[GNCDE_FC_ET_DA] * cd;
+          qv += (float)n * wv;
+          qv += (fc[GNCDE_FC_VR_A] + fc[GNCDE_FC_VC_A]) * s + (fc[GNCDE_FC_VR_DA] + fc[GNCDE_FC_VC_DA]) * sd;
+          qv += uv;
           sRow[l * 16 + t] = wv;
           sRow[(L + l) * 16 + t] = uv;
           sRow[(2 * L + l) * 16 + t] = qv;
