@@ -713,21 +713,17 @@ __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
 // in LDS in a fixed order).  The A operand tgF_im dX_ij is formed in registers (dX_i. held for the whole K loop); W'
 // operands are issued a batch of m ahead, held apart from their use by scheduling barriers (the compiler otherwise
 // sinks each load to its MFMA: one L2 round trip per MFMA).
-// RT row tiles per workgroup share every W' operand (round 6: at config 3, B n = 8,256 rows, one tile per workgroup
-// re-read all 256 KB of W' for every 16 rows — 132 MB of L2 reads per launch; three tiles cut that to a third).  Each
-// output tile keeps the one-tile kernel's MFMA sequence (same m, q order and operands): bitwise the same g_P.
-template <int H, int RT>
+template <int H>
 __global__ void __launch_bounds__(256) k_bwd_head_gemm(int rows, const float* __restrict__ tgF,
                                                        const float* __restrict__ dxo, const float* __restrict__ wl,
                                                        const float* __restrict__ bl, float* __restrict__ gP,
                                                        float* __restrict__ gq) {
   constexpr int CT = H / 16, KP = 4 / CT, MP = H / KP;  // column tiles, waves per tile, m per wave
   constexpr int MB = MP < 8 ? MP : 8;                   // m per W' batch
-  constexpr int RR = 16 * RT;                           // rows per workgroup
-  __shared__ float sg[RR][H + 1];
-  __shared__ float sx[RR][17];
-  __shared__ floatx4 red[4][RT][64];
-  const int r0 = blockIdx.x * RR;
+  __shared__ float sg[16][H + 1];
+  __shared__ float sx[16][17];
+  __shared__ floatx4 red[4][64];
+  const int r0 = blockIdx.x * 16;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lo = lane & 15, hi = lane >> 4;
   const int ct = w % CT, kp = w / CT, m0 = kp * MP;
   // this wave's W' operands: row 16 m + 4 s + hi, column 16 ct + lo (issued before the staging waits)
@@ -737,23 +733,19 @@ __global__ void __launch_bounds__(256) k_bwd_head_gemm(int rows, const float* __
   for (int mm = 0; mm < MB; ++mm)
 #pragma unroll
     for (int q = 0; q < 4; ++q) wv[0][mm][q] = wb[(size_t)(16 * mm + 4 * q) * H];
-  for (int e = tid; e < RR * H; e += 256) {
+  for (int e = tid; e < 16 * H; e += 256) {
     const int R = e / H, c = e % H;
     sg[R][c] = r0 + R < rows ? tgF[(size_t)(r0 + R) * H + c] : 0.f;
   }
-  for (int e = tid; e < RR * 16; e += 256) {
-    const int R = e >> 4, j = e & 15;
+  {
+    const int R = tid >> 4, j = tid & 15;
     sx[R][j] = r0 + R < rows ? dxo[(size_t)(r0 + R) * 16 + j] : 0.f;
   }
   __syncthreads();
-  float dxr[RT][4];
+  float dxr[4];
 #pragma unroll
-  for (int t = 0; t < RT; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dxr[t][q] = sx[16 * t + lo][4 * q + hi];
-  floatx4 acc[RT];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < 4; ++q) dxr[q] = sx[lo][4 * q + hi];
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int mb = 0; mb < MP; mb += MB) {
@@ -766,37 +758,26 @@ __global__ void __launch_bounds__(256) k_bwd_head_gemm(int rows, const float* __
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int mm = 0; mm < MB; ++mm) {
+      const float g = sg[lo][m0 + mb + mm];
 #pragma unroll
-      for (int t = 0; t < RT; ++t) {
-        const float g = sg[16 * t + lo][m0 + mb + mm];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[t] = mfma4(g * dxr[t][q], wv[cur][mm][q], acc[t]);
-      }
+      for (int q = 0; q < 4; ++q) acc = mfma4(g * dxr[q], wv[cur][mm][q], acc);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (KP > 1) {
-#pragma unroll
-    for (int t = 0; t < RT; ++t) red[w][t][lane] = acc[t];
+    red[w][lane] = acc;
     __syncthreads();
     if (kp == 0)
 #pragma unroll
-      for (int t = 0; t < RT; ++t)
-#pragma unroll
-        for (int p = 1; p < KP; ++p) acc[t] += red[w + p * CT][t][lane];
+      for (int p = 1; p < KP; ++p) acc += red[w + p * CT][lane];
   }
   if (kp == 0)
 #pragma unroll
-    for (int t = 0; t < RT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int R = r0 + 16 * t + 4 * hi + r;
-        if (R < rows) gP[(size_t)R * H + 16 * ct + lo] = acc[t][r];
-      }
-  // g_q: row R = tid / 16 (+ 16 per pass), m = cl, cl + 16, ... then the 16 lanes of the row in a fixed butterfly
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const int R = 16 * t + (tid >> 4), cl = tid & 15;
+    for (int r = 0; r < 4; ++r)
+      if (r0 + 4 * hi + r < rows) gP[(size_t)(r0 + 4 * hi + r) * H + 16 * ct + lo] = acc[r];
+  // g_q: row R = tid / 16, m = cl, cl + 16, ... then the 16 lanes of the row in a fixed butterfly
+  {
+    const int R = tid >> 4, cl = tid & 15;
     float p = 0.f;
     for (int m = cl; m < H; m += 16) {
       float k = 0.f;
@@ -808,29 +789,6 @@ __global__ void __launch_bounds__(256) k_bwd_head_gemm(int rows, const float* __
     for (int o = 8; o > 0; o >>= 1) p += __shfl_xor(p, o);
     if (cl == 0 && r0 + R < rows) gq[r0 + R] = p;
   }
-}
-
-// row tiles per k_bwd_head_gemm workgroup: the most that still gives every CU a workgroup, at most 3
-// (GNCDE_BWD_HEAD_TILES overrides: 1 = the one-tile launch)
-int head_gemm_tiles(int rows) {
-  const char* e = getenv("GNCDE_BWD_HEAD_TILES");
-  if (e) {
-    const int v = atoi(e);
-    return v >= 3 ? 3 : (v == 2 ? 2 : 1);
-  }
-  const int cus = device_cu_count() > 0 ? device_cu_count() : 256;
-  for (int rt = 3; rt > 1; --rt)
-    if ((rows + 16 * rt - 1) / (16 * rt) >= cus * 2 / 3) return rt;
-  return 1;
-}
-template <int H>
-void launch_head_gemm(int rows, const float* tgF, const float* dxo, const float* wl, const float* bl, float* gP,
-                      float* gq, hipStream_t st) {
-  const int rt = head_gemm_tiles(rows);
-  const dim3 g((rows + 16 * rt - 1) / (16 * rt));
-  if (rt == 3) hipLaunchKernelGGL((k_bwd_head_gemm<H, 3>), g, dim3(256), 0, st, rows, tgF, dxo, wl, bl, gP, gq);
-  else if (rt == 2) hipLaunchKernelGGL((k_bwd_head_gemm<H, 2>), g, dim3(256), 0, st, rows, tgF, dxo, wl, bl, gP, gq);
-  else hipLaunchKernelGGL((k_bwd_head_gemm<H, 1>), g, dim3(256), 0, st, rows, tgF, dxo, wl, bl, gP, gq);
 }
 
 // CDE read-out weight / bias gradient on MFMA, K = the node rows of every sample:
@@ -1157,9 +1115,10 @@ int rows_vf_vjp(const GncdeProblem& p, const float* t, const float* u, const flo
     else if (H == 32) hipLaunchKernelGGL(k_bwd_head<32>, dim3(B * w.nb), dim3(256), 0, st, h);
     else hipLaunchKernelGGL(k_bwd_head<64>, dim3(B * w.nb), dim3(256), 0, st, h);
     if (cde) {
-      if (H == 16) launch_head_gemm<16>(B * n, w.tgF, w.dx, h.wl, h.bl, h.gP, h.gq, st);
-      else if (H == 32) launch_head_gemm<32>(B * n, w.tgF, w.dx, h.wl, h.bl, h.gP, h.gq, st);
-      else launch_head_gemm<64>(B * n, w.tgF, w.dx, h.wl, h.bl, h.gP, h.gq, st);
+      const dim3 g((B * n + 15) / 16);
+      if (H == 16) hipLaunchKernelGGL(k_bwd_head_gemm<16>, g, dim3(256), 0, st, B * n, w.tgF, w.dx, h.wl, h.bl, h.gP, h.gq);
+      else if (H == 32) hipLaunchKernelGGL(k_bwd_head_gemm<32>, g, dim3(256), 0, st, B * n, w.tgF, w.dx, h.wl, h.bl, h.gP, h.gq);
+      else hipLaunchKernelGGL(k_bwd_head_gemm<64>, g, dim3(256), 0, st, B * n, w.tgF, w.dx, h.wl, h.bl, h.gP, h.gq);
     }
   }
   const int rbw = bwd_rbw(p, w.nb), grid = B * ((w.nb + rbw - 1) / rbw);

@@ -665,32 +665,6 @@ def test_bwd_row_blocks_per_workgroup_bitwise(G, monkeypatch):
     assert all(torch.isfinite(x).all() for x in outs["1"])
 
 
-def test_bwd_head_gemm_row_tiles_bitwise(G, monkeypatch):
-    """k_bwd_head_gemm (the CDE read-out's input cotangents as one GEMM over every sample's node rows) at config 3's
-    shape (B n = 8,256 rows, h = 64) with one, two and three 16-row tiles per workgroup (GNCDE_BWD_HEAD_TILES; the
-    default picks three there): the tiles of a workgroup share the W' operands and keep the one-tile launch's MFMA
-    sequence per output tile, so every gradient is bitwise the same."""
-    B, n, T, H, de, L = 64, 129, 4, 64, 8, 3
-    rng, ts, coeffs, dcoeffs, dco, P, y0 = cde_inputs(34, B, n, T, 3.0, H, de, L, distinct=4)
-    prob = G.make_problem(ts, coeffs, P.kind, P.layers, data_coeffs=dcoeffs, cde_hidden=H, cde_embed=de)
-    grid, ns = G.layout.stack_grids([O.constant_grid(0.0, 0.3, 0.1)] * B)
-    spec = G.SolverSpec(method=G._lib.TSIT5, save_mode=G._lib.SAVE_STEPS, grid=grid, nsteps=ns)
-    ys = G.integrate(prob, spec, torch.tensor(y0, dtype=torch.float32, device="cuda"))
-    gfin = torch.tensor(rng.standard_normal((B, n, H)), dtype=torch.float32, device="cuda")
-    spec.save_mode = G._lib.SAVE_T1
-    outs = {}
-    for r in ("1", "2", "3", None):
-        if r is None:
-            monkeypatch.delenv("GNCDE_BWD_HEAD_TILES", raising=False)
-        else:
-            monkeypatch.setenv("GNCDE_BWD_HEAD_TILES", r)
-        outs[r] = [x.clone() for x in G.integrate_vjp(prob, spec, ys, gfin)[:3]]
-    for r in ("2", "3", None):
-        for k in range(3):
-            assert torch.equal(outs[r][k], outs["1"][k]), (r, k)
-    assert all(torch.isfinite(x).all() for x in outs["1"])
-
-
 @pytest.mark.parametrize("method", ["rk4", "tsit5"])
 def test_activation_record_matches_recompute(G, method):
     """The activation record (GncdeSolver.act_rec, ABI 7) at config 3's shape: the reverse sweep reading the
