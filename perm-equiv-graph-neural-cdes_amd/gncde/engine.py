@@ -115,7 +115,8 @@ def make_problem(ts, coeffs, kind, layers, data_coeffs=None, cde_hidden=0, cde_e
     """Build a Problem from reference-layout inputs (ts [B,T], coeffs (d,c,b,a) [B,T-1,n,n,2], layer dicts).
 
     compute="bf16" runs the n x n products on bf16 MFMA (split pairs, fp32-class results); "bf16_storage" also
-    stores the operator coefficients in bfloat16; "bf16_mfma" stores them in bfloat16 and runs every product on
+    stores the operator coefficients in bfloat16; "bf16_mfma" (retired: the product library refuses it, an experiment
+    build — `make experiment` — still has it) stores them in bfloat16 and runs every product on
     single-plane bf16 MFMA operands (BASELINE config 5's throughput mode; one-launch evaluation shapes only).  Reverse
     mode = the fp32 adjoint over the coefficients read, see gncde.h GNCDE_COMPUTE_*."""
     coef, tcoef = layout.pack_control(coeffs, device=device)
