@@ -47,6 +47,14 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Orders this wave's LDS accesses across lanes (a store by one lane, a later load of it by another) without a
+// workgroup barrier: the LDS executes one wave's DS instructions in issue order, so only the compiler must not
+// move memory accesses across this point.
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int NP>
 __device__ __forceinline__ int swz(int i, int k) {
   return i * (NP + 1) + k;
@@ -533,8 +541,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         gpre[r] = (l < L - 1 && !(prel[slot][l][r] > 0.f)) ? 0.f : gZ[r];
-        sGb[(4 * hi + r) * MS + node] = gpre[r];
-        sMb[(4 * hi + r) * MS + node] = ml[slot][l][r];
+        sGb[(4 * hi + r) * MS + node] = gpre[r];  // (m itself enters G from registers: no m^T staging)
       }
       {
         float cm[4];
@@ -657,7 +664,10 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
         sMb[(4 * hi + r) * MS + node] = zn[r];
         gbA[l][r] += gm[r];  // lane partials: reduced over the wave's nodes once, at the end
       }
-      __syncthreads();
+      // The gW operands below are this wave's own node columns of the restaged gm / zn, so only the wave's own
+      // stores must precede them: the LDS executes one wave's DS instructions in order, and the compiler fence
+      // keeps the reads behind the stores (no workgroup barrier).
+      wave_lds_order();
       {
         const float4 ga = *reinterpret_cast<const float4*>(sGb + lo * MS + 16 * w + 4 * hi);
         const float4 za = *reinterpret_cast<const float4*>(sMb + lo * MS + 16 * w + 4 * hi);
@@ -680,7 +690,10 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
       dot = xor_sum4(dot);
 #pragma unroll
       for (int r = 0; r < 4; ++r) gZ[r] = node_ok ? invl[slot][l] * (gxh[r] - xh[r] * dot * (1.0f / (float)H)) : 0.f;
-      __syncthreads();  // restaged buffers read before the next layer / form writes them
+      // No barrier here: what follows (the next layer's gpre / m stores, a forward's m^T stores) writes only this
+      // wave's own node columns of sGb / sMb, which no other wave reads before the next workgroup barrier, and
+      // sCol[w] was last read before the barrier above; a form or the final reduction starts with a barrier.
+      wave_lds_order();
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) gU[r] = gZ[r];
