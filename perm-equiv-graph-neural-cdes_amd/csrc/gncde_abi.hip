@@ -341,28 +341,41 @@ __global__ void k_affine_grad_x(int rows, int din, int dout, const float* __rest
 
 // One block per weight entry (o, f) (f == din: the bias): gW[o, f] = sum_r g[r, o] x[r, f], gb[o] = sum_r g[r, o].
 // Fixed strided partition + tree reduction: deterministic.
-__global__ void __launch_bounds__(256) k_affine_grad_w(int rows, int din, int dout, const float* __restrict__ x,
-                                                       const float* __restrict__ g, float* __restrict__ gW,
-                                                       float* __restrict__ gb) {
+// One workgroup per weight / bias entry, summing over every node row.  1024 threads, each with four independent
+// accumulators (rows t + 1024 (4 j + u)), so 8 loads per thread are in flight: the sum over B n rows (131 K at
+// config 4) is a handful of memory round trips, not 128 dependent ones.  Fixed order (deterministic, no atomics).
+__global__ void __launch_bounds__(1024) k_affine_grad_w(int rows, int din, int dout, const float* __restrict__ x,
+                                                        const float* __restrict__ g, float* __restrict__ gW,
+                                                        float* __restrict__ gb) {
   const int e = blockIdx.x;
   const int o = e / (din + 1), f = e % (din + 1);
-  float acc = 0.f;
-  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
-    const float gv = g[(size_t)r * dout + o];
-    acc = f < din ? fmaf(gv, x[(size_t)r * din + f], acc) : acc + gv;
+  const bool bias = f == din;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int r = threadIdx.x;
+  for (; r + 3 * 1024 < rows; r += 4 * 1024) {
+    float gv[4], xv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      gv[u] = g[(size_t)(r + u * 1024) * dout + o];
+      xv[u] = bias ? 1.f : x[(size_t)(r + u * 1024) * din + f];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = fmaf(gv[u], xv[u], acc[u]);
   }
-  __shared__ float red[256];
-  red[threadIdx.x] = acc;
+  for (int u = 0; r < rows; r += 1024, ++u) acc[u & 3] = fmaf(g[(size_t)r * dout + o], bias ? 1.f : x[(size_t)r * din + f], acc[u & 3]);
+  float v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  v = wave_sum64(v);
+  __shared__ float red[16];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
   if (threadIdx.x == 0) {
-    if (f < din) {
-      if (gW) gW[(size_t)o * din + f] = red[0];
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w];
+    if (!bias) {
+      if (gW) gW[(size_t)o * din + f] = t;
     } else if (gb) {
-      gb[o] = red[0];
+      gb[o] = t;
     }
   }
 }
@@ -475,7 +488,7 @@ int gncde_node_affine_grad(int32_t rows, int32_t din, int32_t dout, const float*
                        g, gx);
   }
   if (gW || gb)
-    hipLaunchKernelGGL(k_affine_grad_w, dim3((unsigned)(dout * (din + 1))), dim3(256), 0, st, rows, din, dout, x, g,
+    hipLaunchKernelGGL(k_affine_grad_w, dim3((unsigned)(dout * (din + 1))), dim3(1024), 0, st, rows, din, dout, x, g,
                        gW, gb);
   return hipGetLastError() == hipSuccess ? GNCDE_OK : GNCDE_ERR_HIP;
 }
