@@ -929,8 +929,17 @@ __global__ void k_stage_grad_sum(int B, int L, const float* __restrict__ gp, flo
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const int per = L * kGradStride;
   if (j >= per) return;
+  // samples in order (the summation order is fixed); 16 loads in flight per batch of the chain
   float sum = 0.f;
-  for (int b = 0; b < B; ++b) sum += gp[(size_t)b * per + j];
+  int b = 0;
+  for (; b + 16 <= B; b += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = gp[(size_t)(b + u) * per + j];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) sum += v[u];
+  }
+  for (; b < B; ++b) sum += gp[(size_t)b * per + j];
   const int l = j / kGradStride, q = j % kGradStride;
   if (q < kLayerP)
     gparams[l * kLayerP + q] = sum;

@@ -293,7 +293,15 @@ __global__ void v_batch_sum(int B, size_t P, const float* __restrict__ x, float*
   const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= P) return;
   float s = 0.f;
-  for (int b = 0; b < B; ++b) s += x[(size_t)b * P + e];
+  int b = 0;
+  for (; b + 16 <= B; b += 16) {  // the same order, 16 loads in flight per batch
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = x[(size_t)(b + u) * P + e];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += v[u];
+  }
+  for (; b < B; ++b) s += x[(size_t)b * P + e];
   out[e] = s;
 }
 
