@@ -901,6 +901,21 @@ __global__ void k_bwd_data(int B, int n, int H, int T, const float* __restrict__
 }
 
 // Reduce the partial slots (fixed order) into gW'[l] [d_out, H] and gb'[l] [d_out] per layer, and the fusion gradient.
+// sum_k p[k * stride] for k = 0 .. count-1 in order, 16 loads in flight per batch of the chain
+__device__ __forceinline__ float ordered_sum(const float* __restrict__ p, size_t stride, int count) {
+  float s = 0.f;
+  int k = 0;
+  for (; k + 16 <= count; k += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = p[(size_t)(k + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += v[u];
+  }
+  for (; k < count; ++k) s += p[(size_t)k * stride];
+  return s;
+}
+
 __global__ void k_bwd_reduce(int slots, int L, int H, int gw_stride, int cde, int ro_chunks,
                              const float* __restrict__ gfc, const float* __restrict__ gw, const float* __restrict__ gwo,
                              float* __restrict__ gfusion, float* __restrict__ gwp, float* __restrict__ gbp) {
@@ -908,15 +923,12 @@ __global__ void k_bwd_reduce(int slots, int L, int H, int gw_stride, int cde, in
   const int nfc = L * GNCDE_FC;
   const int nh = (cde ? L - 1 : L) * (H * H + H);
   if (e < nfc) {
-    float s = 0.f;
-    for (int k = 0; k < slots; ++k) s += gfc[(size_t)k * nfc + e];
-    gfusion[e] = s;
+    gfusion[e] = ordered_sum(gfc + e, nfc, slots);
     return;
   }
   int q = e - nfc;
   if (q < nh) {
-    float s = 0.f;
-    for (int k = 0; k < slots; ++k) s += gw[(size_t)k * gw_stride + q];
+    const float s = ordered_sum(gw + q, gw_stride, slots);
     const int l = q / (H * H + H), r = q % (H * H + H);
     if (r < H * H) gwp[(size_t)l * H * H + r] = s;  // layers < L-1 (and the ODE output) are H x H
     else gbp[(size_t)l * H + r - H * H] = s;
@@ -924,8 +936,7 @@ __global__ void k_bwd_reduce(int slots, int L, int H, int gw_stride, int cde, in
   }
   q -= nh;
   if (cde && q < 16 * H * (H + 1)) {
-    float s = 0.f;
-    for (int k = 0; k < ro_chunks; ++k) s += gwo[(size_t)k * 16 * H * (H + 1) + q];
+    const float s = ordered_sum(gwo + q, (size_t)16 * H * (H + 1), ro_chunks);
     const int mj = q / (H + 1), c = q % (H + 1);
     const size_t wo = (size_t)(L - 1) * H * H, bo = (size_t)(L - 1) * H;
     if (c < H) gwp[wo + (size_t)mj * H + c] = s;
@@ -954,7 +965,22 @@ __global__ void k_bwd_params(int L, int H, int dlast, const float* __restrict__ 
   for (int jo = threadIdx.x; jo < dout; jo += blockDim.x) g[2 * din + dout * din + jo] = gb_[jo];
   for (int c = threadIdx.x; c < din; c += blockDim.x) {
     float sw = 0.f, sb = 0.f;
-    for (int jo = 0; jo < dout; ++jo) {
+    int jo = 0;
+    for (; jo + 8 <= dout; jo += 8) {  // the same order, the loads of 8 rows in flight
+      float gw8[8], w8[8], gb8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        gw8[u] = gW_[(size_t)(jo + u) * din + c];
+        w8[u] = W[(size_t)(jo + u) * din + c];
+        gb8[u] = gb_[jo + u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        sw = fmaf(gw8[u], w8[u], sw);
+        sb = fmaf(gb8[u], w8[u], sb);
+      }
+    }
+    for (; jo < dout; ++jo) {
       sw = fmaf(gW_[(size_t)jo * din + c], W[(size_t)jo * din + c], sw);
       sb = fmaf(gb_[jo], W[(size_t)jo * din + c], sb);
     }

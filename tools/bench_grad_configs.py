@@ -63,6 +63,9 @@ def main():
                 torch.cuda.synchronize()
                 fw.append(e[0].elapsed_time(e[1]))
                 bw.append(e[1].elapsed_time(e[2]))
+            dump = os.environ.get("GNCDE_BENCH_DUMP")  # A/B checks: the last repetition's gradient
+            if dump:
+                torch.save(params.grad.cpu(), f"{dump}_{c}_{mode}_{int(share > 0)}_{int(replay)}.pt")
             print(json.dumps({"config": name, "compute": mode, "stage_record": share > 0,
                               "pid_backward": ("replay" if replay else "record") if c == "5" else None,
                               "grad_finite": bool(torch.isfinite(params.grad).all()), "forward_ms": round(min(fw[1:]), 3),
