@@ -251,19 +251,30 @@ __global__ void __launch_bounds__(256) k_coef_sums(int n, int T, const CT* __res
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int j = tid; j < n; j += 256) {  // column j: one thread walks it (coalesced across the block)
     float s = 0.f;
-#pragma unroll 8
+#pragma unroll 32
     for (int i = 0; i < n; ++i) s += coef_at(P, (size_t)i * n + j);
     o[(q * 3 + 1) * n + j] = s;
     o[(q * 3 + 2) * n + j] = coef_at(P, (size_t)j * n + j);
   }
   float tot = 0.f;  // lane 0 of wave w: the sum of its rows' sums, in row order
-  for (int i = w; i < n; i += 4) {  // row i: wave w's lanes across it, one wave reduction
-    float s = 0.f;
-    for (int j = lane; j < n; j += 64) s += coef_at(P, (size_t)i * n + j);
+  // row i: wave w's lanes across it, one wave reduction; four rows (i0, i0 + 4, i0 + 8, i0 + 12) per pass, so their
+  // loads are in flight together (each row's and the total's summation order unchanged)
+  for (int i0 = w; i0 < n; i0 += 16) {
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int j = lane; j < n; j += 64)
 #pragma unroll
-    for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
-    if (lane == 0) o[(q * 3) * n + i] = s;
-    tot += s;
+      for (int u = 0; u < 4; ++u)
+        if (i0 + 4 * u < n) s[u] += coef_at(P, (size_t)(i0 + 4 * u) * n + j);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int m = 32; m > 0; m >>= 1) s[u] += __shfl_xor(s[u], m);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + 4 * u < n) {
+        if (lane == 0) o[(q * 3) * n + i0 + 4 * u] = s[u];
+        tot += s[u];
+      }
   }
   __shared__ float wt[4];
   if (lane == 0) wt[w] = tot;

@@ -66,6 +66,9 @@ def run(name, prob, spec, y0, reps, ref=None, ref_steps=None):
         d = (st[:, 0].float() - ref_steps.float()).abs() / ref_steps.float()
         out["steps_max_rel_diff_vs_fp32"] = round(float(d.max()), 4)
     print(json.dumps(out), flush=True)
+    dump = os.environ.get("GNCDE_BENCH_DUMP")  # A/B checks: the solve's output
+    if dump:
+        torch.save(ys.cpu(), f"{dump}_{name}.pt")
     return ys, st[:, 0].clone()
 
 
