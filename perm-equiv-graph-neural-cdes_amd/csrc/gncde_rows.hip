@@ -165,8 +165,18 @@ inline size_t rows_smem(int n, int H, int L, bool bf, bool cache = false) {
                           4 * 64 * 4 + 4) + (cache ? kCoefCacheBytes : 0);
 }
 
+// Every buffer in this file is one sample's (or one interval's) block: its base and size are workgroup-uniform.  They
+// are taken through readfirstlane so that the descriptor is built in SGPRs even where the compiler cannot prove the
+// sample index uniform (the solve's sample queue, values that reach it through LDS or the controller's decisions):
+// a descriptor in VGPRs wraps every buffer access in a waterfall loop.
+// (Only the adaptive solve needs it — its sample queue and controller decisions — and only it takes it: UNI.)
+template <bool UNI = false>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+  if constexpr (!UNI) return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  void* q = (void*)(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
 // MODE 1: ODE output layer.  MODE 2: CDE read-out (de = 8, cde_hidden = H).  Three workgroups per CU (168 VGPRs)
@@ -183,6 +193,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
 template <int H, int MODE, int PREC, int SOLVE>
 __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr bool UNI = (SOLVE & 3) == 1 || (SOLVE & 4) != 0;  // uniform buffer descriptors (rsrc): PID, granules
   constexpr bool CBF = PREC != 0;  // bfloat16 coefficients
   constexpr bool BF = PREC == 1;   // bf16 products
   constexpr int ZS = rows_zs(H);
@@ -224,8 +235,11 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     if (threadIdx.x == 0)
       sFlag[1] = (int)(__hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.ticket0);
     __syncthreads();
-    g = sFlag[1] / nb;
-    rb = sFlag[1] % nb;
+    // readfirstlane: an LDS value is a vector register to the compiler; as a scalar, every address and buffer
+    // descriptor derived from the sample stays in SGPRs (otherwise each buffer access is wrapped in a waterfall loop)
+    const int tk = UNI ? __builtin_amdgcn_readfirstlane(sFlag[1]) : sFlag[1];
+    g = tk / nb;
+    rb = tk % nb;
   } else if (a.G % 8 == 0) {  // a group's workgroups share blockIdx % 8 (bijective for G % 8 == 0)
     const int x = blockIdx.x;
     g = (x & 7) + 8 * (x / (8 * nb));
@@ -285,11 +299,12 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       sFlag[0] = gave_up;
     }
     __syncthreads();
+    if constexpr (UNI) return __builtin_amdgcn_readfirstlane(sFlag[0]) == 0;  // uniform (see rsrc)
     return sFlag[0] == 0;
   };
 
   auto gran_rsrc = [&](unsigned s, int bb) {
-    return rsrc(a.zgran + ((size_t)(s & 1) * a.B + bb) * zgroup * 2, (unsigned)(zgroup * 8));
+    return rsrc<UNI>(a.zgran + ((size_t)(s & 1) * a.B + bb) * zgroup * 2, (unsigned)(zgroup * 8));
   };
   // elements e .. e + 3 (one float4 of a row) as two 16-byte {value, tag, value, tag} stores (every vector element
   // copied to a scalar before its bit cast: a bit cast of an ext-vector element reads element 0, see coef_el)
@@ -395,7 +410,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
     // Both coefficient reads are unconditional coalesced dwordx4 buffer loads from this (sample, interval)'s four
     // planes (the descriptor's range check zero-fills anything past plane a); values outside the matrix are
     // selected to 0 before they reach LDS, so no load sits in a divergent branch.
-    const auto crs = rsrc(cb, (unsigned)(4 * nn * sizeof(CT_)));
+    const auto crs = rsrc<UNI>(cb, (unsigned)(4 * nn * sizeof(CT_)));
     const int RS = NP + 4;                 // LDS row stride of the rows block
     float* sAr = big + 2 * NP * kStrip;    // rows block A(t)[R, :] [16][RS], then dA/dt [16][RS]
     // 1. issue the rows block (thread = (row tid / 16, columns 4 (tid % 16) + 64 u): 256 coalesced bytes per row
@@ -422,7 +437,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
         }
       // the column strip [:, R] = rows R of the transposed planes: the same whole-line pattern as the rows block
       const CT_* cbt = reinterpret_cast<const CT_*>(a.coefT) + ((size_t)b * (T - 1) + idx) * 4 * nn;
-      const auto crt = rsrc(cbt, (unsigned)(4 * nn * sizeof(CT_)));
+      const auto crt = rsrc<UNI>(cbt, (unsigned)(4 * nn * sizeof(CT_)));
 #pragma unroll
       for (int u = 0; u < NU; ++u)
 #pragma unroll
@@ -601,7 +616,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
         const float* zin = l == 0 ? z0
                          : kslab ? kslab + ((size_t)(l - 1) * a.B + b) * zgroup
                                           : a.zbuf[(pub - 1) & 1] + (size_t)zslot * zgroup;
-        const auto rs = rsrc(zin, (unsigned)(zgroup * sizeof(float)));
+        const auto rs = rsrc<UNI>(zin, (unsigned)(zgroup * sizeof(float)));
         for (int e0 = tid; e0 < tot; e0 += 256 * U) {
           floatx4 v[U];
 #pragma unroll
@@ -765,7 +780,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       if constexpr (GRAN) {  // the rows as tagged granules (and, recording, as plain floats into the slab)
         const unsigned tag = hseq + 1;
         const auto rg = gran_rsrc(hseq, b);
-        const auto rk = rsrc(kslab ? kslab + ((size_t)l * a.B + b) * zgroup : a.zbuf[0], (unsigned)(zgroup * 4));
+        const auto rk = rsrc<UNI>(kslab ? kslab + ((size_t)l * a.B + b) * zgroup : a.zbuf[0], (unsigned)(zgroup * 4));
         if (tid < 16 * G4) {
           const int R = tid / G4, q = tid % G4;
           if (r0 + R < n) {
@@ -780,7 +795,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       } else {
         // (an idle round keeps to its group's own buffers: the sample it recomputes is another group's)
         float* zout = kslab ? kslab + ((size_t)l * a.B + b) * zgroup : a.zbuf[pub & 1] + (size_t)zslot * zgroup;
-        const auto rs = rsrc(zout, (unsigned)(zgroup * sizeof(float)));
+        const auto rs = rsrc<UNI>(zout, (unsigned)(zgroup * sizeof(float)));
         if (tid < 16 * G4) {  // write-through 16-byte stores of this workgroup's rows, then one arrival
           const int R = tid / G4, q = tid % G4;
           if (r0 + R < n)
@@ -947,7 +962,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       } else {  // sc1 16-byte stores + one arrival
         if (mine)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, u),
-                                                 rsrc(a.zbuf[pub & 1] + (size_t)b * zgroup, (unsigned)(E * 4)),
+                                                 rsrc<UNI>(a.zbuf[pub & 1] + (size_t)b * zgroup, (unsigned)(E * 4)),
                                                  (int)(((r0 + orow) * H + ocol) * 4), 0, 16);
         arrive();
       }
@@ -982,19 +997,26 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
           p1 += rsum[16 + r];
         }
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, floatx2{p0, p1}),
-                                              rsrc(part, (unsigned)(nb * 8)), rb * 8, 0, 16);
+                                              rsrc<UNI>(part, (unsigned)(nb * 8)), rb * 8, 0, 16);
       }
       arrive();
       const bool ok = wait_all();
-      const auto rs = rsrc(part, (unsigned)(nb * 8));
+      const auto rs = rsrc<UNI>(part, (unsigned)(nb * 8));
       float a0 = 0.f, a1 = 0.f;
       for (int q = 0; q < nb; ++q) {
         const floatx2 v = __builtin_bit_cast(floatx2, __builtin_amdgcn_raw_buffer_load_b64(rs, q * 8, 0, 16));
         a0 += v.x;
         a1 += v.y;
       }
-      s0 = a0;
-      s1 = a1;
+      // every lane holds the same sums: as scalars, the controller's decisions (and everything they steer: the hand-off
+      // counters, the sample's buffers) stay uniform to the compiler, so no buffer access needs a waterfall loop
+      if constexpr (UNI) {
+        s0 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, a0)));
+        s1 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, a1)));
+      } else {
+        s0 = a0;
+        s1 = a1;
+      }
       return ok;
     };
     int steps = 0, rejects = 0, evals = 0, status = 0;
@@ -1357,7 +1379,7 @@ __global__ void __launch_bounds__(256, MODE == 2 || SOLVE != 0 ? 2 : 3) k_rows(R
       sFlag[1] = fault ? a.B : next;
     }
     __syncthreads();
-    const int nx = sFlag[1];
+    const int nx = UNI ? __builtin_amdgcn_readfirstlane(sFlag[1]) : sFlag[1];  // uniform: keeps descriptors scalar
     __syncthreads();  // sFlag is reused by the next sample's barriers
     if (nx >= a.B) break;
     // the group's state for sample nx: its counter line and hand-off buffers start from zero, its knots in registers
