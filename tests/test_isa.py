@@ -37,3 +37,11 @@ def test_every_kernel_has_metadata(isa):
     for name, m in isa["kernels"].items():
         assert {"vgpr", "sgpr", "scratch"} <= set(m), name
         assert m["vgpr"] <= 512, (name, m)  # (gfx950: .vgpr_count is the unified VGPR + AGPR allocation)
+
+
+def test_no_waterfall_loops(isa):
+    """Every buffer descriptor is built in SGPRs: a descriptor the compiler holds in VGPRs wraps each access in a
+    waterfall loop (round 6: the adaptive solve's sample index reached its loop through LDS, 52 such loops in
+    k_rows<32,2,0,1>, removed by readfirstlane'd bases)."""
+    bad = {k: m["waterfalls"] for k, m in isa["kernels"].items() if m["waterfalls"]}
+    assert not bad, bad

@@ -12,7 +12,8 @@ Checks (tests/test_isa.py runs them):
   * no instruction writes through the scalar data cache (scalar stores, scalar atomics, scalar cache write-back);
   * the headline kernel k_fused<64,16,3,rk4> has no scratch, at most 128 VGPRs (four waves per SIMD), and its
     products on v_mfma_f32_16x16x4_f32;
-  * every kernel's scratch is reported (spills are visible, not silent).
+  * every kernel's scratch is reported (spills are visible, not silent);
+  * no kernel wraps a buffer access in a waterfall loop (a descriptor the compiler could not prove uniform).
 This file names scalar-store mnemonics, so it is listed in .gpurunignore (it never runs on the GPU box).
 """
 from __future__ import annotations
@@ -31,6 +32,7 @@ TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 # scalar-data-cache writes: s_store_*, s_buffer_store_*, s_scratch_store_*, s_atomic_*, s_buffer_atomic_*,
 # s_dcache_wb*
 SCALAR_WRITE = re.compile(r"^\s*(s_store_|s_buffer_store_|s_scratch_store_|s_atomic_|s_buffer_atomic_|s_dcache_wb)")
+WATERFALL = re.compile(r"^v_cmp_eq_u64\S*\s+\S+,\s*s\[\d+:\d+\],\s*v\[\d+:\d+\]")
 HEADLINE = "_ZN5gncde12_GLOBAL__N_17k_fusedILi64ELi16ELi3ELi0EEEvNS0_9FusedArgsE"
 
 
@@ -102,6 +104,9 @@ def review(objs=None) -> dict:
                 m["object"] = os.path.basename(o)
                 m["instructions"] = len(ins)
                 m["mfma"] = sum(1 for x in ins if x.startswith("v_mfma"))
+                # waterfall loops (a buffer descriptor the compiler holds in VGPRs: every access compares the
+                # readfirstlane'd SGPR copy with the VGPR one, 64 bits at a time)
+                m["waterfalls"] = sum(1 for x in ins if WATERFALL.match(x))
                 res["kernels"][k] = m
             for k, ins in dis.items():
                 for x in ins:
@@ -133,6 +138,8 @@ def main():
               f"{m.get('scratch', -1):8d} {m.get('lds', -1):7d} {m['instructions']:7d} {m['mfma']:6d}")
     spills = sum(1 for m in ks.values() if m.get("scratch", 0) > 0)
     print(f"kernels with scratch: {spills} of {len(ks)}")
+    wf = {n: m["waterfalls"] for n, m in ks.items() if m["waterfalls"]}
+    print(f"kernels with waterfall loops: {len(wf)}")
 
 
 if __name__ == "__main__":
