@@ -188,6 +188,10 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
   __shared__ float sTs[kTMaxS];
   __shared__ float sFus[L * GNCDE_FC];
   __shared__ float sCol[1][NW][H];
+  // the layers' operand blocks (k_stage_prep), staged once: read from global memory, every Linear and RMSNorm
+  // parameter access was a dependent L1/L2 round trip on the evaluation's critical path (up to seven in a row per
+  // backward layer: tools/isa_review.py disassembly, round 6)
+  __shared__ __attribute__((aligned(16))) float sOp[L * kOpStride];
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -211,6 +215,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
 
   for (int j = tid; j < T; j += NT) sTs[j] = a.ts[(size_t)b * T + j];
   for (int j = tid; j < L * GNCDE_FC; j += NT) sFus[j] = a.fusion[j];
+  for (int j = tid; j < L * kOpStride; j += NT) sOp[j] = a.ops[j];
 
   // step geometry of this sample (padded steps past nsteps have h = 0 and contribute nothing)
   const float* gr = a.grid + (size_t)b * G;
@@ -366,7 +371,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
   auto forward = [&](float (&Z)[4], bool full) __attribute__((always_inline)) {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
-      const float* op = a.ops + (size_t)l * kOpStride;
+      const float* op = sOp + l * kOpStride;
       const float* fc = sFus + l * GNCDE_FC;
 #pragma unroll
       for (int r = 0; r < 4; ++r) Zin[0][l][r] = Z[r];
@@ -437,7 +442,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
   auto forward2 = [&](float (&Za)[4], float (&Zb)[4]) __attribute__((always_inline)) {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
-      const float* op = a.ops + (size_t)l * kOpStride;
+      const float* op = sOp + l * kOpStride;
       const float* fc = sFus + l * GNCDE_FC;
       float mown[2][4];
 #pragma unroll
@@ -535,7 +540,7 @@ __global__ void __launch_bounds__(NP * 4, 1) k_rev(RevArgs a) {
     for (int r = 0; r < 4; ++r) gZ[r] = node_ok ? tg * gK[r] : 0.f;
 #pragma unroll
     for (int l = L - 1; l >= 0; --l) {
-      const float* op = a.ops + (size_t)l * kOpStride;
+      const float* op = sOp + l * kOpStride;
       const float* fc = sFus + l * GNCDE_FC;
       float gpre[4];
 #pragma unroll
