@@ -557,12 +557,25 @@ __global__ void __launch_bounds__(256 * kMaxRbw, 1) k_bwd_layer(BwdArgs a) {
     if (l == 0) {
       if (iin && a.scatter) {  // gncde_vjp.hip's v_stage_scatter arithmetic, fused
         const float hb = a.sc.hcur[b];
+        const int nsc = a.sc.n;  // <= 7 earlier stages
+        // every accumulator element is read before any is written (gy and the gk[j] are distinct buffers): loaded
+        // one after another behind their own stores, they were a chain of up to eight dependent round trips
+        float gyv[U], gkv[U][8];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const size_t o = ((size_t)b * n + r0 + i) * H + cl + 16 * u;
+          gyv[u] = a.sc.gy[o];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gkv[u][j] = j < nsc ? a.sc.gk[j][o] : 0.f;
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const size_t o = ((size_t)b * n + r0 + i) * H + cl + 16 * u;
           const float v = gZ[u];
-          a.sc.gy[o] = fmaf(1.0f, v, a.sc.gy[o]);
-          for (int j = 0; j < a.sc.n; ++j) a.sc.gk[j][o] = fmaf(hb, a.sc.a[j] * v, a.sc.gk[j][o]);
+          a.sc.gy[o] = fmaf(1.0f, v, gyv[u]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < nsc) a.sc.gk[j][o] = fmaf(hb, a.sc.a[j] * v, gkv[u][j]);
         }
       } else if (iin) {
 #pragma unroll
