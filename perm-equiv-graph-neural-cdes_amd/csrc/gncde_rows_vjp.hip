@@ -684,16 +684,30 @@ __global__ void __launch_bounds__(256) k_bwd_head(HeadArgs a) {
   const bool iin = r0 + i < n;
   const int row = iin ? r0 + i : n - 1;
   const float* tc = a.tcoef + ((size_t)b * (T - 1) + idx) * 3 * n + row;
-  const float tg = iin ? fmaf(f, fmaf(3.0f * f, tc[0], 2.0f * tc[n]), tc[2 * n]) : 0.f;
-  for (int c = cl; c < H; c += 16) {
-    const float g = iin ? tg * a.gF[((size_t)b * n + row) * H + c] : 0.f;
+  // every input of the epilogue is requested before its first store (a store to tgF / gout may alias gF for the
+  // compiler, so loads left behind the stores each cost a dependent round trip)
+  const float tc0 = tc[0], tc1 = tc[n], tc2 = tc[2 * n];
+  float gf[H / 16];
+#pragma unroll
+  for (int u = 0; u < H / 16; ++u) gf[u] = a.gF[((size_t)b * n + row) * H + cl + 16 * u];
+  const size_t blk = (size_t)n * 16;
+  float dc0 = 0.f, dc1 = 0.f, dc2 = 0.f;
+  if (a.cde) {
+    const float* dc = a.data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)row * 16 + cl;
+    dc0 = dc[0];
+    dc1 = dc[blk];
+    dc2 = dc[2 * blk];
+  }
+  const float tg = iin ? fmaf(f, fmaf(3.0f * f, tc0, 2.0f * tc1), tc2) : 0.f;
+#pragma unroll
+  for (int u = 0; u < H / 16; ++u) {
+    const int c = cl + 16 * u;
+    const float g = iin ? tg * gf[u] : 0.f;
     sgo[i][c] = g;
     if (iin) (a.cde ? a.tgF : a.gout)[((size_t)b * n + row) * H + c] = g;
   }
   if (a.cde) {  // tg gF and dX only: g_P, g_q are k_bwd_head_gemm's GEMM over all samples' rows
-    const size_t blk = (size_t)n * 16;
-    const float* dc = a.data_coef + ((size_t)b * (T - 1) + idx) * 4 * blk + (size_t)row * 16 + cl;
-    const float dx = iin ? fmaf(f, fmaf(3.0f * f, dc[0], 2.0f * dc[blk]), dc[2 * blk]) : 0.f;
+    const float dx = iin ? fmaf(f, fmaf(3.0f * f, dc0, 2.0f * dc1), dc2) : 0.f;
     if (iin) a.dxo[((size_t)b * n + row) * 16 + cl] = dx;
     return;
   }
